@@ -1,0 +1,161 @@
+/*
+ * stark_gpu.h -- C ABI of the MI355X-native STARK hot path (libstarkgpu.so).
+ *
+ * Drop-in boundary for the reference crate SpekalsG3/zk-stark-tutor (Rust).
+ * Each entry point replaces one reference function; the citation after each
+ * declaration is the file:line (under the reference's src/) of the Rust item
+ * whose signature and semantics it keeps.  A Rust `extern "C"` shim (see
+ * INTEGRATION.md) marshals Vec<FieldElement> into packed sg_fe arrays and maps
+ * negative return codes to the reference's panic!/Err paths.
+ *
+ * Conventions
+ *   - sg_fe is a canonical field element (value < p = 1 + 407*2^119) as two
+ *     little-endian u64 limbs.  Inputs >= p are rejected (SG_ERR_NONCANONICAL)
+ *     where the library reads them on the host, otherwise undefined.
+ *   - The caller owns every host buffer; the library owns device memory it
+ *     allocates.  `_dev` variants take device pointers (hipMalloc'd) and run on
+ *     the context's stream; all calls return after their work is complete.
+ *   - Return value: 0 on success, < 0 on error (sg_last_error() has the text).
+ *     The library never aborts the process.
+ *   - A context is not thread-safe: one context per host thread.
+ */
+#ifndef STARK_GPU_H
+#define STARK_GPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SG_OK 0
+#define SG_ERR_INVALID (-1)      /* argument the reference rejects with panic!/assert */
+#define SG_ERR_HIP (-2)          /* HIP runtime error */
+#define SG_ERR_NONCANONICAL (-3) /* field element >= p */
+#define SG_ERR_CALLBACK (-4)     /* a proof-stream callback returned non-zero */
+#define SG_ERR_NOMEM (-5)
+
+typedef struct {
+  uint64_t lo, hi;
+} sg_fe;
+
+typedef struct sg_ctx sg_ctx;
+
+/* ------------------------------------------------------------ context */
+int sg_ctx_create(int device, sg_ctx** out);
+void sg_ctx_destroy(sg_ctx* ctx);
+const char* sg_last_error(const sg_ctx* ctx);
+/* hipStream_t the context launches on (for callers that time or chain work) */
+void* sg_ctx_stream(sg_ctx* ctx);
+/* release cached device buffers and twiddle tables */
+int sg_ctx_trim(sg_ctx* ctx);
+
+/* ------------------------------------------------------------ field (field/field.rs) */
+sg_fe sg_field_prime(void);                               /* field/field.rs:10 FIELD_PRIME */
+sg_fe sg_field_generator(void);                           /* field/field.rs:41-44 Field::generator */
+int sg_primitive_nth_root(uint64_t n, sg_fe* out);        /* field/field.rs:58-71 Field::primitive_nth_root */
+sg_fe sg_field_sample(const uint8_t* bytes, size_t len);  /* field/field.rs:87-99 Field::sample */
+sg_fe sg_fe_mul(sg_fe a, sg_fe b);                        /* field/field_element.rs:70-78 Mul */
+sg_fe sg_fe_inverse(sg_fe a);                             /* field/field_element.rs:35-40 inverse */
+sg_fe sg_fe_pow(sg_fe a, uint64_t e);                     /* field/field_element.rs:127-143 BitXor<usize> */
+
+/* ------------------------------------------------------------ transforms (fft/) */
+/* fft/ntt.rs:7-49  pub fn ntt(root, inputs: Vec<FieldElement>) -> Vec<FieldElement>
+ * out receives next_pow2(n_in) elements (zero padding as bit_reverse_copy does). */
+int sg_ntt(sg_ctx* ctx, sg_fe root, const sg_fe* inputs, size_t n_in, sg_fe* out);
+/* fft/ntt.rs:51-68  pub fn intt(root, input) -> Vec<FieldElement>; n_in < 2 returns the input */
+int sg_intt(sg_ctx* ctx, sg_fe root, const sg_fe* inputs, size_t n_in, sg_fe* out);
+/* fft/ntt_arithmetics.rs:161-170  pub fn fast_coset_evaluate(generator, root_order, offset, polynomial)
+ * out receives next_pow2(root_order) elements; d > root_order is SG_ERR_INVALID (reference panics). */
+int sg_fast_coset_evaluate(sg_ctx* ctx, sg_fe generator, uint64_t root_order, sg_fe offset,
+                           const sg_fe* coeffs, size_t d, sg_fe* out);
+/* same, with device pointers (inputs resident in HBM) */
+int sg_ntt_dev(sg_ctx* ctx, sg_fe root, const sg_fe* d_inputs, size_t n_in, sg_fe* d_out);
+int sg_intt_dev(sg_ctx* ctx, sg_fe root, const sg_fe* d_inputs, size_t n_in, sg_fe* d_out);
+int sg_fast_coset_evaluate_dev(sg_ctx* ctx, sg_fe generator, uint64_t root_order, sg_fe offset,
+                               const sg_fe* d_coeffs, size_t d, sg_fe* d_out);
+
+/* ------------------------------------------------------------ Merkle (merkle_root.rs) */
+typedef struct sg_tree sg_tree; /* retained device tree: all 2n-1 digests */
+
+/* merkle_root.rs:21-32  MerkleRoot::commit(leafs: &[FieldElement]) -> Bytes (64 bytes) */
+int sg_merkle_commit(sg_ctx* ctx, const sg_fe* leaves, size_t n, uint8_t root[64]);
+/* merkle_root.rs:55-66  MerkleRoot::open(index, leafs) -> Vec<Bytes>; path gets log2(n) x 64 bytes */
+int sg_merkle_open(sg_ctx* ctx, size_t index, const sg_fe* leaves, size_t n, uint8_t* path, size_t* path_len);
+/* merkle_root.rs:89-95  MerkleRoot::verify(root, index, path, leaf) -> bool: returns 1/0, < 0 on error */
+int sg_merkle_verify(const uint8_t root[64], size_t index, const uint8_t* path, size_t path_len, sg_fe leaf);
+/* device-resident tree: build once, open in O(log n) */
+int sg_merkle_build_dev(sg_ctx* ctx, const sg_fe* d_leaves, size_t n, sg_tree** out);
+int sg_tree_root(const sg_tree* t, uint8_t root[64]);
+size_t sg_tree_leaves(const sg_tree* t);
+int sg_tree_open(sg_ctx* ctx, const sg_tree* t, size_t index, uint8_t* path, size_t* path_len);
+void sg_tree_free(sg_ctx* ctx, sg_tree* t);
+
+/* ------------------------------------------------------------ proof stream (proof_stream.rs) */
+/* Object codes = StarkProofStreamEnum discriminants (stark/proof_stream_enum.rs:8-15);
+ * payload = the to_bytes() serialization (stark/proof_stream_enum.rs:67-127). */
+#define SG_OBJ_ROOT 0
+#define SG_OBJ_CODEWORD 1
+#define SG_OBJ_PATH 2
+#define SG_OBJ_LEAFS 3
+#define SG_OBJ_VALUE 4
+
+/* Callback view of any ProofStream impl (proof_stream.rs:6-12): push + fiat_shamir_prover. */
+typedef struct {
+  void* user;
+  int (*push)(void* user, uint8_t code, const uint8_t* payload, size_t len);
+  int (*fiat_shamir_prover)(void* user, size_t num_bytes, uint8_t* out);
+} sg_proof_stream;
+
+/* Native streams: IndependentProofStream (proof_stream.rs:15-78) and
+ * SignatureProofStream (rescue_prime/proof_stream.rs:9-61, prefix = blake2b(document)). */
+typedef struct sg_stream sg_stream;
+sg_stream* sg_stream_create(void);
+sg_stream* sg_stream_create_signature(const uint8_t* document, size_t doc_len);
+void sg_stream_destroy(sg_stream* s);
+sg_proof_stream sg_stream_callbacks(sg_stream* s);
+int sg_stream_push(sg_stream* s, uint8_t code, const uint8_t* payload, size_t len);
+size_t sg_stream_count(const sg_stream* s);
+/* stark/proof_stream_enum.rs:161-190 digest(): pass out=NULL to query the size */
+int sg_stream_digest(const sg_stream* s, uint8_t* out, size_t cap, size_t* len);
+int sg_stream_fiat_shamir_prover(const sg_stream* s, size_t num_bytes, uint8_t* out);
+int sg_stream_fiat_shamir_verifier(const sg_stream* s, size_t num_bytes, uint8_t* out);
+/* proof_stream.rs:54-64 pull(): returns a view valid until the stream is modified */
+int sg_stream_pull(sg_stream* s, uint8_t* code, const uint8_t** payload, size_t* len);
+/* stark/stark.rs:30-67 deser_independent_proof_stream */
+int sg_stream_deserialize(const uint8_t* bytes, size_t len, sg_stream** out);
+
+/* ------------------------------------------------------------ FRI (fri.rs) */
+typedef struct {
+  sg_fe offset;                   /* fri.rs:23-29 FRI::new(offset, omega, domain_length, */
+  sg_fe omega;                    /*                       expansion_factor,               */
+  uint64_t domain_length;         /*                       num_colinearity_tests)          */
+  uint64_t expansion_factor;
+  uint64_t num_colinearity_tests;
+} sg_fri;
+
+typedef struct sg_fri_state sg_fri_state; /* retained codewords + trees of every round */
+
+size_t sg_fri_num_rounds(const sg_fri* fri); /* fri.rs:40-50 */
+/* fri.rs:115-172  FRI::commit: Root per round, alpha = sample(fiat_shamir_prover(32)),
+ * fold, final Codeword.  keep != NULL retains the rounds for sg_fri_query. */
+int sg_fri_commit(sg_ctx* ctx, const sg_fri* fri, const sg_fe* codeword, size_t n,
+                  const sg_proof_stream* ps, sg_fri_state** keep);
+int sg_fri_commit_dev(sg_ctx* ctx, const sg_fri* fri, const sg_fe* d_codeword, size_t n,
+                      const sg_proof_stream* ps, sg_fri_state** keep);
+/* fri.rs:210-248  FRI::prove: commit + sample_indices + query per round.
+ * top_indices receives num_colinearity_tests indices. */
+int sg_fri_prove(sg_ctx* ctx, const sg_fri* fri, const sg_fe* codeword, size_t n,
+                 const sg_proof_stream* ps, size_t* top_indices);
+int sg_fri_prove_dev(sg_ctx* ctx, const sg_fri* fri, const sg_fe* d_codeword, size_t n,
+                     const sg_proof_stream* ps, size_t* top_indices);
+void sg_fri_state_free(sg_ctx* ctx, sg_fri_state* st);
+/* fri.rs:88-113  FRI::sample_indices */
+int sg_fri_sample_indices(const uint8_t* seed, size_t seed_len, size_t size, size_t reduced_size,
+                          size_t number, size_t* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* STARK_GPU_H */

@@ -251,8 +251,12 @@ def merkle_commit(values: Sequence[int]) -> bytes:
 
 def merkle_open(index: int, values: Sequence[int]) -> List[bytes]:
     """merkle_root.rs:34-66 MerkleRoot::open: sibling digests from leaf level up."""
-    levels = merkle_levels(values)
-    n = len(values)
+    return merkle_open_levels(index, merkle_levels(values))
+
+
+def merkle_open_levels(index: int, levels: List[List[bytes]]) -> List[bytes]:
+    """merkle_open on precomputed levels (same output; avoids the reference's O(n) rehash per open)."""
+    n = len(levels[0])
     if not 0 <= index < n:
         raise ValueError("cannot open invalid index")
     if n < 2:
@@ -453,10 +457,11 @@ class FRI:
         b = [i + len(current) // 2 for i in indices_c]
         for s in range(self.num_colinearity_tests):
             proof_stream.push((LEAFS, (current[a[s]], current[b[s]], nxt[indices_c[s]])))
+        lc, ln = merkle_levels(current), merkle_levels(nxt)
         for s in range(self.num_colinearity_tests):
-            proof_stream.push((PATH, merkle_open(a[s], current)))
-            proof_stream.push((PATH, merkle_open(b[s], current)))
-            proof_stream.push((PATH, merkle_open(indices_c[s], nxt)))
+            proof_stream.push((PATH, merkle_open_levels(a[s], lc)))
+            proof_stream.push((PATH, merkle_open_levels(b[s], lc)))
+            proof_stream.push((PATH, merkle_open_levels(indices_c[s], ln)))
         return a + b
 
     def prove(self, codeword: Sequence[int], proof_stream: IndependentProofStream) -> List[int]:

@@ -1,0 +1,802 @@
+// C ABI of libstarkgpu (include/stark_gpu.h): context, transforms, Merkle, proof
+// streams and FRI drivers.  Host logic here restates the reference's control
+// flow (fri.rs, merkle_root.rs, fft/ntt.rs) around the gfx950 kernels.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/stark_gpu.h"
+#include "context.hpp"
+#include "fe128.hpp"
+#include "host_field.hpp"
+#include "host_hash.hpp"
+#include "kernels.hpp"
+#include "transcript.hpp"
+
+using namespace sg;
+
+// ======================================================================== context
+
+void* sg_ctx::alloc(size_t bytes) {
+  size_t r = pool_round(bytes);
+  auto it = free_bufs.find(r);
+  if (it != free_bufs.end()) {
+    void* p = it->second;
+    free_bufs.erase(it);
+    pooled_bytes -= r;
+    return p;
+  }
+  void* p = nullptr;
+  hipError_t e = hipMalloc(&p, r);
+  if (e != hipSuccess) {
+    // drop the cache and retry once
+    trim();
+    e = hipMalloc(&p, r);
+    if (e != hipSuccess) throw Error{SG_ERR_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e)};
+  }
+  return p;
+}
+
+void sg_ctx::release(void* p, size_t bytes) {
+  if (!p) return;
+  size_t r = pool_round(bytes);
+  free_bufs.emplace(r, p);
+  pooled_bytes += r;
+}
+
+void sg_ctx::trim() {
+  (void)hipStreamSynchronize(stream);
+  for (auto& kv : free_bufs) (void)hipFree(kv.second);
+  free_bufs.clear();
+  pooled_bytes = 0;
+}
+
+namespace sg {
+DevBuf::DevBuf(sg_ctx* ctx, size_t bytes) : ctx_(ctx), ptr_(ctx->alloc(bytes)), bytes_(bytes) {}
+DevBuf::~DevBuf() {
+  if (ptr_) ctx_->release(ptr_, bytes_);
+}
+DevBuf& DevBuf::operator=(DevBuf&& o) noexcept {
+  if (this != &o) {
+    if (ptr_) ctx_->release(ptr_, bytes_);
+    ctx_ = o.ctx_;
+    ptr_ = o.ptr_;
+    bytes_ = o.bytes_;
+    o.ptr_ = nullptr;
+  }
+  return *this;
+}
+}  // namespace sg
+
+// Montgomery(root^e), e < count, on the device; cached per (root, count).
+const fe* sg_ctx::pow_table(const fe& root, uint64_t count) {
+  auto key = std::make_pair(std::make_pair(fe_lo(root), fe_hi(root)), count);
+  auto it = pow_tables.find(key);
+  if (it != pow_tables.end()) return reinterpret_cast<const fe*>(it->second.ptr);
+  uint64_t na = count < 4096 ? count : 4096;
+  std::vector<fe> A(na);
+  fe rm = to_mont(root);
+  fe acc = to_mont(fe_one());
+  for (uint64_t i = 0; i < na; ++i) {
+    A[i] = acc;
+    acc = mont_mul(acc, rm);
+  }
+  void* table = nullptr;
+  SG_HIP(hipMalloc(&table, std::max<uint64_t>(count, 1) * sizeof(fe)));
+  if (count <= 4096) {
+    SG_HIP(hipMemcpyAsync(table, A.data(), na * sizeof(fe), hipMemcpyHostToDevice, stream));
+  } else {
+    uint64_t nb = (count + 4095) / 4096;
+    std::vector<fe> B(nb);
+    fe step = acc;  // Montgomery(root^4096)
+    fe b = to_mont(fe_one());
+    for (uint64_t i = 0; i < nb; ++i) {
+      B[i] = b;
+      b = mont_mul(b, step);
+    }
+    DevBuf dA(this, na * sizeof(fe)), dB(this, nb * sizeof(fe));
+    SG_HIP(hipMemcpyAsync(dA.get(), A.data(), na * sizeof(fe), hipMemcpyHostToDevice, stream));
+    SG_HIP(hipMemcpyAsync(dB.get(), B.data(), nb * sizeof(fe), hipMemcpyHostToDevice, stream));
+    SG_HIP(launch_pow_table(reinterpret_cast<fe*>(table), dA.as<fe>(), dB.as<fe>(), count, stream));
+    SG_HIP(hipStreamSynchronize(stream));  // A/B return to the pool below
+  }
+  SG_HIP(hipStreamSynchronize(stream));
+  pow_tables[key] = PowTable{table, count};
+  return reinterpret_cast<const fe*>(table);
+}
+
+// ======================================================================== helpers
+
+namespace {
+
+inline fe to_fe(sg_fe a) { return fe_make(a.lo, a.hi); }
+inline sg_fe from_fe(const fe& a) { return sg_fe{fe_lo(a), fe_hi(a)}; }
+
+template <class F>
+int guard(sg_ctx* ctx, F&& f) {
+  try {
+    f();
+    return SG_OK;
+  } catch (const Error& e) {
+    if (ctx) ctx->last_error = e.msg;
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    if (ctx) ctx->last_error = "host allocation failed";
+    return SG_ERR_NOMEM;
+  } catch (...) {
+    if (ctx) ctx->last_error = "unknown error";
+    return SG_ERR_INVALID;
+  }
+}
+
+inline int ilog2_exact(uint64_t n) {
+  int l = 0;
+  while (((uint64_t)1 << l) < n) ++l;
+  return l;
+}
+inline uint64_t next_pow2(uint64_t n) { return n <= 1 ? 1 : (uint64_t)1 << ilog2_exact(n); }
+
+void check_canonical(const sg_fe* v, size_t n, const char* what) {
+  for (size_t i = 0; i < n; ++i)
+    if (!fe_is_canonical(to_fe(v[i]))) throw Error{SG_ERR_NONCANONICAL, std::string(what) + ": element >= p"};
+}
+
+// In-place DIT NTT on a device buffer already holding the bit-reversed (and
+// zero-padded) input.  post = optional Montgomery constant applied at the end.
+void ntt_core(sg_ctx* ctx, fe* d_data, int logn, const fe& root, const fe* post_host) {
+  uint64_t n = (uint64_t)1 << logn;
+  const fe* tw = logn > 0 ? ctx->pow_table(root, n / 2) : nullptr;
+  DevBuf dpost;
+  const fe* post = nullptr;
+  if (post_host) {
+    dpost = DevBuf(ctx, sizeof(fe));
+    SG_HIP(hipMemcpyAsync(dpost.get(), post_host, sizeof(fe), hipMemcpyHostToDevice, ctx->stream));
+    post = dpost.as<fe>();
+  }
+  SG_HIP(launch_ntt_dit(d_data, tw, logn, post, ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+}
+
+// out (device, next_pow2(n_in)) = ntt(root, in) ; in may alias nothing in out
+void ntt_dev(sg_ctx* ctx, const fe& root, const fe* d_in, uint64_t n_in, fe* d_out, const fe* post,
+             const fe* scale_offset) {
+  SG_REQUIRE(n_in > 0, "ntt: empty input (reference indexes inputs[0])");
+  uint64_t n = next_pow2(n_in);
+  int logn = ilog2_exact(n);
+  const fe* sA = nullptr;
+  const fe* sB = nullptr;
+  if (scale_offset) {
+    sA = ctx->pow_table(*scale_offset, 4096);
+    fe off4096 = fe_pow(*scale_offset, 4096);
+    sB = ctx->pow_table(off4096, (n_in + 4095) / 4096);
+  }
+  if (logn == 0) {
+    // n == 1: bit_reverse_copy returns the input unchanged
+    SG_HIP(launch_bitrev_gather(d_out, d_in, n_in, 0, sA, sB, ctx->stream));
+  } else {
+    SG_HIP(launch_bitrev_gather(d_out, d_in, n_in, logn, sA, sB, ctx->stream));
+  }
+  ntt_core(ctx, d_out, logn, root, post);
+}
+
+}  // namespace
+
+// ======================================================================== C ABI: context
+
+extern "C" int sg_ctx_create(int device, sg_ctx** out) {
+  if (!out) return SG_ERR_INVALID;
+  *out = nullptr;
+  auto* ctx = new (std::nothrow) sg_ctx();
+  if (!ctx) return SG_ERR_NOMEM;
+  ctx->device = device;
+  if (hipSetDevice(device) != hipSuccess || hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete ctx;
+    return SG_ERR_HIP;
+  }
+  *out = ctx;
+  return SG_OK;
+}
+
+extern "C" void sg_ctx_destroy(sg_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  ctx->trim();
+  for (auto& kv : ctx->pow_tables) (void)hipFree(kv.second.ptr);
+  (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+}
+
+extern "C" const char* sg_last_error(const sg_ctx* ctx) { return ctx ? ctx->last_error.c_str() : "null context"; }
+extern "C" void* sg_ctx_stream(sg_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
+extern "C" int sg_ctx_trim(sg_ctx* ctx) {
+  return guard(ctx, [&] {
+    ctx->trim();
+    for (auto& kv : ctx->pow_tables) (void)hipFree(kv.second.ptr);
+    ctx->pow_tables.clear();
+  });
+}
+
+// ======================================================================== C ABI: field
+
+extern "C" sg_fe sg_field_prime(void) { return from_fe(fe_prime()); }
+extern "C" sg_fe sg_field_generator(void) { return from_fe(fe_generator()); }
+extern "C" int sg_primitive_nth_root(uint64_t n, sg_fe* out) {
+  if (!out || n == 0 || (n & (n - 1))) return SG_ERR_INVALID;
+  fe root = fe_generator();
+  unsigned __int128 order = (unsigned __int128)1 << 119;
+  while (order != n) {
+    root = fe_mul(root, root);
+    order >>= 1;
+  }
+  *out = from_fe(root);
+  return SG_OK;
+}
+extern "C" sg_fe sg_field_sample(const uint8_t* bytes, size_t len) { return from_fe(fe_sample(bytes, len)); }
+extern "C" sg_fe sg_fe_mul(sg_fe a, sg_fe b) { return from_fe(fe_mul(to_fe(a), to_fe(b))); }
+extern "C" sg_fe sg_fe_inverse(sg_fe a) { return from_fe(fe_inv(to_fe(a))); }
+extern "C" sg_fe sg_fe_pow(sg_fe a, uint64_t e) { return from_fe(fe_pow(to_fe(a), e)); }
+
+// ======================================================================== C ABI: transforms
+
+extern "C" int sg_ntt_dev(sg_ctx* ctx, sg_fe root, const sg_fe* d_in, size_t n_in, sg_fe* d_out) {
+  return guard(ctx, [&] {
+    SG_HIP(hipSetDevice(ctx->device));
+    ntt_dev(ctx, to_fe(root), reinterpret_cast<const fe*>(d_in), n_in, reinterpret_cast<fe*>(d_out), nullptr,
+            nullptr);
+  });
+}
+
+extern "C" int sg_intt_dev(sg_ctx* ctx, sg_fe root, const sg_fe* d_in, size_t n_in, sg_fe* d_out) {
+  return guard(ctx, [&] {
+    SG_HIP(hipSetDevice(ctx->device));
+    if (n_in < 2) {
+      // fft/ntt.rs:56-58: returned unchanged
+      if (n_in) SG_HIP(hipMemcpyAsync(d_out, d_in, n_in * sizeof(fe), hipMemcpyDeviceToDevice, ctx->stream));
+      SG_HIP(hipStreamSynchronize(ctx->stream));
+      return;
+    }
+    uint64_t n = next_pow2(n_in);
+    fe ninv_m = to_mont(fe_inv(fe_from_u64(n)));
+    fe rinv = fe_inv(to_fe(root));
+    ntt_dev(ctx, rinv, reinterpret_cast<const fe*>(d_in), n_in, reinterpret_cast<fe*>(d_out), &ninv_m, nullptr);
+  });
+}
+
+extern "C" int sg_fast_coset_evaluate_dev(sg_ctx* ctx, sg_fe generator, uint64_t root_order, sg_fe offset,
+                                          const sg_fe* d_coeffs, size_t d, sg_fe* d_out) {
+  return guard(ctx, [&] {
+    SG_HIP(hipSetDevice(ctx->device));
+    SG_REQUIRE(d <= root_order, "fast_coset_evaluate: polynomial longer than root_order");
+    SG_REQUIRE(root_order > 0, "fast_coset_evaluate: empty evaluation domain");
+    fe off = to_fe(offset);
+    // the ntt pads to next_pow2(root_order); coefficients beyond d are zero
+    uint64_t n = next_pow2(root_order);
+    fe* out = reinterpret_cast<fe*>(d_out);
+    const fe* in = reinterpret_cast<const fe*>(d_coeffs);
+    int logn = ilog2_exact(n);
+    const fe* sA = ctx->pow_table(off, 4096);
+    const fe* sB = ctx->pow_table(fe_pow(off, 4096), (std::max<uint64_t>(d, 1) + 4095) / 4096);
+    SG_HIP(launch_bitrev_gather(out, in, d, logn, sA, sB, ctx->stream));
+    ntt_core(ctx, out, logn, to_fe(generator), nullptr);
+  });
+}
+
+namespace {
+// host wrapper: upload, run, download
+template <class F>
+void host_roundtrip(sg_ctx* ctx, const sg_fe* in, size_t n_in, sg_fe* out, size_t n_out, F&& dev_fn) {
+  DevBuf din(ctx, std::max<size_t>(n_in, 1) * sizeof(fe));
+  DevBuf dout(ctx, std::max<size_t>(n_out, 1) * sizeof(fe));
+  if (n_in) SG_HIP(hipMemcpyAsync(din.get(), in, n_in * sizeof(fe), hipMemcpyHostToDevice, ctx->stream));
+  dev_fn(din.as<sg_fe>(), dout.as<sg_fe>());
+  if (n_out) SG_HIP(hipMemcpyAsync(out, dout.get(), n_out * sizeof(fe), hipMemcpyDeviceToHost, ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+}
+void throw_if(int rc, sg_ctx* ctx) {
+  if (rc != SG_OK) throw Error{rc, ctx->last_error};
+}
+}  // namespace
+
+extern "C" int sg_ntt(sg_ctx* ctx, sg_fe root, const sg_fe* in, size_t n_in, sg_fe* out) {
+  return guard(ctx, [&] {
+    SG_REQUIRE(n_in > 0, "ntt: empty input (reference indexes inputs[0])");
+    check_canonical(in, n_in, "ntt input");
+    check_canonical(&root, 1, "ntt root");
+    host_roundtrip(ctx, in, n_in, out, next_pow2(n_in),
+                   [&](sg_fe* di, sg_fe* dout) { throw_if(sg_ntt_dev(ctx, root, di, n_in, dout), ctx); });
+  });
+}
+
+extern "C" int sg_intt(sg_ctx* ctx, sg_fe root, const sg_fe* in, size_t n_in, sg_fe* out) {
+  return guard(ctx, [&] {
+    check_canonical(in, n_in, "intt input");
+    check_canonical(&root, 1, "intt root");
+    size_t n_out = n_in < 2 ? n_in : next_pow2(n_in);
+    host_roundtrip(ctx, in, n_in, out, n_out,
+                   [&](sg_fe* di, sg_fe* dout) { throw_if(sg_intt_dev(ctx, root, di, n_in, dout), ctx); });
+  });
+}
+
+extern "C" int sg_fast_coset_evaluate(sg_ctx* ctx, sg_fe generator, uint64_t root_order, sg_fe offset,
+                                      const sg_fe* coeffs, size_t d, sg_fe* out) {
+  return guard(ctx, [&] {
+    SG_REQUIRE(d <= root_order, "fast_coset_evaluate: polynomial longer than root_order");
+    check_canonical(coeffs, d, "coefficients");
+    check_canonical(&offset, 1, "offset");
+    check_canonical(&generator, 1, "generator");
+    host_roundtrip(ctx, coeffs, d, out, next_pow2(root_order), [&](sg_fe* di, sg_fe* dout) {
+      throw_if(sg_fast_coset_evaluate_dev(ctx, generator, root_order, offset, di, d, dout), ctx);
+    });
+  });
+}
+
+// ======================================================================== C ABI: Merkle
+
+struct sg_tree {
+  uint64_t n = 0;
+  int logn = 0;
+  DevBuf buf;  // (2n - 1) digests x 8 u64
+  uint8_t root[64];
+};
+
+namespace {
+inline uint64_t level_offset(uint64_t n, int level) { return 2 * n - 2 * (n >> level); }
+
+sg_tree* build_tree(sg_ctx* ctx, const fe* d_leaves, uint64_t n) {
+  SG_REQUIRE(n > 0 && (n & (n - 1)) == 0, "Leafs len must be power of two");
+  std::unique_ptr<sg_tree> t(new sg_tree());
+  t->n = n;
+  t->logn = ilog2_exact(n);
+  t->buf = DevBuf(ctx, merkle_tree_digests(n) * 64);
+  SG_HIP(launch_merkle_tree(d_leaves, t->buf.as<uint64_t>(), n, ctx->stream));
+  SG_HIP(hipMemcpyAsync(t->root, t->buf.as<uint8_t>() + (2 * n - 2) * 64, 64, hipMemcpyDeviceToHost, ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  return t.release();
+}
+
+// digest indices of the authentication path of `index` (merkle_root.rs:34-53 order: leaf level first)
+void path_indices(const sg_tree* t, uint64_t index, std::vector<uint64_t>& idx) {
+  for (int lv = 0; lv < t->logn; ++lv) idx.push_back(level_offset(t->n, lv) + ((index >> lv) ^ 1));
+}
+
+void gather_digests(sg_ctx* ctx, const sg_tree* t, const std::vector<uint64_t>& idx, uint8_t* out) {
+  if (idx.empty()) return;
+  DevBuf di(ctx, idx.size() * 8), dout(ctx, idx.size() * 64);
+  SG_HIP(hipMemcpyAsync(di.get(), idx.data(), idx.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+  SG_HIP(launch_gather_digests(t->buf.as<uint64_t>(), di.as<uint64_t>(), dout.as<uint64_t>(), (uint32_t)idx.size(),
+                               ctx->stream));
+  SG_HIP(hipMemcpyAsync(out, dout.get(), idx.size() * 64, hipMemcpyDeviceToHost, ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+}
+}  // namespace
+
+extern "C" int sg_merkle_build_dev(sg_ctx* ctx, const sg_fe* d_leaves, size_t n, sg_tree** out) {
+  return guard(ctx, [&] {
+    SG_HIP(hipSetDevice(ctx->device));
+    *out = build_tree(ctx, reinterpret_cast<const fe*>(d_leaves), n);
+  });
+}
+extern "C" int sg_tree_root(const sg_tree* t, uint8_t root[64]) {
+  if (!t || !root) return SG_ERR_INVALID;
+  memcpy(root, t->root, 64);
+  return SG_OK;
+}
+extern "C" size_t sg_tree_leaves(const sg_tree* t) { return t ? t->n : 0; }
+extern "C" int sg_tree_open(sg_ctx* ctx, const sg_tree* t, size_t index, uint8_t* path, size_t* path_len) {
+  return guard(ctx, [&] {
+    SG_REQUIRE(t && index < t->n, "cannot open invalid index");
+    SG_REQUIRE(t->n >= 2, "cannot open a 1-leaf tree");
+    std::vector<uint64_t> idx;
+    path_indices(t, index, idx);
+    gather_digests(ctx, t, idx, path);
+    if (path_len) *path_len = idx.size();
+  });
+}
+extern "C" void sg_tree_free(sg_ctx* ctx, sg_tree* t) {
+  (void)ctx;
+  delete t;
+}
+
+extern "C" int sg_merkle_commit(sg_ctx* ctx, const sg_fe* leaves, size_t n, uint8_t root[64]) {
+  return guard(ctx, [&] {
+    SG_HIP(hipSetDevice(ctx->device));
+    SG_REQUIRE(n > 0 && (n & (n - 1)) == 0, "Leafs len must be power of two");
+    check_canonical(leaves, n, "leaf");
+    DevBuf d(ctx, n * sizeof(fe));
+    SG_HIP(hipMemcpyAsync(d.get(), leaves, n * sizeof(fe), hipMemcpyHostToDevice, ctx->stream));
+    std::unique_ptr<sg_tree> t(build_tree(ctx, d.as<fe>(), n));
+    memcpy(root, t->root, 64);
+  });
+}
+
+extern "C" int sg_merkle_open(sg_ctx* ctx, size_t index, const sg_fe* leaves, size_t n, uint8_t* path,
+                              size_t* path_len) {
+  return guard(ctx, [&] {
+    SG_HIP(hipSetDevice(ctx->device));
+    SG_REQUIRE(n > 0 && (n & (n - 1)) == 0, "length must be power of two");
+    SG_REQUIRE(index < n, "cannot open invalid index");
+    check_canonical(leaves, n, "leaf");
+    DevBuf d(ctx, n * sizeof(fe));
+    SG_HIP(hipMemcpyAsync(d.get(), leaves, n * sizeof(fe), hipMemcpyHostToDevice, ctx->stream));
+    std::unique_ptr<sg_tree> t(build_tree(ctx, d.as<fe>(), n));
+    SG_REQUIRE(n >= 2, "cannot open a 1-leaf tree");
+    std::vector<uint64_t> idx;
+    path_indices(t.get(), index, idx);
+    gather_digests(ctx, t.get(), idx, path);
+    if (path_len) *path_len = idx.size();
+  });
+}
+
+namespace {
+// decimal string of a canonical element (field_element.rs:46-50)
+std::string fe_decimal(const fe& a) {
+  unsigned __int128 v = fe_to_u128(a);
+  if (v == 0) return "0";
+  std::string s;
+  while (v) {
+    s.push_back((char)('0' + (int)(v % 10)));
+    v /= 10;
+  }
+  std::reverse(s.begin(), s.end());
+  return s;
+}
+}  // namespace
+
+extern "C" int sg_merkle_verify(const uint8_t root[64], size_t index, const uint8_t* path, size_t path_len,
+                                sg_fe leaf) {
+  // merkle_root.rs:69-95
+  if (!root || (path_len && !path)) return SG_ERR_INVALID;
+  if (path_len == 0) return SG_ERR_INVALID;  // reference indexes path[0]
+  if (path_len < 64 && index >= ((size_t)1 << path_len)) return SG_ERR_INVALID;
+  std::string dec = fe_decimal(to_fe(leaf));
+  uint8_t h[64], buf[128];
+  blake2b512(reinterpret_cast<const uint8_t*>(dec.data()), dec.size(), h);
+  for (size_t i = 0; i < path_len; ++i) {
+    if (index % 2 == 0) {
+      memcpy(buf, h, 64);
+      memcpy(buf + 64, path + 64 * i, 64);
+    } else {
+      memcpy(buf, path + 64 * i, 64);
+      memcpy(buf + 64, h, 64);
+    }
+    blake2b512(buf, 128, h);
+    index >>= 1;
+  }
+  return memcmp(h, root, 64) == 0 ? 1 : 0;
+}
+
+// ======================================================================== C ABI: proof streams
+
+struct sg_stream {
+  Stream s;
+};
+
+namespace {
+int stream_push_cb(void* user, uint8_t code, const uint8_t* payload, size_t len) {
+  return sg_stream_push(reinterpret_cast<sg_stream*>(user), code, payload, len);
+}
+int stream_fs_cb(void* user, size_t num_bytes, uint8_t* out) {
+  return sg_stream_fiat_shamir_prover(reinterpret_cast<sg_stream*>(user), num_bytes, out);
+}
+}  // namespace
+
+extern "C" sg_stream* sg_stream_create(void) { return new (std::nothrow) sg_stream(); }
+extern "C" sg_stream* sg_stream_create_signature(const uint8_t* document, size_t doc_len) {
+  auto* s = new (std::nothrow) sg_stream();
+  if (!s) return nullptr;
+  s->s.signature = true;
+  s->s.prefix.resize(64);
+  blake2b512(document, doc_len, s->s.prefix.data());
+  return s;
+}
+extern "C" void sg_stream_destroy(sg_stream* s) { delete s; }
+extern "C" sg_proof_stream sg_stream_callbacks(sg_stream* s) {
+  sg_proof_stream ps;
+  ps.user = s;
+  ps.push = stream_push_cb;
+  ps.fiat_shamir_prover = stream_fs_cb;
+  return ps;
+}
+extern "C" int sg_stream_push(sg_stream* s, uint8_t code, const uint8_t* payload, size_t len) {
+  if (!s || code > 4 || (len && !payload)) return SG_ERR_INVALID;
+  StreamObject o;
+  o.code = code;
+  o.payload.assign(payload, payload + len);
+  s->s.objects.push_back(std::move(o));
+  return SG_OK;
+}
+extern "C" size_t sg_stream_count(const sg_stream* s) { return s ? s->s.objects.size() : 0; }
+extern "C" int sg_stream_digest(const sg_stream* s, uint8_t* out, size_t cap, size_t* len) {
+  if (!s) return SG_ERR_INVALID;
+  std::vector<uint8_t> d = s->s.digest();
+  if (len) *len = d.size();
+  if (out) {
+    if (cap < d.size()) return SG_ERR_INVALID;
+    memcpy(out, d.data(), d.size());
+  }
+  return SG_OK;
+}
+extern "C" int sg_stream_fiat_shamir_prover(const sg_stream* s, size_t num_bytes, uint8_t* out) {
+  if (!s || (num_bytes && !out)) return SG_ERR_INVALID;
+  s->s.fiat_shamir(s->s.objects.size(), num_bytes, out);
+  return SG_OK;
+}
+extern "C" int sg_stream_fiat_shamir_verifier(const sg_stream* s, size_t num_bytes, uint8_t* out) {
+  if (!s || (num_bytes && !out)) return SG_ERR_INVALID;
+  s->s.fiat_shamir(s->s.read_index, num_bytes, out);
+  return SG_OK;
+}
+extern "C" int sg_stream_pull(sg_stream* s, uint8_t* code, const uint8_t** payload, size_t* len) {
+  if (!s) return SG_ERR_INVALID;
+  if (s->s.read_index >= s->s.objects.size()) return SG_ERR_INVALID;  // "Cannot pull, queue is empty"
+  const StreamObject& o = s->s.objects[s->s.read_index++];
+  if (code) *code = o.code;
+  if (payload) *payload = o.payload.data();
+  if (len) *len = o.payload.size();
+  return SG_OK;
+}
+extern "C" int sg_stream_deserialize(const uint8_t* bytes, size_t len, sg_stream** out) {
+  if (!out || (len && !bytes)) return SG_ERR_INVALID;
+  auto* s = new (std::nothrow) sg_stream();
+  if (!s) return SG_ERR_NOMEM;
+  std::string err;
+  if (!deserialize_stream(bytes, len, s->s, err)) {
+    delete s;
+    return SG_ERR_INVALID;
+  }
+  *out = s;
+  return SG_OK;
+}
+
+// ======================================================================== C ABI: FRI
+
+struct sg_fri_state {
+  std::vector<DevBuf> codewords;  // round r codeword (device)
+  std::vector<uint64_t> lengths;
+  std::vector<std::unique_ptr<sg_tree>> trees;
+};
+
+namespace {
+
+size_t fri_num_rounds(const sg_fri* f) {
+  // fri.rs:40-50
+  uint64_t len = f->domain_length;
+  size_t r = 0;
+  while (len > f->expansion_factor && len > 4 * f->num_colinearity_tests) {
+    len /= 2;
+    ++r;
+  }
+  return r;
+}
+
+void push_obj(const sg_proof_stream* ps, uint8_t code, const uint8_t* p, size_t len) {
+  if (ps->push(ps->user, code, p, len) != 0) throw Error{SG_ERR_CALLBACK, "proof stream push callback failed"};
+}
+
+void put_u128_be(std::vector<uint8_t>& out, const fe& a) {
+  uint64_t hi = fe_hi(a), lo = fe_lo(a);
+  for (int i = 7; i >= 0; --i) out.push_back((uint8_t)(hi >> (8 * i)));
+  for (int i = 7; i >= 0; --i) out.push_back((uint8_t)(lo >> (8 * i)));
+}
+
+// fri.rs:115-172.  Retains every round's codeword and tree in `st`.
+void fri_commit_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, const sg_proof_stream* ps,
+                    sg_fri_state& st) {
+  SG_REQUIRE(ps && ps->push && ps->fiat_shamir_prover, "proof stream callbacks required");
+  size_t rounds = fri_num_rounds(f);
+  SG_REQUIRE(rounds >= 1, "FRI: zero rounds for this domain");
+  SG_REQUIRE(n == f->domain_length, "Length of the domain doesnt match the length of initial codeword");
+  fe omega = to_fe(f->omega), offset = to_fe(f->offset);
+  // fold tables for the base omega: w^-e for e < n/2 via (e & 4095, e >> 12)
+  fe winv = fe_inv(omega);
+  const fe* Tlo = ctx->pow_table(winv, 4096);
+  const fe* Thi = ctx->pow_table(fe_pow(winv, 4096), (n / 2 + 4095) / 4096 + 1);
+  fe inv2 = fe_inv(fe_from_u64(2));
+
+  // round 0 codeword: copy into a state-owned buffer
+  st.codewords.emplace_back(ctx, n * sizeof(fe));
+  st.lengths.push_back(n);
+  SG_HIP(hipMemcpyAsync(st.codewords[0].get(), d_cw, n * sizeof(fe), hipMemcpyDeviceToDevice, ctx->stream));
+
+  uint64_t len = n;
+  for (size_t r = 0; r < rounds; ++r) {
+    // assert omega^(n-1) == omega^-1 (fri.rs:133)
+    SG_REQUIRE(fe_eq(fe_pow(omega, len - 1), fe_inv(omega)), "error in commit: omega does not have the right order!");
+    const fe* cw = st.codewords[r].as<fe>();
+    st.trees.emplace_back(build_tree(ctx, cw, len));
+    push_obj(ps, SG_OBJ_ROOT, st.trees.back()->root, 64);
+    if (r == rounds - 1) break;
+    uint8_t chal[32];
+    if (ps->fiat_shamir_prover(ps->user, 32, chal) != 0)
+      throw Error{SG_ERR_CALLBACK, "proof stream fiat_shamir callback failed"};
+    fe alpha = fe_sample(chal, 32);
+    uint64_t half = len / 2;
+    // K = alpha * offset^-1 * 2^-1 (Montgomery); w_r^-i = w^-(i << r)
+    fe K = to_mont(fe_mul(fe_mul(alpha, fe_inv(offset)), inv2));
+    unsigned grid = fri_fold_grid(half);
+    uint64_t stride = (uint64_t)grid * 256;
+    fe wr_inv = fe_inv(omega);  // omega here is already w_r
+    fe Wstride = to_mont(fe_pow(wr_inv, stride));
+    st.codewords.emplace_back(ctx, half * sizeof(fe));
+    st.lengths.push_back(half);
+    SG_HIP(launch_fri_fold(st.codewords[r + 1].as<fe>(), cw, half, Tlo, Thi, (int)r, K, Wstride, grid, ctx->stream));
+    omega = fe_mul(omega, omega);
+    offset = fe_mul(offset, offset);
+    len = half;
+  }
+  // push last codeword (fri.rs:166)
+  uint64_t last_len = st.lengths.back();
+  std::vector<fe> last(last_len);
+  SG_HIP(hipMemcpyAsync(last.data(), st.codewords.back().get(), last_len * sizeof(fe), hipMemcpyDeviceToHost,
+                        ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  std::vector<uint8_t> payload;
+  payload.reserve(last_len * 16);
+  for (auto& v : last) put_u128_be(payload, v);
+  push_obj(ps, SG_OBJ_CODEWORD, payload.data(), payload.size());
+}
+
+// fri.rs:60-86
+size_t sample_index(const uint8_t* bytes, size_t len, size_t size) {
+  int bit = 63 - __builtin_clzll((unsigned long long)size);
+  size_t nbytes = (size_t)bit / 8 + 1;
+  size_t start = nbytes > len ? 0 : len - nbytes;
+  uint64_t acc = 0;
+  for (size_t i = start; i < len; ++i) acc = (acc << 8) ^ bytes[i];
+  return (size_t)(acc % size);
+}
+
+void sample_indices(const uint8_t* seed, size_t seed_len, size_t size, size_t reduced_size, size_t number,
+                    size_t* out) {
+  SG_REQUIRE(size != 0 && reduced_size != 0, "modulo zero is impossible");
+  SG_REQUIRE(number <= 2 * reduced_size, "Not enough entropy in indices with reference to last codeword");
+  SG_REQUIRE(number <= reduced_size, "Cannot sample more indices than available in the last codeword");
+  std::vector<size_t> reduced;
+  std::vector<uint8_t> buf(seed, seed + seed_len);
+  size_t count = 0;
+  uint8_t h[64];
+  while (count < number) {
+    blake2b512(buf.data(), buf.size(), h);
+    size_t index = sample_index(h, 64, size);
+    size_t r = index % reduced_size;
+    buf.push_back(0);  // seed || 0^(counter+1) for the next draw
+    if (std::find(reduced.begin(), reduced.end(), r) == reduced.end()) {
+      out[count++] = index;
+      reduced.push_back(r);
+    }
+  }
+}
+
+// fri.rs:174-208 for every round, then returns top-level indices (fri.rs:210-248)
+void fri_prove_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, const sg_proof_stream* ps,
+                   size_t* top) {
+  sg_fri_state st;
+  fri_commit_dev(ctx, f, d_cw, n, ps, st);
+  SG_REQUIRE(st.codewords.size() >= 2, "FRI prove needs at least two rounds (reference indexes codewords[1])");
+  uint8_t seed[32];
+  if (ps->fiat_shamir_prover(ps->user, 32, seed) != 0)
+    throw Error{SG_ERR_CALLBACK, "proof stream fiat_shamir callback failed"};
+  const size_t c = f->num_colinearity_tests;
+  sample_indices(seed, 32, st.lengths[1], st.lengths.back(), c, top);
+  std::vector<size_t> indices(top, top + c);
+  for (size_t r = 0; r + 1 < st.codewords.size(); ++r) {
+    uint64_t len = st.lengths[r];
+    for (auto& i : indices) i = i % (len / 2);
+    // leafs: current[a], current[b], next[c]
+    std::vector<uint64_t> cur_idx, nxt_idx;
+    for (size_t s = 0; s < c; ++s) {
+      cur_idx.push_back(indices[s]);
+      cur_idx.push_back(indices[s] + len / 2);
+      nxt_idx.push_back(indices[s]);
+    }
+    std::vector<fe> cur_vals(cur_idx.size()), nxt_vals(nxt_idx.size());
+    {
+      DevBuf di(ctx, cur_idx.size() * 8), dv(ctx, cur_idx.size() * sizeof(fe));
+      SG_HIP(hipMemcpyAsync(di.get(), cur_idx.data(), cur_idx.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+      SG_HIP(launch_gather_fe(st.codewords[r].as<fe>(), di.as<uint64_t>(), dv.as<fe>(), (uint32_t)cur_idx.size(),
+                              ctx->stream));
+      SG_HIP(hipMemcpyAsync(cur_vals.data(), dv.get(), cur_idx.size() * sizeof(fe), hipMemcpyDeviceToHost,
+                            ctx->stream));
+      DevBuf dj(ctx, nxt_idx.size() * 8), dw(ctx, nxt_idx.size() * sizeof(fe));
+      SG_HIP(hipMemcpyAsync(dj.get(), nxt_idx.data(), nxt_idx.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+      SG_HIP(launch_gather_fe(st.codewords[r + 1].as<fe>(), dj.as<uint64_t>(), dw.as<fe>(),
+                              (uint32_t)nxt_idx.size(), ctx->stream));
+      SG_HIP(hipMemcpyAsync(nxt_vals.data(), dw.get(), nxt_idx.size() * sizeof(fe), hipMemcpyDeviceToHost,
+                            ctx->stream));
+      SG_HIP(hipStreamSynchronize(ctx->stream));
+    }
+    for (size_t s = 0; s < c; ++s) {
+      std::vector<uint8_t> p;
+      put_u128_be(p, cur_vals[2 * s]);
+      put_u128_be(p, cur_vals[2 * s + 1]);
+      put_u128_be(p, nxt_vals[s]);
+      push_obj(ps, SG_OBJ_LEAFS, p.data(), p.size());
+    }
+    // paths: open(a, current), open(b, current), open(c, next)
+    const sg_tree* tc = st.trees[r].get();
+    const sg_tree* tn = st.trees[r + 1].get();
+    std::vector<uint64_t> pidx_c, pidx_n;
+    for (size_t s = 0; s < c; ++s) {
+      path_indices(tc, indices[s], pidx_c);
+      path_indices(tc, indices[s] + len / 2, pidx_c);
+      path_indices(tn, indices[s], pidx_n);
+    }
+    std::vector<uint8_t> pc(pidx_c.size() * 64), pn(pidx_n.size() * 64);
+    gather_digests(ctx, tc, pidx_c, pc.data());
+    gather_digests(ctx, tn, pidx_n, pn.data());
+    const size_t lc = (size_t)tc->logn, ln = (size_t)tn->logn;
+    for (size_t s = 0; s < c; ++s) {
+      for (int which = 0; which < 3; ++which) {
+        const uint8_t* src = which < 2 ? pc.data() + (2 * s + which) * lc * 64 : pn.data() + s * ln * 64;
+        size_t plen = which < 2 ? lc : ln;
+        std::vector<uint8_t> p;
+        p.reserve(plen * 72);
+        for (size_t k = 0; k < plen; ++k) {
+          for (int i = 7; i >= 0; --i) p.push_back((uint8_t)(64ull >> (8 * i)));
+          p.insert(p.end(), src + k * 64, src + (k + 1) * 64);
+        }
+        push_obj(ps, SG_OBJ_PATH, p.data(), p.size());
+      }
+    }
+  }
+}
+
+}  // namespace
+
+extern "C" size_t sg_fri_num_rounds(const sg_fri* fri) { return fri ? fri_num_rounds(fri) : 0; }
+
+extern "C" int sg_fri_commit_dev(sg_ctx* ctx, const sg_fri* fri, const sg_fe* d_cw, size_t n,
+                                 const sg_proof_stream* ps, sg_fri_state** keep) {
+  return guard(ctx, [&] {
+    SG_HIP(hipSetDevice(ctx->device));
+    std::unique_ptr<sg_fri_state> st(new sg_fri_state());
+    fri_commit_dev(ctx, fri, reinterpret_cast<const fe*>(d_cw), n, ps, *st);
+    if (keep) *keep = st.release();
+  });
+}
+
+extern "C" int sg_fri_commit(sg_ctx* ctx, const sg_fri* fri, const sg_fe* cw, size_t n, const sg_proof_stream* ps,
+                             sg_fri_state** keep) {
+  return guard(ctx, [&] {
+    SG_HIP(hipSetDevice(ctx->device));
+    check_canonical(cw, n, "codeword");
+    DevBuf d(ctx, std::max<size_t>(n, 1) * sizeof(fe));
+    if (n) SG_HIP(hipMemcpyAsync(d.get(), cw, n * sizeof(fe), hipMemcpyHostToDevice, ctx->stream));
+    std::unique_ptr<sg_fri_state> st(new sg_fri_state());
+    fri_commit_dev(ctx, fri, d.as<fe>(), n, ps, *st);
+    if (keep) *keep = st.release();
+  });
+}
+
+extern "C" int sg_fri_prove_dev(sg_ctx* ctx, const sg_fri* fri, const sg_fe* d_cw, size_t n, const sg_proof_stream* ps,
+                                size_t* top) {
+  return guard(ctx, [&] {
+    SG_HIP(hipSetDevice(ctx->device));
+    fri_prove_dev(ctx, fri, reinterpret_cast<const fe*>(d_cw), n, ps, top);
+  });
+}
+
+extern "C" int sg_fri_prove(sg_ctx* ctx, const sg_fri* fri, const sg_fe* cw, size_t n, const sg_proof_stream* ps,
+                            size_t* top) {
+  return guard(ctx, [&] {
+    SG_HIP(hipSetDevice(ctx->device));
+    check_canonical(cw, n, "codeword");
+    DevBuf d(ctx, std::max<size_t>(n, 1) * sizeof(fe));
+    if (n) SG_HIP(hipMemcpyAsync(d.get(), cw, n * sizeof(fe), hipMemcpyHostToDevice, ctx->stream));
+    fri_prove_dev(ctx, fri, d.as<fe>(), n, ps, top);
+  });
+}
+
+extern "C" void sg_fri_state_free(sg_ctx* ctx, sg_fri_state* st) {
+  (void)ctx;
+  delete st;
+}
+
+extern "C" int sg_fri_sample_indices(const uint8_t* seed, size_t seed_len, size_t size, size_t reduced_size,
+                                     size_t number, size_t* out) {
+  return guard(nullptr, [&] { sample_indices(seed, seed_len, size, reduced_size, number, out); });
+}

@@ -1,0 +1,84 @@
+// Library context: device, stream, pooled device buffers, cached twiddle tables.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <map>
+#include <string>
+#include <utility>
+#include <vector>
+#include "fe128.hpp"
+
+struct sg_ctx;
+
+namespace sg {
+
+// Error carrying the C-ABI code; thrown inside the library, caught at the boundary.
+struct Error {
+  int code;
+  std::string msg;
+};
+
+#define SG_HIP(call)                                                                              \
+  do {                                                                                            \
+    hipError_t _e = (call);                                                                       \
+    if (_e != hipSuccess)                                                                         \
+      throw ::sg::Error{-2, std::string(#call) + ": " + hipGetErrorString(_e)};                   \
+  } while (0)
+#define SG_REQUIRE(cond, msg)                    \
+  do {                                           \
+    if (!(cond)) throw ::sg::Error{-1, (msg)};   \
+  } while (0)
+
+// Device buffer from the context pool (returned to the pool on destruction).
+class DevBuf {
+ public:
+  DevBuf() = default;
+  DevBuf(sg_ctx* ctx, size_t bytes);
+  ~DevBuf();
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  DevBuf(DevBuf&& o) noexcept : ctx_(o.ctx_), ptr_(o.ptr_), bytes_(o.bytes_) { o.ptr_ = nullptr; }
+  DevBuf& operator=(DevBuf&& o) noexcept;
+  void* get() const { return ptr_; }
+  template <class T>
+  T* as() const { return reinterpret_cast<T*>(ptr_); }
+  size_t bytes() const { return bytes_; }
+
+ private:
+  sg_ctx* ctx_ = nullptr;
+  void* ptr_ = nullptr;
+  size_t bytes_ = 0;
+};
+
+// Montgomery power table of a root on the device: tw[e] = root^e * R, e < count.
+struct PowTable {
+  void* ptr = nullptr;
+  uint64_t count = 0;
+};
+
+}  // namespace sg
+
+struct sg_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string last_error;
+  // pool: rounded size -> free pointers
+  std::multimap<size_t, void*> free_bufs;
+  size_t pooled_bytes = 0;
+  // power tables keyed by (root limbs, count)
+  std::map<std::pair<std::pair<uint64_t, uint64_t>, uint64_t>, sg::PowTable> pow_tables;
+
+  void* alloc(size_t bytes);
+  void release(void* p, size_t bytes);
+  void trim();
+  // device table of Montgomery(root^e) for e < count (cached)
+  const sg::fe* pow_table(const sg::fe& root, uint64_t count);
+};
+
+namespace sg {
+inline size_t pool_round(size_t bytes) {
+  size_t r = 256;
+  while (r < bytes) r <<= 1;
+  return r;
+}
+}  // namespace sg

@@ -1,0 +1,426 @@
+// HIP kernels for gfx950 (MI355X): NTT / LDE, Merkle tree, FRI fold.
+//
+// NTT: the reference's radix-2 DIT graph (fft/ntt.rs:7-49) executed exactly:
+// bit-reversal gather, then log2(n) stages where stage S (size 2^S) combines
+// (j, j + 2^(S-1)) with twiddle powtable[k * n/2^S], k = j mod 2^(S-1).
+// Stages are grouped into passes over LDS tiles (up to 4096 elements = 64 KiB)
+// and, inside a pass, into radix-8/4/2 register steps (three consecutive
+// radix-2 stages on 8 elements).  Every butterfly sees the same operands and
+// twiddle as in the reference, so the output is bit-identical for ANY root,
+// primitive or not.
+//
+// Merkle: leaf = BLAKE2b(decimal(v)), node = BLAKE2b(left || right)
+// (merkle_root.rs:7-32).  One launch hashes one level from HBM and fuses up to
+// three more levels through LDS; every level's digests are written to a
+// retained tree buffer (levels concatenated, 64 B per digest) so openings are
+// O(log n) gathers.
+//
+// FRI fold (fri.rs:150-159): c'[i] = (c[i] + c[i+h])/2 + K*w^-i*(c[i] - c[i+h])
+// with K = alpha * offset^-1 / 2 in Montgomery form; w^-i advanced by one
+// Montgomery product per grid-stride step, no per-element inverse or pow.
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include "fe128.hpp"
+#include "blake2b.hpp"
+#include "leaf_decimal.hpp"
+#include "kernels.hpp"
+
+namespace sg {
+
+// ------------------------------------------------------------------ helpers
+
+__device__ __forceinline__ fe ld_fe(const fe* p) {
+  uint4 v = *reinterpret_cast<const uint4*>(p);
+  fe r = {{v.x, v.y, v.z, v.w}};
+  return r;
+}
+__device__ __forceinline__ void st_fe(fe* p, const fe& a) {
+  *reinterpret_cast<uint4*>(p) = make_uint4(a.w[0], a.w[1], a.w[2], a.w[3]);
+}
+
+// (a + p) / 2 if a odd else a / 2 -- a * 2^-1 mod p for canonical a
+__device__ __forceinline__ fe fe_halve(const fe& a) {
+  uint64_t a0 = fe_lo(a), a1 = fe_hi(a);
+  uint64_t odd = a0 & 1u;
+  // s = a + odd*p (129 bits)
+  uint64_t s0 = a0 + odd;             // p0 = 1
+  uint64_t c0 = s0 < odd;
+  uint64_t add1 = odd ? ((uint64_t)P3 << 32) : 0;
+  uint64_t s1 = a1 + add1;
+  uint64_t c1 = s1 < add1;
+  uint64_t s1b = s1 + c0;
+  c1 += s1b < c0;
+  uint64_t r0 = (s0 >> 1) | (s1b << 63);
+  uint64_t r1 = (s1b >> 1) | (c1 << 63);
+  return fe_make(r0, r1);
+}
+
+// ------------------------------------------------------------- twiddles
+
+// tw[e] = A[e & 4095] * B[e >> 12] (both Montgomery) => Montgomery of root^e
+__global__ void k_pow_table(fe* __restrict__ tw, const fe* __restrict__ A, const fe* __restrict__ B, uint64_t count) {
+  uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= count) return;
+  st_fe(tw + e, mont_mul(ld_fe(A + (e & 4095)), ld_fe(B + (e >> 12))));
+}
+
+// --------------------------------------------------- bit reversal (+ LDE scale)
+
+// out[j] = x[rev(j)] (* offset^rev(j) when sA != nullptr), zero beyond n_in.
+__global__ void k_bitrev_gather(fe* __restrict__ out, const fe* __restrict__ in, uint64_t n_in, int logn,
+                                const fe* __restrict__ sA, const fe* __restrict__ sB) {
+  uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >> logn) return;
+  uint64_t i = logn ? (__builtin_bitreverse64(j) >> (64 - logn)) : 0;
+  fe v = fe_zero();
+  if (i < n_in) {
+    v = ld_fe(in + i);
+    if (sA) {
+      fe f = mont_mul(ld_fe(sA + (i & 4095)), ld_fe(sB + (i >> 12)));  // Montgomery of offset^i
+      v = mont_mul(v, f);
+    }
+  }
+  st_fe(out + j, v);
+}
+
+// ------------------------------------------------------------- NTT passes
+
+struct PassArgs {
+  fe* data;
+  const fe* tw;        // tw[e] = Montgomery(root^e), e < n/2
+  const fe* post;      // optional Montgomery constant applied on store (INTT n^-1)
+  int logn;
+  int b0;              // index bits below the group bits (= first stage of the pass - 1)
+  int L;               // stages in this pass (group bits [b0, b0+L))
+  int logC;            // columns per tile (consecutive low-bit indices), C <= 2^b0
+};
+
+template <int R>
+__device__ __forceinline__ void radix_step(fe* lds, const PassArgs& a, int t, uint64_t lowbase) {
+  const int logC = a.logC;
+  const uint32_t C = 1u << logC;
+  const uint32_t groups = (1u << (a.L + logC)) >> R;
+  for (uint32_t q = threadIdx.x; q < groups; q += blockDim.x) {
+    uint32_t c = q & (C - 1);
+    uint32_t qq = q >> logC;
+    uint32_t g_low = qq & ((1u << t) - 1);
+    uint32_t g_high = qq >> t;
+    uint32_t g0 = (g_high << (t + R)) | g_low;
+    fe x[1 << R];
+#pragma unroll
+    for (int m = 0; m < (1 << R); ++m) x[m] = lds[((g0 + ((uint32_t)m << t)) << logC) + c];
+    const uint64_t low = lowbase + c;  // cb*C + c: index bits below b0
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      const int S = a.b0 + t + u + 1;  // global stage, 1-based
+#pragma unroll
+      for (int m = 0; m < (1 << R); ++m) {
+        if (m & (1 << u)) continue;
+        uint64_t gmod = (uint64_t)g_low + ((uint64_t)(m & ((1 << u) - 1)) << t);
+        uint64_t k = (gmod << a.b0) + low;
+        uint64_t e = k << (a.logn - S);
+        fe w = ld_fe(a.tw + e);
+        fe o = mont_mul(x[m + (1 << u)], w);
+        fe ev = x[m];
+        x[m] = fe_add(ev, o);
+        x[m + (1 << u)] = fe_sub(ev, o);
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < (1 << R); ++m) lds[((g0 + ((uint32_t)m << t)) << logC) + c] = x[m];
+  }
+  __syncthreads();
+}
+
+__global__ __launch_bounds__(256) void k_ntt_pass(PassArgs a) {
+  extern __shared__ fe lds[];
+  const int logC = a.logC;
+  const uint32_t C = 1u << logC;
+  const uint32_t tile = 1u << (a.L + logC);
+  // tile id -> (h, cb)
+  const uint64_t ncb = (uint64_t)1 << (a.b0 - logC);
+  const uint64_t h = blockIdx.x / ncb;
+  const uint64_t cb = blockIdx.x % ncb;
+  const uint64_t base = (h << (a.b0 + a.L)) + cb * C;
+  for (uint32_t l = threadIdx.x; l < tile; l += blockDim.x) {
+    uint32_t g = l >> logC, c = l & (C - 1);
+    lds[l] = ld_fe(a.data + base + ((uint64_t)g << a.b0) + c);
+  }
+  __syncthreads();
+  int t = 0;
+  while (t < a.L) {
+    int rem = a.L - t;
+    if (rem >= 3) { radix_step<3>(lds, a, t, cb * C); t += 3; }
+    else if (rem == 2) { radix_step<2>(lds, a, t, cb * C); t += 2; }
+    else { radix_step<1>(lds, a, t, cb * C); t += 1; }
+  }
+  const bool post = a.post != nullptr;
+  fe pc = post ? ld_fe(a.post) : fe_zero();
+  for (uint32_t l = threadIdx.x; l < tile; l += blockDim.x) {
+    uint32_t g = l >> logC, c = l & (C - 1);
+    fe v = lds[l];
+    if (post) v = mont_mul(v, pc);
+    st_fe(a.data + base + ((uint64_t)g << a.b0) + c, v);
+  }
+}
+
+// elementwise v *= Montgomery constant (used for tiny INTTs)
+__global__ void k_scale_const(fe* __restrict__ data, uint64_t n, const fe* __restrict__ cst) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  st_fe(data + i, mont_mul(ld_fe(data + i), ld_fe(cst)));
+}
+
+// ------------------------------------------------------------- Merkle
+
+struct Digest {
+  uint64_t h[8];
+};
+
+__device__ __forceinline__ void st_digest(uint64_t* p, const uint64_t d[8]) {
+  uint4* q = reinterpret_cast<uint4*>(p);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    q[i] = make_uint4((uint32_t)d[2 * i], (uint32_t)(d[2 * i] >> 32), (uint32_t)d[2 * i + 1], (uint32_t)(d[2 * i + 1] >> 32));
+}
+__device__ __forceinline__ void ld_digest(const uint64_t* p, uint64_t d[8]) {
+  const uint4* q = reinterpret_cast<const uint4*>(p);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    uint4 v = q[i];
+    d[2 * i] = (uint64_t)v.x | ((uint64_t)v.y << 32);
+    d[2 * i + 1] = (uint64_t)v.z | ((uint64_t)v.w << 32);
+  }
+}
+
+// Hash the first level of a group (leaves when `leaves` != nullptr, else nodes
+// from the children at `child_level`), then `fuse - 1` further levels in LDS.
+// Level k of the tree starts at digest offset level_off[k] in `tree`.
+struct MerkleArgs {
+  const fe* leaves;         // level 0 input (field elements) or nullptr
+  uint64_t* tree;           // retained tree: 8 u64 per digest
+  uint64_t first_level;     // level hashed first by this launch
+  uint64_t first_count;     // digests at first_level
+  int fuse;                 // levels computed by this launch
+  uint64_t off[8];          // digest offsets of levels first_level-1 .. first_level+fuse-1 (off[0] = child level)
+};
+
+__global__ __launch_bounds__(256) void k_merkle_levels(MerkleArgs a) {
+  __shared__ Digest sm[256];
+  const uint32_t tid = threadIdx.x;
+  const uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + tid;
+  uint64_t d[8];
+  if (idx < a.first_count) {
+    if (a.leaves) {
+      uint64_t m[16];
+      uint32_t len = fe_decimal_words(ld_fe(a.leaves + idx), m);
+#pragma unroll
+      for (int i = 5; i < 16; ++i) m[i] = 0;
+      blake2b_single_block(m, len, d);
+    } else {
+      uint64_t l[8], r[8];
+      const uint64_t* child = a.tree + a.off[0] * 8;
+      ld_digest(child + (2 * idx) * 8, l);
+      ld_digest(child + (2 * idx + 1) * 8, r);
+      blake2b_node(l, r, d);
+    }
+    st_digest(a.tree + (a.off[1] + idx) * 8, d);
+  }
+  uint32_t count = blockDim.x;  // digests of this block at the current level
+  for (int lev = 1; lev < a.fuse; ++lev) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) sm[tid].h[i] = d[i];
+    __syncthreads();
+    count >>= 1;
+    if (tid < count) {
+      uint64_t l[8], r[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { l[i] = sm[2 * tid].h[i]; r[i] = sm[2 * tid + 1].h[i]; }
+      blake2b_node(l, r, d);
+      uint64_t gidx = (uint64_t)blockIdx.x * count + tid;
+      st_digest(a.tree + (a.off[lev + 1] + gidx) * 8, d);
+    }
+    __syncthreads();
+  }
+}
+
+// ------------------------------------------------------------- FRI fold
+
+struct FoldArgs {
+  fe* out;
+  const fe* in;
+  uint64_t half;        // output length
+  const fe* Tlo;        // Montgomery(w^-e) for e < 4096 (base omega of the FRI instance)
+  const fe* Thi;        // Montgomery(w^-(4096 e))
+  int shift;            // round r: exponent = i << r
+  fe K;                 // Montgomery(alpha * offset_r^-1 * 2^-1)
+  fe Wstride;           // Montgomery(w_r^-stride), stride = gridDim*blockDim
+};
+
+__global__ __launch_bounds__(256) void k_fri_fold(FoldArgs a) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.half) return;
+  uint64_t e = i << a.shift;
+  fe t = mont_mul(a.K, ld_fe(a.Tlo + (e & 4095)));
+  t = mont_mul(t, ld_fe(a.Thi + (e >> 12)));     // Montgomery(K * w_r^-i)
+  for (; i < a.half; i += stride) {
+    fe x = ld_fe(a.in + i);
+    fe y = ld_fe(a.in + i + a.half);
+    fe s = fe_halve(fe_add(x, y));
+    fe dxy = fe_sub(x, y);
+    fe r = fe_add(s, mont_mul(dxy, t));
+    st_fe(a.out + i, r);
+    t = mont_mul(t, a.Wstride);
+  }
+}
+
+// ------------------------------------------------------------- gathers (openings)
+
+__global__ void k_gather_digests(const uint64_t* __restrict__ tree, const uint64_t* __restrict__ idx,
+                                 uint64_t* __restrict__ out, uint32_t count) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  uint64_t d[8];
+  ld_digest(tree + idx[i] * 8, d);
+  st_digest(out + (uint64_t)i * 8, d);
+}
+
+__global__ void k_gather_fe(const fe* __restrict__ src, const uint64_t* __restrict__ idx, fe* __restrict__ out,
+                            uint32_t count) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  st_fe(out + i, ld_fe(src + idx[i]));
+}
+
+// ------------------------------------------------------------- launchers
+
+hipError_t launch_gather_digests(const uint64_t* tree, const uint64_t* idx, uint64_t* out, uint32_t count,
+                                 hipStream_t s) {
+  if (!count) return hipSuccess;
+  hipLaunchKernelGGL(k_gather_digests, dim3((count + 255) / 256), dim3(256), 0, s, tree, idx, out, count);
+  return hipGetLastError();
+}
+
+hipError_t launch_gather_fe(const fe* src, const uint64_t* idx, fe* out, uint32_t count, hipStream_t s) {
+  if (!count) return hipSuccess;
+  hipLaunchKernelGGL(k_gather_fe, dim3((count + 255) / 256), dim3(256), 0, s, src, idx, out, count);
+  return hipGetLastError();
+}
+
+static inline unsigned nblocks(uint64_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
+
+hipError_t launch_pow_table(fe* tw, const fe* A, const fe* B, uint64_t count, hipStream_t s) {
+  if (count == 0) return hipSuccess;
+  hipLaunchKernelGGL(k_pow_table, dim3(nblocks(count, 256)), dim3(256), 0, s, tw, A, B, count);
+  return hipGetLastError();
+}
+
+hipError_t launch_bitrev_gather(fe* out, const fe* in, uint64_t n_in, int logn, const fe* sA, const fe* sB,
+                                hipStream_t s) {
+  uint64_t n = (uint64_t)1 << logn;
+  hipLaunchKernelGGL(k_bitrev_gather, dim3(nblocks(n, 256)), dim3(256), 0, s, out, in, n_in, logn, sA, sB);
+  return hipGetLastError();
+}
+
+hipError_t launch_scale_const(fe* data, uint64_t n, const fe* cst, hipStream_t s) {
+  hipLaunchKernelGGL(k_scale_const, dim3(nblocks(n, 256)), dim3(256), 0, s, data, n, cst);
+  return hipGetLastError();
+}
+
+// Stage plan: pass 1 = stages 1..min(logn,12) on contiguous 4096-element tiles,
+// later passes = up to 8 stages on 2^L x C tiles with C columns for coalescing.
+hipError_t launch_ntt_dit(fe* data, const fe* tw, int logn, const fe* post, hipStream_t s) {
+  if (logn == 0) {
+    if (post) return launch_scale_const(data, 1, post, s);
+    return hipSuccess;
+  }
+  static bool lds_attr = false;
+  if (!lds_attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)k_ntt_pass, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+    if (e != hipSuccess) return e;
+    lds_attr = true;
+  }
+  int b0 = 0;
+  while (b0 < logn) {
+    PassArgs a;
+    a.data = data;
+    a.tw = tw;
+    a.logn = logn;
+    a.b0 = b0;
+    if (b0 == 0) {
+      a.L = logn < 12 ? logn : 12;
+      a.logC = 0;
+    } else {
+      int rem = logn - b0;
+      a.L = rem < 8 ? rem : 8;
+      int logC = 12 - a.L;
+      a.logC = logC < b0 ? logC : b0;
+    }
+    a.post = (b0 + a.L == logn) ? post : nullptr;
+    uint64_t tile = (uint64_t)1 << (a.L + a.logC);
+    uint64_t ntiles = ((uint64_t)1 << logn) / tile;
+    unsigned threads = tile >= 2048 ? 256 : (unsigned)(tile / 8 > 64 ? tile / 8 : 64);
+    size_t lds = tile * sizeof(fe);
+    hipLaunchKernelGGL(k_ntt_pass, dim3((unsigned)ntiles), dim3(threads), lds, s, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    b0 += a.L;
+  }
+  return hipSuccess;
+}
+
+uint64_t merkle_tree_digests(uint64_t n) { return 2 * n - 1; }
+
+hipError_t launch_merkle_tree(const fe* leaves, uint64_t* tree, uint64_t n, hipStream_t s) {
+  // levels 0..logn, level k has n >> k digests at offset 2n - 2(n >> k)
+  int logn = 0;
+  while (((uint64_t)1 << logn) < n) ++logn;
+  int level = 0;
+  while (level <= logn) {
+    uint64_t count = n >> level;
+    unsigned bs = count < 256 ? (unsigned)count : 256u;
+    int lg_bs = 0;
+    while ((1u << lg_bs) < bs) ++lg_bs;
+    int fuse = (count <= 256) ? (lg_bs + 1) : 4;
+    if (level + fuse - 1 > logn) fuse = logn - level + 1;
+    MerkleArgs a;
+    a.leaves = level == 0 ? leaves : nullptr;
+    a.tree = tree;
+    a.first_level = level;
+    a.first_count = count;
+    a.fuse = fuse;
+    for (int k = 0; k < 8; ++k) {
+      int lv = level - 1 + k;
+      a.off[k] = lv < 0 ? 0 : (2 * n - 2 * (n >> lv));
+    }
+    hipLaunchKernelGGL(k_merkle_levels, dim3(nblocks(count, bs)), dim3(bs), 0, s, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    level += fuse;
+  }
+  return hipSuccess;
+}
+
+hipError_t launch_fri_fold(fe* out, const fe* in, uint64_t half, const fe* Tlo, const fe* Thi, int shift,
+                           const fe& K, const fe& Wstride, unsigned grid, hipStream_t s) {
+  FoldArgs a;
+  a.out = out;
+  a.in = in;
+  a.half = half;
+  a.Tlo = Tlo;
+  a.Thi = Thi;
+  a.shift = shift;
+  a.K = K;
+  a.Wstride = Wstride;
+  hipLaunchKernelGGL(k_fri_fold, dim3(grid), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+unsigned fri_fold_grid(uint64_t half) {
+  uint64_t blocks = (half + 255) / 256;
+  const uint64_t cap = 256 * 16;  // grid-stride beyond 16 blocks per CU
+  return (unsigned)(blocks < cap ? blocks : cap);
+}
+
+}  // namespace sg

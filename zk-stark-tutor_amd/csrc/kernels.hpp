@@ -1,0 +1,23 @@
+// Host-side launchers for the gfx950 kernels in kernels.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include "fe128.hpp"
+
+namespace sg {
+
+hipError_t launch_pow_table(fe* tw, const fe* A, const fe* B, uint64_t count, hipStream_t s);
+hipError_t launch_bitrev_gather(fe* out, const fe* in, uint64_t n_in, int logn, const fe* sA, const fe* sB,
+                                hipStream_t s);
+hipError_t launch_scale_const(fe* data, uint64_t n, const fe* cst, hipStream_t s);
+hipError_t launch_ntt_dit(fe* data, const fe* tw, int logn, const fe* post, hipStream_t s);
+uint64_t merkle_tree_digests(uint64_t n);
+hipError_t launch_merkle_tree(const fe* leaves, uint64_t* tree, uint64_t n, hipStream_t s);
+hipError_t launch_fri_fold(fe* out, const fe* in, uint64_t half, const fe* Tlo, const fe* Thi, int shift,
+                           const fe& K, const fe& Wstride, unsigned grid, hipStream_t s);
+unsigned fri_fold_grid(uint64_t half);
+hipError_t launch_gather_digests(const uint64_t* tree, const uint64_t* idx, uint64_t* out, uint32_t count,
+                                 hipStream_t s);
+hipError_t launch_gather_fe(const fe* src, const uint64_t* idx, fe* out, uint32_t count, hipStream_t s);
+
+}  // namespace sg

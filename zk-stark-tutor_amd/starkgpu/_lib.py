@@ -1,0 +1,117 @@
+"""ctypes binding of libstarkgpu.so (the C ABI in include/stark_gpu.h).
+
+The library is built in-tree by `make -C zk-stark-tutor_amd` (or
+`__graft_entry__.build()`).  There is no fallback: if the shared object is
+missing or cannot be loaded, importing the product path raises.
+"""
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libstarkgpu.so")
+
+
+class StarkGpuError(RuntimeError):
+    """A libstarkgpu call returned a negative status."""
+
+    def __init__(self, code, msg):
+        super().__init__(f"libstarkgpu error {code}: {msg}")
+        self.code = code
+
+
+SG_OK = 0
+SG_ERR_INVALID = -1
+SG_ERR_HIP = -2
+SG_ERR_NONCANONICAL = -3
+SG_ERR_CALLBACK = -4
+SG_ERR_NOMEM = -5
+
+
+class sg_fe(ctypes.Structure):
+    _fields_ = [("lo", ctypes.c_uint64), ("hi", ctypes.c_uint64)]
+
+
+class sg_fri(ctypes.Structure):
+    _fields_ = [("offset", sg_fe), ("omega", sg_fe), ("domain_length", ctypes.c_uint64),
+                ("expansion_factor", ctypes.c_uint64), ("num_colinearity_tests", ctypes.c_uint64)]
+
+
+PUSH_CB = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_uint8, ctypes.POINTER(ctypes.c_uint8),
+                           ctypes.c_size_t)
+FS_CB = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_uint8))
+
+
+class sg_proof_stream(ctypes.Structure):
+    _fields_ = [("user", ctypes.c_void_p), ("push", PUSH_CB), ("fiat_shamir_prover", FS_CB)]
+
+
+# name -> (restype, argtypes)
+_P = ctypes.POINTER
+_vp = ctypes.c_void_p
+_sz = ctypes.c_size_t
+_u8p = _P(ctypes.c_uint8)
+_fep = _P(sg_fe)
+PROTOTYPES = {
+    "sg_ctx_create": (ctypes.c_int, [ctypes.c_int, _P(_vp)]),
+    "sg_ctx_destroy": (None, [_vp]),
+    "sg_last_error": (ctypes.c_char_p, [_vp]),
+    "sg_ctx_stream": (_vp, [_vp]),
+    "sg_ctx_trim": (ctypes.c_int, [_vp]),
+    "sg_field_prime": (sg_fe, []),
+    "sg_field_generator": (sg_fe, []),
+    "sg_primitive_nth_root": (ctypes.c_int, [ctypes.c_uint64, _fep]),
+    "sg_field_sample": (sg_fe, [_u8p, _sz]),
+    "sg_fe_mul": (sg_fe, [sg_fe, sg_fe]),
+    "sg_fe_inverse": (sg_fe, [sg_fe]),
+    "sg_fe_pow": (sg_fe, [sg_fe, ctypes.c_uint64]),
+    "sg_ntt": (ctypes.c_int, [_vp, sg_fe, _vp, _sz, _vp]),
+    "sg_intt": (ctypes.c_int, [_vp, sg_fe, _vp, _sz, _vp]),
+    "sg_fast_coset_evaluate": (ctypes.c_int, [_vp, sg_fe, ctypes.c_uint64, sg_fe, _vp, _sz, _vp]),
+    "sg_ntt_dev": (ctypes.c_int, [_vp, sg_fe, _vp, _sz, _vp]),
+    "sg_intt_dev": (ctypes.c_int, [_vp, sg_fe, _vp, _sz, _vp]),
+    "sg_fast_coset_evaluate_dev": (ctypes.c_int, [_vp, sg_fe, ctypes.c_uint64, sg_fe, _vp, _sz, _vp]),
+    "sg_merkle_commit": (ctypes.c_int, [_vp, _vp, _sz, _vp]),
+    "sg_merkle_open": (ctypes.c_int, [_vp, _sz, _vp, _sz, _vp, _P(_sz)]),
+    "sg_merkle_verify": (ctypes.c_int, [_vp, _sz, _vp, _sz, sg_fe]),
+    "sg_merkle_build_dev": (ctypes.c_int, [_vp, _vp, _sz, _P(_vp)]),
+    "sg_tree_root": (ctypes.c_int, [_vp, _vp]),
+    "sg_tree_leaves": (_sz, [_vp]),
+    "sg_tree_open": (ctypes.c_int, [_vp, _vp, _sz, _vp, _P(_sz)]),
+    "sg_tree_free": (None, [_vp, _vp]),
+    "sg_stream_create": (_vp, []),
+    "sg_stream_create_signature": (_vp, [_vp, _sz]),
+    "sg_stream_destroy": (None, [_vp]),
+    "sg_stream_callbacks": (sg_proof_stream, [_vp]),
+    "sg_stream_push": (ctypes.c_int, [_vp, ctypes.c_uint8, _vp, _sz]),
+    "sg_stream_count": (_sz, [_vp]),
+    "sg_stream_digest": (ctypes.c_int, [_vp, _vp, _sz, _P(_sz)]),
+    "sg_stream_fiat_shamir_prover": (ctypes.c_int, [_vp, _sz, _vp]),
+    "sg_stream_fiat_shamir_verifier": (ctypes.c_int, [_vp, _sz, _vp]),
+    "sg_stream_pull": (ctypes.c_int, [_vp, _P(ctypes.c_uint8), _P(_u8p), _P(_sz)]),
+    "sg_stream_deserialize": (ctypes.c_int, [_vp, _sz, _P(_vp)]),
+    "sg_fri_num_rounds": (_sz, [_P(sg_fri)]),
+    "sg_fri_commit": (ctypes.c_int, [_vp, _P(sg_fri), _vp, _sz, _P(sg_proof_stream), _P(_vp)]),
+    "sg_fri_commit_dev": (ctypes.c_int, [_vp, _P(sg_fri), _vp, _sz, _P(sg_proof_stream), _P(_vp)]),
+    "sg_fri_prove": (ctypes.c_int, [_vp, _P(sg_fri), _vp, _sz, _P(sg_proof_stream), _P(_sz)]),
+    "sg_fri_prove_dev": (ctypes.c_int, [_vp, _P(sg_fri), _vp, _sz, _P(sg_proof_stream), _P(_sz)]),
+    "sg_fri_state_free": (None, [_vp, _vp]),
+    "sg_fri_sample_indices": (ctypes.c_int, [_vp, _sz, _sz, _sz, _sz, _P(_sz)]),
+}
+
+_lib = None
+
+
+def lib():
+    """Load libstarkgpu.so once (raises if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(f"{LIB_PATH} not built: run `make -C zk-stark-tutor_amd` "
+                              "(or __graft_entry__.build()); there is no CPU fallback")
+        l = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in PROTOTYPES.items():
+            fn = getattr(l, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = l
+    return _lib
