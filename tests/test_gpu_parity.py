@@ -95,8 +95,9 @@ def test_intt_vs_oracle(n_in):
 
 
 def test_ntt_rejects_noncanonical():
-    with pytest.raises(ValueError):
+    with pytest.raises(sg.StarkGpuError) as e:
         sg.ntt(o.primitive_nth_root(4), [P, 0, 0, 0])
+    assert e.value.code == -3
     arr = sg.fe_array([0, 0, 0, 0])
     arr[0, 1] = np.uint64(0xFFFFFFFFFFFFFFFF)
     with pytest.raises(sg.StarkGpuError):

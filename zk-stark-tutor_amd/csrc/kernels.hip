@@ -196,13 +196,15 @@ __device__ __forceinline__ void ld_digest(const uint64_t* p, uint64_t d[8]) {
 // Hash the first level of a group (leaves when `leaves` != nullptr, else nodes
 // from the children at `child_level`), then `fuse - 1` further levels in LDS.
 // Level k of the tree starts at digest offset level_off[k] in `tree`.
+constexpr int kMaxFuse = 9;  // 256 threads: up to 9 levels (256 -> 1) in one launch
+
 struct MerkleArgs {
   const fe* leaves;         // level 0 input (field elements) or nullptr
   uint64_t* tree;           // retained tree: 8 u64 per digest
   uint64_t first_level;     // level hashed first by this launch
   uint64_t first_count;     // digests at first_level
   int fuse;                 // levels computed by this launch
-  uint64_t off[8];          // digest offsets of levels first_level-1 .. first_level+fuse-1 (off[0] = child level)
+  uint64_t off[kMaxFuse + 1];  // digest offsets of levels first_level-1 .. first_level+fuse-1 (off[0] = child level)
 };
 
 __global__ __launch_bounds__(256) void k_merkle_levels(MerkleArgs a) {
@@ -384,13 +386,14 @@ hipError_t launch_merkle_tree(const fe* leaves, uint64_t* tree, uint64_t n, hipS
     while ((1u << lg_bs) < bs) ++lg_bs;
     int fuse = (count <= 256) ? (lg_bs + 1) : 4;
     if (level + fuse - 1 > logn) fuse = logn - level + 1;
+    if (fuse < 1 || fuse > kMaxFuse) return hipErrorInvalidValue;
     MerkleArgs a;
     a.leaves = level == 0 ? leaves : nullptr;
     a.tree = tree;
     a.first_level = level;
     a.first_count = count;
     a.fuse = fuse;
-    for (int k = 0; k < 8; ++k) {
+    for (int k = 0; k <= kMaxFuse; ++k) {
       int lv = level - 1 + k;
       a.off[k] = lv < 0 ? 0 : (2 * n - 2 * (n >> lv));
     }
