@@ -1,0 +1,221 @@
+#!/usr/bin/env python3
+"""Benchmark: the STARK prover's LDE + Merkle + FRI hot block on MI355X.
+
+Workload (BASELINE.json metric "NTT Gelem/s + prove ms, Rescue-Prime trace 2^20",
+SURVEY.md §8(d) last row): per step, the Stark::prove LDE+commit block
+(stark/stark.rs:367-386, 425-445, 500-522) for a trace of 2^20 rows with
+m = 2 registers, expansion factor 8 (N = 2^23) and 64 colinearity tests:
+  * 2 boundary-quotient polynomials (2^20 coefficients): LDE -> Merkle commit -> push root
+  * 1 randomizer polynomial:  LDE -> Merkle commit -> push root
+  * Fiat-Shamir weights (stark.rs:447-450)
+  * 1 combination polynomial: LDE -> FRI::prove (commit: 15 folds + 16 Merkle trees; query phase)
+Polynomial coefficients are synthetic (seeded SHAKE256 stream);
+the O(T^2) trace interpolation / quotient algebra that produces them in the
+reference is out of scope.  Inputs are resident in HBM
+before timing starts.
+
+One process per GPU (torchrun); each rank proves its own independent trace
+(weak scaling, no collective on the data path).  Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "zk-stark-tutor_amd"))
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+import starkgpu as sg  # noqa: E402
+
+P = sg.FIELD_PRIME
+LOG_TRACE = 20      # coefficients per polynomial (trace 2^20)
+EXPANSION = 8       # N = 2^23
+COLINEARITY = 64
+REGISTERS = 2       # Rescue-Prime m = 2
+HBM_PEAK_GBS = 8000.0
+
+
+def synthetic_fe(seed: int, tag: bytes, n: int) -> np.ndarray:
+    """SURVEY.md §8(d) generator, vectorized: BE 16-byte chunks of SHAKE256(...) mod p."""
+    import hashlib
+    raw = hashlib.shake_256(b"sg-bench" + seed.to_bytes(8, "big") + tag).digest(16 * n)
+    be = np.frombuffer(raw, dtype=">u8").reshape(n, 2)
+    hi = be[:, 0].astype(np.uint64)
+    lo = be[:, 1].astype(np.uint64)
+    p_hi, p_lo = np.uint64(P >> 64), np.uint64(P & ((1 << 64) - 1))
+    ge = (hi > p_hi) | ((hi == p_hi) & (lo >= p_lo))  # v < 2^128 < 2p: one subtraction
+    borrow = (lo < p_lo) & ge
+    lo = np.where(ge, lo - p_lo, lo)
+    hi = np.where(ge, hi - p_hi - borrow.astype(np.uint64), hi)
+    return np.ascontiguousarray(np.stack([lo, hi], axis=1))
+
+
+def to_device(arr: np.ndarray, device) -> torch.Tensor:
+    return torch.from_numpy(arr.view(np.int64).copy()).to(device)
+
+
+class Workload:
+    def __init__(self, rank: int, device, ctx: sg.Context, log_trace=LOG_TRACE):
+        self.ctx = ctx
+        self.d = 1 << log_trace
+        self.N = self.d * EXPANSION
+        self.omega = sg.primitive_nth_root(self.N)
+        self.offset = sg.generator()
+        tags = [b"bq0", b"bq1", b"rand", b"comb"]
+        self.coeffs = [to_device(synthetic_fe(rank, t, self.d), device) for t in tags]
+        self.codewords = [torch.empty((self.N, 2), dtype=torch.int64, device=device) for _ in tags]
+        self.fri = sg.FRI(self.offset, self.omega, self.N, EXPANSION, COLINEARITY, ctx=ctx)
+
+    def step(self):
+        ctx = self.ctx
+        stream = sg.IndependentProofStream()
+        trees = []
+        for k in range(REGISTERS + 1):  # boundary quotients, then the randomizer
+            sg.fast_coset_evaluate_dev(self.omega, self.N, self.offset, self.coeffs[k].data_ptr(), self.d,
+                                       self.codewords[k].data_ptr(), ctx=ctx)
+            t = sg.DeviceTree(self.codewords[k].data_ptr(), self.N, ctx=ctx)
+            stream.push((sg.ROOT, t.root()))
+            trees.append(t)
+        stream.fiat_shamir_prover(sg.PROOF_BYTES)  # combination weights (stark.rs:447-450)
+        c = REGISTERS + 1
+        sg.fast_coset_evaluate_dev(self.omega, self.N, self.offset, self.coeffs[c].data_ptr(), self.d,
+                                   self.codewords[c].data_ptr(), ctx=ctx)
+        top = self.fri.prove_dev(self.codewords[c].data_ptr(), self.N, stream)
+        for t in trees:
+            t.free()
+        return stream, top
+
+    def elements_per_step(self) -> int:
+        return (REGISTERS + 2) * self.N
+
+
+def cpu_baseline_leg(seconds_budget: float = 20.0):
+    """The oracle restatement (reference algorithms) on host cores, on a bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import stark_oracle as o
+    log_trace = 9
+    d = 1 << log_trace
+    N = d * EXPANSION
+    omega = o.primitive_nth_root(N)
+    polys = [o.synthetic_elements(0, t, d) for t in (b"bq0", b"bq1", b"rand", b"comb")]
+    t0 = time.perf_counter()
+    steps = 0
+    while True:
+        stream = o.IndependentProofStream()
+        for k in range(REGISTERS + 1):
+            cw = o.fast_coset_evaluate(omega, N, o.GENERATOR, polys[k])
+            stream.push((o.ROOT, o.merkle_commit(cw)))
+        stream.fiat_shamir_prover(o.PROOF_BYTES)
+        cw = o.fast_coset_evaluate(omega, N, o.GENERATOR, polys[3])
+        o.FRI(o.GENERATOR, omega, N, EXPANSION, COLINEARITY).prove(cw, stream)
+        steps += 1
+        el = time.perf_counter() - t0
+        if el >= seconds_budget or steps >= 50:
+            break
+    per_step = el / steps
+    return {
+        "value": (REGISTERS + 2) * N / per_step / 1e9,
+        "unit": "Gelem/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": f"same block at trace 2^{log_trace} (N=2^{log_trace + 3}), {steps} step(s), "
+                  f"{per_step * 1e3:.1f} ms/step, Python big-int oracle restatement, single thread",
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--log-trace", type=int, default=LOG_TRACE)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local_rank)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    device = torch.device("cuda", local_rank)
+    torch.cuda.set_device(device)
+
+    ctx = sg.Context(local_rank)
+    wl = Workload(rank, device, ctx, args.log_trace)
+    for _ in range(args.warmup):
+        wl.step()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize(device)
+
+    barrier()
+    ctx.profile(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        wl.step()
+    torch.cuda.synchronize(device)
+    t1 = time.perf_counter()
+    barrier()
+    prof = ctx.profile_report()
+    ctx.profile(False)
+
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    elapsed = float(elapsed.item())
+    ms_per_step = elapsed / args.steps * 1e3
+    total_elems = wl.elements_per_step() * args.steps * world
+
+    # dominant kernel by device time, roofline from its algorithmic bytes per launch
+    dom = max(prof.items(), key=lambda kv: kv[1]["ms"])
+    name, st = dom
+    achieved = st["bytes"] / (st["ms"] * 1e-3) / 1e9
+    phases = {k: {"launches": v["launches"] // args.steps, "ms_per_step": round(v["ms"] / args.steps, 4),
+                  "GBps": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["ms"] > 0 else None}
+              for k, v in sorted(prof.items(), key=lambda kv: -kv[1]["ms"])}
+
+    result = {
+        "metric": "NTT Gelem/s + prove ms, Rescue-Prime trace 2^20, at 1/2/4/8 MI355X",
+        "value": round(total_elems / elapsed / 1e9, 4),
+        "unit": "Gelem/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 3),
+        "prove_ms": round(ms_per_step, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u128 (F_p, p = 1 + 407*2^119)",
+        "data": "synthetic (seeded SHAKE256 coefficients, SURVEY.md 8(d))",
+        "config": {"workload": f"Stark LDE+commit block: trace 2^{args.log_trace}, {REGISTERS} registers, "
+                               f"expansion {EXPANSION} (N=2^{args.log_trace + 3}), FRI prove c={COLINEARITY}",
+                   "codeword_elements_per_step_per_gpu": wl.elements_per_step(),
+                   "parallelism": f"replicas x{world} (independent traces, no data-path collective)"},
+        "roofline": {"kernel": name, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "avg_launch_ms": round(st["ms"] / st["launches"], 4),
+                     "alg_bytes_per_launch": int(st["bytes"] / st["launches"])},
+        "kernels": phases,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline_leg()
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -50,6 +50,11 @@ const char* sg_last_error(const sg_ctx* ctx);
 void* sg_ctx_stream(sg_ctx* ctx);
 /* release cached device buffers and twiddle tables */
 int sg_ctx_trim(sg_ctx* ctx);
+/* per-kernel HIP-event timing on the context stream (instrumentation, no reference counterpart):
+ * enable resets the totals; the report is JSON {kernel: {launches, ms, bytes}} where bytes are
+ * the algorithmic bytes of the launches; len receives the size incl. the NUL. */
+int sg_ctx_profile(sg_ctx* ctx, int enable);
+int sg_ctx_profile_report(sg_ctx* ctx, char* buf, size_t cap, size_t* len);
 
 /* ------------------------------------------------------------ field (field/field.rs) */
 sg_fe sg_field_prime(void);                               /* field/field.rs:10 FIELD_PRIME */

@@ -118,6 +118,11 @@ inline sg_fe from_fe(const fe& a) { return sg_fe{fe_lo(a), fe_hi(a)}; }
 
 template <class F>
 int guard(sg_ctx* ctx, F&& f) {
+  struct ProfBind {
+    KernelProfiler* prev;
+    explicit ProfBind(sg_ctx* c) : prev(g_prof) { g_prof = (c && c->profiling) ? &c->prof : nullptr; }
+    ~ProfBind() { g_prof = prev; }
+  } bind(ctx);
   try {
     f();
     return SG_OK;
@@ -208,6 +213,37 @@ extern "C" void sg_ctx_destroy(sg_ctx* ctx) {
   for (auto& kv : ctx->pow_tables) (void)hipFree(kv.second.ptr);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
+}
+
+extern "C" int sg_ctx_profile(sg_ctx* ctx, int enable) {
+  return guard(ctx, [&] {
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+    ctx->prof.drain();
+    ctx->prof.totals.clear();
+    ctx->profiling = enable != 0;
+  });
+}
+
+extern "C" int sg_ctx_profile_report(sg_ctx* ctx, char* buf, size_t cap, size_t* len) {
+  return guard(ctx, [&] {
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+    ctx->prof.drain();
+    std::string js = "{";
+    bool first = true;
+    for (auto& kv : ctx->prof.totals) {
+      char tmp[256];
+      snprintf(tmp, sizeof(tmp), "%s\"%s\": {\"launches\": %llu, \"ms\": %.6f, \"bytes\": %.0f}", first ? "" : ", ",
+               kv.first.c_str(), (unsigned long long)kv.second.launches, kv.second.ms, kv.second.bytes);
+      js += tmp;
+      first = false;
+    }
+    js += "}";
+    if (len) *len = js.size() + 1;
+    if (buf) {
+      SG_REQUIRE(cap > js.size(), "profile report buffer too small");
+      memcpy(buf, js.c_str(), js.size() + 1);
+    }
+  });
 }
 
 extern "C" const char* sg_last_error(const sg_ctx* ctx) { return ctx ? ctx->last_error.c_str() : "null context"; }

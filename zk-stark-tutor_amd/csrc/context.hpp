@@ -7,6 +7,7 @@
 #include <utility>
 #include <vector>
 #include "fe128.hpp"
+#include "profiler.hpp"
 
 struct sg_ctx;
 
@@ -67,6 +68,9 @@ struct sg_ctx {
   size_t pooled_bytes = 0;
   // power tables keyed by (root limbs, count)
   std::map<std::pair<std::pair<uint64_t, uint64_t>, uint64_t>, sg::PowTable> pow_tables;
+  // per-kernel event timing (sg_ctx_profile)
+  bool profiling = false;
+  sg::KernelProfiler prof;
 
   void* alloc(size_t bytes);
   void release(void* p, size_t bytes);

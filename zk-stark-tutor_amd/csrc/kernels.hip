@@ -24,8 +24,11 @@
 #include "blake2b.hpp"
 #include "leaf_decimal.hpp"
 #include "kernels.hpp"
+#include "profiler.hpp"
 
 namespace sg {
+
+thread_local KernelProfiler* g_prof = nullptr;
 
 // ------------------------------------------------------------------ helpers
 
@@ -207,13 +210,14 @@ struct MerkleArgs {
   uint64_t off[kMaxFuse + 1];  // digest offsets of levels first_level-1 .. first_level+fuse-1 (off[0] = child level)
 };
 
+template <bool LEAF>
 __global__ __launch_bounds__(256) void k_merkle_levels(MerkleArgs a) {
   __shared__ Digest sm[256];
   const uint32_t tid = threadIdx.x;
   const uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + tid;
   uint64_t d[8];
   if (idx < a.first_count) {
-    if (a.leaves) {
+    if (LEAF) {
       uint64_t m[16];
       uint32_t len = fe_decimal_words(ld_fe(a.leaves + idx), m);
 #pragma unroll
@@ -300,12 +304,14 @@ __global__ void k_gather_fe(const fe* __restrict__ src, const uint64_t* __restri
 hipError_t launch_gather_digests(const uint64_t* tree, const uint64_t* idx, uint64_t* out, uint32_t count,
                                  hipStream_t s) {
   if (!count) return hipSuccess;
+  ProfScope ps("gather_digests", 128ull * count, s);
   hipLaunchKernelGGL(k_gather_digests, dim3((count + 255) / 256), dim3(256), 0, s, tree, idx, out, count);
   return hipGetLastError();
 }
 
 hipError_t launch_gather_fe(const fe* src, const uint64_t* idx, fe* out, uint32_t count, hipStream_t s) {
   if (!count) return hipSuccess;
+  ProfScope ps("gather_fe", 32ull * count, s);
   hipLaunchKernelGGL(k_gather_fe, dim3((count + 255) / 256), dim3(256), 0, s, src, idx, out, count);
   return hipGetLastError();
 }
@@ -314,6 +320,7 @@ static inline unsigned nblocks(uint64_t n, unsigned bs) { return (unsigned)((n +
 
 hipError_t launch_pow_table(fe* tw, const fe* A, const fe* B, uint64_t count, hipStream_t s) {
   if (count == 0) return hipSuccess;
+  ProfScope ps("pow_table", 16 * count, s);
   hipLaunchKernelGGL(k_pow_table, dim3(nblocks(count, 256)), dim3(256), 0, s, tw, A, B, count);
   return hipGetLastError();
 }
@@ -321,11 +328,13 @@ hipError_t launch_pow_table(fe* tw, const fe* A, const fe* B, uint64_t count, hi
 hipError_t launch_bitrev_gather(fe* out, const fe* in, uint64_t n_in, int logn, const fe* sA, const fe* sB,
                                 hipStream_t s) {
   uint64_t n = (uint64_t)1 << logn;
+  ProfScope ps("bitrev_gather", 16 * (n_in < n ? n_in : n) + 16 * n, s);
   hipLaunchKernelGGL(k_bitrev_gather, dim3(nblocks(n, 256)), dim3(256), 0, s, out, in, n_in, logn, sA, sB);
   return hipGetLastError();
 }
 
 hipError_t launch_scale_const(fe* data, uint64_t n, const fe* cst, hipStream_t s) {
+  ProfScope ps("scale_const", 32 * n, s);
   hipLaunchKernelGGL(k_scale_const, dim3(nblocks(n, 256)), dim3(256), 0, s, data, n, cst);
   return hipGetLastError();
 }
@@ -364,6 +373,7 @@ hipError_t launch_ntt_dit(fe* data, const fe* tw, int logn, const fe* post, hipS
     uint64_t ntiles = ((uint64_t)1 << logn) / tile;
     unsigned threads = tile >= 2048 ? 256 : (unsigned)(tile / 8 > 64 ? tile / 8 : 64);
     size_t lds = tile * sizeof(fe);
+    ProfScope ps("ntt_pass", 32 * ((uint64_t)1 << logn), s);
     hipLaunchKernelGGL(k_ntt_pass, dim3((unsigned)ntiles), dim3(threads), lds, s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -397,7 +407,14 @@ hipError_t launch_merkle_tree(const fe* leaves, uint64_t* tree, uint64_t n, hipS
       int lv = level - 1 + k;
       a.off[k] = lv < 0 ? 0 : (2 * n - 2 * (n >> lv));
     }
-    hipLaunchKernelGGL(k_merkle_levels, dim3(nblocks(count, bs)), dim3(bs), 0, s, a);
+    // algorithmic bytes: leaves read once (16 B) + every digest of these levels written once (64 B)
+    uint64_t digests = 0;
+    for (int k = 0; k < fuse; ++k) digests += count >> k;
+    ProfScope ps(level == 0 ? "merkle_leaves" : "merkle_nodes", (level == 0 ? 16 * count : 0) + 64 * digests, s);
+    if (level == 0)
+      hipLaunchKernelGGL(k_merkle_levels<true>, dim3(nblocks(count, bs)), dim3(bs), 0, s, a);
+    else
+      hipLaunchKernelGGL(k_merkle_levels<false>, dim3(nblocks(count, bs)), dim3(bs), 0, s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     level += fuse;
@@ -416,6 +433,7 @@ hipError_t launch_fri_fold(fe* out, const fe* in, uint64_t half, const fe* Tlo, 
   a.shift = shift;
   a.K = K;
   a.Wstride = Wstride;
+  ProfScope ps("fri_fold", 48 * half, s);
   hipLaunchKernelGGL(k_fri_fold, dim3(grid), dim3(256), 0, s, a);
   return hipGetLastError();
 }

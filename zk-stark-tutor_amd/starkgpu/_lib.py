@@ -57,6 +57,8 @@ PROTOTYPES = {
     "sg_last_error": (ctypes.c_char_p, [_vp]),
     "sg_ctx_stream": (_vp, [_vp]),
     "sg_ctx_trim": (ctypes.c_int, [_vp]),
+    "sg_ctx_profile": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "sg_ctx_profile_report": (ctypes.c_int, [_vp, ctypes.c_char_p, _sz, _P(_sz)]),
     "sg_field_prime": (sg_fe, []),
     "sg_field_generator": (sg_fe, []),
     "sg_primitive_nth_root": (ctypes.c_int, [ctypes.c_uint64, _fep]),

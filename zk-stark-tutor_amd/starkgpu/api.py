@@ -105,6 +105,19 @@ class Context:
     def stream(self) -> int:
         return self._lib.sg_ctx_stream(self.handle) or 0
 
+    def profile(self, enable: bool) -> None:
+        """Start (resetting totals) or stop per-kernel HIP-event timing."""
+        self.check(self._lib.sg_ctx_profile(self.handle, 1 if enable else 0))
+
+    def profile_report(self) -> dict:
+        """{kernel: {"launches", "ms", "bytes"}} accumulated since profile(True)."""
+        import json
+        n = ctypes.c_size_t()
+        self.check(self._lib.sg_ctx_profile_report(self.handle, None, 0, ctypes.byref(n)))
+        buf = ctypes.create_string_buffer(n.value)
+        self.check(self._lib.sg_ctx_profile_report(self.handle, buf, n.value, ctypes.byref(n)))
+        return json.loads(buf.value.decode())
+
     def trim(self) -> None:
         self.check(self._lib.sg_ctx_trim(self.handle))
 
