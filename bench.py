@@ -73,23 +73,38 @@ class Workload:
         self.codewords = [torch.empty((self.N, 2), dtype=torch.int64, device=device) for _ in tags]
         self.fri = sg.FRI(self.offset, self.omega, self.N, EXPANSION, COLINEARITY, ctx=ctx)
 
-    def step(self):
+    def step(self, phases=None):
+        # every library call returns after its device work, so host clocks time phases
         ctx = self.ctx
+        clk = time.perf_counter
+        t0 = clk()
         stream = sg.IndependentProofStream()
         trees = []
+        t_lde = t_mk = 0.0
         for k in range(REGISTERS + 1):  # boundary quotients, then the randomizer
+            a = clk()
             sg.fast_coset_evaluate_dev(self.omega, self.N, self.offset, self.coeffs[k].data_ptr(), self.d,
                                        self.codewords[k].data_ptr(), ctx=ctx)
+            b = clk()
             t = sg.DeviceTree(self.codewords[k].data_ptr(), self.N, ctx=ctx)
             stream.push((sg.ROOT, t.root()))
             trees.append(t)
+            t_lde += b - a
+            t_mk += clk() - b
         stream.fiat_shamir_prover(sg.PROOF_BYTES)  # combination weights (stark.rs:447-450)
         c = REGISTERS + 1
+        a = clk()
         sg.fast_coset_evaluate_dev(self.omega, self.N, self.offset, self.coeffs[c].data_ptr(), self.d,
                                    self.codewords[c].data_ptr(), ctx=ctx)
+        b = clk()
         top = self.fri.prove_dev(self.codewords[c].data_ptr(), self.N, stream)
+        e = clk()
         for t in trees:
             t.free()
+        if phases is not None:
+            for k, v in (("lde", t_lde + (b - a)), ("merkle_commits", t_mk), ("fri_prove", e - b),
+                         ("step", clk() - t0)):
+                phases[k] = phases.get(k, 0.0) + v
         return stream, top
 
     def elements_per_step(self) -> int:
@@ -160,9 +175,10 @@ def main():
 
     barrier()
     ctx.profile(True)
+    host_phases = {}
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        wl.step()
+        wl.step(host_phases)
     torch.cuda.synchronize(device)
     t1 = time.perf_counter()
     barrier()
@@ -207,6 +223,7 @@ def main():
                      "avg_launch_ms": round(st["ms"] / st["launches"], 4),
                      "alg_bytes_per_launch": int(st["bytes"] / st["launches"])},
         "kernels": phases,
+        "host_phases_ms": {k: round(v / args.steps * 1e3, 3) for k, v in host_phases.items()},
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline_leg()

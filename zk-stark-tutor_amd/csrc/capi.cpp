@@ -627,11 +627,13 @@ void fri_commit_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, co
   SG_REQUIRE(rounds >= 1, "FRI: zero rounds for this domain");
   SG_REQUIRE(n == f->domain_length, "Length of the domain doesnt match the length of initial codeword");
   fe omega = to_fe(f->omega), offset = to_fe(f->offset);
+  SG_REQUIRE(fe_is_canonical(omega) && fe_is_canonical(offset), "FRI omega/offset must be canonical");
   // fold tables for the base omega: w^-e for e < n/2 via (e & 4095, e >> 12)
-  fe winv = fe_inv(omega);
+  fe winv = fe_inv(omega);   // w_r^-1 = (w^-1)^(2^r), carried by squaring
+  fe oinv = fe_inv(offset);  // o_r^-1 likewise
   const fe* Tlo = ctx->pow_table(winv, 4096);
   const fe* Thi = ctx->pow_table(fe_pow(winv, 4096), (n / 2 + 4095) / 4096 + 1);
-  fe inv2 = fe_inv(fe_from_u64(2));
+  const fe inv2 = fe_inv(fe_from_u64(2));
 
   // round 0 codeword: copy into a state-owned buffer
   st.codewords.emplace_back(ctx, n * sizeof(fe));
@@ -641,7 +643,7 @@ void fri_commit_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, co
   uint64_t len = n;
   for (size_t r = 0; r < rounds; ++r) {
     // assert omega^(n-1) == omega^-1 (fri.rs:133)
-    SG_REQUIRE(fe_eq(fe_pow(omega, len - 1), fe_inv(omega)), "error in commit: omega does not have the right order!");
+    SG_REQUIRE(fe_eq(fe_pow(omega, len - 1), winv), "error in commit: omega does not have the right order!");
     const fe* cw = st.codewords[r].as<fe>();
     st.trees.emplace_back(build_tree(ctx, cw, len));
     push_obj(ps, SG_OBJ_ROOT, st.trees.back()->root, 64);
@@ -651,17 +653,18 @@ void fri_commit_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, co
       throw Error{SG_ERR_CALLBACK, "proof stream fiat_shamir callback failed"};
     fe alpha = fe_sample(chal, 32);
     uint64_t half = len / 2;
-    // K = alpha * offset^-1 * 2^-1 (Montgomery); w_r^-i = w^-(i << r)
-    fe K = to_mont(fe_mul(fe_mul(alpha, fe_inv(offset)), inv2));
+    // K = alpha * offset_r^-1 * 2^-1 (Montgomery); w_r^-i = w^-(i << r)
+    fe K = to_mont(fe_mul(fe_mul(alpha, oinv), inv2));
     unsigned grid = fri_fold_grid(half);
     uint64_t stride = (uint64_t)grid * 256;
-    fe wr_inv = fe_inv(omega);  // omega here is already w_r
-    fe Wstride = to_mont(fe_pow(wr_inv, stride));
+    fe Wstride = to_mont(fe_pow(winv, stride));
     st.codewords.emplace_back(ctx, half * sizeof(fe));
     st.lengths.push_back(half);
     SG_HIP(launch_fri_fold(st.codewords[r + 1].as<fe>(), cw, half, Tlo, Thi, (int)r, K, Wstride, grid, ctx->stream));
     omega = fe_mul(omega, omega);
     offset = fe_mul(offset, offset);
+    winv = fe_mul(winv, winv);
+    oinv = fe_mul(oinv, oinv);
     len = half;
   }
   // push last codeword (fri.rs:166)
@@ -718,64 +721,81 @@ void fri_prove_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, con
     throw Error{SG_ERR_CALLBACK, "proof stream fiat_shamir callback failed"};
   const size_t c = f->num_colinearity_tests;
   sample_indices(seed, 32, st.lengths[1], st.lengths.back(), c, top);
-  std::vector<size_t> indices(top, top + c);
-  for (size_t r = 0; r + 1 < st.codewords.size(); ++r) {
+  // Every opening of every round is known once the top indices are: gather all
+  // leaf values and authentication-path digests with one launch each, then push
+  // Leafs / Path objects in the reference's order (fri.rs:174-208, 231-245).
+  const size_t R = st.codewords.size() - 1;  // query rounds
+  std::vector<std::vector<size_t>> idx_per_round(R);
+  {
+    std::vector<size_t> indices(top, top + c);
+    for (size_t r = 0; r < R; ++r) {
+      uint64_t len = st.lengths[r];
+      for (auto& i : indices) i = i % (len / 2);
+      idx_per_round[r] = indices;
+    }
+  }
+  std::vector<uint64_t> fe_addr, dg_addr;
+  fe_addr.reserve(R * c * 3);
+  for (size_t r = 0; r < R; ++r) {
     uint64_t len = st.lengths[r];
-    for (auto& i : indices) i = i % (len / 2);
-    // leafs: current[a], current[b], next[c]
-    std::vector<uint64_t> cur_idx, nxt_idx;
+    uint64_t cur = (uint64_t)(uintptr_t)st.codewords[r].get();
+    uint64_t nxt = (uint64_t)(uintptr_t)st.codewords[r + 1].get();
     for (size_t s = 0; s < c; ++s) {
-      cur_idx.push_back(indices[s]);
-      cur_idx.push_back(indices[s] + len / 2);
-      nxt_idx.push_back(indices[s]);
+      size_t i = idx_per_round[r][s];
+      fe_addr.push_back(cur + 16 * (uint64_t)i);
+      fe_addr.push_back(cur + 16 * (uint64_t)(i + len / 2));
+      fe_addr.push_back(nxt + 16 * (uint64_t)i);
     }
-    std::vector<fe> cur_vals(cur_idx.size()), nxt_vals(nxt_idx.size());
-    {
-      DevBuf di(ctx, cur_idx.size() * 8), dv(ctx, cur_idx.size() * sizeof(fe));
-      SG_HIP(hipMemcpyAsync(di.get(), cur_idx.data(), cur_idx.size() * 8, hipMemcpyHostToDevice, ctx->stream));
-      SG_HIP(launch_gather_fe(st.codewords[r].as<fe>(), di.as<uint64_t>(), dv.as<fe>(), (uint32_t)cur_idx.size(),
-                              ctx->stream));
-      SG_HIP(hipMemcpyAsync(cur_vals.data(), dv.get(), cur_idx.size() * sizeof(fe), hipMemcpyDeviceToHost,
-                            ctx->stream));
-      DevBuf dj(ctx, nxt_idx.size() * 8), dw(ctx, nxt_idx.size() * sizeof(fe));
-      SG_HIP(hipMemcpyAsync(dj.get(), nxt_idx.data(), nxt_idx.size() * 8, hipMemcpyHostToDevice, ctx->stream));
-      SG_HIP(launch_gather_fe(st.codewords[r + 1].as<fe>(), dj.as<uint64_t>(), dw.as<fe>(),
-                              (uint32_t)nxt_idx.size(), ctx->stream));
-      SG_HIP(hipMemcpyAsync(nxt_vals.data(), dw.get(), nxt_idx.size() * sizeof(fe), hipMemcpyDeviceToHost,
-                            ctx->stream));
-      SG_HIP(hipStreamSynchronize(ctx->stream));
-    }
-    for (size_t s = 0; s < c; ++s) {
-      std::vector<uint8_t> p;
-      put_u128_be(p, cur_vals[2 * s]);
-      put_u128_be(p, cur_vals[2 * s + 1]);
-      put_u128_be(p, nxt_vals[s]);
-      push_obj(ps, SG_OBJ_LEAFS, p.data(), p.size());
-    }
-    // paths: open(a, current), open(b, current), open(c, next)
     const sg_tree* tc = st.trees[r].get();
     const sg_tree* tn = st.trees[r + 1].get();
-    std::vector<uint64_t> pidx_c, pidx_n;
+    uint64_t bc = (uint64_t)(uintptr_t)tc->buf.get(), bn = (uint64_t)(uintptr_t)tn->buf.get();
+    std::vector<uint64_t> p;
     for (size_t s = 0; s < c; ++s) {
-      path_indices(tc, indices[s], pidx_c);
-      path_indices(tc, indices[s] + len / 2, pidx_c);
-      path_indices(tn, indices[s], pidx_n);
+      size_t i = idx_per_round[r][s];
+      p.clear();
+      path_indices(tc, i, p);
+      path_indices(tc, i + len / 2, p);
+      for (uint64_t d : p) dg_addr.push_back(bc + 64 * d);
+      p.clear();
+      path_indices(tn, i, p);
+      for (uint64_t d : p) dg_addr.push_back(bn + 64 * d);
     }
-    std::vector<uint8_t> pc(pidx_c.size() * 64), pn(pidx_n.size() * 64);
-    gather_digests(ctx, tc, pidx_c, pc.data());
-    gather_digests(ctx, tn, pidx_n, pn.data());
-    const size_t lc = (size_t)tc->logn, ln = (size_t)tn->logn;
+  }
+  std::vector<fe> vals(fe_addr.size());
+  std::vector<uint8_t> digs(dg_addr.size() * 64);
+  {
+    DevBuf da(ctx, std::max<size_t>(fe_addr.size(), 1) * 8), dv(ctx, std::max<size_t>(fe_addr.size(), 1) * 16);
+    DevBuf db(ctx, std::max<size_t>(dg_addr.size(), 1) * 8), dd(ctx, std::max<size_t>(dg_addr.size(), 1) * 64);
+    SG_HIP(hipMemcpyAsync(da.get(), fe_addr.data(), fe_addr.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+    SG_HIP(hipMemcpyAsync(db.get(), dg_addr.data(), dg_addr.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+    SG_HIP(launch_gather_fe_ptrs(da.as<uint64_t>(), dv.as<fe>(), (uint32_t)fe_addr.size(), ctx->stream));
+    SG_HIP(launch_gather_digest_ptrs(db.as<uint64_t>(), dd.as<uint64_t>(), (uint32_t)dg_addr.size(), ctx->stream));
+    SG_HIP(hipMemcpyAsync(vals.data(), dv.get(), vals.size() * 16, hipMemcpyDeviceToHost, ctx->stream));
+    SG_HIP(hipMemcpyAsync(digs.data(), dd.get(), digs.size(), hipMemcpyDeviceToHost, ctx->stream));
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+  }
+  size_t fpos = 0, dpos = 0;
+  std::vector<uint8_t> obj;
+  for (size_t r = 0; r < R; ++r) {
     for (size_t s = 0; s < c; ++s) {
+      obj.clear();
+      put_u128_be(obj, vals[fpos + 3 * s]);
+      put_u128_be(obj, vals[fpos + 3 * s + 1]);
+      put_u128_be(obj, vals[fpos + 3 * s + 2]);
+      push_obj(ps, SG_OBJ_LEAFS, obj.data(), obj.size());
+    }
+    fpos += 3 * c;
+    const size_t lc = (size_t)st.trees[r]->logn, ln = (size_t)st.trees[r + 1]->logn;
+    for (size_t s = 0; s < c; ++s) {
+      const size_t lens[3] = {lc, lc, ln};
       for (int which = 0; which < 3; ++which) {
-        const uint8_t* src = which < 2 ? pc.data() + (2 * s + which) * lc * 64 : pn.data() + s * ln * 64;
-        size_t plen = which < 2 ? lc : ln;
-        std::vector<uint8_t> p;
-        p.reserve(plen * 72);
-        for (size_t k = 0; k < plen; ++k) {
-          for (int i = 7; i >= 0; --i) p.push_back((uint8_t)(64ull >> (8 * i)));
-          p.insert(p.end(), src + k * 64, src + (k + 1) * 64);
+        obj.clear();
+        for (size_t k = 0; k < lens[which]; ++k) {
+          for (int b = 7; b >= 0; --b) obj.push_back((uint8_t)(64ull >> (8 * b)));
+          obj.insert(obj.end(), digs.begin() + (dpos + k) * 64, digs.begin() + (dpos + k + 1) * 64);
         }
-        push_obj(ps, SG_OBJ_PATH, p.data(), p.size());
+        dpos += lens[which];
+        push_obj(ps, SG_OBJ_PATH, obj.data(), obj.size());
       }
     }
   }

@@ -34,11 +34,14 @@ inline fe from_mont(const fe& a) { return mont_mul(a, fe_one()); }
 // canonical product
 inline fe fe_mul(const fe& a, const fe& b) { return mont_mul(mont_mul(a, b), fe_r2()); }
 
-// a^e (field_element.rs:108-143 computes the same unique value)
+// a^e (field_element.rs:108-143 computes the same unique value); cost ~2 bitlen(e) products
 inline fe fe_pow(const fe& a, unsigned __int128 e) {
   fe acc = to_mont(fe_one());
+  if (e == 0) return fe_one();
   fe am = to_mont(a);
-  for (int i = 127; i >= 0; --i) {
+  int top = 127;
+  while (!((e >> top) & 1)) --top;
+  for (int i = top; i >= 0; --i) {
     acc = mont_mul(acc, acc);
     if ((e >> i) & 1) acc = mont_mul(acc, am);
   }

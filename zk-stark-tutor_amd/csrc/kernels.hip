@@ -199,7 +199,7 @@ __device__ __forceinline__ void ld_digest(const uint64_t* p, uint64_t d[8]) {
 // Hash the first level of a group (leaves when `leaves` != nullptr, else nodes
 // from the children at `child_level`), then `fuse - 1` further levels in LDS.
 // Level k of the tree starts at digest offset level_off[k] in `tree`.
-constexpr int kMaxFuse = 9;  // 256 threads: up to 9 levels (256 -> 1) in one launch
+constexpr int kMaxFuse = 11;  // 1024 threads: up to 11 levels (1024 -> 1) in one launch
 
 struct MerkleArgs {
   const fe* leaves;         // level 0 input (field elements) or nullptr
@@ -210,9 +210,9 @@ struct MerkleArgs {
   uint64_t off[kMaxFuse + 1];  // digest offsets of levels first_level-1 .. first_level+fuse-1 (off[0] = child level)
 };
 
-template <bool LEAF>
-__global__ __launch_bounds__(256) void k_merkle_levels(MerkleArgs a) {
-  __shared__ Digest sm[256];
+template <bool LEAF, int MAXB>
+__global__ __launch_bounds__(MAXB) void k_merkle_levels(MerkleArgs a) {
+  __shared__ Digest sm[MAXB];
   const uint32_t tid = threadIdx.x;
   const uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + tid;
   uint64_t d[8];
@@ -299,7 +299,36 @@ __global__ void k_gather_fe(const fe* __restrict__ src, const uint64_t* __restri
   st_fe(out + i, ld_fe(src + idx[i]));
 }
 
+// gather from a list of absolute device addresses (one launch for every round's openings)
+__global__ void k_gather_digest_ptrs(const uint64_t* __restrict__ addrs, uint64_t* __restrict__ out, uint32_t count) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  uint64_t d[8];
+  ld_digest(reinterpret_cast<const uint64_t*>(addrs[i]), d);
+  st_digest(out + (uint64_t)i * 8, d);
+}
+
+__global__ void k_gather_fe_ptrs(const uint64_t* __restrict__ addrs, fe* __restrict__ out, uint32_t count) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  st_fe(out + i, ld_fe(reinterpret_cast<const fe*>(addrs[i])));
+}
+
 // ------------------------------------------------------------- launchers
+
+hipError_t launch_gather_digest_ptrs(const uint64_t* addrs, uint64_t* out, uint32_t count, hipStream_t s) {
+  if (!count) return hipSuccess;
+  ProfScope ps("gather_digests", 128ull * count, s);
+  hipLaunchKernelGGL(k_gather_digest_ptrs, dim3((count + 255) / 256), dim3(256), 0, s, addrs, out, count);
+  return hipGetLastError();
+}
+
+hipError_t launch_gather_fe_ptrs(const uint64_t* addrs, fe* out, uint32_t count, hipStream_t s) {
+  if (!count) return hipSuccess;
+  ProfScope ps("gather_fe", 40ull * count, s);
+  hipLaunchKernelGGL(k_gather_fe_ptrs, dim3((count + 255) / 256), dim3(256), 0, s, addrs, out, count);
+  return hipGetLastError();
+}
 
 hipError_t launch_gather_digests(const uint64_t* tree, const uint64_t* idx, uint64_t* out, uint32_t count,
                                  hipStream_t s) {
@@ -384,6 +413,12 @@ hipError_t launch_ntt_dit(fe* data, const fe* tw, int logn, const fe* post, hipS
 
 uint64_t merkle_tree_digests(uint64_t n) { return 2 * n - 1; }
 
+// Launch plan: while a level has more than kTail digests, hash it with 256-thread
+// blocks and fuse 3 more levels through LDS; the rest of the tree (<= kTail
+// digests at its first level) is one 1024-thread block that runs to the root,
+// so the latency-bound top of the tree costs one launch.
+constexpr uint64_t kTail = 1024;
+
 hipError_t launch_merkle_tree(const fe* leaves, uint64_t* tree, uint64_t n, hipStream_t s) {
   // levels 0..logn, level k has n >> k digests at offset 2n - 2(n >> k)
   int logn = 0;
@@ -391,10 +426,9 @@ hipError_t launch_merkle_tree(const fe* leaves, uint64_t* tree, uint64_t n, hipS
   int level = 0;
   while (level <= logn) {
     uint64_t count = n >> level;
-    unsigned bs = count < 256 ? (unsigned)count : 256u;
-    int lg_bs = 0;
-    while ((1u << lg_bs) < bs) ++lg_bs;
-    int fuse = (count <= 256) ? (lg_bs + 1) : 4;
+    const bool tail = count <= kTail;
+    unsigned bs = tail ? (unsigned)count : 256u;
+    int fuse = tail ? (logn - level + 1) : 4;
     if (level + fuse - 1 > logn) fuse = logn - level + 1;
     if (fuse < 1 || fuse > kMaxFuse) return hipErrorInvalidValue;
     MerkleArgs a;
@@ -411,10 +445,14 @@ hipError_t launch_merkle_tree(const fe* leaves, uint64_t* tree, uint64_t n, hipS
     uint64_t digests = 0;
     for (int k = 0; k < fuse; ++k) digests += count >> k;
     ProfScope ps(level == 0 ? "merkle_leaves" : "merkle_nodes", (level == 0 ? 16 * count : 0) + 64 * digests, s);
-    if (level == 0)
-      hipLaunchKernelGGL(k_merkle_levels<true>, dim3(nblocks(count, bs)), dim3(bs), 0, s, a);
-    else
-      hipLaunchKernelGGL(k_merkle_levels<false>, dim3(nblocks(count, bs)), dim3(bs), 0, s, a);
+    dim3 grid(nblocks(count, bs));
+    if (level == 0) {
+      if (tail) hipLaunchKernelGGL((k_merkle_levels<true, 1024>), grid, dim3(bs), 0, s, a);
+      else hipLaunchKernelGGL((k_merkle_levels<true, 256>), grid, dim3(bs), 0, s, a);
+    } else {
+      if (tail) hipLaunchKernelGGL((k_merkle_levels<false, 1024>), grid, dim3(bs), 0, s, a);
+      else hipLaunchKernelGGL((k_merkle_levels<false, 256>), grid, dim3(bs), 0, s, a);
+    }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     level += fuse;

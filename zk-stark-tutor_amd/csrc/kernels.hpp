@@ -18,6 +18,8 @@ hipError_t launch_fri_fold(fe* out, const fe* in, uint64_t half, const fe* Tlo, 
 unsigned fri_fold_grid(uint64_t half);
 hipError_t launch_gather_digests(const uint64_t* tree, const uint64_t* idx, uint64_t* out, uint32_t count,
                                  hipStream_t s);
+hipError_t launch_gather_digest_ptrs(const uint64_t* addrs, uint64_t* out, uint32_t count, hipStream_t s);
+hipError_t launch_gather_fe_ptrs(const uint64_t* addrs, fe* out, uint32_t count, hipStream_t s);
 hipError_t launch_gather_fe(const fe* src, const uint64_t* idx, fe* out, uint32_t count, hipStream_t s);
 
 }  // namespace sg
