@@ -111,37 +111,55 @@ class Workload:
         return (REGISTERS + 2) * self.N
 
 
-def cpu_baseline_leg(seconds_budget: float = 20.0):
-    """The oracle restatement (reference algorithms) on host cores, on a bounded sample."""
+def cpu_baseline_leg(seconds_budget: float = 15.0):
+    """The reference-faithful C restatement (oracle/ref_cpu.c) on one host core, on a bounded sample.
+
+    Same block as the GPU step (4 LDEs, 3 Merkle commits, FRI commit + query
+    with the reference's O(n)-per-opening Merkle::open), at trace 2^9
+    (N = 2^12), repeated until ~seconds_budget of CPU time.
+    """
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import ref_cpu as rc
     import stark_oracle as o
     log_trace = 9
     d = 1 << log_trace
     N = d * EXPANSION
     omega = o.primitive_nth_root(N)
-    polys = [o.synthetic_elements(0, t, d) for t in (b"bq0", b"bq1", b"rand", b"comb")]
-    t0 = time.perf_counter()
+    polys = [synthetic_fe(0, t, d) for t in (b"bq0", b"bq1", b"rand", b"comb")]
+    fri = o.FRI(o.GENERATOR, omega, N, EXPANSION, COLINEARITY)
     steps = 0
+    t0 = time.perf_counter()
     while True:
-        stream = o.IndependentProofStream()
+        stream = bytes(16)
         for k in range(REGISTERS + 1):
-            cw = o.fast_coset_evaluate(omega, N, o.GENERATOR, polys[k])
-            stream.push((o.ROOT, o.merkle_commit(cw)))
-        stream.fiat_shamir_prover(o.PROOF_BYTES)
-        cw = o.fast_coset_evaluate(omega, N, o.GENERATOR, polys[3])
-        o.FRI(o.GENERATOR, omega, N, EXPANSION, COLINEARITY).prove(cw, stream)
+            cw = rc.fast_coset_evaluate(omega, N, o.GENERATOR, polys[k])
+            stream += bytes([0]) + (64).to_bytes(8, "big") + rc.merkle_commit(cw)
+        o.shake256(stream, o.PROOF_BYTES)  # combination weights
+        cw = rc.fast_coset_evaluate(omega, N, o.GENERATOR, polys[3])
+        stream, roots, cws = rc.fri_commit(o.GENERATOR, omega, cw, EXPANSION, COLINEARITY, prefix=stream,
+                                           want_codewords=True)
+        top = fri.sample_indices(o.shake256(stream, o.PROOF_BYTES), len(cws[1]), len(cws[-1]), COLINEARITY)
+        idx = list(top)
+        for r in range(len(cws) - 1):  # fri.rs:231-245 -> query (fri.rs:174-208)
+            half = len(cws[r]) // 2
+            idx = [i % half for i in idx]
+            for i in idx:
+                rc.merkle_open(i, cws[r])
+                rc.merkle_open(i + half, cws[r])
+                rc.merkle_open(i, cws[r + 1])
         steps += 1
         el = time.perf_counter() - t0
-        if el >= seconds_budget or steps >= 50:
+        if el >= seconds_budget or steps >= 20:
             break
     per_step = el / steps
     return {
-        "value": (REGISTERS + 2) * N / per_step / 1e9,
+        "value": round((REGISTERS + 2) * N / per_step / 1e9, 8),
         "unit": "Gelem/s",
         "cores": 1,
         "kind": "port",
-        "sample": f"same block at trace 2^{log_trace} (N=2^{log_trace + 3}), {steps} step(s), "
-                  f"{per_step * 1e3:.1f} ms/step, Python big-int oracle restatement, single thread",
+        "sample": f"same block at trace 2^{log_trace} (N=2^{log_trace + 3}, c={COLINEARITY}), {steps} step(s), "
+                  f"{per_step * 1e3:.1f} ms/step; oracle/ref_cpu.c: bit-serial mul_mod, xgcd inverse, "
+                  f"per-element pow+div fold, O(n) Merkle opens, single thread",
     }
 
 

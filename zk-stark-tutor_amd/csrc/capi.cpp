@@ -109,6 +109,20 @@ const fe* sg_ctx::pow_table(const fe& root, uint64_t count) {
   return reinterpret_cast<const fe*>(table);
 }
 
+const fe* sg_ctx::stage_twiddles(const fe& root, int logn) {
+  auto key = std::make_pair(std::make_pair(fe_lo(root), fe_hi(root)), logn);
+  auto it = stage_tables.find(key);
+  if (it != stage_tables.end()) return reinterpret_cast<const fe*>(it->second);
+  uint64_t n = (uint64_t)1 << logn;
+  const fe* pw = pow_table(root, n / 2);
+  void* t = nullptr;
+  SG_HIP(hipMalloc(&t, std::max<uint64_t>(n - 1, 1) * sizeof(fe)));
+  SG_HIP(launch_stage_twiddles(reinterpret_cast<fe*>(t), pw, logn, stream));
+  SG_HIP(hipStreamSynchronize(stream));
+  stage_tables[key] = t;
+  return reinterpret_cast<const fe*>(t);
+}
+
 // ======================================================================== helpers
 
 namespace {
@@ -152,9 +166,10 @@ void check_canonical(const sg_fe* v, size_t n, const char* what) {
 
 // In-place DIT NTT on a device buffer already holding the bit-reversed (and
 // zero-padded) input.  post = optional Montgomery constant applied at the end.
-void ntt_core(sg_ctx* ctx, fe* d_data, int logn, const fe& root, const fe* post_host) {
+void ntt_core(sg_ctx* ctx, fe* d_data, int logn, const fe& root, const fe* post_host, int skip = 0) {
   uint64_t n = (uint64_t)1 << logn;
-  const fe* tw = logn > 0 ? ctx->pow_table(root, n / 2) : nullptr;
+  const fe* tw = logn > 0 ? ctx->stage_twiddles(root, logn) : nullptr;
+  (void)n;
   DevBuf dpost;
   const fe* post = nullptr;
   if (post_host) {
@@ -162,7 +177,7 @@ void ntt_core(sg_ctx* ctx, fe* d_data, int logn, const fe& root, const fe* post_
     SG_HIP(hipMemcpyAsync(dpost.get(), post_host, sizeof(fe), hipMemcpyHostToDevice, ctx->stream));
     post = dpost.as<fe>();
   }
-  SG_HIP(launch_ntt_dit(d_data, tw, logn, post, ctx->stream));
+  SG_HIP(launch_ntt_dit(d_data, tw, logn, post, skip, ctx->stream));
   SG_HIP(hipStreamSynchronize(ctx->stream));
 }
 
@@ -179,12 +194,8 @@ void ntt_dev(sg_ctx* ctx, const fe& root, const fe* d_in, uint64_t n_in, fe* d_o
     fe off4096 = fe_pow(*scale_offset, 4096);
     sB = ctx->pow_table(off4096, (n_in + 4095) / 4096);
   }
-  if (logn == 0) {
-    // n == 1: bit_reverse_copy returns the input unchanged
-    SG_HIP(launch_bitrev_gather(d_out, d_in, n_in, 0, sA, sB, ctx->stream));
-  } else {
-    SG_HIP(launch_bitrev_gather(d_out, d_in, n_in, logn, sA, sB, ctx->stream));
-  }
+  // n == 1: bit_reverse_copy returns the input unchanged (logn == 0 gather is a copy)
+  SG_HIP(launch_bitrev_gather(d_out, d_in, n_in, logn, sA, sB, 0, ctx->stream));
   ntt_core(ctx, d_out, logn, root, post);
 }
 
@@ -211,6 +222,7 @@ extern "C" void sg_ctx_destroy(sg_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   ctx->trim();
   for (auto& kv : ctx->pow_tables) (void)hipFree(kv.second.ptr);
+  for (auto& kv : ctx->stage_tables) (void)hipFree(kv.second);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -253,6 +265,8 @@ extern "C" int sg_ctx_trim(sg_ctx* ctx) {
     ctx->trim();
     for (auto& kv : ctx->pow_tables) (void)hipFree(kv.second.ptr);
     ctx->pow_tables.clear();
+    for (auto& kv : ctx->stage_tables) (void)hipFree(kv.second);
+    ctx->stage_tables.clear();
   });
 }
 
@@ -316,8 +330,12 @@ extern "C" int sg_fast_coset_evaluate_dev(sg_ctx* ctx, sg_fe generator, uint64_t
     int logn = ilog2_exact(n);
     const fe* sA = ctx->pow_table(off, 4096);
     const fe* sB = ctx->pow_table(fe_pow(off, 4096), (std::max<uint64_t>(d, 1) + 4095) / 4096);
-    SG_HIP(launch_bitrev_gather(out, in, d, logn, sA, sB, ctx->stream));
-    ntt_core(ctx, out, logn, to_fe(generator), nullptr);
+    // coefficients occupy the first d of n slots: the first `skip` DIT stages
+    // are exact copies (k_bitrev_gather) when d <= n >> skip
+    int skip = 0;
+    while (skip < logn && ((uint64_t)std::max<uint64_t>(d, 1) << (skip + 1)) <= n) ++skip;
+    SG_HIP(launch_bitrev_gather(out, in, d, logn, sA, sB, skip, ctx->stream));
+    ntt_core(ctx, out, logn, to_fe(generator), nullptr, skip);
   });
 }
 

@@ -77,6 +77,9 @@ struct sg_ctx {
   void trim();
   // device table of Montgomery(root^e) for e < count (cached)
   const sg::fe* pow_table(const sg::fe& root, uint64_t count);
+  // stage-major NTT twiddles of `root` for a 2^logn transform (cached)
+  const sg::fe* stage_twiddles(const sg::fe& root, int logn);
+  std::map<std::pair<std::pair<uint64_t, uint64_t>, int>, void*> stage_tables;
 };
 
 namespace sg {

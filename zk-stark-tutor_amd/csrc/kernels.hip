@@ -20,6 +20,7 @@
 // Montgomery product per grid-stride step, no per-element inverse or pow.
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <cstdlib>
 #include "fe128.hpp"
 #include "blake2b.hpp"
 #include "leaf_decimal.hpp"
@@ -67,14 +68,30 @@ __global__ void k_pow_table(fe* __restrict__ tw, const fe* __restrict__ A, const
   st_fe(tw + e, mont_mul(ld_fe(A + (e & 4095)), ld_fe(B + (e >> 12))));
 }
 
+// Stage-major twiddles: for stage S = 1..logn, entries [2^(S-1) - 1, 2^S - 1)
+// hold Montgomery(root^(k * n / 2^S)), k < 2^(S-1): a pass reads consecutive k
+// with consecutive lanes (coalesced) instead of striding the power table by n/2^S.
+__global__ void k_stage_twiddles(fe* __restrict__ out, const fe* __restrict__ pw, int logn) {
+  uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // < n - 1
+  if (idx + 1 >= ((uint64_t)1 << logn)) return;
+  int S = 63 - __builtin_clzll(idx + 1) + 1;  // idx in [2^(S-1) - 1, 2^S - 1)
+  uint64_t k = idx + 1 - ((uint64_t)1 << (S - 1));
+  st_fe(out + idx, ld_fe(pw + (k << (logn - S))));
+}
+
 // --------------------------------------------------- bit reversal (+ LDE scale)
 
 // out[j] = x[rev(j)] (* offset^rev(j) when sA != nullptr), zero beyond n_in.
+// skip > 0 (requires n_in <= n >> skip): the first `skip` DIT stages only see
+// (a, 0) pairs, and a butterfly (a, 0) -> (a + 0*w, a - 0*w) = (a, a) exactly,
+// so their output is x[rev(j & ~(2^skip - 1))] replicated; the caller starts
+// the butterflies at stage skip + 1.
 __global__ void k_bitrev_gather(fe* __restrict__ out, const fe* __restrict__ in, uint64_t n_in, int logn,
-                                const fe* __restrict__ sA, const fe* __restrict__ sB) {
+                                const fe* __restrict__ sA, const fe* __restrict__ sB, int skip) {
   uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >> logn) return;
-  uint64_t i = logn ? (__builtin_bitreverse64(j) >> (64 - logn)) : 0;
+  uint64_t jj = (j >> skip) << skip;
+  uint64_t i = logn ? (__builtin_bitreverse64(jj) >> (64 - logn)) : 0;
   fe v = fe_zero();
   if (i < n_in) {
     v = ld_fe(in + i);
@@ -90,7 +107,7 @@ __global__ void k_bitrev_gather(fe* __restrict__ out, const fe* __restrict__ in,
 
 struct PassArgs {
   fe* data;
-  const fe* tw;        // tw[e] = Montgomery(root^e), e < n/2
+  const fe* tw;        // stage-major twiddles (see ntt_stage_twiddles), Montgomery form
   const fe* post;      // optional Montgomery constant applied on store (INTT n^-1)
   int logn;
   int b0;              // index bits below the group bits (= first stage of the pass - 1)
@@ -121,8 +138,8 @@ __device__ __forceinline__ void radix_step(fe* lds, const PassArgs& a, int t, ui
         if (m & (1 << u)) continue;
         uint64_t gmod = (uint64_t)g_low + ((uint64_t)(m & ((1 << u) - 1)) << t);
         uint64_t k = (gmod << a.b0) + low;
-        uint64_t e = k << (a.logn - S);
-        fe w = ld_fe(a.tw + e);
+        // stage-major table: stage S's twiddles root^(k * n/2^S), k < 2^(S-1), start at 2^(S-1) - 1
+        fe w = ld_fe(a.tw + (((uint64_t)1 << (S - 1)) - 1) + k);
         fe o = mont_mul(x[m + (1 << u)], w);
         fe ev = x[m];
         x[m] = fe_add(ev, o);
@@ -135,6 +152,11 @@ __device__ __forceinline__ void radix_step(fe* lds, const PassArgs& a, int t, ui
   __syncthreads();
 }
 
+// One pass: load a 2^L x C tile into LDS, run L radix-2 stages as radix-8/4/2
+// register steps, store.  TL > 0: the tile is exactly 2^TL elements handled
+// by 256 threads, so the loads/stores are unrolled (all 2^TL/256 global loads
+// of a thread in flight at once); TL == 0: generic loop for small transforms.
+template <int TL>
 __global__ __launch_bounds__(256) void k_ntt_pass(PassArgs a) {
   extern __shared__ fe lds[];
   const int logC = a.logC;
@@ -145,9 +167,22 @@ __global__ __launch_bounds__(256) void k_ntt_pass(PassArgs a) {
   const uint64_t h = blockIdx.x / ncb;
   const uint64_t cb = blockIdx.x % ncb;
   const uint64_t base = (h << (a.b0 + a.L)) + cb * C;
-  for (uint32_t l = threadIdx.x; l < tile; l += blockDim.x) {
-    uint32_t g = l >> logC, c = l & (C - 1);
-    lds[l] = ld_fe(a.data + base + ((uint64_t)g << a.b0) + c);
+  if constexpr (TL > 0) {
+    constexpr int PER = (1 << TL) / 256;
+    fe v[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      uint32_t l = threadIdx.x + 256u * k;
+      uint32_t g = l >> logC, c = l & (C - 1);
+      v[k] = ld_fe(a.data + base + ((uint64_t)g << a.b0) + c);
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) lds[threadIdx.x + 256u * k] = v[k];
+  } else {
+    for (uint32_t l = threadIdx.x; l < tile; l += blockDim.x) {
+      uint32_t g = l >> logC, c = l & (C - 1);
+      lds[l] = ld_fe(a.data + base + ((uint64_t)g << a.b0) + c);
+    }
   }
   __syncthreads();
   int t = 0;
@@ -159,11 +194,23 @@ __global__ __launch_bounds__(256) void k_ntt_pass(PassArgs a) {
   }
   const bool post = a.post != nullptr;
   fe pc = post ? ld_fe(a.post) : fe_zero();
-  for (uint32_t l = threadIdx.x; l < tile; l += blockDim.x) {
-    uint32_t g = l >> logC, c = l & (C - 1);
-    fe v = lds[l];
-    if (post) v = mont_mul(v, pc);
-    st_fe(a.data + base + ((uint64_t)g << a.b0) + c, v);
+  if constexpr (TL > 0) {
+    constexpr int PER = (1 << TL) / 256;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      uint32_t l = threadIdx.x + 256u * k;
+      uint32_t g = l >> logC, c = l & (C - 1);
+      fe v = lds[l];
+      if (post) v = mont_mul(v, pc);
+      st_fe(a.data + base + ((uint64_t)g << a.b0) + c, v);
+    }
+  } else {
+    for (uint32_t l = threadIdx.x; l < tile; l += blockDim.x) {
+      uint32_t g = l >> logC, c = l & (C - 1);
+      fe v = lds[l];
+      if (post) v = mont_mul(v, pc);
+      st_fe(a.data + base + ((uint64_t)g << a.b0) + c, v);
+    }
   }
 }
 
@@ -354,11 +401,19 @@ hipError_t launch_pow_table(fe* tw, const fe* A, const fe* B, uint64_t count, hi
   return hipGetLastError();
 }
 
+hipError_t launch_stage_twiddles(fe* out, const fe* pw, int logn, hipStream_t s) {
+  uint64_t n = (uint64_t)1 << logn;
+  if (n < 2) return hipSuccess;
+  ProfScope ps("stage_twiddles", 32 * n, s);
+  hipLaunchKernelGGL(k_stage_twiddles, dim3(nblocks(n - 1, 256)), dim3(256), 0, s, out, pw, logn);
+  return hipGetLastError();
+}
+
 hipError_t launch_bitrev_gather(fe* out, const fe* in, uint64_t n_in, int logn, const fe* sA, const fe* sB,
-                                hipStream_t s) {
+                                int skip, hipStream_t s) {
   uint64_t n = (uint64_t)1 << logn;
   ProfScope ps("bitrev_gather", 16 * (n_in < n ? n_in : n) + 16 * n, s);
-  hipLaunchKernelGGL(k_bitrev_gather, dim3(nblocks(n, 256)), dim3(256), 0, s, out, in, n_in, logn, sA, sB);
+  hipLaunchKernelGGL(k_bitrev_gather, dim3(nblocks(n, 256)), dim3(256), 0, s, out, in, n_in, logn, sA, sB, skip);
   return hipGetLastError();
 }
 
@@ -368,42 +423,53 @@ hipError_t launch_scale_const(fe* data, uint64_t n, const fe* cst, hipStream_t s
   return hipGetLastError();
 }
 
-// Stage plan: pass 1 = stages 1..min(logn,12) on contiguous 4096-element tiles,
-// later passes = up to 8 stages on 2^L x C tiles with C columns for coalescing.
-hipError_t launch_ntt_dit(fe* data, const fe* tw, int logn, const fe* post, hipStream_t s) {
-  if (logn == 0) {
-    if (post) return launch_scale_const(data, 1, post, s);
-    return hipSuccess;
-  }
+// Stage plan from `first_b0` (stages first_b0+1 .. logn): each pass runs L
+// stages on 2^L x C tiles (<= 4096 elements = 64 KiB of LDS), with C
+// consecutive low-bit indices per tile so global accesses are C*16-byte runs.
+hipError_t launch_ntt_dit(fe* data, const fe* tw, int logn, const fe* post, int first_b0, hipStream_t s) {
   static bool lds_attr = false;
   if (!lds_attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)k_ntt_pass, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+    hipError_t e = hipFuncSetAttribute((const void*)k_ntt_pass<0>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_ntt_pass<12>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_ntt_pass<11>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
     if (e != hipSuccess) return e;
     lds_attr = true;
   }
-  int b0 = 0;
+  static const int tile_log = [] {
+    const char* v = getenv("SG_NTT_TILE_LOG");
+    int t = v ? atoi(v) : 12;
+    return (t == 11 || t == 12) ? t : 12;
+  }();
+  if (first_b0 >= logn) {
+    if (post) return launch_scale_const(data, (uint64_t)1 << logn, post, s);
+    return hipSuccess;
+  }
+  int b0 = first_b0;
   while (b0 < logn) {
     PassArgs a;
     a.data = data;
     a.tw = tw;
     a.logn = logn;
     a.b0 = b0;
-    if (b0 == 0) {
-      a.L = logn < 12 ? logn : 12;
-      a.logC = 0;
-    } else {
-      int rem = logn - b0;
-      a.L = rem < 8 ? rem : 8;
-      int logC = 12 - a.L;
-      a.logC = logC < b0 ? logC : b0;
-    }
+    int rem = logn - b0;
+    int lc_min = b0 < 4 ? b0 : 4;
+    a.L = rem < tile_log - lc_min ? rem : tile_log - lc_min;
+    a.logC = b0 < tile_log - a.L ? b0 : tile_log - a.L;
     a.post = (b0 + a.L == logn) ? post : nullptr;
     uint64_t tile = (uint64_t)1 << (a.L + a.logC);
     uint64_t ntiles = ((uint64_t)1 << logn) / tile;
     unsigned threads = tile >= 2048 ? 256 : (unsigned)(tile / 8 > 64 ? tile / 8 : 64);
     size_t lds = tile * sizeof(fe);
-    ProfScope ps("ntt_pass", 32 * ((uint64_t)1 << logn), s);
-    hipLaunchKernelGGL(k_ntt_pass, dim3((unsigned)ntiles), dim3(threads), lds, s, a);
+    static const char* names[] = {"ntt_pass1", "ntt_pass2", "ntt_pass3", "ntt_pass4", "ntt_pass5"};
+    int pi = 0;
+    for (int bb = first_b0, q = 0; bb < b0; ++q) { int r2 = logn - bb; int lm = bb < 4 ? bb : 4; bb += r2 < tile_log - lm ? r2 : tile_log - lm; pi = q + 1; }
+    ProfScope ps(names[pi < 4 ? pi : 4], 32 * ((uint64_t)1 << logn), s);
+    if (tile == 4096 && threads == 256)
+      hipLaunchKernelGGL(k_ntt_pass<12>, dim3((unsigned)ntiles), dim3(256), lds, s, a);
+    else if (tile == 2048 && threads == 256)
+      hipLaunchKernelGGL(k_ntt_pass<11>, dim3((unsigned)ntiles), dim3(256), lds, s, a);
+    else
+      hipLaunchKernelGGL(k_ntt_pass<0>, dim3((unsigned)ntiles), dim3(threads), lds, s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     b0 += a.L;
