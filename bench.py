@@ -79,18 +79,19 @@ class Workload:
         clk = time.perf_counter
         t0 = clk()
         stream = sg.IndependentProofStream()
-        trees = []
-        t_lde = t_mk = 0.0
-        for k in range(REGISTERS + 1):  # boundary quotients, then the randomizer
-            a = clk()
-            sg.fast_coset_evaluate_dev(self.omega, self.N, self.offset, self.coeffs[k].data_ptr(), self.d,
-                                       self.codewords[k].data_ptr(), ctx=ctx)
-            b = clk()
-            t = sg.DeviceTree(self.codewords[k].data_ptr(), self.N, ctx=ctx)
+        # boundary quotients + randomizer: independent, so their LDEs and trees
+        # run as one batched launch sequence each (stark.rs:367-386, 435-445)
+        k3 = REGISTERS + 1
+        a = clk()
+        sg.fast_coset_evaluate_batch_dev(self.omega, self.N, self.offset,
+                                         [t.data_ptr() for t in self.coeffs[:k3]], self.d,
+                                         [t.data_ptr() for t in self.codewords[:k3]], ctx=ctx)
+        b = clk()
+        trees = sg.DeviceTree.build_batch([t.data_ptr() for t in self.codewords[:k3]], self.N, ctx=ctx)
+        for t in trees:
             stream.push((sg.ROOT, t.root()))
-            trees.append(t)
-            t_lde += b - a
-            t_mk += clk() - b
+        t_lde = b - a
+        t_mk = clk() - b
         stream.fiat_shamir_prover(sg.PROOF_BYTES)  # combination weights (stark.rs:447-450)
         c = REGISTERS + 1
         a = clk()

@@ -80,6 +80,10 @@ int sg_ntt_dev(sg_ctx* ctx, sg_fe root, const sg_fe* d_inputs, size_t n_in, sg_f
 int sg_intt_dev(sg_ctx* ctx, sg_fe root, const sg_fe* d_inputs, size_t n_in, sg_fe* d_out);
 int sg_fast_coset_evaluate_dev(sg_ctx* ctx, sg_fe generator, uint64_t root_order, sg_fe offset,
                                const sg_fe* d_coeffs, size_t d, sg_fe* d_out);
+/* batch (1..4) independent LDEs of equal length in one launch sequence -- stark/stark.rs:367-386
+ * evaluates one boundary quotient per register with identical (generator, root_order, offset) */
+int sg_fast_coset_evaluate_batch_dev(sg_ctx* ctx, sg_fe generator, uint64_t root_order, sg_fe offset,
+                                     const sg_fe* const* d_coeffs, size_t d, sg_fe* const* d_out, size_t batch);
 
 /* ------------------------------------------------------------ Merkle (merkle_root.rs) */
 typedef struct sg_tree sg_tree; /* retained device tree: all 2n-1 digests */
@@ -92,6 +96,8 @@ int sg_merkle_open(sg_ctx* ctx, size_t index, const sg_fe* leaves, size_t n, uin
 int sg_merkle_verify(const uint8_t root[64], size_t index, const uint8_t* path, size_t path_len, sg_fe leaf);
 /* device-resident tree: build once, open in O(log n) */
 int sg_merkle_build_dev(sg_ctx* ctx, const sg_fe* d_leaves, size_t n, sg_tree** out);
+/* batch (1..4) equal-size trees built together (stark/stark.rs:380 commits one per register) */
+int sg_merkle_build_batch_dev(sg_ctx* ctx, const sg_fe* const* d_leaves, size_t n, size_t batch, sg_tree** out);
 int sg_tree_root(const sg_tree* t, uint8_t root[64]);
 size_t sg_tree_leaves(const sg_tree* t);
 int sg_tree_open(sg_ctx* ctx, const sg_tree* t, size_t index, uint8_t* path, size_t* path_len);

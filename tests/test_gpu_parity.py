@@ -258,3 +258,24 @@ def test_large_ntt_roundtrip_and_spot_checks():
     for k in [0, 1, n - 1] + [rng.randrange(n) for _ in range(3)]:
         wk = o.fpow(root, k)
         assert sg.to_ints(X[k:k + 1])[0] == o.evaluate(xs, wk)
+
+
+def test_batched_lde_and_trees_match_single():
+    """sg_fast_coset_evaluate_batch_dev / sg_merkle_build_batch_dev == per-item calls == oracle."""
+    import torch
+    dev = torch.device("cuda", 0)
+    N, d = 1 << 12, 1 << 9
+    w = o.primitive_nth_root(N)
+    polys = [rnd(s, d, b"batch") for s in range(3)]
+    ins = [torch.from_numpy(sg.fe_array(p).view(np.int64)).to(dev) for p in polys]
+    outs = [torch.empty((N, 2), dtype=torch.int64, device=dev) for _ in polys]
+    sg.fast_coset_evaluate_batch_dev(w, N, o.GENERATOR, [t.data_ptr() for t in ins], d,
+                                     [t.data_ptr() for t in outs])
+    torch.cuda.synchronize()
+    expect = [o.fast_coset_evaluate(w, N, o.GENERATOR, p) for p in polys]
+    for out, e in zip(outs, expect):
+        assert sg.to_ints(out.cpu().numpy().view(np.uint64)) == e
+    trees = sg.DeviceTree.build_batch([t.data_ptr() for t in outs], N)
+    for t, e in zip(trees, expect):
+        assert t.root() == o.merkle_commit(e)
+        assert t.open(77) == o.merkle_open(77, e)

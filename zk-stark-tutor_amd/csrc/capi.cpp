@@ -166,7 +166,8 @@ void check_canonical(const sg_fe* v, size_t n, const char* what) {
 
 // In-place DIT NTT on a device buffer already holding the bit-reversed (and
 // zero-padded) input.  post = optional Montgomery constant applied at the end.
-void ntt_core(sg_ctx* ctx, fe* d_data, int logn, const fe& root, const fe* post_host, int skip = 0) {
+void ntt_core(sg_ctx* ctx, fe* const* d_data, int batch, int logn, const fe& root, const fe* post_host,
+              int skip = 0) {
   uint64_t n = (uint64_t)1 << logn;
   const fe* tw = logn > 0 ? ctx->stage_twiddles(root, logn) : nullptr;
   (void)n;
@@ -177,7 +178,7 @@ void ntt_core(sg_ctx* ctx, fe* d_data, int logn, const fe& root, const fe* post_
     SG_HIP(hipMemcpyAsync(dpost.get(), post_host, sizeof(fe), hipMemcpyHostToDevice, ctx->stream));
     post = dpost.as<fe>();
   }
-  SG_HIP(launch_ntt_dit(d_data, tw, logn, post, skip, ctx->stream));
+  SG_HIP(launch_ntt_dit(d_data, batch, tw, logn, post, skip, ctx->stream));
   SG_HIP(hipStreamSynchronize(ctx->stream));
 }
 
@@ -195,8 +196,8 @@ void ntt_dev(sg_ctx* ctx, const fe& root, const fe* d_in, uint64_t n_in, fe* d_o
     sB = ctx->pow_table(off4096, (n_in + 4095) / 4096);
   }
   // n == 1: bit_reverse_copy returns the input unchanged (logn == 0 gather is a copy)
-  SG_HIP(launch_bitrev_gather(d_out, d_in, n_in, logn, sA, sB, 0, ctx->stream));
-  ntt_core(ctx, d_out, logn, root, post);
+  SG_HIP(launch_bitrev_gather(&d_out, &d_in, 1, n_in, logn, sA, sB, 0, ctx->stream));
+  ntt_core(ctx, &d_out, 1, logn, root, post);
 }
 
 }  // namespace
@@ -316,26 +317,46 @@ extern "C" int sg_intt_dev(sg_ctx* ctx, sg_fe root, const sg_fe* d_in, size_t n_
   });
 }
 
+namespace {
+// fft/ntt_arithmetics.rs:161-170 for `batch` polynomials of equal length d (one launch per pass)
+void coset_evaluate_batch(sg_ctx* ctx, const fe& generator, uint64_t root_order, const fe& off,
+                          const fe* const* in, size_t d, fe* const* out, int batch) {
+  SG_REQUIRE(d <= root_order, "fast_coset_evaluate: polynomial longer than root_order");
+  SG_REQUIRE(root_order > 0, "fast_coset_evaluate: empty evaluation domain");
+  SG_REQUIRE(batch >= 1 && batch <= 4, "batch must be 1..4");
+  // the ntt pads to next_pow2(root_order); coefficients beyond d are zero
+  uint64_t n = next_pow2(root_order);
+  int logn = ilog2_exact(n);
+  const fe* sA = ctx->pow_table(off, 4096);
+  const fe* sB = ctx->pow_table(fe_pow(off, 4096), (std::max<uint64_t>(d, 1) + 4095) / 4096);
+  // coefficients occupy the first d of n slots: the first `skip` DIT stages
+  // are exact copies (k_bitrev_gather) when d <= n >> skip
+  int skip = 0;
+  while (skip < logn && ((uint64_t)std::max<uint64_t>(d, 1) << (skip + 1)) <= n) ++skip;
+  SG_HIP(launch_bitrev_gather(out, in, batch, d, logn, sA, sB, skip, ctx->stream));
+  ntt_core(ctx, out, batch, logn, generator, nullptr, skip);
+}
+}  // namespace
+
 extern "C" int sg_fast_coset_evaluate_dev(sg_ctx* ctx, sg_fe generator, uint64_t root_order, sg_fe offset,
                                           const sg_fe* d_coeffs, size_t d, sg_fe* d_out) {
   return guard(ctx, [&] {
     SG_HIP(hipSetDevice(ctx->device));
-    SG_REQUIRE(d <= root_order, "fast_coset_evaluate: polynomial longer than root_order");
-    SG_REQUIRE(root_order > 0, "fast_coset_evaluate: empty evaluation domain");
-    fe off = to_fe(offset);
-    // the ntt pads to next_pow2(root_order); coefficients beyond d are zero
-    uint64_t n = next_pow2(root_order);
-    fe* out = reinterpret_cast<fe*>(d_out);
     const fe* in = reinterpret_cast<const fe*>(d_coeffs);
-    int logn = ilog2_exact(n);
-    const fe* sA = ctx->pow_table(off, 4096);
-    const fe* sB = ctx->pow_table(fe_pow(off, 4096), (std::max<uint64_t>(d, 1) + 4095) / 4096);
-    // coefficients occupy the first d of n slots: the first `skip` DIT stages
-    // are exact copies (k_bitrev_gather) when d <= n >> skip
-    int skip = 0;
-    while (skip < logn && ((uint64_t)std::max<uint64_t>(d, 1) << (skip + 1)) <= n) ++skip;
-    SG_HIP(launch_bitrev_gather(out, in, d, logn, sA, sB, skip, ctx->stream));
-    ntt_core(ctx, out, logn, to_fe(generator), nullptr, skip);
+    fe* out = reinterpret_cast<fe*>(d_out);
+    coset_evaluate_batch(ctx, to_fe(generator), root_order, to_fe(offset), &in, d, &out, 1);
+  });
+}
+
+extern "C" int sg_fast_coset_evaluate_batch_dev(sg_ctx* ctx, sg_fe generator, uint64_t root_order, sg_fe offset,
+                                                const sg_fe* const* d_coeffs, size_t d, sg_fe* const* d_out,
+                                                size_t batch) {
+  return guard(ctx, [&] {
+    SG_HIP(hipSetDevice(ctx->device));
+    SG_REQUIRE(d_coeffs && d_out && batch >= 1 && batch <= 4, "batch must be 1..4");
+    coset_evaluate_batch(ctx, to_fe(generator), root_order, to_fe(offset),
+                         reinterpret_cast<const fe* const*>(d_coeffs), d, reinterpret_cast<fe* const*>(d_out),
+                         (int)batch);
   });
 }
 
@@ -400,15 +421,28 @@ struct sg_tree {
 namespace {
 inline uint64_t level_offset(uint64_t n, int level) { return 2 * n - 2 * (n >> level); }
 
-sg_tree* build_tree(sg_ctx* ctx, const fe* d_leaves, uint64_t n) {
+// merkle_root.rs:21-32 for `batch` equal-size trees in one launch sequence
+void build_trees(sg_ctx* ctx, const fe* const* d_leaves, int batch, uint64_t n, std::unique_ptr<sg_tree>* out) {
   SG_REQUIRE(n > 0 && (n & (n - 1)) == 0, "Leafs len must be power of two");
-  std::unique_ptr<sg_tree> t(new sg_tree());
-  t->n = n;
-  t->logn = ilog2_exact(n);
-  t->buf = DevBuf(ctx, merkle_tree_digests(n) * 64);
-  SG_HIP(launch_merkle_tree(d_leaves, t->buf.as<uint64_t>(), n, ctx->stream));
-  SG_HIP(hipMemcpyAsync(t->root, t->buf.as<uint8_t>() + (2 * n - 2) * 64, 64, hipMemcpyDeviceToHost, ctx->stream));
+  SG_REQUIRE(batch >= 1 && batch <= 4, "batch must be 1..4");
+  uint64_t* bufs[4] = {nullptr, nullptr, nullptr, nullptr};
+  for (int b = 0; b < batch; ++b) {
+    out[b].reset(new sg_tree());
+    out[b]->n = n;
+    out[b]->logn = ilog2_exact(n);
+    out[b]->buf = DevBuf(ctx, merkle_tree_digests(n) * 64);
+    bufs[b] = out[b]->buf.as<uint64_t>();
+  }
+  SG_HIP(launch_merkle_tree(d_leaves, bufs, batch, n, ctx->stream));
+  for (int b = 0; b < batch; ++b)
+    SG_HIP(hipMemcpyAsync(out[b]->root, out[b]->buf.as<uint8_t>() + (2 * n - 2) * 64, 64, hipMemcpyDeviceToHost,
+                          ctx->stream));
   SG_HIP(hipStreamSynchronize(ctx->stream));
+}
+
+sg_tree* build_tree(sg_ctx* ctx, const fe* d_leaves, uint64_t n) {
+  std::unique_ptr<sg_tree> t;
+  build_trees(ctx, &d_leaves, 1, n, &t);
   return t.release();
 }
 
@@ -434,6 +468,17 @@ extern "C" int sg_merkle_build_dev(sg_ctx* ctx, const sg_fe* d_leaves, size_t n,
     *out = build_tree(ctx, reinterpret_cast<const fe*>(d_leaves), n);
   });
 }
+extern "C" int sg_merkle_build_batch_dev(sg_ctx* ctx, const sg_fe* const* d_leaves, size_t n, size_t batch,
+                                         sg_tree** out) {
+  return guard(ctx, [&] {
+    SG_HIP(hipSetDevice(ctx->device));
+    SG_REQUIRE(d_leaves && out && batch >= 1 && batch <= 4, "batch must be 1..4");
+    std::unique_ptr<sg_tree> t[4];
+    build_trees(ctx, reinterpret_cast<const fe* const*>(d_leaves), (int)batch, n, t);
+    for (size_t b = 0; b < batch; ++b) out[b] = t[b].release();
+  });
+}
+
 extern "C" int sg_tree_root(const sg_tree* t, uint8_t root[64]) {
   if (!t || !root) return SG_ERR_INVALID;
   memcpy(root, t->root, 64);

@@ -31,6 +31,8 @@ namespace sg {
 
 thread_local KernelProfiler* g_prof = nullptr;
 
+constexpr int kMaxBatch = 4;  // transforms / trees per launch (blockIdx.y)
+
 // ------------------------------------------------------------------ helpers
 
 __device__ __forceinline__ fe ld_fe(const fe* p) {
@@ -86,8 +88,15 @@ __global__ void k_stage_twiddles(fe* __restrict__ out, const fe* __restrict__ pw
 // (a, 0) pairs, and a butterfly (a, 0) -> (a + 0*w, a - 0*w) = (a, a) exactly,
 // so their output is x[rev(j & ~(2^skip - 1))] replicated; the caller starts
 // the butterflies at stage skip + 1.
-__global__ void k_bitrev_gather(fe* __restrict__ out, const fe* __restrict__ in, uint64_t n_in, int logn,
-                                const fe* __restrict__ sA, const fe* __restrict__ sB, int skip) {
+struct GatherArgs {
+  fe* out[kMaxBatch];
+  const fe* in[kMaxBatch];
+};
+
+__global__ void k_bitrev_gather(GatherArgs ga, uint64_t n_in, int logn, const fe* __restrict__ sA,
+                                const fe* __restrict__ sB, int skip) {
+  fe* __restrict__ out = ga.out[blockIdx.y];
+  const fe* __restrict__ in = ga.in[blockIdx.y];
   uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >> logn) return;
   uint64_t jj = (j >> skip) << skip;
@@ -106,7 +115,7 @@ __global__ void k_bitrev_gather(fe* __restrict__ out, const fe* __restrict__ in,
 // ------------------------------------------------------------- NTT passes
 
 struct PassArgs {
-  fe* data;
+  fe* data[kMaxBatch];  // one transform per blockIdx.y
   const fe* tw;        // stage-major twiddles (see ntt_stage_twiddles), Montgomery form
   const fe* post;      // optional Montgomery constant applied on store (INTT n^-1)
   int logn;
@@ -167,6 +176,7 @@ __global__ __launch_bounds__(256) void k_ntt_pass(PassArgs a) {
   const uint64_t h = blockIdx.x / ncb;
   const uint64_t cb = blockIdx.x % ncb;
   const uint64_t base = (h << (a.b0 + a.L)) + cb * C;
+  fe* __restrict__ data = a.data[blockIdx.y];
   if constexpr (TL > 0) {
     constexpr int PER = (1 << TL) / 256;
     fe v[PER];
@@ -174,14 +184,14 @@ __global__ __launch_bounds__(256) void k_ntt_pass(PassArgs a) {
     for (int k = 0; k < PER; ++k) {
       uint32_t l = threadIdx.x + 256u * k;
       uint32_t g = l >> logC, c = l & (C - 1);
-      v[k] = ld_fe(a.data + base + ((uint64_t)g << a.b0) + c);
+      v[k] = ld_fe(data + base + ((uint64_t)g << a.b0) + c);
     }
 #pragma unroll
     for (int k = 0; k < PER; ++k) lds[threadIdx.x + 256u * k] = v[k];
   } else {
     for (uint32_t l = threadIdx.x; l < tile; l += blockDim.x) {
       uint32_t g = l >> logC, c = l & (C - 1);
-      lds[l] = ld_fe(a.data + base + ((uint64_t)g << a.b0) + c);
+      lds[l] = ld_fe(data + base + ((uint64_t)g << a.b0) + c);
     }
   }
   __syncthreads();
@@ -202,14 +212,14 @@ __global__ __launch_bounds__(256) void k_ntt_pass(PassArgs a) {
       uint32_t g = l >> logC, c = l & (C - 1);
       fe v = lds[l];
       if (post) v = mont_mul(v, pc);
-      st_fe(a.data + base + ((uint64_t)g << a.b0) + c, v);
+      st_fe(data + base + ((uint64_t)g << a.b0) + c, v);
     }
   } else {
     for (uint32_t l = threadIdx.x; l < tile; l += blockDim.x) {
       uint32_t g = l >> logC, c = l & (C - 1);
       fe v = lds[l];
       if (post) v = mont_mul(v, pc);
-      st_fe(a.data + base + ((uint64_t)g << a.b0) + c, v);
+      st_fe(data + base + ((uint64_t)g << a.b0) + c, v);
     }
   }
 }
@@ -249,8 +259,8 @@ __device__ __forceinline__ void ld_digest(const uint64_t* p, uint64_t d[8]) {
 constexpr int kMaxFuse = 11;  // 1024 threads: up to 11 levels (1024 -> 1) in one launch
 
 struct MerkleArgs {
-  const fe* leaves;         // level 0 input (field elements) or nullptr
-  uint64_t* tree;           // retained tree: 8 u64 per digest
+  const fe* leaves[kMaxBatch];  // level 0 input (field elements) per tree (blockIdx.y)
+  uint64_t* tree[kMaxBatch];    // retained trees: 8 u64 per digest
   uint64_t first_level;     // level hashed first by this launch
   uint64_t first_count;     // digests at first_level
   int fuse;                 // levels computed by this launch
@@ -262,22 +272,23 @@ __global__ __launch_bounds__(MAXB) void k_merkle_levels(MerkleArgs a) {
   __shared__ Digest sm[MAXB];
   const uint32_t tid = threadIdx.x;
   const uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + tid;
+  uint64_t* __restrict__ tree = a.tree[blockIdx.y];
   uint64_t d[8];
   if (idx < a.first_count) {
     if (LEAF) {
       uint64_t m[16];
-      uint32_t len = fe_decimal_words(ld_fe(a.leaves + idx), m);
+      uint32_t len = fe_decimal_words(ld_fe(a.leaves[blockIdx.y] + idx), m);
 #pragma unroll
       for (int i = 5; i < 16; ++i) m[i] = 0;
       blake2b_single_block(m, len, d);
     } else {
       uint64_t l[8], r[8];
-      const uint64_t* child = a.tree + a.off[0] * 8;
+      const uint64_t* child = tree + a.off[0] * 8;
       ld_digest(child + (2 * idx) * 8, l);
       ld_digest(child + (2 * idx + 1) * 8, r);
       blake2b_node(l, r, d);
     }
-    st_digest(a.tree + (a.off[1] + idx) * 8, d);
+    st_digest(tree + (a.off[1] + idx) * 8, d);
   }
   uint32_t count = blockDim.x;  // digests of this block at the current level
   for (int lev = 1; lev < a.fuse; ++lev) {
@@ -291,7 +302,7 @@ __global__ __launch_bounds__(MAXB) void k_merkle_levels(MerkleArgs a) {
       for (int i = 0; i < 8; ++i) { l[i] = sm[2 * tid].h[i]; r[i] = sm[2 * tid + 1].h[i]; }
       blake2b_node(l, r, d);
       uint64_t gidx = (uint64_t)blockIdx.x * count + tid;
-      st_digest(a.tree + (a.off[lev + 1] + gidx) * 8, d);
+      st_digest(tree + (a.off[lev + 1] + gidx) * 8, d);
     }
     __syncthreads();
   }
@@ -409,11 +420,17 @@ hipError_t launch_stage_twiddles(fe* out, const fe* pw, int logn, hipStream_t s)
   return hipGetLastError();
 }
 
-hipError_t launch_bitrev_gather(fe* out, const fe* in, uint64_t n_in, int logn, const fe* sA, const fe* sB,
-                                int skip, hipStream_t s) {
+hipError_t launch_bitrev_gather(fe* const* out, const fe* const* in, int batch, uint64_t n_in, int logn,
+                                const fe* sA, const fe* sB, int skip, hipStream_t s) {
+  if (batch < 1 || batch > kMaxBatch) return hipErrorInvalidValue;
   uint64_t n = (uint64_t)1 << logn;
-  ProfScope ps("bitrev_gather", 16 * (n_in < n ? n_in : n) + 16 * n, s);
-  hipLaunchKernelGGL(k_bitrev_gather, dim3(nblocks(n, 256)), dim3(256), 0, s, out, in, n_in, logn, sA, sB, skip);
+  GatherArgs ga;
+  for (int b = 0; b < kMaxBatch; ++b) {
+    ga.out[b] = b < batch ? out[b] : nullptr;
+    ga.in[b] = b < batch ? in[b] : nullptr;
+  }
+  ProfScope ps("bitrev_gather", batch * (16 * (n_in < n ? n_in : n) + 16 * n), s);
+  hipLaunchKernelGGL(k_bitrev_gather, dim3(nblocks(n, 256), batch), dim3(256), 0, s, ga, n_in, logn, sA, sB, skip);
   return hipGetLastError();
 }
 
@@ -426,7 +443,9 @@ hipError_t launch_scale_const(fe* data, uint64_t n, const fe* cst, hipStream_t s
 // Stage plan from `first_b0` (stages first_b0+1 .. logn): each pass runs L
 // stages on 2^L x C tiles (<= 4096 elements = 64 KiB of LDS), with C
 // consecutive low-bit indices per tile so global accesses are C*16-byte runs.
-hipError_t launch_ntt_dit(fe* data, const fe* tw, int logn, const fe* post, int first_b0, hipStream_t s) {
+hipError_t launch_ntt_dit(fe* const* data, int batch, const fe* tw, int logn, const fe* post, int first_b0,
+                          hipStream_t s) {
+  if (batch < 1 || batch > kMaxBatch) return hipErrorInvalidValue;
   static bool lds_attr = false;
   if (!lds_attr) {
     hipError_t e = hipFuncSetAttribute((const void*)k_ntt_pass<0>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
@@ -441,13 +460,16 @@ hipError_t launch_ntt_dit(fe* data, const fe* tw, int logn, const fe* post, int 
     return (t == 11 || t == 12) ? t : 12;
   }();
   if (first_b0 >= logn) {
-    if (post) return launch_scale_const(data, (uint64_t)1 << logn, post, s);
+    for (int b = 0; post && b < batch; ++b) {
+      hipError_t e = launch_scale_const(data[b], (uint64_t)1 << logn, post, s);
+      if (e != hipSuccess) return e;
+    }
     return hipSuccess;
   }
   int b0 = first_b0;
   while (b0 < logn) {
     PassArgs a;
-    a.data = data;
+    for (int b = 0; b < kMaxBatch; ++b) a.data[b] = b < batch ? data[b] : nullptr;
     a.tw = tw;
     a.logn = logn;
     a.b0 = b0;
@@ -463,13 +485,14 @@ hipError_t launch_ntt_dit(fe* data, const fe* tw, int logn, const fe* post, int 
     static const char* names[] = {"ntt_pass1", "ntt_pass2", "ntt_pass3", "ntt_pass4", "ntt_pass5"};
     int pi = 0;
     for (int bb = first_b0, q = 0; bb < b0; ++q) { int r2 = logn - bb; int lm = bb < 4 ? bb : 4; bb += r2 < tile_log - lm ? r2 : tile_log - lm; pi = q + 1; }
-    ProfScope ps(names[pi < 4 ? pi : 4], 32 * ((uint64_t)1 << logn), s);
+    ProfScope ps(names[pi < 4 ? pi : 4], batch * 32 * ((uint64_t)1 << logn), s);
+    dim3 grid((unsigned)ntiles, batch);
     if (tile == 4096 && threads == 256)
-      hipLaunchKernelGGL(k_ntt_pass<12>, dim3((unsigned)ntiles), dim3(256), lds, s, a);
+      hipLaunchKernelGGL(k_ntt_pass<12>, grid, dim3(256), lds, s, a);
     else if (tile == 2048 && threads == 256)
-      hipLaunchKernelGGL(k_ntt_pass<11>, dim3((unsigned)ntiles), dim3(256), lds, s, a);
+      hipLaunchKernelGGL(k_ntt_pass<11>, grid, dim3(256), lds, s, a);
     else
-      hipLaunchKernelGGL(k_ntt_pass<0>, dim3((unsigned)ntiles), dim3(threads), lds, s, a);
+      hipLaunchKernelGGL(k_ntt_pass<0>, grid, dim3(threads), lds, s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     b0 += a.L;
@@ -485,7 +508,8 @@ uint64_t merkle_tree_digests(uint64_t n) { return 2 * n - 1; }
 // so the latency-bound top of the tree costs one launch.
 constexpr uint64_t kTail = 1024;
 
-hipError_t launch_merkle_tree(const fe* leaves, uint64_t* tree, uint64_t n, hipStream_t s) {
+hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, int batch, uint64_t n, hipStream_t s) {
+  if (batch < 1 || batch > kMaxBatch) return hipErrorInvalidValue;
   // levels 0..logn, level k has n >> k digests at offset 2n - 2(n >> k)
   int logn = 0;
   while (((uint64_t)1 << logn) < n) ++logn;
@@ -498,8 +522,10 @@ hipError_t launch_merkle_tree(const fe* leaves, uint64_t* tree, uint64_t n, hipS
     if (level + fuse - 1 > logn) fuse = logn - level + 1;
     if (fuse < 1 || fuse > kMaxFuse) return hipErrorInvalidValue;
     MerkleArgs a;
-    a.leaves = level == 0 ? leaves : nullptr;
-    a.tree = tree;
+    for (int b = 0; b < kMaxBatch; ++b) {
+      a.leaves[b] = (level == 0 && b < batch) ? leaves[b] : nullptr;
+      a.tree[b] = b < batch ? tree[b] : nullptr;
+    }
     a.first_level = level;
     a.first_count = count;
     a.fuse = fuse;
@@ -510,8 +536,8 @@ hipError_t launch_merkle_tree(const fe* leaves, uint64_t* tree, uint64_t n, hipS
     // algorithmic bytes: leaves read once (16 B) + every digest of these levels written once (64 B)
     uint64_t digests = 0;
     for (int k = 0; k < fuse; ++k) digests += count >> k;
-    ProfScope ps(level == 0 ? "merkle_leaves" : "merkle_nodes", (level == 0 ? 16 * count : 0) + 64 * digests, s);
-    dim3 grid(nblocks(count, bs));
+    ProfScope ps(level == 0 ? "merkle_leaves" : "merkle_nodes", batch * ((level == 0 ? 16 * count : 0) + 64 * digests), s);
+    dim3 grid(nblocks(count, bs), batch);
     if (level == 0) {
       if (tail) hipLaunchKernelGGL((k_merkle_levels<true, 1024>), grid, dim3(bs), 0, s, a);
       else hipLaunchKernelGGL((k_merkle_levels<true, 256>), grid, dim3(bs), 0, s, a);

@@ -4,7 +4,8 @@ include/stark_gpu.h.  See DESIGN.md."""
 from ._lib import LIB_PATH, StarkGpuError, lib
 from .api import (CODEWORD, FIELD_PRIME, LEAFS, PATH, PROOF_BYTES, ROOT, VALUE, CallbackProofStream, Context,
                   DeviceTree, FRI, IndependentProofStream, MerkleRoot, SignatureProofStream, decode_object,
-                  encode_object, fast_coset_evaluate, fast_coset_evaluate_dev, fe_array, fe_inverse, fe_mul, fe_pow,
+                  encode_object, fast_coset_evaluate, fast_coset_evaluate_batch_dev,
+                  fast_coset_evaluate_dev, fe_array, fe_inverse, fe_mul, fe_pow,
                   generator, intt, intt_dev, ntt, ntt_dev, primitive_nth_root, sample, to_ints)
 
 __all__ = [n for n in dir() if not n.startswith("_")]

@@ -72,10 +72,13 @@ PROTOTYPES = {
     "sg_ntt_dev": (ctypes.c_int, [_vp, sg_fe, _vp, _sz, _vp]),
     "sg_intt_dev": (ctypes.c_int, [_vp, sg_fe, _vp, _sz, _vp]),
     "sg_fast_coset_evaluate_dev": (ctypes.c_int, [_vp, sg_fe, ctypes.c_uint64, sg_fe, _vp, _sz, _vp]),
+    "sg_fast_coset_evaluate_batch_dev": (ctypes.c_int, [_vp, sg_fe, ctypes.c_uint64, sg_fe, _P(_vp), _sz, _P(_vp),
+                                                        _sz]),
     "sg_merkle_commit": (ctypes.c_int, [_vp, _vp, _sz, _vp]),
     "sg_merkle_open": (ctypes.c_int, [_vp, _sz, _vp, _sz, _vp, _P(_sz)]),
     "sg_merkle_verify": (ctypes.c_int, [_vp, _sz, _vp, _sz, sg_fe]),
     "sg_merkle_build_dev": (ctypes.c_int, [_vp, _vp, _sz, _P(_vp)]),
+    "sg_merkle_build_batch_dev": (ctypes.c_int, [_vp, _P(_vp), _sz, _sz, _P(_vp)]),
     "sg_tree_root": (ctypes.c_int, [_vp, _vp]),
     "sg_tree_leaves": (_sz, [_vp]),
     "sg_tree_open": (ctypes.c_int, [_vp, _vp, _sz, _vp, _P(_sz)]),

@@ -233,6 +233,17 @@ def fast_coset_evaluate_dev(generator_: int, root_order: int, offset: int, d_coe
                                               ctypes.c_void_p(d_coeffs), d, ctypes.c_void_p(d_out)))
 
 
+def fast_coset_evaluate_batch_dev(generator_: int, root_order: int, offset: int, d_coeffs: Sequence[int], d: int,
+                                  d_outs: Sequence[int], ctx: Optional[Context] = None) -> None:
+    """Up to 4 LDEs with the same (generator, root_order, offset) in one launch sequence."""
+    c = _ctx(ctx)
+    k = len(d_coeffs)
+    ins = (ctypes.c_void_p * k)(*d_coeffs)
+    outs = (ctypes.c_void_p * k)(*d_outs)
+    c.check(c._lib.sg_fast_coset_evaluate_batch_dev(c.handle, _fe(generator_), root_order, _fe(offset), ins, d,
+                                                    outs, k))
+
+
 # ------------------------------------------------------------------ Merkle
 
 class MerkleRoot:
@@ -269,13 +280,26 @@ class MerkleRoot:
 class DeviceTree:
     """A retained device Merkle tree (build once, open in O(log n))."""
 
-    def __init__(self, d_leaves: int, n: int, ctx: Optional[Context] = None):
+    def __init__(self, d_leaves: int, n: int, ctx: Optional[Context] = None, _handle=None):
         self.ctx = _ctx(ctx)
+        self.n = n
+        if _handle is not None:
+            self.handle = _handle
+            return
         h = ctypes.c_void_p()
         self.ctx.check(self.ctx._lib.sg_merkle_build_dev(self.ctx.handle, ctypes.c_void_p(d_leaves), n,
                                                          ctypes.byref(h)))
         self.handle = h
-        self.n = n
+
+    @classmethod
+    def build_batch(cls, d_leaves: Sequence[int], n: int, ctx: Optional[Context] = None) -> List["DeviceTree"]:
+        """Up to 4 equal-size trees built in one launch sequence."""
+        c = _ctx(ctx)
+        k = len(d_leaves)
+        ins = (ctypes.c_void_p * k)(*d_leaves)
+        outs = (ctypes.c_void_p * k)()
+        c.check(c._lib.sg_merkle_build_batch_dev(c.handle, ins, n, k, outs))
+        return [cls(0, n, ctx=c, _handle=ctypes.c_void_p(outs[i])) for i in range(k)]
 
     def root(self) -> bytes:
         r = (ctypes.c_uint8 * 64)()
