@@ -279,3 +279,13 @@ def test_batched_lde_and_trees_match_single():
     for t, e in zip(trees, expect):
         assert t.root() == o.merkle_commit(e)
         assert t.open(77) == o.merkle_open(77, e)
+
+
+def test_large_merkle_vs_c_oracle():
+    """2^20 leaves exercise every launch kind (fused leaves, 1-lane nodes, quad nodes)."""
+    import ref_cpu
+    n = 1 << 20
+    x = np.random.default_rng(3).integers(0, 2**63, size=(n, 2), dtype=np.uint64)
+    x[:, 1] %= np.uint64(0xCB80000000000000)
+    root = sg.MerkleRoot.commit(x)
+    assert root == ref_cpu.merkle_commit(x)

@@ -308,6 +308,143 @@ __global__ __launch_bounds__(MAXB) void k_merkle_levels(MerkleArgs a) {
   }
 }
 
+// ---------------------------------------------------- Merkle: 4 lanes per hash
+//
+// The top of a tree is latency-bound: a level of a few thousand nodes or less
+// cannot fill the chip, and each level waits for the one below.  Here one
+// compression is split over a quad of lanes (BLAKE2b's four independent G
+// columns): lane q holds column q (v[q], v[4+q], v[8+q], v[12+q]), the
+// diagonal step rotates rows 1..3 across the quad with DPP quad_perm moves,
+// and message words are read from LDS at the round's sigma positions.
+// ~2.4x fewer dependent instructions per level than one lane per hash.
+
+// packed sigma nibbles for one lane of the quad: round r (0..9) occupies bits
+// [16r, 16r+16) as (col_x, col_y, diag_x, diag_y) = sigma[r][2q], [2q+1], [8+2q], [9+2q]
+struct SigmaPack {
+  uint32_t w[5];
+};
+__host__ __device__ constexpr uint32_t sigma_nib(int r, int q) {
+  constexpr uint8_t S[10][16] = {
+      {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15}, {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3},
+      {11, 8, 12, 0, 5, 2, 15, 13, 10, 14, 3, 6, 7, 1, 9, 4}, {7, 9, 3, 1, 13, 12, 11, 14, 2, 6, 5, 10, 4, 0, 15, 8},
+      {9, 0, 5, 7, 2, 4, 10, 15, 14, 1, 11, 12, 6, 8, 3, 13}, {2, 12, 6, 10, 0, 11, 8, 3, 4, 13, 7, 5, 15, 14, 1, 9},
+      {12, 5, 1, 15, 14, 13, 4, 10, 0, 7, 6, 3, 9, 2, 8, 11}, {13, 11, 7, 14, 12, 1, 3, 9, 5, 0, 15, 4, 8, 6, 2, 10},
+      {6, 15, 14, 9, 11, 3, 0, 8, 12, 2, 13, 7, 1, 4, 10, 5}, {10, 2, 8, 4, 7, 6, 1, 5, 15, 11, 9, 14, 3, 12, 13, 0}};
+  return (uint32_t)S[r][2 * q] | ((uint32_t)S[r][2 * q + 1] << 4) | ((uint32_t)S[r][8 + 2 * q] << 8) |
+         ((uint32_t)S[r][9 + 2 * q] << 12);
+}
+__device__ __forceinline__ SigmaPack sigma_pack(int q) {
+  SigmaPack p;
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    uint32_t v0 = q == 0 ? sigma_nib(2 * k, 0) : q == 1 ? sigma_nib(2 * k, 1) : q == 2 ? sigma_nib(2 * k, 2) : sigma_nib(2 * k, 3);
+    uint32_t v1 = q == 0 ? sigma_nib(2 * k + 1, 0) : q == 1 ? sigma_nib(2 * k + 1, 1) : q == 2 ? sigma_nib(2 * k + 1, 2)
+                                                                                              : sigma_nib(2 * k + 1, 3);
+    p.w[k] = v0 | (v1 << 16);
+  }
+  return p;
+}
+
+template <int CTRL>
+__device__ __forceinline__ uint64_t quad_perm64(uint64_t x) {
+  uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)x, CTRL, 0xF, 0xF, false);
+  uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(x >> 32), CTRL, 0xF, 0xF, false);
+  return ((uint64_t)hi << 32) | lo;
+}
+// quad_perm encodings: lane i takes lane sel[i]
+constexpr int QP_NEXT1 = 1 | (2 << 2) | (3 << 4) | (0 << 6);  // from (q+1)%4
+constexpr int QP_NEXT2 = 2 | (3 << 2) | (0 << 4) | (1 << 6);  // from (q+2)%4
+constexpr int QP_NEXT3 = 3 | (0 << 2) | (1 << 4) | (2 << 6);  // from (q+3)%4
+
+#define SG_QG(a, b, c, d, x, y)   \
+  a = a + b + (x);                \
+  d = rotr64(d ^ a, 32);          \
+  c = c + d;                      \
+  b = rotr64(b ^ c, 24);          \
+  a = a + b + (y);                \
+  d = rotr64(d ^ a, 16);          \
+  c = c + d;                      \
+  b = rotr64(b ^ c, 63);
+
+// One BLAKE2b single-block compression (final block, counter t) computed by a
+// quad.  msg: the 16 message words in LDS.  Returns h[q] and h[4+q].
+__device__ __forceinline__ void blake2b_quad(const uint64_t* msg, uint64_t t, int q, const SigmaPack& sp,
+                                             uint64_t& out_lo, uint64_t& out_hi) {
+  const uint64_t ivq = q == 0 ? SG_B2B_IV0 : q == 1 ? SG_B2B_IV1 : q == 2 ? SG_B2B_IV2 : SG_B2B_IV3;
+  const uint64_t iv4q = q == 0 ? SG_B2B_IV4 : q == 1 ? SG_B2B_IV5 : q == 2 ? SG_B2B_IV6 : SG_B2B_IV7;
+  const uint64_t hq = q == 0 ? (SG_B2B_IV0 ^ 0x01010040ull) : ivq;
+  uint64_t a = hq, b = iv4q, c = ivq;
+  uint64_t d = iv4q ^ (q == 0 ? t : 0) ^ (q == 2 ? ~0ull : 0);
+#pragma unroll
+  for (int r = 0; r < 12; ++r) {
+    const int rr = r % 10;
+    const uint32_t nib = (sp.w[rr >> 1] >> (16 * (rr & 1))) & 0xFFFFu;
+    uint64_t mx = msg[nib & 15], my = msg[(nib >> 4) & 15];
+    uint64_t dx = msg[(nib >> 8) & 15], dy = msg[nib >> 12];
+    SG_QG(a, b, c, d, mx, my)
+    b = quad_perm64<QP_NEXT1>(b);
+    c = quad_perm64<QP_NEXT2>(c);
+    d = quad_perm64<QP_NEXT3>(d);
+    SG_QG(a, b, c, d, dx, dy)
+    b = quad_perm64<QP_NEXT3>(b);
+    c = quad_perm64<QP_NEXT2>(c);
+    d = quad_perm64<QP_NEXT1>(d);
+  }
+  out_lo = hq ^ a ^ c;
+  out_hi = iv4q ^ b ^ d;
+}
+
+// Node levels with a quad per node: 256 threads = 64 nodes at the first level,
+// `fuse` levels computed (64 -> 1 at most 7).  Children of the first level are
+// read from HBM (level first_level-1), every produced digest is written to the tree.
+__global__ __launch_bounds__(256) void k_merkle_quad(MerkleArgs a) {
+  __shared__ uint64_t msg[64][16];
+  const int tid = threadIdx.x;
+  const int q = tid & 3;
+  const int node = tid >> 2;
+  uint64_t* __restrict__ tree = a.tree[blockIdx.y];
+  const SigmaPack sp = sigma_pack(q);
+  uint32_t count = blockDim.x >> 2;  // nodes of this block at the current level
+  const uint64_t gnode = (uint64_t)blockIdx.x * count + node;
+  const bool valid = gnode < a.first_count;
+  {
+    // message of node gnode = its two children, 16 consecutive words in the child level
+    const uint64_t* child = tree + (a.off[0] + 2 * gnode) * 8;
+    if (valid) {
+      uint4 v0 = reinterpret_cast<const uint4*>(child)[2 * q];
+      uint4 v1 = reinterpret_cast<const uint4*>(child)[2 * q + 1];
+      msg[node][4 * q + 0] = (uint64_t)v0.x | ((uint64_t)v0.y << 32);
+      msg[node][4 * q + 1] = (uint64_t)v0.z | ((uint64_t)v0.w << 32);
+      msg[node][4 * q + 2] = (uint64_t)v1.x | ((uint64_t)v1.y << 32);
+      msg[node][4 * q + 3] = (uint64_t)v1.z | ((uint64_t)v1.w << 32);
+    }
+  }
+  __syncthreads();
+  uint64_t hlo = 0, hhi = 0;
+  if (valid) {
+    blake2b_quad(msg[node], 128, q, sp, hlo, hhi);
+    uint64_t* dst = tree + (a.off[1] + gnode) * 8;
+    dst[q] = hlo;
+    dst[4 + q] = hhi;
+  }
+  for (int lev = 1; lev < a.fuse; ++lev) {
+    __syncthreads();  // everyone finished reading msg
+    if (node < (int)count) {
+      msg[node >> 1][(node & 1) * 8 + q] = hlo;
+      msg[node >> 1][(node & 1) * 8 + 4 + q] = hhi;
+    }
+    __syncthreads();
+    count >>= 1;
+    if (node < (int)count) {
+      blake2b_quad(msg[node], 128, q, sp, hlo, hhi);
+      uint64_t gidx = (uint64_t)blockIdx.x * count + node;
+      uint64_t* dst = tree + (a.off[lev + 1] + gidx) * 8;
+      dst[q] = hlo;
+      dst[4 + q] = hhi;
+    }
+  }
+}
+
 // ------------------------------------------------------------- FRI fold
 
 struct FoldArgs {
@@ -456,8 +593,8 @@ hipError_t launch_ntt_dit(fe* const* data, int batch, const fe* tw, int logn, co
   }
   static const int tile_log = [] {
     const char* v = getenv("SG_NTT_TILE_LOG");
-    int t = v ? atoi(v) : 12;
-    return (t == 11 || t == 12) ? t : 12;
+    int t = v ? atoi(v) : 11;
+    return (t == 11 || t == 12) ? t : 11;
   }();
   if (first_b0 >= logn) {
     for (int b = 0; post && b < batch; ++b) {
@@ -502,25 +639,21 @@ hipError_t launch_ntt_dit(fe* const* data, int batch, const fe* tw, int logn, co
 
 uint64_t merkle_tree_digests(uint64_t n) { return 2 * n - 1; }
 
-// Launch plan: while a level has more than kTail digests, hash it with 256-thread
-// blocks and fuse 3 more levels through LDS; the rest of the tree (<= kTail
-// digests at its first level) is one 1024-thread block that runs to the root,
-// so the latency-bound top of the tree costs one launch.
-constexpr uint64_t kTail = 1024;
 
 hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, int batch, uint64_t n, hipStream_t s) {
   if (batch < 1 || batch > kMaxBatch) return hipErrorInvalidValue;
-  // levels 0..logn, level k has n >> k digests at offset 2n - 2(n >> k)
+  // Launch plan.  Levels 0..logn; level k has n >> k digests at offset 2n - 2(n >> k).
+  //  * leaves: one lane per leaf (decimal + hash); 3 more levels fused through LDS
+  //    when the tree is large enough to be throughput-bound, else the leaf level only;
+  //    a tree of <= 1024 leaves with nothing above runs in one 1024-thread block.
+  //  * node levels with >= kQuadBelow digests: one lane per node, 4 levels fused;
+  //  * smaller levels (latency-bound): a quad of lanes per node, up to 7 levels fused.
+  constexpr uint64_t kQuadBelow = (uint64_t)1 << 16;
   int logn = 0;
   while (((uint64_t)1 << logn) < n) ++logn;
   int level = 0;
   while (level <= logn) {
     uint64_t count = n >> level;
-    const bool tail = count <= kTail;
-    unsigned bs = tail ? (unsigned)count : 256u;
-    int fuse = tail ? (logn - level + 1) : 4;
-    if (level + fuse - 1 > logn) fuse = logn - level + 1;
-    if (fuse < 1 || fuse > kMaxFuse) return hipErrorInvalidValue;
     MerkleArgs a;
     for (int b = 0; b < kMaxBatch; ++b) {
       a.leaves[b] = (level == 0 && b < batch) ? leaves[b] : nullptr;
@@ -528,22 +661,45 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
     }
     a.first_level = level;
     a.first_count = count;
+    int fuse;
+    unsigned bs;
+    int kind;  // 0: leaf 256, 1: leaf tail 1024, 2: node 256, 3: quad
+    if (level == 0) {
+      if (count <= 64) {
+        kind = 1; bs = (unsigned)count; fuse = logn + 1;
+      } else {
+        kind = 0; bs = count < 256 ? (unsigned)count : 256u;
+        fuse = count >= ((uint64_t)1 << 18) ? 4 : 1;
+      }
+    } else if (count >= kQuadBelow) {
+      kind = 2; bs = 256u; fuse = 4;
+    } else {
+      kind = 3;
+      uint64_t nodes = count < 64 ? count : 64;
+      bs = (unsigned)(4 * nodes);
+      int lg = 0;
+      while (((uint64_t)1 << lg) < nodes) ++lg;
+      fuse = lg + 1;
+    }
+    if (level + fuse - 1 > logn) fuse = logn - level + 1;
+    if (fuse < 1 || fuse > kMaxFuse) return hipErrorInvalidValue;
     a.fuse = fuse;
     for (int k = 0; k <= kMaxFuse; ++k) {
       int lv = level - 1 + k;
-      a.off[k] = lv < 0 ? 0 : (2 * n - 2 * (n >> lv));
+      a.off[k] = (lv < 0 || lv > logn) ? 0 : (2 * n - 2 * (n >> lv));
     }
     // algorithmic bytes: leaves read once (16 B) + every digest of these levels written once (64 B)
     uint64_t digests = 0;
     for (int k = 0; k < fuse; ++k) digests += count >> k;
-    ProfScope ps(level == 0 ? "merkle_leaves" : "merkle_nodes", batch * ((level == 0 ? 16 * count : 0) + 64 * digests), s);
-    dim3 grid(nblocks(count, bs), batch);
-    if (level == 0) {
-      if (tail) hipLaunchKernelGGL((k_merkle_levels<true, 1024>), grid, dim3(bs), 0, s, a);
-      else hipLaunchKernelGGL((k_merkle_levels<true, 256>), grid, dim3(bs), 0, s, a);
-    } else {
-      if (tail) hipLaunchKernelGGL((k_merkle_levels<false, 1024>), grid, dim3(bs), 0, s, a);
-      else hipLaunchKernelGGL((k_merkle_levels<false, 256>), grid, dim3(bs), 0, s, a);
+    ProfScope ps(level == 0 ? "merkle_leaves" : (kind == 3 ? "merkle_nodes_quad" : "merkle_nodes"),
+                 batch * ((level == 0 ? 16 * count : 0) + 64 * digests), s);
+    const uint64_t per_block = kind == 3 ? bs / 4 : bs;
+    dim3 grid((unsigned)((count + per_block - 1) / per_block), batch);
+    switch (kind) {
+      case 0: hipLaunchKernelGGL((k_merkle_levels<true, 256>), grid, dim3(bs), 0, s, a); break;
+      case 1: hipLaunchKernelGGL((k_merkle_levels<true, 1024>), grid, dim3(bs), 0, s, a); break;
+      case 2: hipLaunchKernelGGL((k_merkle_levels<false, 256>), grid, dim3(bs), 0, s, a); break;
+      default: hipLaunchKernelGGL(k_merkle_quad, grid, dim3(bs), 0, s, a); break;
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;

@@ -106,10 +106,26 @@ PROTOTYPES = {
 _lib = None
 
 
+def _prefer_torch_runtime():
+    """Load PyTorch's HIP runtime before libstarkgpu's when torch is importable.
+
+    torch ships its own libamdhip64.so.7 / libhsa-runtime64.so.1 with the same
+    sonames as /opt/rocm's; whichever is loaded first serves the whole process.
+    torch only initializes on its own copy, so in a Python process that may
+    also use torch (tests, bench) torch must be loaded first.  Processes that
+    never import torch (e.g. a Rust binary) use /opt/rocm's runtime.
+    """
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
+
+
 def lib():
     """Load libstarkgpu.so once (raises if it was not built)."""
     global _lib
     if _lib is None:
+        _prefer_torch_runtime()
         if not os.path.exists(LIB_PATH):
             raise ImportError(f"{LIB_PATH} not built: run `make -C zk-stark-tutor_amd` "
                               "(or __graft_entry__.build()); there is no CPU fallback")
