@@ -54,6 +54,8 @@ int sg_ctx_trim(sg_ctx* ctx);
  * enable resets the totals; the report is JSON {kernel: {launches, ms, bytes}} where bytes are
  * the algorithmic bytes of the launches; len receives the size incl. the NUL. */
 int sg_ctx_profile(sg_ctx* ctx, int enable);
+/* restrict the timing to launches of one kernel name (NULL or "" = all) to keep event overhead low */
+int sg_ctx_profile_only(sg_ctx* ctx, const char* kernel);
 int sg_ctx_profile_report(sg_ctx* ctx, char* buf, size_t cap, size_t* len);
 
 /* ------------------------------------------------------------ field (field/field.rs) */

@@ -214,6 +214,16 @@ extern "C" int sg_ctx_create(int device, sg_ctx** out) {
     delete ctx;
     return SG_ERR_HIP;
   }
+  void* pinned = nullptr;
+  void* pinned_dev = nullptr;
+  if (hipHostMalloc(&pinned, 4 * 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+      hipHostGetDevicePointer(&pinned_dev, pinned, 0) != hipSuccess) {
+    (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return SG_ERR_HIP;
+  }
+  ctx->pinned_roots = reinterpret_cast<uint64_t*>(pinned);
+  ctx->pinned_roots_dev = reinterpret_cast<uint64_t*>(pinned_dev);
   *out = ctx;
   return SG_OK;
 }
@@ -224,6 +234,7 @@ extern "C" void sg_ctx_destroy(sg_ctx* ctx) {
   ctx->trim();
   for (auto& kv : ctx->pow_tables) (void)hipFree(kv.second.ptr);
   for (auto& kv : ctx->stage_tables) (void)hipFree(kv.second);
+  if (ctx->pinned_roots) (void)hipHostFree(ctx->pinned_roots);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -235,6 +246,10 @@ extern "C" int sg_ctx_profile(sg_ctx* ctx, int enable) {
     ctx->prof.totals.clear();
     ctx->profiling = enable != 0;
   });
+}
+
+extern "C" int sg_ctx_profile_only(sg_ctx* ctx, const char* kernel) {
+  return guard(ctx, [&] { ctx->prof.only = kernel ? kernel : ""; });
 }
 
 extern "C" int sg_ctx_profile_report(sg_ctx* ctx, char* buf, size_t cap, size_t* len) {
@@ -433,11 +448,13 @@ void build_trees(sg_ctx* ctx, const fe* const* d_leaves, int batch, uint64_t n, 
     out[b]->buf = DevBuf(ctx, merkle_tree_digests(n) * 64);
     bufs[b] = out[b]->buf.as<uint64_t>();
   }
-  SG_HIP(launch_merkle_tree(d_leaves, bufs, batch, n, ctx->stream));
-  for (int b = 0; b < batch; ++b)
-    SG_HIP(hipMemcpyAsync(out[b]->root, out[b]->buf.as<uint8_t>() + (2 * n - 2) * 64, 64, hipMemcpyDeviceToHost,
-                          ctx->stream));
+  // the kernel that computes each root also stores it into pinned host memory,
+  // so reading the roots needs only the stream synchronization
+  uint64_t* roots_dev[4] = {nullptr, nullptr, nullptr, nullptr};
+  for (int b = 0; b < batch; ++b) roots_dev[b] = ctx->pinned_roots_dev + 8 * b;
+  SG_HIP(launch_merkle_tree(d_leaves, bufs, batch, n, roots_dev, ctx->stream));
   SG_HIP(hipStreamSynchronize(ctx->stream));
+  for (int b = 0; b < batch; ++b) memcpy(out[b]->root, ctx->pinned_roots + 8 * b, 64);
 }
 
 sg_tree* build_tree(sg_ctx* ctx, const fe* d_leaves, uint64_t n) {
@@ -621,7 +638,8 @@ extern "C" int sg_stream_digest(const sg_stream* s, uint8_t* out, size_t cap, si
 }
 extern "C" int sg_stream_fiat_shamir_prover(const sg_stream* s, size_t num_bytes, uint8_t* out) {
   if (!s || (num_bytes && !out)) return SG_ERR_INVALID;
-  s->s.fiat_shamir(s->s.objects.size(), num_bytes, out);
+  // the incremental sponge cache is not part of the stream's logical state
+  const_cast<sg_stream*>(s)->s.fiat_shamir_all(num_bytes, out);
   return SG_OK;
 }
 extern "C" int sg_stream_fiat_shamir_verifier(const sg_stream* s, size_t num_bytes, uint8_t* out) {

@@ -68,6 +68,9 @@ struct sg_ctx {
   size_t pooled_bytes = 0;
   // power tables keyed by (root limbs, count)
   std::map<std::pair<std::pair<uint64_t, uint64_t>, uint64_t>, sg::PowTable> pow_tables;
+  // host-coherent pinned slots for tree roots (written by the kernel that computes them)
+  uint64_t* pinned_roots = nullptr;      // host view, 4 x 64 bytes
+  uint64_t* pinned_roots_dev = nullptr;  // device view of the same memory
   // per-kernel event timing (sg_ctx_profile)
   bool profiling = false;
   sg::KernelProfiler prof;

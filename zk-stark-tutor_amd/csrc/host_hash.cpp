@@ -18,49 +18,106 @@ static const uint64_t KECCAK_RC[24] = {
     0x000000008000808bull, 0x800000000000008bull, 0x8000000000008089ull, 0x8000000000008003ull,
     0x8000000000008002ull, 0x8000000000000080ull, 0x000000000000800aull, 0x800000008000000aull,
     0x8000000080008081ull, 0x8000000000008080ull, 0x0000000080000001ull, 0x8000000080008008ull};
-static const int KECCAK_ROT[25] = {0, 1, 62, 28, 27, 36, 44, 6, 55, 20, 3, 10, 43,
-                                   25, 39, 41, 45, 15, 21, 8, 18, 2, 61, 56, 14};
 
-static inline uint64_t rotl(uint64_t x, int n) { return n == 0 ? x : (x << n) | (x >> (64 - n)); }
+static inline uint64_t rotl(uint64_t x, int n) { return (x << n) | (x >> ((64 - n) & 63)); }
 
-static void keccak_f1600(uint64_t st[25]) {
+// Unrolled Keccak-f[1600] (lanes a[x + 5y]).
+void keccak_f1600(uint64_t a[25]) {
   for (int round = 0; round < 24; ++round) {
-    uint64_t c[5], d[5], b[25];
-    for (int x = 0; x < 5; ++x) c[x] = st[x] ^ st[x + 5] ^ st[x + 10] ^ st[x + 15] ^ st[x + 20];
-    for (int x = 0; x < 5; ++x) d[x] = c[(x + 4) % 5] ^ rotl(c[(x + 1) % 5], 1);
-    for (int i = 0; i < 25; ++i) st[i] ^= d[i % 5];
-    // rho + pi: b[y, 2x+3y] = rotl(a[x, y], r[x, y])
-    for (int x = 0; x < 5; ++x)
-      for (int y = 0; y < 5; ++y) b[y + 5 * ((2 * x + 3 * y) % 5)] = rotl(st[x + 5 * y], KECCAK_ROT[x + 5 * y]);
-    for (int x = 0; x < 5; ++x)
-      for (int y = 0; y < 5; ++y)
-        st[x + 5 * y] = b[x + 5 * y] ^ ((~b[(x + 1) % 5 + 5 * y]) & b[(x + 2) % 5 + 5 * y]);
-    st[0] ^= KECCAK_RC[round];
+    uint64_t c0 = a[0] ^ a[5] ^ a[10] ^ a[15] ^ a[20];
+    uint64_t c1 = a[1] ^ a[6] ^ a[11] ^ a[16] ^ a[21];
+    uint64_t c2 = a[2] ^ a[7] ^ a[12] ^ a[17] ^ a[22];
+    uint64_t c3 = a[3] ^ a[8] ^ a[13] ^ a[18] ^ a[23];
+    uint64_t c4 = a[4] ^ a[9] ^ a[14] ^ a[19] ^ a[24];
+    uint64_t d0 = c4 ^ rotl(c1, 1), d1 = c0 ^ rotl(c2, 1), d2 = c1 ^ rotl(c3, 1);
+    uint64_t d3 = c2 ^ rotl(c4, 1), d4 = c3 ^ rotl(c0, 1);
+    // theta + rho + pi: b[y, 2x+3y] = rotl(a[x,y] ^ d[x], r[x,y])
+    uint64_t b00 = a[0] ^ d0;
+    uint64_t b10 = rotl(a[6] ^ d1, 44);
+    uint64_t b20 = rotl(a[12] ^ d2, 43);
+    uint64_t b30 = rotl(a[18] ^ d3, 21);
+    uint64_t b40 = rotl(a[24] ^ d4, 14);
+    uint64_t b01 = rotl(a[3] ^ d3, 28);
+    uint64_t b11 = rotl(a[9] ^ d4, 20);
+    uint64_t b21 = rotl(a[10] ^ d0, 3);
+    uint64_t b31 = rotl(a[16] ^ d1, 45);
+    uint64_t b41 = rotl(a[22] ^ d2, 61);
+    uint64_t b02 = rotl(a[1] ^ d1, 1);
+    uint64_t b12 = rotl(a[7] ^ d2, 6);
+    uint64_t b22 = rotl(a[13] ^ d3, 25);
+    uint64_t b32 = rotl(a[19] ^ d4, 8);
+    uint64_t b42 = rotl(a[20] ^ d0, 18);
+    uint64_t b03 = rotl(a[4] ^ d4, 27);
+    uint64_t b13 = rotl(a[5] ^ d0, 36);
+    uint64_t b23 = rotl(a[11] ^ d1, 10);
+    uint64_t b33 = rotl(a[17] ^ d2, 15);
+    uint64_t b43 = rotl(a[23] ^ d3, 56);
+    uint64_t b04 = rotl(a[2] ^ d2, 62);
+    uint64_t b14 = rotl(a[8] ^ d3, 55);
+    uint64_t b24 = rotl(a[14] ^ d4, 39);
+    uint64_t b34 = rotl(a[15] ^ d0, 41);
+    uint64_t b44 = rotl(a[21] ^ d1, 2);
+    // chi (+ iota on lane 0); row y holds b[0..4][y]
+    a[0] = b00 ^ (~b10 & b20) ^ KECCAK_RC[round];
+    a[1] = b10 ^ (~b20 & b30);
+    a[2] = b20 ^ (~b30 & b40);
+    a[3] = b30 ^ (~b40 & b00);
+    a[4] = b40 ^ (~b00 & b10);
+    a[5] = b01 ^ (~b11 & b21);
+    a[6] = b11 ^ (~b21 & b31);
+    a[7] = b21 ^ (~b31 & b41);
+    a[8] = b31 ^ (~b41 & b01);
+    a[9] = b41 ^ (~b01 & b11);
+    a[10] = b02 ^ (~b12 & b22);
+    a[11] = b12 ^ (~b22 & b32);
+    a[12] = b22 ^ (~b32 & b42);
+    a[13] = b32 ^ (~b42 & b02);
+    a[14] = b42 ^ (~b02 & b12);
+    a[15] = b03 ^ (~b13 & b23);
+    a[16] = b13 ^ (~b23 & b33);
+    a[17] = b23 ^ (~b33 & b43);
+    a[18] = b33 ^ (~b43 & b03);
+    a[19] = b43 ^ (~b03 & b13);
+    a[20] = b04 ^ (~b14 & b24);
+    a[21] = b14 ^ (~b24 & b34);
+    a[22] = b24 ^ (~b34 & b44);
+    a[23] = b34 ^ (~b44 & b04);
+    a[24] = b44 ^ (~b04 & b14);
+  }
+}
+
+static const size_t SHAKE_RATE = 136;
+
+void ShakeSponge::absorb_blocks(const uint8_t* in, size_t nblocks) {
+  uint8_t* sb = reinterpret_cast<uint8_t*>(st);  // little-endian lanes (x86 host)
+  for (size_t b = 0; b < nblocks; ++b) {
+    for (size_t i = 0; i < SHAKE_RATE; ++i) sb[i] ^= in[b * SHAKE_RATE + i];
+    keccak_f1600(st);
+  }
+}
+
+void ShakeSponge::finish(const uint8_t* tail, size_t len, uint8_t* out, size_t outlen) const {
+  uint64_t s[25];
+  memcpy(s, st, sizeof(s));
+  uint8_t* sb = reinterpret_cast<uint8_t*>(s);
+  for (size_t i = 0; i < len; ++i) sb[i] ^= tail[i];
+  sb[len] ^= 0x1F;
+  sb[SHAKE_RATE - 1] ^= 0x80;
+  keccak_f1600(s);
+  while (outlen > 0) {
+    size_t k = outlen < SHAKE_RATE ? outlen : SHAKE_RATE;
+    memcpy(out, sb, k);
+    out += k;
+    outlen -= k;
+    if (outlen) keccak_f1600(s);
   }
 }
 
 void shake256(const uint8_t* in, size_t len, uint8_t* out, size_t outlen) {
-  const size_t rate = 136;
-  uint64_t st[25];
-  memset(st, 0, sizeof(st));
-  uint8_t* sb = reinterpret_cast<uint8_t*>(st);  // little-endian lane bytes (x86/AMD host)
-  while (len >= rate) {
-    for (size_t i = 0; i < rate; ++i) sb[i] ^= in[i];
-    keccak_f1600(st);
-    in += rate;
-    len -= rate;
-  }
-  for (size_t i = 0; i < len; ++i) sb[i] ^= in[i];
-  sb[len] ^= 0x1F;
-  sb[rate - 1] ^= 0x80;
-  keccak_f1600(st);
-  while (outlen > 0) {
-    size_t k = outlen < rate ? outlen : rate;
-    memcpy(out, sb, k);
-    out += k;
-    outlen -= k;
-    if (outlen) keccak_f1600(st);
-  }
+  ShakeSponge sp;
+  size_t full = len / SHAKE_RATE;
+  sp.absorb_blocks(in, full);
+  sp.finish(in + full * SHAKE_RATE, len - full * SHAKE_RATE, out, outlen);
 }
 
 // ------------------------------------------------------------ BLAKE2b-512

@@ -265,6 +265,8 @@ struct MerkleArgs {
   uint64_t first_count;     // digests at first_level
   int fuse;                 // levels computed by this launch
   uint64_t off[kMaxFuse + 1];  // digest offsets of levels first_level-1 .. first_level+fuse-1 (off[0] = child level)
+  uint64_t* root_host[kMaxBatch];  // optional host-coherent copy of the root (written by the launch reaching it)
+  uint64_t root_level;             // log2(n): the level whose single digest is the root
 };
 
 template <bool LEAF, int MAXB>
@@ -289,6 +291,8 @@ __global__ __launch_bounds__(MAXB) void k_merkle_levels(MerkleArgs a) {
       blake2b_node(l, r, d);
     }
     st_digest(tree + (a.off[1] + idx) * 8, d);
+    if (a.first_level == a.root_level && a.root_host[blockIdx.y])
+      for (int i = 0; i < 8; ++i) a.root_host[blockIdx.y][i] = d[i];
   }
   uint32_t count = blockDim.x;  // digests of this block at the current level
   for (int lev = 1; lev < a.fuse; ++lev) {
@@ -303,6 +307,8 @@ __global__ __launch_bounds__(MAXB) void k_merkle_levels(MerkleArgs a) {
       blake2b_node(l, r, d);
       uint64_t gidx = (uint64_t)blockIdx.x * count + tid;
       st_digest(tree + (a.off[lev + 1] + gidx) * 8, d);
+      if (a.first_level + lev == a.root_level && a.root_host[blockIdx.y])
+        for (int i = 0; i < 8; ++i) a.root_host[blockIdx.y][i] = d[i];
     }
     __syncthreads();
   }
@@ -426,6 +432,10 @@ __global__ __launch_bounds__(256) void k_merkle_quad(MerkleArgs a) {
     uint64_t* dst = tree + (a.off[1] + gnode) * 8;
     dst[q] = hlo;
     dst[4 + q] = hhi;
+    if (a.first_level == a.root_level && a.root_host[blockIdx.y]) {
+      a.root_host[blockIdx.y][q] = hlo;
+      a.root_host[blockIdx.y][4 + q] = hhi;
+    }
   }
   for (int lev = 1; lev < a.fuse; ++lev) {
     __syncthreads();  // everyone finished reading msg
@@ -441,6 +451,10 @@ __global__ __launch_bounds__(256) void k_merkle_quad(MerkleArgs a) {
       uint64_t* dst = tree + (a.off[lev + 1] + gidx) * 8;
       dst[q] = hlo;
       dst[4 + q] = hhi;
+      if (a.first_level + lev == a.root_level && a.root_host[blockIdx.y]) {
+        a.root_host[blockIdx.y][q] = hlo;
+        a.root_host[blockIdx.y][4 + q] = hhi;
+      }
     }
   }
 }
@@ -640,7 +654,8 @@ hipError_t launch_ntt_dit(fe* const* data, int batch, const fe* tw, int logn, co
 uint64_t merkle_tree_digests(uint64_t n) { return 2 * n - 1; }
 
 
-hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, int batch, uint64_t n, hipStream_t s) {
+hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, int batch, uint64_t n,
+                              uint64_t* const* root_host, hipStream_t s) {
   if (batch < 1 || batch > kMaxBatch) return hipErrorInvalidValue;
   // Launch plan.  Levels 0..logn; level k has n >> k digests at offset 2n - 2(n >> k).
   //  * leaves: one lane per leaf (decimal + hash); 3 more levels fused through LDS
@@ -658,7 +673,9 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
     for (int b = 0; b < kMaxBatch; ++b) {
       a.leaves[b] = (level == 0 && b < batch) ? leaves[b] : nullptr;
       a.tree[b] = b < batch ? tree[b] : nullptr;
+      a.root_host[b] = (root_host && b < batch) ? root_host[b] : nullptr;
     }
+    a.root_level = (uint64_t)logn;
     a.first_level = level;
     a.first_count = count;
     int fuse;

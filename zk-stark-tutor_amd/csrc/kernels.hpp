@@ -15,7 +15,9 @@ hipError_t launch_scale_const(fe* data, uint64_t n, const fe* cst, hipStream_t s
 hipError_t launch_ntt_dit(fe* const* data, int batch, const fe* tw, int logn, const fe* post, int first_b0,
                           hipStream_t s);
 uint64_t merkle_tree_digests(uint64_t n);
-hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, int batch, uint64_t n, hipStream_t s);
+// root_host (optional, per tree): host-coherent 64-byte slots that receive the root
+hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, int batch, uint64_t n,
+                              uint64_t* const* root_host, hipStream_t s);
 hipError_t launch_fri_fold(fe* out, const fe* in, uint64_t half, const fe* Tlo, const fe* Thi, int shift,
                            const fe& K, const fe& Wstride, unsigned grid, hipStream_t s);
 unsigned fri_fold_grid(uint64_t half);

@@ -13,6 +13,8 @@
 namespace sg {
 
 struct KernelProfiler {
+  // empty: every launch; else only launches whose name equals `only`
+  std::string only;
   struct Rec {
     const char* name;
     hipEvent_t a, b;
@@ -64,6 +66,7 @@ struct ProfScope {
   KernelProfiler::Rec r;
   hipStream_t s;
   ProfScope(const char* name, uint64_t bytes, hipStream_t stream) : p(g_prof), s(stream) {
+    if (p && !p->only.empty() && p->only != name) p = nullptr;
     if (p) {
       r.name = name;
       r.bytes = bytes;

@@ -44,6 +44,42 @@ std::vector<uint8_t> serialize_objects(const std::vector<StreamObject>& objs, si
 
 std::vector<uint8_t> Stream::digest(size_t count) const { return serialize_objects(objects, count); }
 
+void Stream::fiat_shamir_all(size_t num_bytes, uint8_t* out) {
+  // header state if all objects are included
+  bool field = fs_field;
+  for (size_t i = fs_objects; i < objects.size(); ++i) field = field || carries_field(objects[i].code, objects[i].payload.size());
+  if (fs_objects == 0 || field != fs_field) {
+    // (re)build: [len u64 BE || prefix] for a signature stream, then header, then objects
+    fs_input.clear();
+    if (signature) {
+      put_be64(fs_input, (uint64_t)prefix.size());
+      fs_input.insert(fs_input.end(), prefix.begin(), prefix.end());
+    }
+    std::vector<uint8_t> d = serialize_objects(objects, objects.size());
+    fs_input.insert(fs_input.end(), d.begin(), d.end());
+    fs_objects = objects.size();
+    fs_field = field;
+    fs_sponge = ShakeSponge();
+    fs_absorbed = 0;
+  } else {
+    for (size_t i = fs_objects; i < objects.size(); ++i) {
+      const StreamObject& o = objects[i];
+      fs_input.push_back(o.code);
+      put_be64(fs_input, (uint64_t)o.payload.size());
+      fs_input.insert(fs_input.end(), o.payload.begin(), o.payload.end());
+    }
+    fs_objects = objects.size();
+  }
+  const size_t rate = 136;
+  size_t full = fs_input.size() / rate;
+  size_t done = fs_absorbed / rate;
+  if (full > done) {
+    fs_sponge.absorb_blocks(fs_input.data() + done * rate, full - done);
+    fs_absorbed = full * rate;
+  }
+  fs_sponge.finish(fs_input.data() + fs_absorbed, fs_input.size() - fs_absorbed, out, num_bytes);
+}
+
 void Stream::fiat_shamir(size_t count, size_t num_bytes, uint8_t* out) const {
   std::vector<uint8_t> d = digest(count);
   if (signature) {

@@ -109,6 +109,10 @@ class Context:
         """Start (resetting totals) or stop per-kernel HIP-event timing."""
         self.check(self._lib.sg_ctx_profile(self.handle, 1 if enable else 0))
 
+    def profile_only(self, kernel: Optional[str]) -> None:
+        """Time only launches of `kernel` (None = all)."""
+        self.check(self._lib.sg_ctx_profile_only(self.handle, (kernel or "").encode()))
+
     def profile_report(self) -> dict:
         """{kernel: {"launches", "ms", "bytes"}} accumulated since profile(True)."""
         import json
