@@ -227,6 +227,15 @@ def main():
     # roofline of the dominant kernel: its algorithmic bytes over its event-timed device time
     name, st = dominant, prof[dominant]
     achieved = st["bytes"] / (st["ms"] * 1e-3) / 1e9
+    # measured HBM bytes per launch of that kernel (rocprofv3 PMC passes on this code, committed under
+    # profiles/; the live bench cannot collect PMC counters itself)
+    traffic, traffic_src = None, None
+    pmc_file = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+    if os.path.exists(pmc_file):
+        pmc = json.load(open(pmc_file))["kernels"].get(name)
+        if pmc:
+            traffic = int(pmc["hbm_bytes_per_launch"])
+            traffic_src = "profiles/r01_pmc_traffic.json (FETCH_SIZE x2 + WRITE_SIZE per launch)"
     phases = {k: {"launches": v["launches"], "ms_per_step": round(v["ms"], 4),
                   "GBps": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["ms"] > 0 else None}
               for k, v in sorted(breakdown.items(), key=lambda kv: -kv[1]["ms"])}
@@ -250,7 +259,8 @@ def main():
                    "codeword_elements_per_step_per_gpu": wl.elements_per_step(),
                    "parallelism": f"replicas x{world} (independent traces, no data-path collective)"},
         "roofline": {"kernel": name, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": None,
+                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "traffic_source": traffic_src,
                      "avg_launch_ms": round(st["ms"] / st["launches"], 4),
                      "launches": st["launches"],
                      "alg_bytes_per_launch": int(st["bytes"] / st["launches"]),

@@ -1,0 +1,52 @@
+#!/usr/bin/env python3
+"""Per-kernel HBM traffic per launch from two rocprofv3 --pmc passes (FETCH_SIZE, WRITE_SIZE).
+
+gfx950 correction (MI355X_MICROARCH.md, HBM): FETCH_SIZE reports half the bytes of a
+wide coalesced streaming read, so read bytes = 2 * FETCH_SIZE * 1024; WRITE_SIZE is
+exact for 16-byte-per-lane streaming stores.  Kernels are keyed by the name the bench
+reports (merkle_leaves = k_merkle_levels<true,...>, ...).
+
+usage: pmc_traffic.py FETCH_CSV WRITE_CSV OUT_JSON
+"""
+import collections
+import csv
+import json
+import sys
+
+ALIASES = [("k_merkle_levels<true", "merkle_leaves"), ("k_merkle_levels<false", "merkle_nodes"),
+           ("k_merkle_quad", "merkle_nodes_quad"), ("k_ntt_pass", "ntt_pass"), ("k_bitrev_gather", "bitrev_gather"),
+           ("k_fri_fold", "fri_fold")]
+
+
+def alias(name):
+    for k, v in ALIASES:
+        if k in name:
+            return v
+    return None
+
+
+def load(fn):
+    out = collections.defaultdict(list)
+    for r in csv.DictReader(open(fn)):
+        a = alias(r["Kernel_Name"])
+        if a:
+            out[a].append(float(r["Counter_Value"]) * 1024.0)
+    return out
+
+
+def main():
+    fetch, write = load(sys.argv[1]), load(sys.argv[2])
+    res = {}
+    for k in sorted(set(fetch) & set(write)):
+        n = min(len(fetch[k]), len(write[k]))
+        rd = 2.0 * sum(fetch[k][:n]) / n
+        wr = sum(write[k][:n]) / n
+        res[k] = {"launches": n, "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
+                  "hbm_bytes_per_launch": rd + wr}
+    json.dump({"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes; read = 2*FETCH_SIZE",
+               "kernels": res}, open(sys.argv[3], "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()
