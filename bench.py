@@ -112,6 +112,62 @@ class Workload:
         return (REGISTERS + 2) * self.N
 
 
+def side_measurements(ctx: sg.Context, device, iters: int = 5) -> dict:
+    """The other two configs BASELINE.json names, timed the same way (inputs in HBM):
+    C2 = 2^22-point forward + inverse NTT; north star = 2^24 LDE (2^21 coefficients) + FRI commit."""
+    out = {}
+    n = 1 << 22
+    x = to_device(synthetic_fe(7, b"c2", n), device)
+    y = torch.empty_like(x)
+    z = torch.empty_like(x)
+    w = sg.primitive_nth_root(n)
+    sg.ntt_dev(w, x.data_ptr(), n, y.data_ptr(), ctx=ctx)
+    sg.intt_dev(w, y.data_ptr(), n, z.data_ptr(), ctx=ctx)
+    assert torch.equal(x, z), "C2 INTT(NTT(x)) != x"
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        sg.ntt_dev(w, x.data_ptr(), n, y.data_ptr(), ctx=ctx)
+        sg.intt_dev(w, y.data_ptr(), n, z.data_ptr(), ctx=ctx)
+    torch.cuda.synchronize(device)
+    t = (time.perf_counter() - t0) / iters
+    out["c2_ntt_fwd_inv_2p22_ms"] = round(t * 1e3, 3)
+    out["c2_ntt_gelem_s"] = round(2 * n / t / 1e9, 3)
+    del x, y, z
+    d, N = 1 << 21, 1 << 24
+    coeffs = to_device(synthetic_fe(8, b"ns", d), device)
+    cw = torch.empty((N, 2), dtype=torch.int64, device=device)
+    wN = sg.primitive_nth_root(N)
+    fri = sg.FRI(sg.generator(), wN, N, EXPANSION, COLINEARITY, ctx=ctx)
+
+    def once():
+        sg.fast_coset_evaluate_dev(wN, N, sg.generator(), coeffs.data_ptr(), d, cw.data_ptr(), ctx=ctx)
+        fri.commit_dev(cw.data_ptr(), N, sg.IndependentProofStream())
+    once()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(max(iters // 2, 1)):
+        once()
+    torch.cuda.synchronize(device)
+    t = (time.perf_counter() - t0) / max(iters // 2, 1)
+    out["north_star_lde_fri_commit_2p24_ms"] = round(t * 1e3, 3)
+    # algorithmic bytes (SURVEY 8(d)): LDE 16(d+N) + sum of Merkle(n) and fold(n) over the FRI rounds
+    rounds, ln, alg = 0, N, 16 * (d + N)
+    while ln > EXPANSION and ln > 4 * COLINEARITY:
+        ln //= 2
+        rounds += 1
+    ln = N
+    for r in range(rounds):
+        alg += 16 * ln + 64 * (2 * ln - 1)
+        if r < rounds - 1:
+            alg += 24 * ln
+        ln //= 2
+    out["north_star_alg_bytes"] = alg
+    out["north_star_hbm_frac"] = round(alg / t / (HBM_PEAK_GBS * 1e9), 4)
+    ctx.trim()
+    return out
+
+
 def cpu_baseline_leg(seconds_budget: float = 15.0):
     """The reference-faithful C restatement (oracle/ref_cpu.c) on one host core, on a bounded sample.
 
@@ -171,6 +227,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--log-trace", type=int, default=LOG_TRACE)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-side", action="store_true", help="skip the C2 NTT and 2^24 north-star side measurements")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -268,6 +325,8 @@ def main():
         "kernels_one_step": phases,  # every launch timed, last warmup step
         "host_phases_ms": {k: round(v / args.steps * 1e3, 3) for k, v in host_phases.items()},
     }
+    if world == 1 and not args.no_side:
+        result["side"] = side_measurements(ctx, device)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline_leg()
     if rank == 0:
