@@ -164,13 +164,14 @@ void check_canonical(const sg_fe* v, size_t n, const char* what) {
     if (!fe_is_canonical(to_fe(v[i]))) throw Error{SG_ERR_NONCANONICAL, std::string(what) + ": element >= p"};
 }
 
-// In-place DIT NTT on a device buffer already holding the bit-reversed (and
-// zero-padded) input.  post = optional Montgomery constant applied at the end.
-void ntt_core(sg_ctx* ctx, fe* const* d_data, int batch, int logn, const fe& root, const fe* post_host,
-              int skip = 0) {
-  uint64_t n = (uint64_t)1 << logn;
+bool ranges_overlap(const fe* a, uint64_t na, const fe* b, uint64_t nb) {
+  return a < b + nb && b < a + na;
+}
+
+// bit-reversal gather (fused into the first pass when large enough) + DIT stages
+void ntt_run(sg_ctx* ctx, fe* const* out, const fe* const* in, int batch, uint64_t n_in, int logn, const fe& root,
+             const fe* sA, const fe* sB, int skip, const fe* post_host) {
   const fe* tw = logn > 0 ? ctx->stage_twiddles(root, logn) : nullptr;
-  (void)n;
   DevBuf dpost;
   const fe* post = nullptr;
   if (post_host) {
@@ -178,7 +179,7 @@ void ntt_core(sg_ctx* ctx, fe* const* d_data, int batch, int logn, const fe& roo
     SG_HIP(hipMemcpyAsync(dpost.get(), post_host, sizeof(fe), hipMemcpyHostToDevice, ctx->stream));
     post = dpost.as<fe>();
   }
-  SG_HIP(launch_ntt_dit(d_data, batch, tw, logn, post, skip, ctx->stream));
+  SG_HIP(launch_ntt_fused(out, in, batch, n_in, logn, tw, sA, sB, skip, post, ctx->stream));
   SG_HIP(hipStreamSynchronize(ctx->stream));
 }
 
@@ -195,9 +196,8 @@ void ntt_dev(sg_ctx* ctx, const fe& root, const fe* d_in, uint64_t n_in, fe* d_o
     fe off4096 = fe_pow(*scale_offset, 4096);
     sB = ctx->pow_table(off4096, (n_in + 4095) / 4096);
   }
-  // n == 1: bit_reverse_copy returns the input unchanged (logn == 0 gather is a copy)
-  SG_HIP(launch_bitrev_gather(&d_out, &d_in, 1, n_in, logn, sA, sB, 0, ctx->stream));
-  ntt_core(ctx, &d_out, 1, logn, root, post);
+  SG_REQUIRE(!ranges_overlap(d_in, n_in, d_out, n), "ntt: output must not alias the input");
+  ntt_run(ctx, &d_out, &d_in, 1, n_in, logn, root, sA, sB, 0, post);
 }
 
 }  // namespace
@@ -345,11 +345,12 @@ void coset_evaluate_batch(sg_ctx* ctx, const fe& generator, uint64_t root_order,
   const fe* sA = ctx->pow_table(off, 4096);
   const fe* sB = ctx->pow_table(fe_pow(off, 4096), (std::max<uint64_t>(d, 1) + 4095) / 4096);
   // coefficients occupy the first d of n slots: the first `skip` DIT stages
-  // are exact copies (k_bitrev_gather) when d <= n >> skip
+  // are exact copies (replicated by the gather / first pass) when d <= n >> skip
   int skip = 0;
   while (skip < logn && ((uint64_t)std::max<uint64_t>(d, 1) << (skip + 1)) <= n) ++skip;
-  SG_HIP(launch_bitrev_gather(out, in, batch, d, logn, sA, sB, skip, ctx->stream));
-  ntt_core(ctx, out, batch, logn, generator, nullptr, skip);
+  for (int b = 0; b < batch; ++b)
+    SG_REQUIRE(!ranges_overlap(in[b], d, out[b], n), "fast_coset_evaluate: output must not alias the input");
+  ntt_run(ctx, out, in, batch, d, logn, generator, sA, sB, skip, nullptr);
 }
 }  // namespace
 

@@ -124,7 +124,9 @@ struct PassArgs {
   int logC;            // columns per tile (consecutive low-bit indices), C <= 2^b0
 };
 
-template <int R>
+// COLK: the tile's columns are consecutive low index bits (they enter the twiddle
+// index k); false when the columns are independent transforms' tiles (first pass).
+template <int R, bool COLK = true>
 __device__ __forceinline__ void radix_step(fe* lds, const PassArgs& a, int t, uint64_t lowbase) {
   const int logC = a.logC;
   const uint32_t C = 1u << logC;
@@ -138,7 +140,7 @@ __device__ __forceinline__ void radix_step(fe* lds, const PassArgs& a, int t, ui
     fe x[1 << R];
 #pragma unroll
     for (int m = 0; m < (1 << R); ++m) x[m] = lds[((g0 + ((uint32_t)m << t)) << logC) + c];
-    const uint64_t low = lowbase + c;  // cb*C + c: index bits below b0
+    const uint64_t low = COLK ? lowbase + c : 0;  // cb*C + c: index bits below b0
 #pragma unroll
     for (int u = 0; u < R; ++u) {
       const int S = a.b0 + t + u + 1;  // global stage, 1-based
@@ -221,6 +223,78 @@ __global__ __launch_bounds__(256) void k_ntt_pass(PassArgs a) {
       if (post) v = mont_mul(v, pc);
       st_fe(data + base + ((uint64_t)g << a.b0) + c, v);
     }
+  }
+}
+
+// First pass with the bit-reversal fused in (fft/ntt.rs:14 bit_reverse_copy).
+// Positions j = h*2^L + t of the bit-reversed array hold x[rev_m(j)] =
+// x[rev_{m-L}(h) + rev_L(t) * 2^(m-L)], so the C = 2^logC tiles whose
+// c = rev_{m-L}(h) are consecutive read C-element runs of x per row u = rev_L(t).
+// Rows past n_in are zero; with skip leading trivial stages (n_in <= n >> skip)
+// only rows u < 2^(L-skip) can be non-zero and each lands replicated on 2^skip
+// positions (a butterfly (a, 0) is (a, a) exactly).  Optional LDE scale by
+// offset^index (Montgomery tables sA/sB).  Stages skip+1..L then run in LDS and
+// every tile is written back as one contiguous 2^L run.
+struct FirstArgs {
+  fe* out[kMaxBatch];
+  const fe* in[kMaxBatch];
+  const fe* tw;
+  const fe* sA;
+  const fe* sB;
+  uint64_t n_in;
+  int logn;
+  int L;
+  int logC;
+  int skip;
+};
+
+template <int TL>
+__global__ __launch_bounds__(256) void k_ntt_first(FirstArgs a) {
+  extern __shared__ fe lds[];
+  const int L = a.L, logC = a.logC, m = a.logn;
+  const uint32_t C = 1u << logC;
+  const int skip = a.skip < L ? a.skip : L;
+  // XCD-aware: workgroups are dealt round-robin to the 8 XCDs, so give each XCD
+  // a contiguous range of column groups; neighbouring C-runs then share its L2
+  uint32_t bx = blockIdx.x;
+  if ((gridDim.x & 7) == 0) bx = (bx & 7) * (gridDim.x >> 3) + (bx >> 3);
+  const uint64_t c0 = (uint64_t)bx << logC;
+  const fe* __restrict__ in = a.in[blockIdx.y];
+  fe* __restrict__ out = a.out[blockIdx.y];
+  const uint32_t rows = 1u << (L - skip);
+  const uint32_t rep = 1u << skip;
+  for (uint32_t l = threadIdx.x; l < rows * C; l += blockDim.x) {
+    const uint32_t k = l & (C - 1), u = l >> logC;
+    const uint64_t idx = c0 + k + ((uint64_t)u << (m - L));
+    fe v = fe_zero();
+    if (idx < a.n_in) {
+      v = ld_fe(in + idx);
+      if (a.sA) v = mont_mul(v, mont_mul(ld_fe(a.sA + (idx & 4095)), ld_fe(a.sB + (idx >> 12))));
+    }
+    const uint32_t t = __builtin_bitreverse32(u) >> (32 - L);
+    for (uint32_t r = 0; r < rep; ++r) lds[((t + r) << logC) + k] = v;
+  }
+  __syncthreads();
+  PassArgs pa;
+  pa.tw = a.tw;
+  pa.post = nullptr;
+  pa.logn = m;
+  pa.b0 = 0;
+  pa.L = L;
+  pa.logC = logC;
+  int t = skip;
+  while (t < L) {
+    int rem = L - t;
+    if (rem >= 3) { radix_step<3, false>(lds, pa, t, 0); t += 3; }
+    else if (rem == 2) { radix_step<2, false>(lds, pa, t, 0); t += 2; }
+    else { radix_step<1, false>(lds, pa, t, 0); t += 1; }
+  }
+  const uint32_t tile = 1u << (L + logC);
+  for (uint32_t l = threadIdx.x; l < tile; l += blockDim.x) {
+    const uint32_t tt = l & ((1u << L) - 1), k = l >> L;
+    const uint64_t c = c0 + k;
+    const uint64_t h = __builtin_bitreverse64(c) >> (64 - (m - L));
+    st_fe(out + (h << L) + tt, lds[(tt << logC) + k]);
   }
 }
 
@@ -649,6 +723,48 @@ hipError_t launch_ntt_dit(fe* const* data, int batch, const fe* tw, int logn, co
     b0 += a.L;
   }
   return hipSuccess;
+}
+
+// Whole transform: fused bit-reversal first pass (when logn leaves room for a
+// later pass), then launch_ntt_dit from stage L1 + 1.  `out` must not alias `in`.
+hipError_t launch_ntt_fused(fe* const* out, const fe* const* in, int batch, uint64_t n_in, int logn, const fe* tw,
+                            const fe* sA, const fe* sB, int skip, const fe* post, hipStream_t s) {
+  if (batch < 1 || batch > kMaxBatch) return hipErrorInvalidValue;
+  static bool lds_attr = false;
+  if (!lds_attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)k_ntt_first<11>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+    if (e != hipSuccess) return e;
+    lds_attr = true;
+  }
+  constexpr int TL = 11, LOGC1 = 2, L1 = TL - LOGC1;
+  if (logn <= L1 + LOGC1 || logn - L1 > 63) {
+    hipError_t e = launch_bitrev_gather(out, in, batch, n_in, logn, sA, sB, skip, s);
+    if (e != hipSuccess) return e;
+    return launch_ntt_dit(out, batch, tw, logn, post, skip, s);
+  }
+  FirstArgs a;
+  for (int b = 0; b < kMaxBatch; ++b) {
+    a.out[b] = b < batch ? out[b] : nullptr;
+    a.in[b] = b < batch ? in[b] : nullptr;
+  }
+  a.tw = tw;
+  a.sA = sA;
+  a.sB = sB;
+  a.n_in = n_in;
+  a.logn = logn;
+  a.L = L1;
+  a.logC = LOGC1;
+  a.skip = skip;
+  uint64_t n = (uint64_t)1 << logn;
+  {
+    ProfScope ps("ntt_first", batch * (16 * (n_in < n ? n_in : n) + 16 * n), s);
+    hipLaunchKernelGGL(k_ntt_first<TL>, dim3((unsigned)(n >> TL), batch), dim3(256), (size_t)16 << TL, s, a);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  // trivial stages beyond L1 are not replicated across tiles: later passes run
+  // them as real butterflies on zeros, (a, 0) -> (a, a), which is exact
+  return launch_ntt_dit(out, batch, tw, logn, post, L1, s);
 }
 
 uint64_t merkle_tree_digests(uint64_t n) { return 2 * n - 1; }

@@ -14,6 +14,9 @@ hipError_t launch_bitrev_gather(fe* const* out, const fe* const* in, int batch, 
 hipError_t launch_scale_const(fe* data, uint64_t n, const fe* cst, hipStream_t s);
 hipError_t launch_ntt_dit(fe* const* data, int batch, const fe* tw, int logn, const fe* post, int first_b0,
                           hipStream_t s);
+// bit-reversal (+ LDE scale, + `skip` trivial stages) fused into the first pass; out must not alias in
+hipError_t launch_ntt_fused(fe* const* out, const fe* const* in, int batch, uint64_t n_in, int logn, const fe* tw,
+                            const fe* sA, const fe* sB, int skip, const fe* post, hipStream_t s);
 uint64_t merkle_tree_digests(uint64_t n);
 // root_host (optional, per tree): host-coherent 64-byte slots that receive the root
 hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, int batch, uint64_t n,
