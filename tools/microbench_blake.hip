@@ -47,6 +47,17 @@ __device__ __forceinline__ uint64_t rotr_pm(uint64_t x, int n) {
   return rotr_ab(x, n);
 }
 
+// ---- variant 4: alignbit for 16/24, rotl1 via lshl_add_u64 for 63
+__device__ __forceinline__ uint64_t rotr_ab1(uint64_t x, int n) {
+  if (n == 63) {
+    uint64_t t = (uint64_t)((uint32_t)(x >> 32) >> 31);
+    uint64_t r;
+    asm("v_lshl_add_u64 %0, %1, 1, %2" : "=v"(r) : "v"(x), "v"(t));
+    return r;
+  }
+  return rotr_ab(x, n);
+}
+
 #define G(R, a, b, c, d, x, y) \
   a = a + b + (x); d = R(d ^ a, 32); c = c + d; b = R(b ^ c, 24); \
   a = a + b + (y); d = R(d ^ a, 16); c = c + d; b = R(b ^ c, 63);
@@ -84,6 +95,7 @@ __global__ __launch_bounds__(256) void k_blake(uint64_t* out, uint64_t seed) {
     if (V == 0) { COMPRESS(rotr_c) }
     else if (V == 1) { COMPRESS(rotr_ab) }
     else if (V == 2) { COMPRESS(rotr_pm) }
+    else if (V == 4) { COMPRESS(rotr_ab1) }
     else { COMPRESS(rotr_pm2) }
     // rotate message words so the next compression depends on this one
     uint64_t t = m[0]; for (int i = 0; i < 15; ++i) m[i] = m[i + 1]; m[15] = t;
@@ -117,7 +129,8 @@ int main() {
   run<1>("alignbit", ref);
   run<2>("perm", ref);
   run<3>("perm+rotl1", ref);
+  run<4>("ab+rotl1", ref);
   run<1>("alignbit", ref);
-  run<3>("perm+rotl1", ref);
+  run<4>("ab+rotl1", ref);
   return 0;
 }

@@ -124,6 +124,89 @@ __global__ void k_pk_fma_f32(uint32_t* out, uint32_t seed) {
   float s = 0; for (int i = 0; i < 8; ++i) s += a[i].x + a[i].y; out[blockIdx.x * blockDim.x + threadIdx.x] = (uint32_t)s;
 }
 
+
+#define K1(NAME, ASMSTR) \
+__global__ void NAME(uint32_t* out, uint32_t seed) { \
+  uint32_t a[8]; for (int i = 0; i < 8; ++i) a[i] = seed + threadIdx.x + i; \
+  uint32_t b = seed * 3 + 1, c = seed ^ 0x0c0d0e0f; \
+  for (int it = 0; it < ITERS; ++it) { \
+    _Pragma("unroll") for (int i = 0; i < 8; ++i) asm volatile(ASMSTR : "+v"(a[i]) : "v"(b), "v"(c)); \
+  } \
+  uint32_t s = 0; for (int i = 0; i < 8; ++i) s ^= a[i]; out[blockIdx.x * blockDim.x + threadIdx.x] = s; }
+K1(k_perm, "v_perm_b32 %0, %0, %1, %2")
+K1(k_xor, "v_xor_b32 %0, %0, %1")
+K1(k_xor_e64, "v_xor_b32_e64 %0, %0, %1")
+K1(k_add_e64, "v_add_u32_e64 %0, %0, %1")
+K1(k_lshl_e64, "v_lshlrev_b32_e64 %0, 7, %0")
+K1(k_and_or, "v_and_or_b32 %0, %0, %1, %2")
+K1(k_sub_u32, "v_sub_u32 %0, %1, %0")
+K1(k_mov_dpp, "v_mov_b32_dpp %0, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf")
+K1(k_add_sdwa, "v_add_u32_sdwa %0, %0, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD")
+K1(k_pk_add_u16, "v_pk_add_u16 %0, %0, %1")
+K1(k_lshl_or, "v_lshl_or_b32 %0, %0, 1, %1")
+K1(k_add3, "v_add3_u32 %0, %0, %1, %2")
+K1(k_lshr, "v_lshrrev_b32 %0, 7, %0")
+K1(k_alignbyte, "v_alignbyte_b32 %0, %0, %1, 3")
+K1(k_xad, "v_xad_u32 %0, %0, %1, %2")
+__global__ void k_add64_pair(uint32_t* out, uint32_t seed) {
+  // 64-bit add as co/addc pairs with a distinct SGPR-pair carry per chain
+  uint32_t lo[8], hi[8]; for (int i = 0; i < 8; ++i) { lo[i] = seed + threadIdx.x + i; hi[i] = i; }
+  uint32_t bl = seed * 3 + 1, bh = seed;
+  for (int it = 0; it < ITERS; ++it) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      uint64_t cy;
+      asm volatile("v_add_co_u32 %0, %2, %0, %3\n v_addc_co_u32 %1, %2, %1, %4, %2" : "+v"(lo[i]), "+v"(hi[i]), "=&s"(cy) : "v"(bl), "v"(bh));
+    }
+  }
+  uint32_t s = 0; for (int i = 0; i < 8; ++i) s ^= lo[i] ^ hi[i]; out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+__global__ void k_lshlrev64(uint32_t* out, uint32_t seed) {
+  uint64_t a[8]; for (int i = 0; i < 8; ++i) a[i] = seed + threadIdx.x + i;
+  for (int it = 0; it < ITERS; ++it) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) asm volatile("v_lshlrev_b64 %0, 1, %0" : "+v"(a[i]));
+  }
+  uint64_t s = 0; for (int i = 0; i < 8; ++i) s ^= a[i]; out[blockIdx.x * blockDim.x + threadIdx.x] = (uint32_t)(s ^ (s >> 32));
+}
+__global__ void k_mix_xor_perm(uint32_t* out, uint32_t seed) {
+  // interleaved xor + perm (dual-issue check)
+  uint32_t a[8]; for (int i = 0; i < 8; ++i) a[i] = seed + threadIdx.x + i;
+  uint32_t b = seed * 3 + 1, c = seed ^ 0x0c0d0e0f;
+  for (int it = 0; it < ITERS; ++it) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (i & 1) asm volatile("v_perm_b32 %0, %0, %1, %2" : "+v"(a[i]) : "v"(b), "v"(c));
+      else asm volatile("v_xor_b32 %0, %0, %1" : "+v"(a[i]) : "v"(b));
+    }
+  }
+  uint32_t s = 0; for (int i = 0; i < 8; ++i) s ^= a[i]; out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+__global__ void k_mix_xor_align(uint32_t* out, uint32_t seed) {
+  uint32_t a[8]; for (int i = 0; i < 8; ++i) a[i] = seed + threadIdx.x + i;
+  uint32_t b = seed * 3 + 1;
+  for (int it = 0; it < ITERS; ++it) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (i & 1) asm volatile("v_alignbit_b32 %0, %0, %1, 24" : "+v"(a[i]) : "v"(b));
+      else asm volatile("v_xor_b32 %0, %0, %1" : "+v"(a[i]) : "v"(b));
+    }
+  }
+  uint32_t s = 0; for (int i = 0; i < 8; ++i) s ^= a[i]; out[blockIdx.x * blockDim.x + threadIdx.x] = s;
+}
+__global__ void k_mix_xor_lshladd(uint32_t* out, uint32_t seed) {
+  uint64_t a[8]; for (int i = 0; i < 8; ++i) a[i] = seed + threadIdx.x + i;
+  uint64_t b = seed * 3ull + 1;
+  for (int it = 0; it < ITERS; ++it) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      if (i & 1) asm volatile("v_lshl_add_u64 %0, %0, 0, %1" : "+v"(a[i]) : "v"(b));
+      else asm volatile("v_xor_b32 %0, %0, %1" : "+v"(((uint32_t*)&a[i])[0]) : "v"((uint32_t)b));
+    }
+  }
+  uint64_t s = 0; for (int i = 0; i < 8; ++i) s ^= a[i]; out[blockIdx.x * blockDim.x + threadIdx.x] = (uint32_t)(s ^ (s >> 32));
+}
+
 typedef void (*kfn)(uint32_t*, uint32_t);
 static int run(const char* name, kfn k, int instr_per_step) {
   const int threads = 256, blocks = 256 * 8;
@@ -156,5 +239,25 @@ int main() {
   run("v_bitop3_b32", k_xor3, 1);
   run("v_fma_f64", k_fma_f64, 1);
   run("v_pk_fma_f32", k_pk_fma_f32, 1);
+  run("v_perm_b32", k_perm, 1);
+  run("v_xor_b32", k_xor, 1);
+  run("v_xor_b32_e64", k_xor_e64, 1);
+  run("v_add_u32_e64", k_add_e64, 1);
+  run("v_lshlrev_b32_e64", k_lshl_e64, 1);
+  run("v_and_or_b32", k_and_or, 1);
+  run("v_sub_u32", k_sub_u32, 1);
+  run("v_mov_b32_dpp", k_mov_dpp, 1);
+  run("v_add_u32_sdwa", k_add_sdwa, 1);
+  run("v_pk_add_u16", k_pk_add_u16, 1);
+  run("v_lshl_or_b32", k_lshl_or, 1);
+  run("v_add3_u32", k_add3, 1);
+  run("v_lshrrev_b32", k_lshr, 1);
+  run("v_alignbyte_b32", k_alignbyte, 1);
+  run("v_xad_u32", k_xad, 1);
+  run("add64 pair(sgpr)", k_add64_pair, 2);
+  run("v_lshlrev_b64", k_lshlrev64, 1);
+  run("xor+perm mix", k_mix_xor_perm, 1);
+  run("xor+alignbit mix", k_mix_xor_align, 1);
+  run("xor+lshladd mix", k_mix_xor_lshladd, 1);
   return 0;
 }

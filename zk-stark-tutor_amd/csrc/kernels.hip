@@ -599,6 +599,12 @@ __global__ void k_gather_fe_ptrs(const uint64_t* __restrict__ addrs, fe* __restr
 
 // ------------------------------------------------------------- launchers
 
+// tuning knob from the environment (plan experiments); `def` when unset
+static int env_int(const char* name, int def) {
+  const char* v = getenv(name);
+  return v && *v ? atoi(v) : def;
+}
+
 hipError_t launch_gather_digest_ptrs(const uint64_t* addrs, uint64_t* out, uint32_t count, hipStream_t s) {
   if (!count) return hipSuccess;
   ProfScope ps("gather_digests", 128ull * count, s);
@@ -680,8 +686,7 @@ hipError_t launch_ntt_dit(fe* const* data, int batch, const fe* tw, int logn, co
     lds_attr = true;
   }
   static const int tile_log = [] {
-    const char* v = getenv("SG_NTT_TILE_LOG");
-    int t = v ? atoi(v) : 11;
+    int t = env_int("SG_NTT_TILE_LOG", 11);
     return (t == 11 || t == 12) ? t : 11;
   }();
   if (first_b0 >= logn) {
@@ -774,8 +779,9 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
                               uint64_t* const* root_host, hipStream_t s) {
   if (batch < 1 || batch > kMaxBatch) return hipErrorInvalidValue;
   // Launch plan.  Levels 0..logn; level k has n >> k digests at offset 2n - 2(n >> k).
-  //  * leaves: one lane per leaf (decimal + hash); 3 more levels fused through LDS
-  //    when the tree is large enough to be throughput-bound, else the leaf level only;
+  //  * leaves: one lane per leaf (decimal + hash) in 512-lane blocks; 3 more levels
+  //    fused through LDS (512 -> 64 lanes: every active wave full) when the tree is
+  //    large enough to be throughput-bound, else the leaf level only;
   //    a tree of <= 1024 leaves with nothing above runs in one 1024-thread block.
   //  * node levels with >= kQuadBelow digests: one lane per node, 4 levels fused;
   //  * smaller levels (latency-bound): a quad of lanes per node, up to 7 levels fused.
@@ -796,16 +802,22 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
     a.first_count = count;
     int fuse;
     unsigned bs;
-    int kind;  // 0: leaf 256, 1: leaf tail 1024, 2: node 256, 3: quad
+    int kind;  // 0: leaf 256, 1: leaf tail 1024, 2: node 256, 3: quad, 4: leaf 512
     if (level == 0) {
       if (count <= 64) {
         kind = 1; bs = (unsigned)count; fuse = logn + 1;
       } else {
-        kind = 0; bs = count < 256 ? (unsigned)count : 256u;
-        fuse = count >= ((uint64_t)1 << 18) ? 4 : 1;
+        static const int env_bs = env_int("SG_MERKLE_LEAF_BS", 512);
+        static const int env_fuse = env_int("SG_MERKLE_LEAF_FUSE", 4);
+        unsigned lbs = env_bs == 512 ? 512u : 256u;
+        kind = lbs == 512 ? 4 : 0;
+        bs = count < lbs ? (unsigned)count : lbs;
+        fuse = count >= ((uint64_t)1 << 18) ? env_fuse : 1;
+        if (bs < lbs) kind = 0;
       }
     } else if (count >= kQuadBelow) {
-      kind = 2; bs = 256u; fuse = 4;
+      static const int env_nfuse = env_int("SG_MERKLE_NODE_FUSE", 4);
+      kind = 2; bs = 256u; fuse = env_nfuse;
     } else {
       kind = 3;
       uint64_t nodes = count < 64 ? count : 64;
@@ -832,6 +844,7 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
       case 0: hipLaunchKernelGGL((k_merkle_levels<true, 256>), grid, dim3(bs), 0, s, a); break;
       case 1: hipLaunchKernelGGL((k_merkle_levels<true, 1024>), grid, dim3(bs), 0, s, a); break;
       case 2: hipLaunchKernelGGL((k_merkle_levels<false, 256>), grid, dim3(bs), 0, s, a); break;
+      case 4: hipLaunchKernelGGL((k_merkle_levels<true, 512>), grid, dim3(bs), 0, s, a); break;
       default: hipLaunchKernelGGL(k_merkle_quad, grid, dim3(bs), 0, s, a); break;
     }
     hipError_t e = hipGetLastError();

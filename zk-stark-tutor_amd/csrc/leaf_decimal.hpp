@@ -19,19 +19,21 @@
 
 namespace sg {
 
+// 4 decimal digits of v (< 10^4) as ASCII, most significant digit in byte 0.
+// Two-lane SWAR: t = (v / 100) | (v % 100) << 16, then one multiply splits both
+// 2-digit lanes into tens/ones ((x * 103) >> 10 == x / 10 for x < 100).
+__host__ __device__ __forceinline__ uint32_t ascii4(uint32_t v) {
+  uint32_t a = (v * 5243u) >> 19;  // v / 100 for v < 10^4
+  uint32_t t = a | ((v - a * 100u) << 16);
+  uint32_t tens = ((t * 103u) >> 10) & 0x000F000Fu;
+  uint32_t ones = t - tens * 10u;
+  return tens | (ones << 8) | 0x30303030u;
+}
+
 // 8 decimal digits of c (< 10^8) as ASCII, most significant digit in byte 0.
 __host__ __device__ __forceinline__ uint64_t ascii8(uint32_t c) {
   uint32_t hi4 = c / 10000u;
-  uint32_t lo4 = c - hi4 * 10000u;
-  uint32_t a = hi4 / 100u, b = hi4 - a * 100u;   // digits 0-1, 2-3
-  uint32_t d = lo4 / 100u, e = lo4 - d * 100u;   // digits 4-5, 6-7
-  uint32_t a1 = a / 10u, a0 = a - a1 * 10u;
-  uint32_t b1 = b / 10u, b0 = b - b1 * 10u;
-  uint32_t d1 = d / 10u, d0 = d - d1 * 10u;
-  uint32_t e1 = e / 10u, e0 = e - e1 * 10u;
-  uint32_t w0 = a1 | (a0 << 8) | (b1 << 16) | (b0 << 24);
-  uint32_t w1 = d1 | (d0 << 8) | (e1 << 16) | (e0 << 24);
-  return ((uint64_t)(w0 | 0x30303030u)) | ((uint64_t)(w1 | 0x30303030u) << 32);
+  return (uint64_t)ascii4(hi4) | ((uint64_t)ascii4(c - hi4 * 10000u) << 32);
 }
 
 // number of decimal digits of c (c < 10^8), 1 for c == 0
@@ -85,12 +87,13 @@ __host__ __device__ __forceinline__ uint32_t fe_decimal_words(const fe& a, uint6
   }
   c[0] = l0;  // < 2^128 / 10^32 < 3.5e6
   // length: 8 digits per chunk below the first non-zero chunk
-  uint32_t len;
-  if (c[0]) len = 32 + ndigits8(c[0]);
-  else if (c[1]) len = 24 + ndigits8(c[1]);
-  else if (c[2]) len = 16 + ndigits8(c[2]);
-  else if (c[3]) len = 8 + ndigits8(c[3]);
-  else len = ndigits8(c[4]);
+  // (select the leading chunk first so ndigits8 is evaluated once)
+  uint32_t lead = c[4], base = 0;
+  if (c[3]) { lead = c[3]; base = 8; }
+  if (c[2]) { lead = c[2]; base = 16; }
+  if (c[1]) { lead = c[1]; base = 24; }
+  if (c[0]) { lead = c[0]; base = 32; }
+  uint32_t len = base + ndigits8(lead);
   // 40-byte zero-padded string as ten LE 32-bit words
   uint32_t w[11];
 #pragma unroll
