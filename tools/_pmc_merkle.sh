@@ -1,0 +1,6 @@
+set -e
+cd /tmp && export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+timeout -k 10 120 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE -d $R/gpurun_out/pmcm1 -o run -- python3 $R/tools/bench_merkle.py 23 3 > $R/gpurun_out/pmcm1.log 2>&1
+timeout -k 10 120 rocprofv3 --kernel-trace --pmc SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_WAVES SQ_THREAD_CYCLES_VALU -d $R/gpurun_out/pmcm2 -o run -- python3 $R/tools/bench_merkle.py 23 3 > $R/gpurun_out/pmcm2.log 2>&1
+timeout -k 10 120 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU_INT SQ_INSTS_VALU_IOPS SQ_INST_LEVEL_LDS SQ_LEVEL_WAVES SQ_INSTS_VMEM_WR SQ_IFETCH -d $R/gpurun_out/pmcm3 -o run -- python3 $R/tools/bench_merkle.py 23 3 > $R/gpurun_out/pmcm3.log 2>&1
