@@ -168,6 +168,47 @@ void sg_fri_state_free(sg_ctx* ctx, sg_fri_state* st);
 int sg_fri_sample_indices(const uint8_t* seed, size_t seed_len, size_t size, size_t reduced_size,
                           size_t number, size_t* out);
 
+
+/* ------------------------------------------------ row-sharded blocks (multi-GPU)
+ * the four-step NTT, the sharded Merkle commit and the FRI fold
+ * over a codeword distributed as runs.  The reference is single-threaded and has
+ * no counterpart; these are the local steps a multi-GPU Rust caller (or
+ * starkgpu/dist.py) composes around one all-to-all and per-tree all-gathers.
+ * Shards are row-major arrays of canonical elements in device memory. */
+typedef struct sg_forest sg_forest; /* `runs` Merkle trees of `run` leaves each */
+
+/* `rows` independent ntt()s (fft/ntt.rs:7-49 per row): row r reads n_in elements at
+ * d_in + r*n_in (zero-padded to n) and writes n at d_out + r*n.  Output must not
+ * alias the input. */
+int sg_ntt_rows_dev(sg_ctx* ctx, sg_fe root, const sg_fe* d_in, size_t n_in, size_t rows,
+                    sg_fe* d_out, size_t n);
+/* d[i] *= c for i < n (the n^-1 of an inverse transform, fft/ntt.rs:62-67) */
+int sg_scale_dev(sg_ctx* ctx, sg_fe* d_data, size_t n, sg_fe c);
+/* d[r][c] *= base^((a0 + a1 r) c + b0 + b1 r), exponents < 2^36: four-step twiddles
+ * omega^(j1 k2) and the coset scale offset^j (field/polynomial.rs:109-121) */
+int sg_mul_pow_dev(sg_ctx* ctx, sg_fe base, sg_fe* d_data, size_t rows, size_t cols,
+                   uint64_t a0, uint64_t a1, uint64_t b0, uint64_t b1);
+/* out[b][a][c] = in[a][b][c] for an A x B x C array */
+int sg_transpose_dev(sg_ctx* ctx, const sg_fe* d_in, sg_fe* d_out, size_t A, size_t B, size_t C);
+/* merkle_root.rs:21-32 on each of `runs` consecutive runs of `run` leaves (retained) */
+int sg_merkle_forest_dev(sg_ctx* ctx, const sg_fe* d_leaves, size_t run, size_t runs, sg_forest** out);
+/* the runs' roots, 64 bytes each, into device memory (runs x 64 bytes) */
+int sg_forest_roots_dev(sg_ctx* ctx, const sg_forest* f, uint8_t* d_roots);
+/* merkle_root.rs:34-53 path of leaf `index` inside tree `tree` of the forest */
+int sg_forest_open(sg_ctx* ctx, const sg_forest* f, size_t tree, size_t index, uint8_t* path,
+                   size_t* path_len);
+void sg_forest_free(sg_ctx* ctx, sg_forest* f);
+/* merkle_root.rs:7-19 node levels over n given digests (device, n x 64 bytes): the
+ * top of a tree whose lower levels are the runs' subtrees.  Root via sg_tree_root. */
+int sg_merkle_top_dev(sg_ctx* ctx, const uint8_t* d_digests, size_t n, sg_tree** out);
+/* fri.rs:151-159 fold of a run-sharded codeword of global length n_global with this
+ * round's omega / offset and alpha: local element l is global index
+ * (l / run) * run_stride + run_off + l % run and its partner (global + n_global/2)
+ * must be local l + n_local/2.  Writes n_local/2 elements. */
+int sg_fri_fold_runs_dev(sg_ctx* ctx, sg_fe omega, sg_fe offset, sg_fe alpha, const sg_fe* d_in,
+                         size_t n_local, size_t run, size_t run_stride, size_t run_off,
+                         size_t n_global, sg_fe* d_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,240 @@
+"""GPU tests of the row-sharded C ABI and the multi-GPU driver (starkgpu/dist.py).
+
+* the new entry points (sg_ntt_rows_dev, sg_mul_pow_dev, sg_transpose_dev,
+  sg_merkle_forest_dev / sg_merkle_top_dev, sg_fri_fold_runs_dev) against the
+  oracle and the single-GPU path;
+* DistStark with the HIP backend at world size 1 (in process) and world size 2
+  (two processes sharing this box's one GPU over gloo, device tensors staged
+  through the host): four-step NTT / INTT, sharded LDE, Merkle root and FRI
+  commit proof-stream bytes equal the single-GPU results (which the parity
+  suite pins to the oracle).
+"""
+import ctypes
+import os
+import socket
+
+import numpy as np
+import pytest
+
+import stark_oracle as o
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev():
+    import torch
+    return torch.device("cuda", 0)
+
+
+def _t(arr):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(arr).view(np.int64).reshape(-1).copy()).to(_dev())
+
+
+def _np(t):
+    return t.cpu().numpy().view(np.uint64).reshape(-1, 2)
+
+
+def _rand(seed, n):
+    x = np.random.default_rng(seed).integers(0, 2**63, size=(n, 2), dtype=np.uint64)
+    x[:, 1] %= np.uint64(0xCB80000000000000)
+    return x
+
+
+def _ints(a):
+    import starkgpu as sg
+    return sg.to_ints(a)
+
+
+# ------------------------------------------------------------------ row-sharded ABI
+
+@pytest.mark.parametrize("n,n_in,rows", [(1, 1, 3), (2, 1, 5), (16, 16, 7), (64, 9, 4), (1 << 12, 1 << 12, 3),
+                                         (1 << 13, 1 << 10, 2), (1 << 14, 1 << 14, 5)])
+def test_ntt_rows_matches_oracle(n, n_in, rows):
+    import torch
+    from starkgpu import dist as D
+    import ref_cpu
+    be = D.GpuRows()
+    root = o.primitive_nth_root(n)
+    x = _rand(n + rows, rows * n_in)
+    src = _t(x)
+    dst = torch.empty(2 * rows * n, dtype=torch.int64, device=_dev())
+    be.ntt_rows(root, src, n_in, rows, dst, n)
+    out = _np(dst)
+    for r in range(rows):
+        row = np.zeros((n, 2), dtype=np.uint64)
+        row[:n_in] = x[r * n_in:(r + 1) * n_in]
+        assert np.array_equal(out[r * n:(r + 1) * n], ref_cpu.ntt(root, row)), r
+
+
+def test_ntt_rows_beyond_grid_limit():
+    """70000 rows (> 65535 per launch) of n = 8: chunked launches, every row right."""
+    import torch
+    from starkgpu import dist as D
+    be = D.GpuRows()
+    n, rows = 8, 70000
+    root = o.primitive_nth_root(n)
+    pats = _rand(5, 3 * n).reshape(3, n, 2)
+    x = np.concatenate([pats[r % 3] for r in range(rows)])
+    dst = torch.empty(2 * rows * n, dtype=torch.int64, device=_dev())
+    be.ntt_rows(root, _t(x), n, rows, dst, n)
+    out = _np(dst).reshape(rows, n, 2)
+    expect = [o.ntt(root, _ints(pats[k])) for k in range(3)]
+    for r in [0, 1, 2, 65534, 65535, 65536, 69999]:
+        assert _ints(out[r]) == expect[r % 3], r
+
+
+def test_mul_pow_and_transpose():
+    import torch
+    from starkgpu import dist as D
+    be = D.GpuRows()
+    rows, cols = 37, 53
+    base = o.synthetic_elements(1, b"base", 1)[0]
+    x = _rand(11, rows * cols)
+    buf = _t(x)
+    a0, a1, b0, b1 = 5, 3, 7, 11
+    be.mul_pow(base, buf, rows, cols, a0, a1, b0, b1)
+    got = _ints(_np(buf))
+    xi = _ints(x)
+    for r in (0, 1, 17, 36):
+        for c in (0, 1, 30, 52):
+            e = (a0 + a1 * r) * c + b0 + b1 * r
+            assert got[r * cols + c] == o.mul_mod(xi[r * cols + c], o.fpow(base, e))
+    for A, B, C in [(37, 53, 1), (3, 5, 16), (64, 8, 4), (1, 9, 2), (300, 2, 1)]:
+        y = _rand(A * B * C, A * B * C)
+        dst = torch.empty(2 * A * B * C, dtype=torch.int64, device=_dev())
+        be.transpose(_t(y), dst, A, B, C)
+        expect = y.reshape(A, B, C, 2).transpose(1, 0, 2, 3).reshape(-1, 2)
+        assert np.array_equal(_np(dst), expect), (A, B, C)
+
+
+def test_forest_top_and_fold_runs():
+    import torch
+    import starkgpu as sg
+    from starkgpu import dist as D
+    be = D.GpuRows()
+    run, runs = 1 << 10, 8
+    x = _rand(21, run * runs)
+    buf = _t(x)
+    roots = be.forest_roots(buf, run, runs).cpu().numpy().tobytes()
+    for k in range(runs):
+        assert roots[64 * k:64 * (k + 1)] == sg.MerkleRoot.commit(x[k * run:(k + 1) * run])
+    # the top over the run roots (natural run order) is the root of the whole vector
+    top = be.top_root(be.forest_roots(buf, run, runs), runs)
+    assert top == sg.MerkleRoot.commit(x)
+    one = be.top_root(be.forest_roots(buf[:2 * run], run, 1), 1)
+    assert one == sg.MerkleRoot.commit(x[:run])
+    # fold of the whole codeword as one run == the reference fold (fri.rs:150-159)
+    n = 1 << 8
+    w = o.primitive_nth_root(n)
+    cw = o.synthetic_elements(2, b"fold", n)
+    alpha = o.synthetic_elements(3, b"alpha", 1)[0]
+    dst = torch.empty(n, dtype=torch.int64, device=_dev())
+    be.fold_runs(w, o.GENERATOR, alpha, be.from_ints(cw), n, n // 2, n // 2, 0, n, dst)
+    assert be.to_ints(dst) == o.FRI.fold(cw, alpha, w, o.GENERATOR)
+    # same fold over a shard holding runs [k1][4] of a 2-rank split (rank 1)
+    G, n1 = 2, 16
+    n2 = n // n1
+    R = n2 // G
+    shard = [cw[k1 * n2 + R + c] for k1 in range(n1) for c in range(R)]
+    dst2 = torch.empty(n, dtype=torch.int64, device=_dev())
+    be.fold_runs(w, o.GENERATOR, alpha, be.from_ints(shard), n1 * R, R, n2, R, n, dst2)
+    full = o.FRI.fold(cw, alpha, w, o.GENERATOR)
+    assert be.to_ints(dst2, n1 * R // 2) == [full[k1 * n2 + R + c] for k1 in range(n1 // 2) for c in range(R)]
+
+
+# ------------------------------------------------------------------ DistStark, world size 1
+
+@pytest.mark.parametrize("logn", [12, 16, 20])
+def test_dist_world1_ntt_lde_merkle(logn):
+    import torch
+    import starkgpu as sg
+    from starkgpu import dist as D
+    ds = D.DistStark(D.GpuRows(), D.Comm())
+    n = 1 << logn
+    root = sg.primitive_nth_root(n)
+    x = _rand(logn, n)
+    cols, row = D.scatter_columns_np(x, n, 1, 0)
+    out = ds.ntt(root, _t(cols), row, n)
+    got = D.gather_runs_np([_np(out)], n, 1)
+    ref = torch.empty(2 * n, dtype=torch.int64, device=_dev())
+    xt = _t(x)
+    sg.ntt_dev(root, xt.data_ptr(), n, ref.data_ptr())
+    assert np.array_equal(got, _np(ref))
+    back = ds.intt(root, out, n)
+    assert np.array_equal(_np(back), cols)
+    # LDE d = n/8 on the coset, then the Merkle root of the run shard
+    d = n // 8
+    coeffs = x[:d]
+    cc, crow = D.scatter_columns_np(coeffs, n, 1, 0)
+    cw = ds.coset_evaluate(root, n, sg.generator(), _t(cc), crow)
+    ref_cw = torch.empty(2 * n, dtype=torch.int64, device=_dev())
+    sg.fast_coset_evaluate_dev(root, n, sg.generator(), _t(coeffs).data_ptr(), d, ref_cw.data_ptr())
+    assert np.array_equal(D.gather_runs_np([_np(cw)], n, 1), _np(ref_cw))
+    n1, n2 = D.plan(n, 1)
+    assert ds.merkle_root(cw, n1, n2) == sg.DeviceTree(ref_cw.data_ptr(), n).root()
+
+
+def test_dist_world1_fri_commit_stream():
+    import torch
+    import starkgpu as sg
+    from starkgpu import dist as D
+    ds = D.DistStark(D.GpuRows(), D.Comm())
+    n, exp, c = 1 << 14, 8, 16
+    w = sg.primitive_nth_root(n)
+    cw = _rand(77, n)
+    ref = sg.IndependentProofStream()
+    sg.FRI(sg.generator(), w, n, exp, c).commit(cw, ref)
+    n1, n2 = D.plan(n, 1)
+    shard = cw.reshape(n1, n2, 2).reshape(-1, 2)   # world 1: the run shard is the natural order
+    got = sg.IndependentProofStream()
+    ds.fri_commit(sg.generator(), w, _t(shard), n, exp, c, got)
+    assert got.digest() == ref.digest()
+
+
+# ------------------------------------------------------------------ DistStark, world size 2 on one GPU
+
+def _world2_worker(rank, world, port, logn):
+    import torch
+    import torch.distributed as dist
+    import starkgpu as sg
+    from starkgpu import dist as D
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ctx = sg.Context(0)
+        ds = D.DistStark(D.GpuRows(ctx), D.Comm())
+        n = 1 << logn
+        root = sg.primitive_nth_root(n)
+        x = _rand(logn, n)
+        cols, row = D.scatter_columns_np(x, n, world, rank)
+        out = ds.ntt(root, _t(cols), row, n)
+        shards = [None] * world
+        dist.all_gather_object(shards, _np(out))
+        full = D.gather_runs_np(shards, n, world)
+        assert np.array_equal(full, sg.ntt(root, x, ctx=ctx)), "ntt"
+        assert np.array_equal(_np(ds.intt(root, out, n)), cols), "intt"
+        d = n // 8
+        cc, crow = D.scatter_columns_np(x[:d], n, world, rank)
+        cw = ds.coset_evaluate(root, n, sg.generator(), _t(cc), crow)
+        dist.all_gather_object(shards, _np(cw))
+        cw_full = D.gather_runs_np(shards, n, world)
+        assert np.array_equal(cw_full, sg.fast_coset_evaluate(root, n, sg.generator(), x[:d], ctx=ctx)), "lde"
+        n1, n2 = D.plan(n, world)
+        assert ds.merkle_root(cw, n1, n2 // world) == sg.MerkleRoot.commit(cw_full, ctx=ctx), "merkle"
+        ref = sg.IndependentProofStream()
+        sg.FRI(sg.generator(), root, n, 8, 16, ctx=ctx).commit(cw_full, ref)
+        got = sg.IndependentProofStream()
+        ds.fri_commit(sg.generator(), root, cw, n, 8, 16, got)
+        assert got.digest() == ref.digest(), "fri stream"
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dist_world2_one_gpu_gloo():
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.spawn(_world2_worker, args=(2, port, 14), nprocs=2, join=True)

@@ -938,3 +938,210 @@ extern "C" int sg_fri_sample_indices(const uint8_t* seed, size_t seed_len, size_
                                      size_t number, size_t* out) {
   return guard(nullptr, [&] { sample_indices(seed, seed_len, size, reduced_size, number, out); });
 }
+
+// ======================================================================== C ABI: row-sharded blocks
+//
+// Building blocks of the multi-GPU path: the four-step NTT's
+// local transforms / twiddles / transposes, Merkle forests over runs with the
+// top tree over gathered run roots, and the run-sharded FRI fold.  The
+// exchange itself (one all-to-all, one all-gather per tree) is done by the
+// caller's communicator (starkgpu/dist.py: torch.distributed over RCCL).
+
+struct sg_forest {
+  uint64_t run = 0;   // leaves per tree
+  uint64_t runs = 0;  // trees
+  int logn = 0;
+  DevBuf buf;         // runs x (2 run - 1) digests x 8 u64
+};
+
+namespace {
+// three 4096-entry Montgomery power tables of `base` (exponents < 2^36)
+void pow_tables3(sg_ctx* ctx, const fe& base, const fe** T) {
+  T[0] = ctx->pow_table(base, 4096);
+  T[1] = ctx->pow_table(fe_pow(base, (uint64_t)1 << 12), 4096);
+  T[2] = ctx->pow_table(fe_pow(base, (uint64_t)1 << 24), 4096);
+}
+constexpr uint64_t kRowsPerLaunch = 65535;  // grid.y limit
+}  // namespace
+
+extern "C" int sg_ntt_rows_dev(sg_ctx* ctx, sg_fe root, const sg_fe* d_in, size_t n_in, size_t rows, sg_fe* d_out,
+                               size_t n) {
+  return guard(ctx, [&] {
+    SG_HIP(hipSetDevice(ctx->device));
+    SG_REQUIRE(d_in && d_out, "null buffer");
+    SG_REQUIRE(n > 0 && (n & (n - 1)) == 0, "ntt rows: n must be a power of two");
+    SG_REQUIRE(n_in > 0 && n_in <= n, "ntt rows: need 0 < n_in <= n");
+    if (rows == 0) return;
+    const fe* in = reinterpret_cast<const fe*>(d_in);
+    fe* out = reinterpret_cast<fe*>(d_out);
+    SG_REQUIRE(!ranges_overlap(in, n_in * rows, out, n * rows), "ntt rows: output must not alias the input");
+    const fe r = to_fe(root);
+    SG_REQUIRE(fe_is_canonical(r), "root must be canonical");
+    const int logn = ilog2_exact(n);
+    // a zero tail of 2^skip per row makes the first `skip` stages exact copies
+    int skip = 0;
+    while (skip < logn && ((uint64_t)n_in << (skip + 1)) <= n) ++skip;
+    const fe* tw = logn > 0 ? ctx->stage_twiddles(r, logn) : nullptr;
+    for (uint64_t r0 = 0; r0 < rows; r0 += kRowsPerLaunch) {
+      const int cnt = (int)std::min<uint64_t>(kRowsPerLaunch, rows - r0);
+      fe* o = out + r0 * n;
+      const fe* i = in + r0 * n_in;
+      SG_HIP(launch_ntt_fused(&o, &i, cnt, n_in, logn, tw, nullptr, nullptr, skip, nullptr, ctx->stream, n_in, n));
+    }
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+  });
+}
+
+extern "C" int sg_scale_dev(sg_ctx* ctx, sg_fe* d_data, size_t n, sg_fe c) {
+  return guard(ctx, [&] {
+    SG_HIP(hipSetDevice(ctx->device));
+    SG_REQUIRE(fe_is_canonical(to_fe(c)), "scale: constant must be canonical");
+    if (n == 0) return;
+    fe cm = to_mont(to_fe(c));
+    DevBuf dc(ctx, sizeof(fe));
+    SG_HIP(hipMemcpyAsync(dc.get(), &cm, sizeof(fe), hipMemcpyHostToDevice, ctx->stream));
+    SG_HIP(launch_scale_const(reinterpret_cast<fe*>(d_data), n, dc.as<fe>(), ctx->stream));
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+  });
+}
+
+extern "C" int sg_mul_pow_dev(sg_ctx* ctx, sg_fe base, sg_fe* d_data, size_t rows, size_t cols, uint64_t a0,
+                              uint64_t a1, uint64_t b0, uint64_t b1) {
+  return guard(ctx, [&] {
+    SG_HIP(hipSetDevice(ctx->device));
+    const fe b = to_fe(base);
+    SG_REQUIRE(fe_is_canonical(b), "mul_pow: base must be canonical");
+    if (rows == 0 || cols == 0) return;
+    // largest exponent (a0 + a1 (rows-1)) (cols-1) + b0 + b1 (rows-1) must stay below 2^36
+    unsigned __int128 emax = ((unsigned __int128)a0 + (unsigned __int128)a1 * (rows - 1)) * (cols - 1) + b0 +
+                             (unsigned __int128)b1 * (rows - 1);
+    SG_REQUIRE(emax < ((unsigned __int128)1 << 36), "mul_pow: exponent range exceeds 2^36");
+    const fe* T[3];
+    pow_tables3(ctx, b, T);
+    SG_HIP(launch_mul_pow(reinterpret_cast<fe*>(d_data), rows, cols, a0, a1, b0, b1, T[0], T[1], T[2], ctx->stream));
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+  });
+}
+
+extern "C" int sg_transpose_dev(sg_ctx* ctx, const sg_fe* d_in, sg_fe* d_out, size_t A, size_t B, size_t C) {
+  return guard(ctx, [&] {
+    SG_HIP(hipSetDevice(ctx->device));
+    const uint64_t total = (uint64_t)A * B * C;
+    if (total == 0) return;
+    SG_REQUIRE(!ranges_overlap(reinterpret_cast<const fe*>(d_in), total, reinterpret_cast<const fe*>(d_out), total),
+               "transpose: output must not alias the input");
+    SG_HIP(launch_swap01(reinterpret_cast<const fe*>(d_in), reinterpret_cast<fe*>(d_out), A, B, C, ctx->stream));
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+  });
+}
+
+extern "C" int sg_merkle_forest_dev(sg_ctx* ctx, const sg_fe* d_leaves, size_t run, size_t runs, sg_forest** out) {
+  return guard(ctx, [&] {
+    SG_HIP(hipSetDevice(ctx->device));
+    SG_REQUIRE(out && d_leaves, "null argument");
+    SG_REQUIRE(run > 0 && (run & (run - 1)) == 0, "Leafs len must be power of two");
+    SG_REQUIRE(runs >= 1, "forest: zero runs");
+    std::unique_ptr<sg_forest> f(new sg_forest());
+    f->run = run;
+    f->runs = runs;
+    f->logn = ilog2_exact(run);
+    const uint64_t per = merkle_tree_digests(run) * 8;  // u64 per tree
+    f->buf = DevBuf(ctx, runs * per * 8);
+    const fe* leaves = reinterpret_cast<const fe*>(d_leaves);
+    for (uint64_t r0 = 0; r0 < runs; r0 += kRowsPerLaunch) {
+      const int cnt = (int)std::min<uint64_t>(kRowsPerLaunch, runs - r0);
+      const fe* lv = leaves + r0 * run;
+      uint64_t* tr = f->buf.as<uint64_t>() + r0 * per;
+      SG_HIP(launch_merkle_tree(&lv, &tr, cnt, run, nullptr, ctx->stream, run, per, 0));
+    }
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+    *out = f.release();
+  });
+}
+
+extern "C" int sg_forest_roots_dev(sg_ctx* ctx, const sg_forest* f, uint8_t* d_roots) {
+  return guard(ctx, [&] {
+    SG_HIP(hipSetDevice(ctx->device));
+    SG_REQUIRE(f && d_roots, "null argument");
+    const uint64_t per = merkle_tree_digests(f->run) * 8;
+    const uint64_t root_off = (2 * f->run - 2) * 8;
+    SG_HIP(launch_gather_roots(f->buf.as<uint64_t>(), per, root_off, reinterpret_cast<uint64_t*>(d_roots), f->runs,
+                               ctx->stream));
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+  });
+}
+
+extern "C" int sg_forest_open(sg_ctx* ctx, const sg_forest* f, size_t tree, size_t index, uint8_t* path,
+                              size_t* path_len) {
+  return guard(ctx, [&] {
+    SG_REQUIRE(f && tree < f->runs && index < f->run, "cannot open invalid index");
+    std::vector<uint64_t> idx;
+    const uint64_t base = (uint64_t)tree * merkle_tree_digests(f->run);
+    for (int lv = 0; lv < f->logn; ++lv) idx.push_back(base + level_offset(f->run, lv) + ((index >> lv) ^ 1));
+    if (!idx.empty()) {
+      DevBuf di(ctx, idx.size() * 8), dout(ctx, idx.size() * 64);
+      SG_HIP(hipMemcpyAsync(di.get(), idx.data(), idx.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+      SG_HIP(launch_gather_digests(f->buf.as<uint64_t>(), di.as<uint64_t>(), dout.as<uint64_t>(),
+                                   (uint32_t)idx.size(), ctx->stream));
+      SG_HIP(hipMemcpyAsync(path, dout.get(), idx.size() * 64, hipMemcpyDeviceToHost, ctx->stream));
+      SG_HIP(hipStreamSynchronize(ctx->stream));
+    }
+    if (path_len) *path_len = idx.size();
+  });
+}
+
+extern "C" void sg_forest_free(sg_ctx* ctx, sg_forest* f) {
+  (void)ctx;
+  delete f;
+}
+
+extern "C" int sg_merkle_top_dev(sg_ctx* ctx, const uint8_t* d_digests, size_t n, sg_tree** out) {
+  return guard(ctx, [&] {
+    SG_HIP(hipSetDevice(ctx->device));
+    SG_REQUIRE(out && d_digests, "null argument");
+    SG_REQUIRE(n > 0 && (n & (n - 1)) == 0, "Leafs len must be power of two");
+    std::unique_ptr<sg_tree> t(new sg_tree());
+    t->n = n;
+    t->logn = ilog2_exact(n);
+    t->buf = DevBuf(ctx, merkle_tree_digests(n) * 64);
+    SG_HIP(hipMemcpyAsync(t->buf.get(), d_digests, n * 64, hipMemcpyDeviceToDevice, ctx->stream));
+    uint64_t* tr = t->buf.as<uint64_t>();
+    uint64_t* root_dev = ctx->pinned_roots_dev;
+    if (n > 1) SG_HIP(launch_merkle_tree(nullptr, &tr, 1, n, &root_dev, ctx->stream, 0, 0, 1));
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+    if (n > 1)
+      memcpy(t->root, ctx->pinned_roots, 64);
+    else
+      SG_HIP(hipMemcpy(t->root, d_digests, 64, hipMemcpyDeviceToHost));
+    *out = t.release();
+  });
+}
+
+extern "C" int sg_fri_fold_runs_dev(sg_ctx* ctx, sg_fe omega, sg_fe offset, sg_fe alpha, const sg_fe* d_in,
+                                    size_t n_local, size_t run, size_t run_stride, size_t run_off, size_t n_global,
+                                    sg_fe* d_out) {
+  return guard(ctx, [&] {
+    SG_HIP(hipSetDevice(ctx->device));
+    SG_REQUIRE(d_in && d_out, "null buffer");
+    SG_REQUIRE(n_global >= 2 && (n_global & (n_global - 1)) == 0, "fold: global length must be a power of two >= 2");
+    SG_REQUIRE(n_local >= 2 && n_local % 2 == 0 && run > 0, "fold: bad local shape");
+    const uint64_t half = n_local / 2;
+    SG_REQUIRE(half % run == 0, "fold: runs must tile each half of the shard");
+    SG_REQUIRE((half / run) * run_stride == n_global / 2, "fold: partner i + n/2 must be local l + n_local/2");
+    SG_REQUIRE(run_off + run <= run_stride, "fold: run offset outside its stride");
+    const fe w = to_fe(omega), o = to_fe(offset), a = to_fe(alpha);
+    SG_REQUIRE(fe_is_canonical(w) && fe_is_canonical(o) && fe_is_canonical(a), "fold: scalars must be canonical");
+    const fe winv = fe_inv(w);
+    // fri.rs:133: omega must have order exactly n_global
+    SG_REQUIRE(fe_eq(fe_pow(w, n_global - 1), winv), "error in commit: omega does not have the right order!");
+    SG_REQUIRE(n_global / 2 <= ((uint64_t)1 << 36), "fold: codeword too long");
+    const fe* T[3];
+    pow_tables3(ctx, winv, T);
+    const fe K = to_mont(fe_mul(fe_mul(a, fe_inv(o)), fe_inv(fe_from_u64(2))));
+    SG_REQUIRE(!ranges_overlap(reinterpret_cast<const fe*>(d_in), n_local, reinterpret_cast<const fe*>(d_out), half),
+               "fold: output must not alias the input");
+    SG_HIP(launch_fri_fold_runs(reinterpret_cast<fe*>(d_out), reinterpret_cast<const fe*>(d_in), half, run, run_stride,
+                                run_off, T[0], T[1], T[2], K, ctx->stream));
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+  });
+}

@@ -91,12 +91,13 @@ __global__ void k_stage_twiddles(fe* __restrict__ out, const fe* __restrict__ pw
 struct GatherArgs {
   fe* out[kMaxBatch];
   const fe* in[kMaxBatch];
+  uint64_t in_ys, out_ys;  // != 0: strided rows, row blockIdx.y at in[0] + y * in_ys / out[0] + y * out_ys
 };
 
 __global__ void k_bitrev_gather(GatherArgs ga, uint64_t n_in, int logn, const fe* __restrict__ sA,
                                 const fe* __restrict__ sB, int skip) {
-  fe* __restrict__ out = ga.out[blockIdx.y];
-  const fe* __restrict__ in = ga.in[blockIdx.y];
+  fe* __restrict__ out = ga.out_ys ? ga.out[0] + (uint64_t)blockIdx.y * ga.out_ys : ga.out[blockIdx.y];
+  const fe* __restrict__ in = ga.in_ys ? ga.in[0] + (uint64_t)blockIdx.y * ga.in_ys : ga.in[blockIdx.y];
   uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >> logn) return;
   uint64_t jj = (j >> skip) << skip;
@@ -122,6 +123,7 @@ struct PassArgs {
   int b0;              // index bits below the group bits (= first stage of the pass - 1)
   int L;               // stages in this pass (group bits [b0, b0+L))
   int logC;            // columns per tile (consecutive low-bit indices), C <= 2^b0
+  uint64_t ys;         // != 0: strided rows, transform blockIdx.y at data[0] + y * ys
 };
 
 // COLK: the tile's columns are consecutive low index bits (they enter the twiddle
@@ -167,8 +169,11 @@ __device__ __forceinline__ void radix_step(fe* lds, const PassArgs& a, int t, ui
 // register steps, store.  TL > 0: the tile is exactly 2^TL elements handled
 // by 256 threads, so the loads/stores are unrolled (all 2^TL/256 global loads
 // of a thread in flight at once); TL == 0: generic loop for small transforms.
+#ifndef SG_NTT_WPE
+#define SG_NTT_WPE 1
+#endif
 template <int TL>
-__global__ __launch_bounds__(256) void k_ntt_pass(PassArgs a) {
+__global__ __launch_bounds__(256, SG_NTT_WPE) void k_ntt_pass(PassArgs a) {
   extern __shared__ fe lds[];
   const int logC = a.logC;
   const uint32_t C = 1u << logC;
@@ -178,7 +183,7 @@ __global__ __launch_bounds__(256) void k_ntt_pass(PassArgs a) {
   const uint64_t h = blockIdx.x / ncb;
   const uint64_t cb = blockIdx.x % ncb;
   const uint64_t base = (h << (a.b0 + a.L)) + cb * C;
-  fe* __restrict__ data = a.data[blockIdx.y];
+  fe* __restrict__ data = a.ys ? a.data[0] + (uint64_t)blockIdx.y * a.ys : a.data[blockIdx.y];
   if constexpr (TL > 0) {
     constexpr int PER = (1 << TL) / 256;
     fe v[PER];
@@ -246,10 +251,11 @@ struct FirstArgs {
   int L;
   int logC;
   int skip;
+  uint64_t in_ys, out_ys;  // != 0: strided rows (see GatherArgs)
 };
 
 template <int TL>
-__global__ __launch_bounds__(256) void k_ntt_first(FirstArgs a) {
+__global__ __launch_bounds__(256, SG_NTT_WPE) void k_ntt_first(FirstArgs a) {
   extern __shared__ fe lds[];
   const int L = a.L, logC = a.logC, m = a.logn;
   const uint32_t C = 1u << logC;
@@ -259,8 +265,8 @@ __global__ __launch_bounds__(256) void k_ntt_first(FirstArgs a) {
   uint32_t bx = blockIdx.x;
   if ((gridDim.x & 7) == 0) bx = (bx & 7) * (gridDim.x >> 3) + (bx >> 3);
   const uint64_t c0 = (uint64_t)bx << logC;
-  const fe* __restrict__ in = a.in[blockIdx.y];
-  fe* __restrict__ out = a.out[blockIdx.y];
+  const fe* __restrict__ in = a.in_ys ? a.in[0] + (uint64_t)blockIdx.y * a.in_ys : a.in[blockIdx.y];
+  fe* __restrict__ out = a.out_ys ? a.out[0] + (uint64_t)blockIdx.y * a.out_ys : a.out[blockIdx.y];
   const uint32_t rows = 1u << (L - skip);
   const uint32_t rep = 1u << skip;
   for (uint32_t l = threadIdx.x; l < rows * C; l += blockDim.x) {
@@ -341,19 +347,31 @@ struct MerkleArgs {
   uint64_t off[kMaxFuse + 1];  // digest offsets of levels first_level-1 .. first_level+fuse-1 (off[0] = child level)
   uint64_t* root_host[kMaxBatch];  // optional host-coherent copy of the root (written by the launch reaching it)
   uint64_t root_level;             // log2(n): the level whose single digest is the root
+  uint64_t leaves_ys, tree_ys;     // != 0: strided rows of trees (leaves[0] + y * leaves_ys, tree[0] + y * tree_ys)
 };
+
+__device__ __forceinline__ uint64_t* merkle_tree_ptr(const MerkleArgs& a) {
+  return a.tree_ys ? a.tree[0] + (uint64_t)blockIdx.y * a.tree_ys : a.tree[blockIdx.y];
+}
+__device__ __forceinline__ const fe* merkle_leaves_ptr(const MerkleArgs& a) {
+  return a.leaves_ys ? a.leaves[0] + (uint64_t)blockIdx.y * a.leaves_ys : a.leaves[blockIdx.y];
+}
+__device__ __forceinline__ uint64_t* merkle_root_slot(const MerkleArgs& a) {
+  return a.tree_ys ? nullptr : a.root_host[blockIdx.y];
+}
 
 template <bool LEAF, int MAXB>
 __global__ __launch_bounds__(MAXB) void k_merkle_levels(MerkleArgs a) {
   __shared__ Digest sm[MAXB];
   const uint32_t tid = threadIdx.x;
   const uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + tid;
-  uint64_t* __restrict__ tree = a.tree[blockIdx.y];
+  uint64_t* __restrict__ tree = merkle_tree_ptr(a);
+  uint64_t* const root_slot = merkle_root_slot(a);
   uint64_t d[8];
   if (idx < a.first_count) {
     if (LEAF) {
       uint64_t m[16];
-      uint32_t len = fe_decimal_words(ld_fe(a.leaves[blockIdx.y] + idx), m);
+      uint32_t len = fe_decimal_words(ld_fe(merkle_leaves_ptr(a) + idx), m);
 #pragma unroll
       for (int i = 5; i < 16; ++i) m[i] = 0;
       blake2b_single_block(m, len, d);
@@ -365,8 +383,8 @@ __global__ __launch_bounds__(MAXB) void k_merkle_levels(MerkleArgs a) {
       blake2b_node(l, r, d);
     }
     st_digest(tree + (a.off[1] + idx) * 8, d);
-    if (a.first_level == a.root_level && a.root_host[blockIdx.y])
-      for (int i = 0; i < 8; ++i) a.root_host[blockIdx.y][i] = d[i];
+    if (a.first_level == a.root_level && root_slot)
+      for (int i = 0; i < 8; ++i) root_slot[i] = d[i];
   }
   uint32_t count = blockDim.x;  // digests of this block at the current level
   for (int lev = 1; lev < a.fuse; ++lev) {
@@ -381,8 +399,8 @@ __global__ __launch_bounds__(MAXB) void k_merkle_levels(MerkleArgs a) {
       blake2b_node(l, r, d);
       uint64_t gidx = (uint64_t)blockIdx.x * count + tid;
       st_digest(tree + (a.off[lev + 1] + gidx) * 8, d);
-      if (a.first_level + lev == a.root_level && a.root_host[blockIdx.y])
-        for (int i = 0; i < 8; ++i) a.root_host[blockIdx.y][i] = d[i];
+      if (a.first_level + lev == a.root_level && root_slot)
+        for (int i = 0; i < 8; ++i) root_slot[i] = d[i];
     }
     __syncthreads();
   }
@@ -482,7 +500,8 @@ __global__ __launch_bounds__(256) void k_merkle_quad(MerkleArgs a) {
   const int tid = threadIdx.x;
   const int q = tid & 3;
   const int node = tid >> 2;
-  uint64_t* __restrict__ tree = a.tree[blockIdx.y];
+  uint64_t* __restrict__ tree = merkle_tree_ptr(a);
+  uint64_t* const root_slot = merkle_root_slot(a);
   const SigmaPack sp = sigma_pack(q);
   uint32_t count = blockDim.x >> 2;  // nodes of this block at the current level
   const uint64_t gnode = (uint64_t)blockIdx.x * count + node;
@@ -506,9 +525,9 @@ __global__ __launch_bounds__(256) void k_merkle_quad(MerkleArgs a) {
     uint64_t* dst = tree + (a.off[1] + gnode) * 8;
     dst[q] = hlo;
     dst[4 + q] = hhi;
-    if (a.first_level == a.root_level && a.root_host[blockIdx.y]) {
-      a.root_host[blockIdx.y][q] = hlo;
-      a.root_host[blockIdx.y][4 + q] = hhi;
+    if (a.first_level == a.root_level && root_slot) {
+      root_slot[q] = hlo;
+      root_slot[4 + q] = hhi;
     }
   }
   for (int lev = 1; lev < a.fuse; ++lev) {
@@ -525,9 +544,9 @@ __global__ __launch_bounds__(256) void k_merkle_quad(MerkleArgs a) {
       uint64_t* dst = tree + (a.off[lev + 1] + gidx) * 8;
       dst[q] = hlo;
       dst[4 + q] = hhi;
-      if (a.first_level + lev == a.root_level && a.root_host[blockIdx.y]) {
-        a.root_host[blockIdx.y][q] = hlo;
-        a.root_host[blockIdx.y][4 + q] = hhi;
+      if (a.first_level + lev == a.root_level && root_slot) {
+        root_slot[q] = hlo;
+        root_slot[4 + q] = hhi;
       }
     }
   }
@@ -562,6 +581,105 @@ __global__ __launch_bounds__(256) void k_fri_fold(FoldArgs a) {
     st_fe(a.out + i, r);
     t = mont_mul(t, a.Wstride);
   }
+}
+
+// ---------------------------------------------- row-sharded helpers (four-step)
+//
+// Multi-GPU transforms work on 2-D shards: rows x cols of field
+// elements, row-major.  These kernels are the local steps around the all-to-all.
+
+// data[r][c] *= base^e, e = (a0 + a1*r)*c + b0 + b1*r < 2^36, via three 4096-entry
+// Montgomery power tables (T0: base^i, T1: base^(i<<12), T2: base^(i<<24)).
+// Twiddles of the four-step (omega^(j1*k2)) and the coset scale (offset^j) are
+// both of this form.
+struct MulPowArgs {
+  fe* data;
+  uint64_t rows, cols;
+  uint64_t a0, a1, b0, b1;
+  const fe* T0;
+  const fe* T1;
+  const fe* T2;
+};
+
+__global__ __launch_bounds__(256) void k_mul_pow(MulPowArgs a) {
+  const uint64_t total = a.rows * a.cols;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t l = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; l < total; l += stride) {
+    const uint64_t r = l / a.cols, c = l - r * a.cols;
+    const uint64_t e = (a.a0 + a.a1 * r) * c + a.b0 + a.b1 * r;
+    fe w = mont_mul(ld_fe(a.T0 + (e & 4095)), ld_fe(a.T1 + ((e >> 12) & 4095)));
+    w = mont_mul(w, ld_fe(a.T2 + (e >> 24)));
+    st_fe(a.data + l, mont_mul(ld_fe(a.data + l), w));
+  }
+}
+
+// out[b][a][c] = in[a][b][c] for an A x B x C array (swap the two outer axes).
+// C >= 16: every (a, b) run of C elements is a coalesced copy.  C < 16: 32 x 32
+// tiles of (a, b) through LDS so both the reads and the writes are coalesced.
+__global__ __launch_bounds__(256) void k_swap01_runs(const fe* __restrict__ in, fe* __restrict__ out, uint64_t A,
+                                                     uint64_t B, uint64_t C) {
+  const uint64_t total = A * B * C;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t l = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; l < total; l += stride) {
+    const uint64_t c = l % C, ab = l / C;
+    const uint64_t b = ab % B, aa = ab / B;  // l = ((aa * B) + b) * C + c (input order)
+    st_fe(out + (b * A + aa) * C + c, ld_fe(in + l));
+  }
+}
+
+__global__ __launch_bounds__(256) void k_swap01_tiled(const fe* __restrict__ in, fe* __restrict__ out, uint64_t A,
+                                                      uint64_t B, uint64_t C) {
+  __shared__ fe tile[32][33];
+  // blockIdx.x: tile over b (32 wide), blockIdx.y: tile over a, blockIdx.z: c
+  const uint64_t b0 = (uint64_t)blockIdx.x * 32, a0 = (uint64_t)blockIdx.y * 32, c = blockIdx.z;
+  const uint32_t tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+  for (uint32_t k = ty; k < 32; k += 8) {
+    const uint64_t aa = a0 + k, b = b0 + tx;
+    if (aa < A && b < B) tile[k][tx] = ld_fe(in + (aa * B + b) * C + c);
+  }
+  __syncthreads();
+  for (uint32_t k = ty; k < 32; k += 8) {
+    const uint64_t b = b0 + k, aa = a0 + tx;
+    if (aa < A && b < B) st_fe(out + (b * A + aa) * C + c, tile[tx][k]);
+  }
+}
+
+// FRI fold of a run-sharded codeword (fri.rs:151-159).  Local element l is
+// global index i(l) = (l / run) * run_stride + run_off + l % run; its partner
+// i + n/2 is local l + half (the caller checks the layout guarantees it).
+struct FoldRunsArgs {
+  fe* out;
+  const fe* in;
+  uint64_t half;       // local outputs
+  uint64_t run, run_stride, run_off;
+  const fe* T0;        // Montgomery(w_r^-e): e & 4095, (e >> 12) & 4095, e >> 24
+  const fe* T1;
+  const fe* T2;
+  fe K;                // Montgomery(alpha * offset_r^-1 * 2^-1)
+};
+
+__global__ __launch_bounds__(256) void k_fri_fold_runs(FoldRunsArgs a) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t l = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; l < a.half; l += stride) {
+    const uint64_t q = l / a.run;
+    const uint64_t e = q * a.run_stride + a.run_off + (l - q * a.run);
+    fe t = mont_mul(a.K, ld_fe(a.T0 + (e & 4095)));
+    t = mont_mul(t, ld_fe(a.T1 + ((e >> 12) & 4095)));
+    t = mont_mul(t, ld_fe(a.T2 + (e >> 24)));
+    const fe x = ld_fe(a.in + l);
+    const fe y = ld_fe(a.in + l + a.half);
+    st_fe(a.out + l, fe_add(fe_halve(fe_add(x, y)), mont_mul(fe_sub(x, y), t)));
+  }
+}
+
+// roots of `count` strided trees (root digest at tree + y * tree_ys + root_off) -> contiguous
+__global__ void k_gather_roots(const uint64_t* __restrict__ tree, uint64_t tree_ys, uint64_t root_off,
+                               uint64_t* __restrict__ out, uint64_t count) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  uint64_t d[8];
+  ld_digest(tree + i * tree_ys + root_off, d);
+  st_digest(out + i * 8, d);
 }
 
 // ------------------------------------------------------------- gathers (openings)
@@ -651,15 +769,23 @@ hipError_t launch_stage_twiddles(fe* out, const fe* pw, int logn, hipStream_t s)
   return hipGetLastError();
 }
 
+static bool batch_ok(int batch, uint64_t ys) {
+  return batch >= 1 && (ys ? batch <= 65535 : batch <= kMaxBatch);
+}
+
 hipError_t launch_bitrev_gather(fe* const* out, const fe* const* in, int batch, uint64_t n_in, int logn,
-                                const fe* sA, const fe* sB, int skip, hipStream_t s) {
-  if (batch < 1 || batch > kMaxBatch) return hipErrorInvalidValue;
+                                const fe* sA, const fe* sB, int skip, hipStream_t s, uint64_t in_ys,
+                                uint64_t out_ys) {
+  if (!batch_ok(batch, out_ys) || (in_ys != 0) != (out_ys != 0)) return hipErrorInvalidValue;
   uint64_t n = (uint64_t)1 << logn;
   GatherArgs ga;
+  const int np = out_ys ? 1 : batch;
   for (int b = 0; b < kMaxBatch; ++b) {
-    ga.out[b] = b < batch ? out[b] : nullptr;
-    ga.in[b] = b < batch ? in[b] : nullptr;
+    ga.out[b] = b < np ? out[b] : nullptr;
+    ga.in[b] = b < np ? in[b] : nullptr;
   }
+  ga.in_ys = in_ys;
+  ga.out_ys = out_ys;
   ProfScope ps("bitrev_gather", batch * (16 * (n_in < n ? n_in : n) + 16 * n), s);
   hipLaunchKernelGGL(k_bitrev_gather, dim3(nblocks(n, 256), batch), dim3(256), 0, s, ga, n_in, logn, sA, sB, skip);
   return hipGetLastError();
@@ -675,8 +801,10 @@ hipError_t launch_scale_const(fe* data, uint64_t n, const fe* cst, hipStream_t s
 // stages on 2^L x C tiles (<= 4096 elements = 64 KiB of LDS), with C
 // consecutive low-bit indices per tile so global accesses are C*16-byte runs.
 hipError_t launch_ntt_dit(fe* const* data, int batch, const fe* tw, int logn, const fe* post, int first_b0,
-                          hipStream_t s) {
-  if (batch < 1 || batch > kMaxBatch) return hipErrorInvalidValue;
+                          hipStream_t s, uint64_t ys) {
+  if (!batch_ok(batch, ys)) return hipErrorInvalidValue;
+  if (ys && ys != ((uint64_t)1 << logn)) return hipErrorInvalidValue;  // rows are contiguous transforms
+  const int np = ys ? 1 : batch;
   static bool lds_attr = false;
   if (!lds_attr) {
     hipError_t e = hipFuncSetAttribute((const void*)k_ntt_pass<0>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
@@ -690,8 +818,8 @@ hipError_t launch_ntt_dit(fe* const* data, int batch, const fe* tw, int logn, co
     return (t == 11 || t == 12) ? t : 11;
   }();
   if (first_b0 >= logn) {
-    for (int b = 0; post && b < batch; ++b) {
-      hipError_t e = launch_scale_const(data[b], (uint64_t)1 << logn, post, s);
+    for (int b = 0; post && b < np; ++b) {
+      hipError_t e = launch_scale_const(data[b], ((uint64_t)1 << logn) * (ys ? (uint64_t)batch : 1), post, s);
       if (e != hipSuccess) return e;
     }
     return hipSuccess;
@@ -699,7 +827,8 @@ hipError_t launch_ntt_dit(fe* const* data, int batch, const fe* tw, int logn, co
   int b0 = first_b0;
   while (b0 < logn) {
     PassArgs a;
-    for (int b = 0; b < kMaxBatch; ++b) a.data[b] = b < batch ? data[b] : nullptr;
+    for (int b = 0; b < kMaxBatch; ++b) a.data[b] = b < np ? data[b] : nullptr;
+    a.ys = ys;
     a.tw = tw;
     a.logn = logn;
     a.b0 = b0;
@@ -733,8 +862,10 @@ hipError_t launch_ntt_dit(fe* const* data, int batch, const fe* tw, int logn, co
 // Whole transform: fused bit-reversal first pass (when logn leaves room for a
 // later pass), then launch_ntt_dit from stage L1 + 1.  `out` must not alias `in`.
 hipError_t launch_ntt_fused(fe* const* out, const fe* const* in, int batch, uint64_t n_in, int logn, const fe* tw,
-                            const fe* sA, const fe* sB, int skip, const fe* post, hipStream_t s) {
-  if (batch < 1 || batch > kMaxBatch) return hipErrorInvalidValue;
+                            const fe* sA, const fe* sB, int skip, const fe* post, hipStream_t s, uint64_t in_ys,
+                            uint64_t out_ys) {
+  if (!batch_ok(batch, out_ys) || (in_ys != 0) != (out_ys != 0)) return hipErrorInvalidValue;
+  const int np = out_ys ? 1 : batch;
   static bool lds_attr = false;
   if (!lds_attr) {
     hipError_t e = hipFuncSetAttribute((const void*)k_ntt_first<11>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
@@ -743,15 +874,17 @@ hipError_t launch_ntt_fused(fe* const* out, const fe* const* in, int batch, uint
   }
   constexpr int TL = 11, LOGC1 = 2, L1 = TL - LOGC1;
   if (logn <= L1 + LOGC1 || logn - L1 > 63) {
-    hipError_t e = launch_bitrev_gather(out, in, batch, n_in, logn, sA, sB, skip, s);
+    hipError_t e = launch_bitrev_gather(out, in, batch, n_in, logn, sA, sB, skip, s, in_ys, out_ys);
     if (e != hipSuccess) return e;
-    return launch_ntt_dit(out, batch, tw, logn, post, skip, s);
+    return launch_ntt_dit(out, batch, tw, logn, post, skip, s, out_ys);
   }
   FirstArgs a;
   for (int b = 0; b < kMaxBatch; ++b) {
-    a.out[b] = b < batch ? out[b] : nullptr;
-    a.in[b] = b < batch ? in[b] : nullptr;
+    a.out[b] = b < np ? out[b] : nullptr;
+    a.in[b] = b < np ? in[b] : nullptr;
   }
+  a.in_ys = in_ys;
+  a.out_ys = out_ys;
   a.tw = tw;
   a.sA = sA;
   a.sB = sB;
@@ -769,15 +902,17 @@ hipError_t launch_ntt_fused(fe* const* out, const fe* const* in, int batch, uint
   }
   // trivial stages beyond L1 are not replicated across tiles: later passes run
   // them as real butterflies on zeros, (a, 0) -> (a, a), which is exact
-  return launch_ntt_dit(out, batch, tw, logn, post, L1, s);
+  return launch_ntt_dit(out, batch, tw, logn, post, L1, s, out_ys);
 }
 
 uint64_t merkle_tree_digests(uint64_t n) { return 2 * n - 1; }
 
 
 hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, int batch, uint64_t n,
-                              uint64_t* const* root_host, hipStream_t s) {
-  if (batch < 1 || batch > kMaxBatch) return hipErrorInvalidValue;
+                              uint64_t* const* root_host, hipStream_t s, uint64_t leaves_ys, uint64_t tree_ys,
+                              int start_level) {
+  if (!batch_ok(batch, tree_ys) || (start_level == 0 && (leaves_ys != 0) != (tree_ys != 0))) return hipErrorInvalidValue;
+  const int np = tree_ys ? 1 : batch;
   // Launch plan.  Levels 0..logn; level k has n >> k digests at offset 2n - 2(n >> k).
   //  * leaves: one lane per leaf (decimal + hash) in 512-lane blocks; 3 more levels
   //    fused through LDS (512 -> 64 lanes: every active wave full) when the tree is
@@ -788,15 +923,17 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
   constexpr uint64_t kQuadBelow = (uint64_t)1 << 16;
   int logn = 0;
   while (((uint64_t)1 << logn) < n) ++logn;
-  int level = 0;
+  int level = start_level;
   while (level <= logn) {
     uint64_t count = n >> level;
     MerkleArgs a;
     for (int b = 0; b < kMaxBatch; ++b) {
-      a.leaves[b] = (level == 0 && b < batch) ? leaves[b] : nullptr;
-      a.tree[b] = b < batch ? tree[b] : nullptr;
-      a.root_host[b] = (root_host && b < batch) ? root_host[b] : nullptr;
+      a.leaves[b] = (level == 0 && b < np) ? leaves[b] : nullptr;
+      a.tree[b] = b < np ? tree[b] : nullptr;
+      a.root_host[b] = (root_host && b < np && !tree_ys) ? root_host[b] : nullptr;
     }
+    a.leaves_ys = leaves_ys;
+    a.tree_ys = tree_ys;
     a.root_level = (uint64_t)logn;
     a.first_level = level;
     a.first_count = count;
@@ -874,6 +1011,56 @@ unsigned fri_fold_grid(uint64_t half) {
   uint64_t blocks = (half + 255) / 256;
   const uint64_t cap = 256 * 16;  // grid-stride beyond 16 blocks per CU
   return (unsigned)(blocks < cap ? blocks : cap);
+}
+
+
+// ---------------------------------------------- row-sharded helpers: launchers
+
+static unsigned grid_stride_blocks(uint64_t n) {
+  uint64_t blocks = (n + 255) / 256;
+  const uint64_t cap = 256 * 16;
+  return (unsigned)(blocks < cap ? (blocks ? blocks : 1) : cap);
+}
+
+hipError_t launch_mul_pow(fe* data, uint64_t rows, uint64_t cols, uint64_t a0, uint64_t a1, uint64_t b0,
+                          uint64_t b1, const fe* T0, const fe* T1, const fe* T2, hipStream_t s) {
+  if (rows * cols == 0) return hipSuccess;
+  MulPowArgs a{data, rows, cols, a0, a1, b0, b1, T0, T1, T2};
+  ProfScope ps("mul_pow", 32 * rows * cols, s);
+  hipLaunchKernelGGL(k_mul_pow, dim3(grid_stride_blocks(rows * cols)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_swap01(const fe* in, fe* out, uint64_t A, uint64_t B, uint64_t C, hipStream_t s) {
+  if (A * B * C == 0) return hipSuccess;
+  ProfScope ps("transpose", 32 * A * B * C, s);
+  if (C >= 16 || A == 1 || B == 1) {
+    hipLaunchKernelGGL(k_swap01_runs, dim3(grid_stride_blocks(A * B * C)), dim3(256), 0, s, in, out, A, B, C);
+  } else {
+    uint64_t gx = (B + 31) / 32, gy = (A + 31) / 32;
+    if (gx > 0x7FFFFFFFull || gy > 65535 || C > 65535) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_swap01_tiled, dim3((unsigned)gx, (unsigned)gy, (unsigned)C), dim3(256), 0, s, in, out, A,
+                       B, C);
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_fri_fold_runs(fe* out, const fe* in, uint64_t half, uint64_t run, uint64_t run_stride,
+                                uint64_t run_off, const fe* T0, const fe* T1, const fe* T2, const fe& K,
+                                hipStream_t s) {
+  if (half == 0) return hipSuccess;
+  FoldRunsArgs a{out, in, half, run, run_stride, run_off, T0, T1, T2, K};
+  ProfScope ps("fri_fold", 48 * half, s);
+  hipLaunchKernelGGL(k_fri_fold_runs, dim3(grid_stride_blocks(half)), dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_gather_roots(const uint64_t* tree, uint64_t tree_ys, uint64_t root_off, uint64_t* out,
+                               uint64_t count, hipStream_t s) {
+  if (count == 0) return hipSuccess;
+  ProfScope ps("gather_roots", 128 * count, s);
+  hipLaunchKernelGGL(k_gather_roots, dim3(nblocks(count, 256)), dim3(256), 0, s, tree, tree_ys, root_off, out, count);
+  return hipGetLastError();
 }
 
 }  // namespace sg

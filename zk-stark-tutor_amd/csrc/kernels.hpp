@@ -8,19 +8,25 @@ namespace sg {
 
 hipError_t launch_stage_twiddles(fe* out, const fe* pw, int logn, hipStream_t s);
 hipError_t launch_pow_table(fe* tw, const fe* A, const fe* B, uint64_t count, hipStream_t s);
-// batched over up to 4 independent transforms / trees (one per blockIdx.y)
+// Batched over up to 4 independent transforms / trees (one pointer each, blockIdx.y),
+// or, with a non-zero row stride (`ys`), over up to 65535 strided rows from
+// pointer [0] (row y at ptr[0] + y * stride).
 hipError_t launch_bitrev_gather(fe* const* out, const fe* const* in, int batch, uint64_t n_in, int logn,
-                                const fe* sA, const fe* sB, int skip, hipStream_t s);
+                                const fe* sA, const fe* sB, int skip, hipStream_t s, uint64_t in_ys = 0,
+                                uint64_t out_ys = 0);
 hipError_t launch_scale_const(fe* data, uint64_t n, const fe* cst, hipStream_t s);
 hipError_t launch_ntt_dit(fe* const* data, int batch, const fe* tw, int logn, const fe* post, int first_b0,
-                          hipStream_t s);
+                          hipStream_t s, uint64_t ys = 0);
 // bit-reversal (+ LDE scale, + `skip` trivial stages) fused into the first pass; out must not alias in
 hipError_t launch_ntt_fused(fe* const* out, const fe* const* in, int batch, uint64_t n_in, int logn, const fe* tw,
-                            const fe* sA, const fe* sB, int skip, const fe* post, hipStream_t s);
+                            const fe* sA, const fe* sB, int skip, const fe* post, hipStream_t s, uint64_t in_ys = 0,
+                            uint64_t out_ys = 0);
 uint64_t merkle_tree_digests(uint64_t n);
-// root_host (optional, per tree): host-coherent 64-byte slots that receive the root
+// root_host (optional, per tree; pointer mode only): host-coherent 64-byte slots that receive the root.
+// start_level 1: level 0 of `tree` already holds n digests (a tree over given digests).
 hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, int batch, uint64_t n,
-                              uint64_t* const* root_host, hipStream_t s);
+                              uint64_t* const* root_host, hipStream_t s, uint64_t leaves_ys = 0,
+                              uint64_t tree_ys = 0, int start_level = 0);
 hipError_t launch_fri_fold(fe* out, const fe* in, uint64_t half, const fe* Tlo, const fe* Thi, int shift,
                            const fe& K, const fe& Wstride, unsigned grid, hipStream_t s);
 unsigned fri_fold_grid(uint64_t half);
@@ -29,5 +35,15 @@ hipError_t launch_gather_digests(const uint64_t* tree, const uint64_t* idx, uint
 hipError_t launch_gather_digest_ptrs(const uint64_t* addrs, uint64_t* out, uint32_t count, hipStream_t s);
 hipError_t launch_gather_fe_ptrs(const uint64_t* addrs, fe* out, uint32_t count, hipStream_t s);
 hipError_t launch_gather_fe(const fe* src, const uint64_t* idx, fe* out, uint32_t count, hipStream_t s);
+
+// row-sharded helpers (four-step NTT, sharded Merkle / FRI)
+hipError_t launch_mul_pow(fe* data, uint64_t rows, uint64_t cols, uint64_t a0, uint64_t a1, uint64_t b0,
+                          uint64_t b1, const fe* T0, const fe* T1, const fe* T2, hipStream_t s);
+hipError_t launch_swap01(const fe* in, fe* out, uint64_t A, uint64_t B, uint64_t C, hipStream_t s);
+hipError_t launch_fri_fold_runs(fe* out, const fe* in, uint64_t half, uint64_t run, uint64_t run_stride,
+                                uint64_t run_off, const fe* T0, const fe* T1, const fe* T2, const fe& K,
+                                hipStream_t s);
+hipError_t launch_gather_roots(const uint64_t* tree, uint64_t tree_ys, uint64_t root_off, uint64_t* out,
+                               uint64_t count, hipStream_t s);
 
 }  // namespace sg

@@ -8,7 +8,8 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libstarkgpu.so")
+# SG_LIB_PATH: load a differently-built copy (plan experiments); default in-tree build
+LIB_PATH = os.environ.get("SG_LIB_PATH") or os.path.join(_HERE, "libstarkgpu.so")
 
 
 class StarkGpuError(RuntimeError):
@@ -102,6 +103,18 @@ PROTOTYPES = {
     "sg_fri_prove_dev": (ctypes.c_int, [_vp, _P(sg_fri), _vp, _sz, _P(sg_proof_stream), _P(_sz)]),
     "sg_fri_state_free": (None, [_vp, _vp]),
     "sg_fri_sample_indices": (ctypes.c_int, [_vp, _sz, _sz, _sz, _sz, _P(_sz)]),
+    # row-sharded blocks (multi-GPU)
+    "sg_ntt_rows_dev": (ctypes.c_int, [_vp, sg_fe, _vp, _sz, _sz, _vp, _sz]),
+    "sg_scale_dev": (ctypes.c_int, [_vp, _vp, _sz, sg_fe]),
+    "sg_mul_pow_dev": (ctypes.c_int, [_vp, sg_fe, _vp, _sz, _sz, ctypes.c_uint64, ctypes.c_uint64,
+                                      ctypes.c_uint64, ctypes.c_uint64]),
+    "sg_transpose_dev": (ctypes.c_int, [_vp, _vp, _vp, _sz, _sz, _sz]),
+    "sg_merkle_forest_dev": (ctypes.c_int, [_vp, _vp, _sz, _sz, _P(_vp)]),
+    "sg_forest_roots_dev": (ctypes.c_int, [_vp, _vp, _vp]),
+    "sg_forest_open": (ctypes.c_int, [_vp, _vp, _sz, _sz, _vp, _P(_sz)]),
+    "sg_forest_free": (None, [_vp, _vp]),
+    "sg_merkle_top_dev": (ctypes.c_int, [_vp, _vp, _sz, _P(_vp)]),
+    "sg_fri_fold_runs_dev": (ctypes.c_int, [_vp, sg_fe, sg_fe, sg_fe, _vp, _sz, _sz, _sz, _sz, _sz, _vp]),
 }
 
 _lib = None

@@ -1,0 +1,411 @@
+"""Multi-GPU LDE / NTT / Merkle / FRI commit over one node.
+
+One process per GPU; ranks talk through ``torch.distributed`` (backend "nccl",
+which is RCCL over xGMI on ROCm).  The reference is single-threaded; this module
+shards its path the way the north star asks: the codeword is split across the
+ranks and the only data exchange of a transform is ONE all-to-all at the
+four-step transpose.  Everything else is local HIP work behind the C ABI
+(``sg_ntt_rows_dev``, ``sg_mul_pow_dev``, ``sg_transpose_dev``,
+``sg_merkle_forest_dev``, ``sg_merkle_top_dev``, ``sg_fri_fold_runs_dev``).
+
+Four-step decomposition (n = N1 * N2, G ranks, N1 % G == N2 % G == 0):
+
+  input index  j = j1 + N1 * j2         output index  k = k2 + N2 * k1
+  X[k2 + N2 k1] = sum_j1 w_N1^(j1 k1) * w^(j1 k2) * sum_j2 w_N2^(j2 k2) x[j1 + N1 j2]
+
+with w_N2 = w^N1 and w_N1 = w^N2.  For a root of order exactly n the DFT is
+unique, so the result is bit-identical to the reference's radix-2 DIT
+(fft/ntt.rs:7-49); a root of smaller order is rejected (the reference's own
+callers always pass primitive roots).
+
+Shard layouts (rank g, R = N2 / G):
+
+  column shard  [N1/G][row]  row r = x[(g N1/G + r) + N1 j2] for j2 < row length
+  run shard     [N1][R]      element [k1][c] = X[k1 N2 + g R + c]
+
+The run shard is what the Merkle commit and FRI need: every k1 holds a run of R
+consecutive codeword positions, so each rank hashes N1 subtrees of R leaves,
+the N1*G run roots are all-gathered (64 B each) and every rank finishes the
+(small) top of the tree itself.  The FRI fold pairs i with i + n/2 = same k2,
+k1 + N1/2: always on the same rank, so folds are local until one run per rank
+is left, after which the (N2-element) codeword is all-gathered and the
+remaining rounds run on each rank's GPU.  Every rank computes the same roots,
+hence the same Fiat-Shamir challenges, with no broadcast.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+import torch.distributed as dist
+
+from . import api
+from ._lib import StarkGpuError, lib
+
+P = api.FIELD_PRIME
+ROOT, CODEWORD = api.ROOT, api.CODEWORD
+
+
+# ---------------------------------------------------------------- helpers
+
+def _log2(n: int) -> int:
+    if n <= 0 or n & (n - 1):
+        raise ValueError(f"{n} is not a power of two")
+    return n.bit_length() - 1
+
+
+def plan(n: int, world: int) -> Tuple[int, int]:
+    """(N1, N2) for an n-point transform over `world` ranks: N1 = 2^floor(log n / 2)."""
+    logn = _log2(n)
+    _log2(world)
+    n1 = 1 << (logn // 2)
+    n2 = n // n1
+    if n1 % world or n2 % world:
+        raise ValueError(f"n = {n} is too small for {world} ranks (needs n >= world^2)")
+    return n1, n2
+
+
+def _check_primitive(root: int, n: int) -> None:
+    # order exactly n  <=>  root^(n/2) == -1 (n a power of two >= 2)
+    if n >= 2 and api.fe_pow(root, n // 2) != P - 1:
+        raise ValueError("distributed ntt needs a root of order exactly n")
+    if n == 1 and root % P == 0:
+        raise ValueError("root must be non-zero")
+
+
+def scatter_columns(values: Sequence[int], n: int, world: int, rank: int) -> List[List[int]]:
+    """Host helper: rank `rank`'s column shard of a length-<=n vector (zero padded).
+
+    Row r is x[(rank N1/G + r) + N1 j2] for j2 < ceil(len / N1).  This is the
+    host-controlled input scatter of the four-step (inputs arrive strided).
+    """
+    n1, _ = plan(n, world)
+    d = len(values)
+    row = max(1, -(-d // n1))
+    rows = n1 // world
+    out = []
+    for r in range(rows):
+        j1 = rank * rows + r
+        out.append([int(values[j1 + n1 * j2]) if j1 + n1 * j2 < d else 0 for j2 in range(row)])
+    return out
+
+
+def scatter_columns_np(values, n: int, world: int, rank: int):
+    """scatter_columns for a (d, 2) uint64 array: returns ((N1/G) * row, 2) and the row length."""
+    import numpy as np
+    n1, _ = plan(n, world)
+    d = values.shape[0]
+    row = max(1, -(-d // n1))
+    pad = np.zeros((n1 * row, 2), dtype=np.uint64)
+    pad[:d] = values
+    rows = n1 // world
+    cols = pad.reshape(row, n1, 2).transpose(1, 0, 2)[rank * rows:(rank + 1) * rows]
+    return np.ascontiguousarray(cols).reshape(-1, 2), row
+
+
+def gather_runs_np(shards, n: int, world: int):
+    """gather_runs for (N1 * R, 2) uint64 arrays -> (n, 2) natural order."""
+    import numpy as np
+    n1, n2 = plan(n, world)
+    r = n2 // world
+    parts = [np.asarray(sh).reshape(n1, r, 2) for sh in shards]
+    return np.ascontiguousarray(np.stack(parts, axis=1)).reshape(n, 2)
+
+
+def gather_runs(shards: Sequence[Sequence[int]], n: int, world: int) -> List[int]:
+    """Host helper: natural-order vector from every rank's flattened run shard."""
+    n1, n2 = plan(n, world)
+    r = n2 // world
+    out = [0] * n
+    for g, sh in enumerate(shards):
+        for k1 in range(n1):
+            base = k1 * n2 + g * r
+            out[base:base + r] = sh[k1 * r:(k1 + 1) * r]
+    return out
+
+
+# ---------------------------------------------------------------- communicator
+
+class Comm:
+    """Equal-split all-to-all / all-gather over a torch.distributed group.
+
+    With the "nccl" (RCCL) backend device tensors go straight over xGMI; with
+    another backend (gloo) device tensors are staged through host memory.
+    """
+
+    def __init__(self, group=None):
+        self.group = group
+        if dist.is_available() and dist.is_initialized():
+            self.world = dist.get_world_size(group)
+            self.rank = dist.get_rank(group)
+            self.backend = dist.get_backend(group)
+        else:
+            self.world, self.rank, self.backend = 1, 0, "none"
+
+    def _staged(self, t: torch.Tensor) -> bool:
+        return t.is_cuda and self.backend != "nccl"
+
+    @staticmethod
+    def _sync(t: torch.Tensor) -> None:
+        if t.is_cuda:
+            torch.cuda.current_stream(t.device).synchronize()
+
+    def all_to_all(self, out: torch.Tensor, inp: torch.Tensor) -> None:
+        if self.world == 1:
+            out.copy_(inp)
+        elif self._staged(inp):
+            o = torch.empty(out.shape, dtype=out.dtype)
+            dist.all_to_all_single(o, inp.cpu(), group=self.group)
+            out.copy_(o)
+        else:
+            dist.all_to_all_single(out, inp, group=self.group)
+        self._sync(out)
+
+    def all_gather(self, out: torch.Tensor, inp: torch.Tensor) -> None:
+        if self.world == 1:
+            out.copy_(inp)
+        elif self._staged(inp):
+            o = torch.empty(out.shape, dtype=out.dtype)
+            dist.all_gather_into_tensor(o, inp.cpu(), group=self.group)
+            out.copy_(o)
+        else:
+            dist.all_gather_into_tensor(out, inp, group=self.group)
+        self._sync(out)
+
+
+# ---------------------------------------------------------------- GPU row backend
+
+class GpuRows:
+    """Local steps on this rank's GPU through libstarkgpu (the product backend).
+
+    Field buffers are int64 device tensors of 2 * count words (lo, hi limbs);
+    digest buffers are uint8 device tensors of 64 bytes per digest.
+    """
+
+    def __init__(self, ctx: Optional[api.Context] = None):
+        self.ctx = api._ctx(ctx)
+        self.device = torch.device("cuda", self.ctx.device)
+        self._lib = lib()
+
+    # buffers
+    def alloc(self, count: int) -> torch.Tensor:
+        return torch.empty(2 * count, dtype=torch.int64, device=self.device)
+
+    def alloc_digests(self, count: int) -> torch.Tensor:
+        return torch.empty(64 * count, dtype=torch.uint8, device=self.device)
+
+    def from_ints(self, values: Sequence[int]) -> torch.Tensor:
+        a = api.fe_array(values)
+        return torch.from_numpy(a.view("int64").reshape(-1).copy()).to(self.device)
+
+    def to_ints(self, buf: torch.Tensor, count: Optional[int] = None) -> List[int]:
+        t = buf.cpu().numpy().view("uint64")
+        if count is not None:
+            t = t[:2 * count]
+        return api.to_ints(t.reshape(-1, 2))
+
+    @staticmethod
+    def _p(t: torch.Tensor) -> ctypes.c_void_p:
+        return ctypes.c_void_p(t.data_ptr())
+
+    # local steps
+    def ntt_rows(self, root: int, src, n_in: int, rows: int, dst, n: int) -> None:
+        self.ctx.check(self._lib.sg_ntt_rows_dev(self.ctx.handle, api._fe(root), self._p(src), n_in, rows,
+                                                 self._p(dst), n))
+
+    def mul_pow(self, base: int, buf, rows: int, cols: int, a0: int, a1: int, b0: int, b1: int) -> None:
+        self.ctx.check(self._lib.sg_mul_pow_dev(self.ctx.handle, api._fe(base), self._p(buf), rows, cols,
+                                                a0, a1, b0, b1))
+
+    def scale(self, buf, count: int, c: int) -> None:
+        self.ctx.check(self._lib.sg_scale_dev(self.ctx.handle, self._p(buf), count, api._fe(c)))
+
+    def transpose(self, src, dst, A: int, B: int, C: int) -> None:
+        self.ctx.check(self._lib.sg_transpose_dev(self.ctx.handle, self._p(src), self._p(dst), A, B, C))
+
+    def forest_roots(self, buf, run: int, runs: int) -> torch.Tensor:
+        h = ctypes.c_void_p()
+        self.ctx.check(self._lib.sg_merkle_forest_dev(self.ctx.handle, self._p(buf), run, runs, ctypes.byref(h)))
+        try:
+            roots = self.alloc_digests(runs)
+            self.ctx.check(self._lib.sg_forest_roots_dev(self.ctx.handle, h, self._p(roots)))
+        finally:
+            self._lib.sg_forest_free(self.ctx.handle, h)
+        return roots
+
+    def digest_transpose(self, src, dst, A: int, B: int) -> None:
+        # a digest is 4 field-element slots (64 bytes)
+        self.ctx.check(self._lib.sg_transpose_dev(self.ctx.handle, self._p(src), self._p(dst), A, B, 4))
+
+    def top_root(self, digests, count: int) -> bytes:
+        h = ctypes.c_void_p()
+        self.ctx.check(self._lib.sg_merkle_top_dev(self.ctx.handle, self._p(digests), count, ctypes.byref(h)))
+        root = (ctypes.c_uint8 * 64)()
+        self._lib.sg_tree_root(h, root)
+        self._lib.sg_tree_free(self.ctx.handle, h)
+        return bytes(root)
+
+    def fold_runs(self, omega: int, offset: int, alpha: int, src, n_local: int, run: int, run_stride: int,
+                  run_off: int, n_global: int, dst) -> None:
+        self.ctx.check(self._lib.sg_fri_fold_runs_dev(self.ctx.handle, api._fe(omega), api._fe(offset),
+                                                      api._fe(alpha), self._p(src), n_local, run, run_stride,
+                                                      run_off, n_global, self._p(dst)))
+
+    def fri_commit(self, offset: int, omega: int, n: int, expansion: int, c: int, buf, proof_stream) -> None:
+        fri = api.FRI(offset, omega, n, expansion, c, ctx=self.ctx)
+        fri.commit_dev(buf.data_ptr(), n, proof_stream)
+
+    @staticmethod
+    def sample(data: bytes) -> int:
+        return api.sample(data)
+
+    @staticmethod
+    def num_rounds(n: int, expansion: int, c: int) -> int:
+        return api.FRI(1, 1, n, expansion, c).num_rounds()
+
+
+# ---------------------------------------------------------------- the distributed path
+
+class DistStark:
+    """The sharded LDE -> Merkle -> FRI-commit pipeline for one rank.
+
+    ``rows`` is the local backend (GpuRows in production); ``comm`` the group.
+    """
+
+    def __init__(self, rows=None, comm: Optional[Comm] = None):
+        self.rows = rows if rows is not None else GpuRows()
+        self.comm = comm if comm is not None else Comm()
+        self.G, self.g = self.comm.world, self.comm.rank
+
+    # ---- four-step NTT: column shard -> run shard (one all-to-all)
+    def _four_step(self, root: int, shard, row_len: int, n1: int, n2: int):
+        """X = DFT_root(x) for n = n1 n2: column shard of (n1, n2) in, run shard [n1][n2/G] out."""
+        G, g, be = self.G, self.g, self.rows
+        rows, R = n1 // G, n2 // G
+        if not 1 <= row_len <= n2:
+            raise ValueError("row length must be in [1, N2]")
+        z = be.alloc(rows * n2)
+        be.ntt_rows(api.fe_pow(root, n1), shard, row_len, rows, z, n2)        # size-N2 DFTs over j2
+        be.mul_pow(root, z, rows, n2, g * rows, 1, 0, 0)                       # * w^(j1 k2)
+        send = be.alloc(rows * n2)
+        be.transpose(z, send, rows, G, R)                                      # [j1][h][c] -> [h][j1][c]
+        del z
+        recv = be.alloc(n1 * R)
+        self.comm.all_to_all(recv, send)                                       # [j1 (all)][c]
+        del send
+        t = be.alloc(n1 * R)
+        be.transpose(recv, t, n1, R, 1)                                        # [c][j1]
+        del recv
+        u = be.alloc(n1 * R)
+        be.ntt_rows(api.fe_pow(root, n2), t, n1, R, u, n1)                     # size-N1 DFTs over j1
+        del t
+        out = be.alloc(n1 * R)
+        be.transpose(u, out, R, n1, 1)                                         # [k1][c]: run shard
+        return out
+
+    def ntt(self, root: int, shard, row_len: int, n: int):
+        """fft/ntt.rs:7-49 on a column shard (row_len <= N2 entries per row, zero padded)."""
+        _check_primitive(root, n)
+        n1, n2 = plan(n, self.G)
+        return self._four_step(root, shard, row_len, n1, n2)
+
+    def intt(self, root: int, run_shard, n: int):
+        """fft/ntt.rs:51-68 on a run shard; returns the column shard (rows of length N2).
+
+        The run shard of (N1, N2) is, transposed, the column shard of (N2, N1):
+        index k1 N2 + (g R + c) = j1' + N2 j2' with j1' = g R + c, j2' = k1.
+        So the inverse is the four-step with the factors swapped and root^-1,
+        whose run shard [N2][N1/G] transposes back to the column shard of x.
+        """
+        G, be = self.G, self.rows
+        if n < 2:
+            raise ValueError("distributed intt needs n >= 2")
+        inv_root = api.fe_inverse(root)
+        _check_primitive(inv_root, n)
+        n1, n2 = plan(n, G)
+        R = n2 // G
+        col = be.alloc(n1 * R)
+        be.transpose(run_shard, col, n1, R, 1)                     # [c][k1]: column shard of (N2, N1)
+        y = self._four_step(inv_root, col, n1, n2, n1)             # run shard [N2][N1/G]
+        be.scale(y, n1 * R, api.fe_inverse(n % P))
+        out = be.alloc(n1 * R)
+        be.transpose(y, out, n2, n1 // G, 1)                       # [N1/G][N2]
+        return out
+
+    # ---- LDE: scale by offset^j then the four-step (fft/ntt_arithmetics.rs:161-170)
+    def coset_evaluate(self, generator: int, root_order: int, offset: int, shard, row_len: int):
+        """fast_coset_evaluate on a column shard of the coefficients; returns a run shard."""
+        n = root_order
+        _log2(n)
+        n1, _ = plan(n, self.G)
+        rows = n1 // self.G
+        scaled = self.rows.alloc(rows * row_len)
+        scaled.copy_(shard[:2 * rows * row_len])
+        # coefficient j = (g rows + r) + N1 c gets offset^j
+        self.rows.mul_pow(offset, scaled, rows, row_len, n1, 0, self.g * rows, 1)
+        return self.ntt(generator, scaled, row_len, n)
+
+    # ---- Merkle root of a run shard (merkle_root.rs:21-32)
+    def merkle_root(self, run_shard, n1: int, run: int) -> bytes:
+        """Root of the natural-order codeword whose runs [k1][run] are held per rank."""
+        be, G = self.rows, self.G
+        roots = be.forest_roots(run_shard, run, n1)                # [k1] local run roots
+        allr = be.alloc_digests(G * n1)
+        self.comm.all_gather(allr, roots)                          # [g][k1]
+        ordered = be.alloc_digests(G * n1)
+        be.digest_transpose(allr, ordered, G, n1)                  # [k1][g]: global run order
+        return be.top_root(ordered, G * n1)
+
+    # ---- FRI commit on a run shard (fri.rs:115-172)
+    def fri_commit(self, offset: int, omega: int, run_shard, n: int, expansion: int, c: int, proof_stream) -> None:
+        G, g, be = self.G, self.g, self.rows
+        n1, n2 = plan(n, G)
+        R = n2 // G
+        rounds = be.num_rounds(n, expansion, c)
+        if rounds < 1:
+            raise ValueError("FRI: zero rounds for this domain")
+        cur, k1s, length = run_shard, n1, n
+        r = 0
+        while k1s > 1 and r < rounds:
+            if api.fe_pow(omega, length - 1) != api.fe_inverse(omega):
+                raise ValueError("error in commit: omega does not have the right order!")
+            proof_stream.push((ROOT, self.merkle_root(cur, k1s, R)))
+            if r == rounds - 1:
+                break
+            alpha = be.sample(proof_stream.fiat_shamir_prover(api.PROOF_BYTES))
+            nxt = be.alloc(k1s * R // 2)
+            be.fold_runs(omega, offset, alpha, cur, k1s * R, R, n2, g * R, length, nxt)
+            cur, k1s, length = nxt, k1s // 2, length // 2
+            omega = api.fe_pow(omega, 2)
+            offset = api.fe_pow(offset, 2)
+            r += 1
+        if r == rounds - 1 and k1s > 1:
+            # every round done while still sharded: gather the last codeword (fri.rs:166)
+            full = be.alloc(G * k1s * R)
+            self.comm.all_gather(full, cur)
+            shards = [be.to_ints(full[2 * q * k1s * R:2 * (q + 1) * k1s * R]) for q in range(G)]
+            proof_stream.push((CODEWORD, gather_runs_sized(shards, k1s, n2, G)))
+            return
+        # one run per rank left: the codeword (length N2) is block-distributed; gather it
+        full = be.alloc(G * R)
+        self.comm.all_gather(full, cur)
+        left = rounds - r
+        if be.num_rounds(length, expansion, c) != left:
+            raise AssertionError("FRI tail round count mismatch")
+        be.fri_commit(offset, omega, length, expansion, c, full, proof_stream)
+
+
+def gather_runs_sized(shards: Sequence[Sequence[int]], n1: int, n2: int, world: int) -> List[int]:
+    """Natural order of a codeword of n1 * n2 held as run shards [n1][n2 / world]."""
+    r = n2 // world
+    out = [0] * (n1 * n2)
+    for g, sh in enumerate(shards):
+        for k1 in range(n1):
+            out[k1 * n2 + g * r:k1 * n2 + (g + 1) * r] = sh[k1 * r:(k1 + 1) * r]
+    return out
+
+
+__all__ = ["Comm", "DistStark", "GpuRows", "plan", "scatter_columns", "scatter_columns_np", "gather_runs",
+           "gather_runs_np", "gather_runs_sized",
+           "StarkGpuError"]
