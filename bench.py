@@ -22,7 +22,9 @@ import json
 import os
 import subprocess
 import sys
+import threading
 import time
+from datetime import timedelta
 
 import numpy as np
 
@@ -168,6 +170,89 @@ def side_measurements(ctx: sg.Context, device, iters: int = 5) -> dict:
     return out
 
 
+def allreduce_max(value: float, device) -> float:
+    """max over ranks (device tensor on RCCL, host tensor on gloo)."""
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return value
+    on = device if dist.get_backend() == "nccl" else torch.device("cpu")
+    t = torch.tensor([value], dtype=torch.float64, device=on)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def c5_single_gpu(ctx: sg.Context, device, iters: int = 3) -> dict:
+    """C5's transform size (2^27, 2 GiB) as one single-GPU NTT: the 1-GPU point of the C5 curve."""
+    n = 1 << 27
+    root = sg.primitive_nth_root(n)
+    x = to_device(synthetic_fe(0, b"c5", n), device)
+    y = torch.empty_like(x)
+    sg.ntt_dev(root, x.data_ptr(), n, y.data_ptr(), ctx=ctx)
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        sg.ntt_dev(root, x.data_ptr(), n, y.data_ptr(), ctx=ctx)
+    torch.cuda.synchronize(device)
+    t = (time.perf_counter() - t0) / iters
+    del x, y
+    ctx.trim()
+    return {"c5_ntt_2p27_ms": round(t * 1e3, 3), "c5_gelem_s": round(n / t / 1e9, 3), "c5_ranks": 1,
+            "c5_alg_hbm_frac": round(32 * n / t / (HBM_PEAK_GBS * 1e9), 4)}
+
+
+def side_sharded(ctx: sg.Context, device, world: int, rank: int, iters: int = 3) -> dict:
+    """Strong-scaling side measurements over all ranks (BASELINE config C5).
+
+    * C5: one 2^27-point NTT sharded across the ranks: four-step, ONE RCCL
+      all-to-all (starkgpu/dist.py), time = max over ranks.
+    * the north-star block sharded: LDE 2^21 -> 2^24 on the coset + FRI commit
+      (exp 8, c = 64) with run-sharded Merkle trees and folds.
+    """
+    from starkgpu import dist as D
+    ds = D.DistStark(D.GpuRows(ctx), D.Comm())
+    out = {"sharded_ranks": world}
+
+    def timed(fn):
+        fn()
+        dist.barrier()
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            fn()
+        torch.cuda.synchronize(device)
+        return allreduce_max((time.perf_counter() - t0) / iters, device)
+
+    # every rank runs the same code on the same shapes, so an error is raised on all of them
+    try:
+        n = 1 << 27
+        n1, n2 = D.plan(n, world)
+        shard = to_device(synthetic_fe(rank, b"c5", (n1 // world) * n2), device)
+        root = sg.primitive_nth_root(n)
+        t = timed(lambda: ds.ntt(root, shard, n2, n))
+        out["c5_ntt_2p27_ms"] = round(t * 1e3, 3)
+        out["c5_gelem_s"] = round(n / t / 1e9, 3)
+        out["c5_plan"] = f"N1=2^{n1.bit_length() - 1} x N2=2^{n2.bit_length() - 1}, one all-to-all of " \
+                         f"{16 * n // world // 2**20} MiB per rank"
+        del shard
+    except Exception as e:  # noqa: BLE001
+        out["c5_error"] = f"{type(e).__name__}: {e}"
+    try:
+        N = 1 << 24
+        d = N // EXPANSION
+        cols, row = D.scatter_columns_np(synthetic_fe(0, b"ns", d), N, world, rank)
+        cs = to_device(cols, device)
+        omega, off = sg.primitive_nth_root(N), sg.generator()
+
+        def lde_fri():
+            cw = ds.coset_evaluate(omega, N, off, cs, row)
+            ds.fri_commit(off, omega, cw, N, EXPANSION, COLINEARITY, sg.IndependentProofStream())
+
+        out["sharded_lde_fri_commit_2p24_ms"] = round(timed(lde_fri) * 1e3, 3)
+    except Exception as e:  # noqa: BLE001
+        out["sharded_lde_fri_error"] = f"{type(e).__name__}: {e}"
+    ctx.trim()
+    return out
+
+
 def cpu_baseline_leg(seconds_budget: float = 15.0):
     """The reference-faithful C restatement (oracle/ref_cpu.c) on one host core, on a bounded sample.
 
@@ -233,13 +318,18 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
-        torch.cuda.set_device(local_rank)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    device = torch.device("cuda", local_rank)
+    # one rank per GPU; SG_BENCH_BACKEND=gloo (host-staged) lets a one-GPU box rehearse N > 1
+    backend = os.environ.get("SG_BENCH_BACKEND", "nccl")
+    gpu = local_rank % max(torch.cuda.device_count(), 1)
+    device = torch.device("cuda", gpu)
     torch.cuda.set_device(device)
+    if world > 1:
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=device, timeout=timedelta(seconds=600))
+        else:
+            dist.init_process_group(backend, timeout=timedelta(seconds=600))
 
-    ctx = sg.Context(local_rank)
+    ctx = sg.Context(gpu)
     wl = Workload(rank, device, ctx, args.log_trace)
     # warmup; the last warmup step runs with every launch timed, which yields the
     # per-kernel breakdown and picks the dominant kernel for the roofline
@@ -274,10 +364,7 @@ def main():
     ctx.profile(False)
     ctx.profile_only(None)
 
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=device)
-    if world > 1:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    elapsed = float(elapsed.item())
+    elapsed = allreduce_max(t1 - t0, device)
     ms_per_step = elapsed / args.steps * 1e3
     total_elems = wl.elements_per_step() * args.steps * world
 
@@ -327,6 +414,24 @@ def main():
     }
     if world == 1 and not args.no_side:
         result["side"] = side_measurements(ctx, device)
+        result["side"].update(c5_single_gpu(ctx, device))
+    if world > 1 and not args.no_side:
+        # a hang in a collective must not cost the main line: rank 0 prints it and exits
+        watchdog = None
+        if rank == 0:
+            def on_timeout():
+                result["side"] = {"error": "sharded side measurements timed out"}
+                print(json.dumps(result), flush=True)
+                os._exit(0)
+            watchdog = threading.Timer(300.0, on_timeout)
+            watchdog.daemon = True
+            watchdog.start()
+        try:
+            result["side"] = side_sharded(ctx, device, world, rank)
+        except Exception as e:  # noqa: BLE001 - reported in the JSON line, main metric stands
+            result["side"] = {"error": f"{type(e).__name__}: {e}"}
+        if watchdog is not None:
+            watchdog.cancel()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline_leg()
     if rank == 0:

@@ -341,7 +341,7 @@ class DistStark:
         n1, _ = plan(n, self.G)
         rows = n1 // self.G
         scaled = self.rows.alloc(rows * row_len)
-        scaled.copy_(shard[:2 * rows * row_len])
+        scaled.copy_(shard.reshape(-1)[:2 * rows * row_len])
         # coefficient j = (g rows + r) + N1 c gets offset^j
         self.rows.mul_pow(offset, scaled, rows, row_len, n1, 0, self.g * rows, 1)
         return self.ntt(generator, scaled, row_len, n)
