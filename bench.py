@@ -76,10 +76,14 @@ class Workload:
         self.fri = sg.FRI(self.offset, self.omega, self.N, EXPANSION, COLINEARITY, ctx=ctx)
 
     def step(self, phases=None):
-        # every library call returns after its device work, so host clocks time phases
+        # host clocks time the phases (a phase ends when its roots are on the host)
         ctx = self.ctx
         clk = time.perf_counter
         t0 = clk()
+        # stream-ordered device transforms: the LDEs return once enqueued and the tree
+        # builds / FRI that consume them follow on the same stream (roots are read by
+        # spinning on flags the root kernels raise), so no host round trip per stage
+        ctx.set_async(True)
         stream = sg.IndependentProofStream()
         # boundary quotients + randomizer: independent, so their LDEs and trees
         # run as one batched launch sequence each (stark.rs:367-386, 435-445)
@@ -102,6 +106,7 @@ class Workload:
         b = clk()
         top = self.fri.prove_dev(self.codewords[c].data_ptr(), self.N, stream)
         e = clk()
+        ctx.set_async(False)
         for t in trees:
             t.free()
         if phases is not None:

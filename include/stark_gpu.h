@@ -53,6 +53,12 @@ int sg_ctx_trim(sg_ctx* ctx);
 /* per-kernel HIP-event timing on the context stream (instrumentation, no reference counterpart):
  * enable resets the totals; the report is JSON {kernel: {launches, ms, bytes}} where bytes are
  * the algorithmic bytes of the launches; len receives the size incl. the NUL. */
+/* Device-pointer transforms (sg_ntt_dev, sg_intt_dev, sg_fast_coset_evaluate*_dev) return
+ * after their work completes (default) or, with async enabled, once it is enqueued on the
+ * context's stream: later library calls on the same context are ordered after it, and
+ * sg_ctx_synchronize waits for everything (needed before reading results elsewhere). */
+int sg_ctx_set_async(sg_ctx* ctx, int enable);
+int sg_ctx_synchronize(sg_ctx* ctx);
 int sg_ctx_profile(sg_ctx* ctx, int enable);
 /* restrict the timing to launches of one kernel name (NULL or "" = all) to keep event overhead low */
 int sg_ctx_profile_only(sg_ctx* ctx, const char* kernel);

@@ -289,3 +289,32 @@ def test_large_merkle_vs_c_oracle():
     x[:, 1] %= np.uint64(0xCB80000000000000)
     root = sg.MerkleRoot.commit(x)
     assert root == ref_cpu.merkle_commit(x)
+
+
+def test_async_device_transforms_are_stream_ordered():
+    """sg_ctx_set_async: LDE + tree build + FRI enqueue back to back; results unchanged."""
+    import torch
+    dev = torch.device("cuda", 0)
+    ctx = sg.Context(0)
+    N, d = 1 << 14, 1 << 11
+    w = o.primitive_nth_root(N)
+    coeffs = rnd(5, d, b"async")
+    cin = torch.from_numpy(sg.fe_array(coeffs).view(np.int64)).to(dev)
+    cw = torch.empty((N, 2), dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+    ctx.set_async(True)
+    try:
+        for _ in range(3):
+            sg.fast_coset_evaluate_dev(w, N, o.GENERATOR, cin.data_ptr(), d, cw.data_ptr(), ctx=ctx)
+            root = sg.DeviceTree(cw.data_ptr(), N, ctx=ctx).root()
+            stream = sg.IndependentProofStream()
+            top = sg.FRI(o.GENERATOR, w, N, 8, 16, ctx=ctx).prove_dev(cw.data_ptr(), N, stream)
+        ctx.synchronize()
+    finally:
+        ctx.set_async(False)
+    expect = o.fast_coset_evaluate(w, N, o.GENERATOR, coeffs)
+    assert sg.to_ints(cw.cpu().numpy().view(np.uint64)) == expect
+    assert root == o.merkle_commit(expect)
+    ref = o.IndependentProofStream()
+    assert top == o.FRI(o.GENERATOR, w, N, 8, 16).prove(expect, ref)
+    assert stream.digest() == ref.digest()

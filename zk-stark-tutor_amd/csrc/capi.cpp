@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -180,7 +181,8 @@ void ntt_run(sg_ctx* ctx, fe* const* out, const fe* const* in, int batch, uint64
     post = dpost.as<fe>();
   }
   SG_HIP(launch_ntt_fused(out, in, batch, n_in, logn, tw, sA, sB, skip, post, ctx->stream));
-  SG_HIP(hipStreamSynchronize(ctx->stream));
+  // async mode (sg_ctx_set_async): stream-ordered, the caller synchronizes
+  if (!ctx->async_dev) SG_HIP(hipStreamSynchronize(ctx->stream));
 }
 
 // out (device, next_pow2(n_in)) = ntt(root, in) ; in may alias nothing in out
@@ -216,7 +218,8 @@ extern "C" int sg_ctx_create(int device, sg_ctx** out) {
   }
   void* pinned = nullptr;
   void* pinned_dev = nullptr;
-  if (hipHostMalloc(&pinned, 4 * 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+  // 4 root slots (64 B) + 4 ready flags (u64), host-coherent
+  if (hipHostMalloc(&pinned, 4 * 64 + 4 * 8, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
       hipHostGetDevicePointer(&pinned_dev, pinned, 0) != hipSuccess) {
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -224,6 +227,7 @@ extern "C" int sg_ctx_create(int device, sg_ctx** out) {
   }
   ctx->pinned_roots = reinterpret_cast<uint64_t*>(pinned);
   ctx->pinned_roots_dev = reinterpret_cast<uint64_t*>(pinned_dev);
+  memset(pinned, 0, 4 * 64 + 4 * 8);
   *out = ctx;
   return SG_OK;
 }
@@ -237,6 +241,16 @@ extern "C" void sg_ctx_destroy(sg_ctx* ctx) {
   if (ctx->pinned_roots) (void)hipHostFree(ctx->pinned_roots);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
+}
+
+extern "C" int sg_ctx_set_async(sg_ctx* ctx, int enable) {
+  if (!ctx) return SG_ERR_INVALID;
+  ctx->async_dev = enable != 0;
+  return SG_OK;
+}
+
+extern "C" int sg_ctx_synchronize(sg_ctx* ctx) {
+  return guard(ctx, [&] { SG_HIP(hipStreamSynchronize(ctx->stream)); });
 }
 
 extern "C" int sg_ctx_profile(sg_ctx* ctx, int enable) {
@@ -437,6 +451,28 @@ struct sg_tree {
 namespace {
 inline uint64_t level_offset(uint64_t n, int level) { return 2 * n - 2 * (n >> level); }
 
+// Spin until the tree kernels have published `batch` roots (flag == seq).  The
+// stream is queried now and then so a finished-without-flag stream or a kernel
+// error surfaces instead of spinning forever.
+void wait_roots(sg_ctx* ctx, int batch, uint64_t seq) {
+  volatile uint64_t* flags = ctx->pinned_roots + 32;
+  for (int b = 0; b < batch; ++b) {
+    uint32_t spins = 0;
+    while (flags[b] != seq) {
+      if ((++spins & 255) == 0) {
+        hipError_t q = hipStreamQuery(ctx->stream);
+        if (q == hipSuccess) {
+          if (flags[b] != seq) throw Error{SG_ERR_HIP, "tree root was not published"};
+          break;
+        }
+        if (q != hipErrorNotReady) SG_HIP(q);
+      }
+      __builtin_ia32_pause();
+    }
+  }
+  std::atomic_thread_fence(std::memory_order_acquire);
+}
+
 // merkle_root.rs:21-32 for `batch` equal-size trees in one launch sequence
 void build_trees(sg_ctx* ctx, const fe* const* d_leaves, int batch, uint64_t n, std::unique_ptr<sg_tree>* out) {
   SG_REQUIRE(n > 0 && (n & (n - 1)) == 0, "Leafs len must be power of two");
@@ -449,13 +485,32 @@ void build_trees(sg_ctx* ctx, const fe* const* d_leaves, int batch, uint64_t n, 
     out[b]->buf = DevBuf(ctx, merkle_tree_digests(n) * 64);
     bufs[b] = out[b]->buf.as<uint64_t>();
   }
-  // the kernel that computes each root also stores it into pinned host memory,
-  // so reading the roots needs only the stream synchronization
+  // the kernel that computes each root also stores it into pinned host memory and
+  // then raises a ready flag: the host spins on the flags instead of a blocking
+  // stream synchronisation, so its next launches (Fiat-Shamir -> fold -> next
+  // tree) follow the root within microseconds
   uint64_t* roots_dev[4] = {nullptr, nullptr, nullptr, nullptr};
-  for (int b = 0; b < batch; ++b) roots_dev[b] = ctx->pinned_roots_dev + 8 * b;
-  SG_HIP(launch_merkle_tree(d_leaves, bufs, batch, n, roots_dev, ctx->stream));
-  SG_HIP(hipStreamSynchronize(ctx->stream));
+  uint64_t* flags_dev[4] = {nullptr, nullptr, nullptr, nullptr};
+  for (int b = 0; b < batch; ++b) {
+    roots_dev[b] = ctx->pinned_roots_dev + 8 * b;
+    flags_dev[b] = ctx->pinned_roots_dev + 32 + b;
+  }
+  const uint64_t seq = ++ctx->root_seq;
+  SG_HIP(launch_merkle_tree(d_leaves, bufs, batch, n, roots_dev, ctx->stream, 0, 0, 0, flags_dev, seq));
+  wait_roots(ctx, batch, seq);
   for (int b = 0; b < batch; ++b) memcpy(out[b]->root, ctx->pinned_roots + 8 * b, 64);
+}
+
+// build into a tree whose buffer is already allocated; with `fold`, the leaves are
+// the FRI fold of fold->src, computed by the leaf kernel and stored to d_leaves
+void fill_tree(sg_ctx* ctx, const fe* d_leaves, sg_tree* t, const FoldLeaves* fold = nullptr) {
+  uint64_t* buf = t->buf.as<uint64_t>();
+  uint64_t* root_dev = ctx->pinned_roots_dev;
+  uint64_t* flag_dev = ctx->pinned_roots_dev + 32;
+  const uint64_t seq = ++ctx->root_seq;
+  SG_HIP(launch_merkle_tree(&d_leaves, &buf, 1, t->n, &root_dev, ctx->stream, 0, 0, 0, &flag_dev, seq, fold));
+  wait_roots(ctx, 1, seq);
+  memcpy(t->root, ctx->pinned_roots, 64);
 }
 
 sg_tree* build_tree(sg_ctx* ctx, const fe* d_leaves, uint64_t n) {
@@ -673,7 +728,8 @@ extern "C" int sg_stream_deserialize(const uint8_t* bytes, size_t len, sg_stream
 // ======================================================================== C ABI: FRI
 
 struct sg_fri_state {
-  std::vector<DevBuf> codewords;  // round r codeword (device)
+  std::vector<DevBuf> codewords;  // round r codeword (device); [0] empty when borrowed
+  std::vector<const sg::fe*> cw;  // round r codeword pointer (the caller's buffer for a borrowed round 0)
   std::vector<uint64_t> lengths;
   std::vector<std::unique_ptr<sg_tree>> trees;
 };
@@ -695,6 +751,12 @@ void push_obj(const sg_proof_stream* ps, uint8_t code, const uint8_t* p, size_t 
   if (ps->push(ps->user, code, p, len) != 0) throw Error{SG_ERR_CALLBACK, "proof stream push callback failed"};
 }
 
+void put_u128_be_at(uint8_t* out, const fe& a) {
+  uint64_t hi = fe_hi(a), lo = fe_lo(a);
+  for (int i = 0; i < 8; ++i) out[i] = (uint8_t)(hi >> (8 * (7 - i)));
+  for (int i = 0; i < 8; ++i) out[8 + i] = (uint8_t)(lo >> (8 * (7 - i)));
+}
+
 void put_u128_be(std::vector<uint8_t>& out, const fe& a) {
   uint64_t hi = fe_hi(a), lo = fe_lo(a);
   for (int i = 7; i >= 0; --i) out.push_back((uint8_t)(hi >> (8 * i)));
@@ -703,7 +765,7 @@ void put_u128_be(std::vector<uint8_t>& out, const fe& a) {
 
 // fri.rs:115-172.  Retains every round's codeword and tree in `st`.
 void fri_commit_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, const sg_proof_stream* ps,
-                    sg_fri_state& st) {
+                    sg_fri_state& st, bool borrow_input = false) {
   SG_REQUIRE(ps && ps->push && ps->fiat_shamir_prover, "proof stream callbacks required");
   size_t rounds = fri_num_rounds(f);
   SG_REQUIRE(rounds >= 1, "FRI: zero rounds for this domain");
@@ -718,41 +780,76 @@ void fri_commit_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, co
   const fe inv2 = fe_inv(fe_from_u64(2));
 
   // round 0 codeword: copy into a state-owned buffer
-  st.codewords.emplace_back(ctx, n * sizeof(fe));
+  // round 0 codeword: borrowed when the state dies inside the call (prove), else copied
+  if (borrow_input) {
+    st.codewords.emplace_back();
+    st.cw.push_back(d_cw);
+  } else {
+    st.codewords.emplace_back(ctx, n * sizeof(fe));
+    SG_HIP(hipMemcpyAsync(st.codewords[0].get(), d_cw, n * sizeof(fe), hipMemcpyDeviceToDevice, ctx->stream));
+    st.cw.push_back(st.codewords[0].as<fe>());
+  }
   st.lengths.push_back(n);
-  SG_HIP(hipMemcpyAsync(st.codewords[0].get(), d_cw, n * sizeof(fe), hipMemcpyDeviceToDevice, ctx->stream));
 
-  uint64_t len = n;
+  // Everything that does not depend on a challenge is prepared before round 0
+  // (buffers, fold constants, the fri.rs:133 order checks), so between a root
+  // reaching the host and the fold starting there is only Fiat-Shamir + K.
+  struct RoundPlan {
+    uint64_t len;
+    fe omega, oinv, winv;
+  };
+  std::vector<RoundPlan> plan(rounds);
+  {
+    uint64_t len = n;
+    for (size_t r = 0; r < rounds; ++r) {
+      plan[r] = {len, omega, oinv, winv};
+      omega = fe_mul(omega, omega);
+      winv = fe_mul(winv, winv);
+      oinv = fe_mul(oinv, oinv);
+      len /= 2;
+    }
+  }
+  std::vector<std::unique_ptr<sg_tree>> trees(rounds);
   for (size_t r = 0; r < rounds; ++r) {
+    trees[r].reset(new sg_tree());
+    trees[r]->n = plan[r].len;
+    trees[r]->logn = ilog2_exact(plan[r].len);
+    trees[r]->buf = DevBuf(ctx, merkle_tree_digests(plan[r].len) * 64);
+    if (r + 1 < rounds) {
+      st.codewords.emplace_back(ctx, (plan[r].len / 2) * sizeof(fe));
+      st.cw.push_back(st.codewords.back().as<fe>());
+      st.lengths.push_back(plan[r].len / 2);
+    }
+  }
+  // Round r >= 1 hashes the fold of round r-1 in the same launch that computes it
+  // (the fold is written out too: later rounds and the query phase read it).
+  FoldLeaves fold{};
+  for (size_t r = 0; r < rounds; ++r) {
+    const uint64_t len = plan[r].len;
     // assert omega^(n-1) == omega^-1 (fri.rs:133)
-    SG_REQUIRE(fe_eq(fe_pow(omega, len - 1), winv), "error in commit: omega does not have the right order!");
-    const fe* cw = st.codewords[r].as<fe>();
-    st.trees.emplace_back(build_tree(ctx, cw, len));
+    SG_REQUIRE(fe_eq(fe_pow(plan[r].omega, len - 1), plan[r].winv),
+               "error in commit: omega does not have the right order!");
+    fill_tree(ctx, st.cw[r], trees[r].get(), r ? &fold : nullptr);
+    st.trees.push_back(std::move(trees[r]));
     push_obj(ps, SG_OBJ_ROOT, st.trees.back()->root, 64);
     if (r == rounds - 1) break;
     uint8_t chal[32];
     if (ps->fiat_shamir_prover(ps->user, 32, chal) != 0)
       throw Error{SG_ERR_CALLBACK, "proof stream fiat_shamir callback failed"};
     fe alpha = fe_sample(chal, 32);
-    uint64_t half = len / 2;
-    // K = alpha * offset_r^-1 * 2^-1 (Montgomery); w_r^-i = w^-(i << r)
-    fe K = to_mont(fe_mul(fe_mul(alpha, oinv), inv2));
-    unsigned grid = fri_fold_grid(half);
-    uint64_t stride = (uint64_t)grid * 256;
-    fe Wstride = to_mont(fe_pow(winv, stride));
-    st.codewords.emplace_back(ctx, half * sizeof(fe));
-    st.lengths.push_back(half);
-    SG_HIP(launch_fri_fold(st.codewords[r + 1].as<fe>(), cw, half, Tlo, Thi, (int)r, K, Wstride, grid, ctx->stream));
-    omega = fe_mul(omega, omega);
-    offset = fe_mul(offset, offset);
-    winv = fe_mul(winv, winv);
-    oinv = fe_mul(oinv, oinv);
-    len = half;
+    // c'[i] = (c[i] + c[i + n/2]) / 2 + K w_r^-i (c[i] - c[i + n/2]), K = alpha offset_r^-1 2^-1,
+    // w_r^-i = w^-(i << r) from the round-0 tables
+    fold.src = st.cw[r];
+    fold.dst = const_cast<fe*>(st.cw[r + 1]);
+    fold.Tlo = Tlo;
+    fold.Thi = Thi;
+    fold.shift = (int)r;
+    fold.K = to_mont(fe_mul(fe_mul(alpha, plan[r].oinv), inv2));
   }
   // push last codeword (fri.rs:166)
   uint64_t last_len = st.lengths.back();
   std::vector<fe> last(last_len);
-  SG_HIP(hipMemcpyAsync(last.data(), st.codewords.back().get(), last_len * sizeof(fe), hipMemcpyDeviceToHost,
+  SG_HIP(hipMemcpyAsync(last.data(), st.cw.back(), last_len * sizeof(fe), hipMemcpyDeviceToHost,
                         ctx->stream));
   SG_HIP(hipStreamSynchronize(ctx->stream));
   std::vector<uint8_t> payload;
@@ -796,7 +893,7 @@ void sample_indices(const uint8_t* seed, size_t seed_len, size_t size, size_t re
 void fri_prove_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, const sg_proof_stream* ps,
                    size_t* top) {
   sg_fri_state st;
-  fri_commit_dev(ctx, f, d_cw, n, ps, st);
+  fri_commit_dev(ctx, f, d_cw, n, ps, st, /*borrow_input=*/true);
   SG_REQUIRE(st.codewords.size() >= 2, "FRI prove needs at least two rounds (reference indexes codewords[1])");
   uint8_t seed[32];
   if (ps->fiat_shamir_prover(ps->user, 32, seed) != 0)
@@ -820,8 +917,8 @@ void fri_prove_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, con
   fe_addr.reserve(R * c * 3);
   for (size_t r = 0; r < R; ++r) {
     uint64_t len = st.lengths[r];
-    uint64_t cur = (uint64_t)(uintptr_t)st.codewords[r].get();
-    uint64_t nxt = (uint64_t)(uintptr_t)st.codewords[r + 1].get();
+    uint64_t cur = (uint64_t)(uintptr_t)st.cw[r];
+    uint64_t nxt = (uint64_t)(uintptr_t)st.cw[r + 1];
     for (size_t s = 0; s < c; ++s) {
       size_t i = idx_per_round[r][s];
       fe_addr.push_back(cur + 16 * (uint64_t)i);
@@ -856,25 +953,27 @@ void fri_prove_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, con
     SG_HIP(hipMemcpyAsync(digs.data(), dd.get(), digs.size(), hipMemcpyDeviceToHost, ctx->stream));
     SG_HIP(hipStreamSynchronize(ctx->stream));
   }
+  // payloads are written in place (memcpy) into one reused buffer per object kind
   size_t fpos = 0, dpos = 0;
+  uint8_t leafs[48];
   std::vector<uint8_t> obj;
   for (size_t r = 0; r < R; ++r) {
     for (size_t s = 0; s < c; ++s) {
-      obj.clear();
-      put_u128_be(obj, vals[fpos + 3 * s]);
-      put_u128_be(obj, vals[fpos + 3 * s + 1]);
-      put_u128_be(obj, vals[fpos + 3 * s + 2]);
-      push_obj(ps, SG_OBJ_LEAFS, obj.data(), obj.size());
+      for (int k = 0; k < 3; ++k) put_u128_be_at(leafs + 16 * k, vals[fpos + 3 * s + k]);
+      push_obj(ps, SG_OBJ_LEAFS, leafs, 48);
     }
     fpos += 3 * c;
     const size_t lc = (size_t)st.trees[r]->logn, ln = (size_t)st.trees[r + 1]->logn;
     for (size_t s = 0; s < c; ++s) {
       const size_t lens[3] = {lc, lc, ln};
       for (int which = 0; which < 3; ++which) {
-        obj.clear();
-        for (size_t k = 0; k < lens[which]; ++k) {
-          for (int b = 7; b >= 0; --b) obj.push_back((uint8_t)(64ull >> (8 * b)));
-          obj.insert(obj.end(), digs.begin() + (dpos + k) * 64, digs.begin() + (dpos + k + 1) * 64);
+        // Path payload: per digest [len u64 BE = 64][64 bytes] (proof_stream_enum.rs:95-110)
+        obj.resize(lens[which] * 72);
+        uint8_t* p = obj.data();
+        for (size_t k = 0; k < lens[which]; ++k, p += 72) {
+          static const uint8_t len64[8] = {0, 0, 0, 0, 0, 0, 0, 64};
+          memcpy(p, len64, 8);
+          memcpy(p + 8, digs.data() + (dpos + k) * 64, 64);
         }
         dpos += lens[which];
         push_obj(ps, SG_OBJ_PATH, obj.data(), obj.size());
@@ -892,7 +991,7 @@ extern "C" int sg_fri_commit_dev(sg_ctx* ctx, const sg_fri* fri, const sg_fe* d_
   return guard(ctx, [&] {
     SG_HIP(hipSetDevice(ctx->device));
     std::unique_ptr<sg_fri_state> st(new sg_fri_state());
-    fri_commit_dev(ctx, fri, reinterpret_cast<const fe*>(d_cw), n, ps, *st);
+    fri_commit_dev(ctx, fri, reinterpret_cast<const fe*>(d_cw), n, ps, *st, /*borrow_input=*/keep == nullptr);
     if (keep) *keep = st.release();
   });
 }

@@ -69,8 +69,10 @@ struct sg_ctx {
   // power tables keyed by (root limbs, count)
   std::map<std::pair<std::pair<uint64_t, uint64_t>, uint64_t>, sg::PowTable> pow_tables;
   // host-coherent pinned slots for tree roots (written by the kernel that computes them)
-  uint64_t* pinned_roots = nullptr;      // host view, 4 x 64 bytes
+  uint64_t* pinned_roots = nullptr;      // host view, 4 x 64 bytes, then 4 x u64 ready flags
   uint64_t* pinned_roots_dev = nullptr;  // device view of the same memory
+  uint64_t root_seq = 0;                 // last sequence number handed to a tree build
+  bool async_dev = false;                // sg_ctx_set_async: _dev transforms return once enqueued
   // per-kernel event timing (sg_ctx_profile)
   bool profiling = false;
   sg::KernelProfiler prof;

@@ -348,6 +348,18 @@ struct MerkleArgs {
   uint64_t* root_host[kMaxBatch];  // optional host-coherent copy of the root (written by the launch reaching it)
   uint64_t root_level;             // log2(n): the level whose single digest is the root
   uint64_t leaves_ys, tree_ys;     // != 0: strided rows of trees (leaves[0] + y * leaves_ys, tree[0] + y * tree_ys)
+  uint64_t* root_flag[kMaxBatch];  // with root_host: set to root_seq (system scope) once the root is visible
+  uint64_t root_seq;
+  // FRI: the leaves are the fold of the previous round's codeword (fri.rs:151-159),
+  // computed here and also stored (dst) -- one launch instead of fold + leaf hash
+  struct {
+    const fe* src;   // previous codeword (2 * first_count elements)
+    fe* dst;         // this round's codeword
+    const fe* Tlo;   // Montgomery(w^-e) tables of the round-0 omega: e & 4095, e >> 12
+    const fe* Thi;
+    int shift;       // previous round r: exponent = i << r
+    fe K;            // Montgomery(alpha * offset_r^-1 * 2^-1)
+  } fold;
 };
 
 __device__ __forceinline__ uint64_t* merkle_tree_ptr(const MerkleArgs& a) {
@@ -359,8 +371,13 @@ __device__ __forceinline__ const fe* merkle_leaves_ptr(const MerkleArgs& a) {
 __device__ __forceinline__ uint64_t* merkle_root_slot(const MerkleArgs& a) {
   return a.tree_ys ? nullptr : a.root_host[blockIdx.y];
 }
+// publish: every lane's root stores reach system scope before the ready flag
+__device__ __forceinline__ void merkle_root_publish(const MerkleArgs& a, bool writer) {
+  __threadfence_system();
+  if (writer && a.root_flag[blockIdx.y]) *(volatile uint64_t*)a.root_flag[blockIdx.y] = a.root_seq;
+}
 
-template <bool LEAF, int MAXB>
+template <bool LEAF, int MAXB, bool FOLD = false>
 __global__ __launch_bounds__(MAXB) void k_merkle_levels(MerkleArgs a) {
   __shared__ Digest sm[MAXB];
   const uint32_t tid = threadIdx.x;
@@ -371,7 +388,19 @@ __global__ __launch_bounds__(MAXB) void k_merkle_levels(MerkleArgs a) {
   if (idx < a.first_count) {
     if (LEAF) {
       uint64_t m[16];
-      uint32_t len = fe_decimal_words(ld_fe(merkle_leaves_ptr(a) + idx), m);
+      fe v;
+      if constexpr (FOLD) {
+        const fe x = ld_fe(a.fold.src + idx);
+        const fe y = ld_fe(a.fold.src + idx + a.first_count);
+        const uint64_t e = idx << a.fold.shift;
+        fe t = mont_mul(a.fold.K, ld_fe(a.fold.Tlo + (e & 4095)));
+        t = mont_mul(t, ld_fe(a.fold.Thi + (e >> 12)));
+        v = fe_add(fe_halve(fe_add(x, y)), mont_mul(fe_sub(x, y), t));
+        st_fe(a.fold.dst + idx, v);
+      } else {
+        v = ld_fe(merkle_leaves_ptr(a) + idx);
+      }
+      uint32_t len = fe_decimal_words(v, m);
 #pragma unroll
       for (int i = 5; i < 16; ++i) m[i] = 0;
       blake2b_single_block(m, len, d);
@@ -383,8 +412,10 @@ __global__ __launch_bounds__(MAXB) void k_merkle_levels(MerkleArgs a) {
       blake2b_node(l, r, d);
     }
     st_digest(tree + (a.off[1] + idx) * 8, d);
-    if (a.first_level == a.root_level && root_slot)
+    if (a.first_level == a.root_level && root_slot) {
       for (int i = 0; i < 8; ++i) root_slot[i] = d[i];
+      merkle_root_publish(a, true);
+    }
   }
   uint32_t count = blockDim.x;  // digests of this block at the current level
   for (int lev = 1; lev < a.fuse; ++lev) {
@@ -399,8 +430,10 @@ __global__ __launch_bounds__(MAXB) void k_merkle_levels(MerkleArgs a) {
       blake2b_node(l, r, d);
       uint64_t gidx = (uint64_t)blockIdx.x * count + tid;
       st_digest(tree + (a.off[lev + 1] + gidx) * 8, d);
-      if (a.first_level + lev == a.root_level && root_slot)
+      if (a.first_level + lev == a.root_level && root_slot) {
         for (int i = 0; i < 8; ++i) root_slot[i] = d[i];
+        merkle_root_publish(a, true);
+      }
     }
     __syncthreads();
   }
@@ -528,6 +561,7 @@ __global__ __launch_bounds__(256) void k_merkle_quad(MerkleArgs a) {
     if (a.first_level == a.root_level && root_slot) {
       root_slot[q] = hlo;
       root_slot[4 + q] = hhi;
+      merkle_root_publish(a, q == 0);  // the quad is one wavefront: its fence covers all 4 lanes
     }
   }
   for (int lev = 1; lev < a.fuse; ++lev) {
@@ -547,39 +581,9 @@ __global__ __launch_bounds__(256) void k_merkle_quad(MerkleArgs a) {
       if (a.first_level + lev == a.root_level && root_slot) {
         root_slot[q] = hlo;
         root_slot[4 + q] = hhi;
+        merkle_root_publish(a, q == 0);
       }
     }
-  }
-}
-
-// ------------------------------------------------------------- FRI fold
-
-struct FoldArgs {
-  fe* out;
-  const fe* in;
-  uint64_t half;        // output length
-  const fe* Tlo;        // Montgomery(w^-e) for e < 4096 (base omega of the FRI instance)
-  const fe* Thi;        // Montgomery(w^-(4096 e))
-  int shift;            // round r: exponent = i << r
-  fe K;                 // Montgomery(alpha * offset_r^-1 * 2^-1)
-  fe Wstride;           // Montgomery(w_r^-stride), stride = gridDim*blockDim
-};
-
-__global__ __launch_bounds__(256) void k_fri_fold(FoldArgs a) {
-  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= a.half) return;
-  uint64_t e = i << a.shift;
-  fe t = mont_mul(a.K, ld_fe(a.Tlo + (e & 4095)));
-  t = mont_mul(t, ld_fe(a.Thi + (e >> 12)));     // Montgomery(K * w_r^-i)
-  for (; i < a.half; i += stride) {
-    fe x = ld_fe(a.in + i);
-    fe y = ld_fe(a.in + i + a.half);
-    fe s = fe_halve(fe_add(x, y));
-    fe dxy = fe_sub(x, y);
-    fe r = fe_add(s, mont_mul(dxy, t));
-    st_fe(a.out + i, r);
-    t = mont_mul(t, a.Wstride);
   }
 }
 
@@ -910,7 +914,8 @@ uint64_t merkle_tree_digests(uint64_t n) { return 2 * n - 1; }
 
 hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, int batch, uint64_t n,
                               uint64_t* const* root_host, hipStream_t s, uint64_t leaves_ys, uint64_t tree_ys,
-                              int start_level) {
+                              int start_level, uint64_t* const* root_flag, uint64_t root_seq,
+                              const FoldLeaves* fold) {
   if (!batch_ok(batch, tree_ys) || (start_level == 0 && (leaves_ys != 0) != (tree_ys != 0))) return hipErrorInvalidValue;
   const int np = tree_ys ? 1 : batch;
   // Launch plan.  Levels 0..logn; level k has n >> k digests at offset 2n - 2(n >> k).
@@ -931,7 +936,16 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
       a.leaves[b] = (level == 0 && b < np) ? leaves[b] : nullptr;
       a.tree[b] = b < np ? tree[b] : nullptr;
       a.root_host[b] = (root_host && b < np && !tree_ys) ? root_host[b] : nullptr;
+      a.root_flag[b] = (a.root_host[b] && root_flag) ? root_flag[b] : nullptr;
     }
+    a.root_seq = root_seq;
+    const bool fold_here = fold && level == 0;
+    a.fold.src = fold_here ? fold->src : nullptr;
+    a.fold.dst = fold_here ? fold->dst : nullptr;
+    a.fold.Tlo = fold_here ? fold->Tlo : nullptr;
+    a.fold.Thi = fold_here ? fold->Thi : nullptr;
+    a.fold.shift = fold_here ? fold->shift : 0;
+    a.fold.K = fold_here ? fold->K : fe_zero();
     a.leaves_ys = leaves_ys;
     a.tree_ys = tree_ys;
     a.root_level = (uint64_t)logn;
@@ -973,15 +987,26 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
     // algorithmic bytes: leaves read once (16 B) + every digest of these levels written once (64 B)
     uint64_t digests = 0;
     for (int k = 0; k < fuse; ++k) digests += count >> k;
-    ProfScope ps(level == 0 ? "merkle_leaves" : (kind == 3 ? "merkle_nodes_quad" : "merkle_nodes"),
-                 batch * ((level == 0 ? 16 * count : 0) + 64 * digests), s);
+    // a fused fold reads 2 source elements and writes the folded one instead of reading the leaf
+    ProfScope ps(level == 0 ? (fold_here ? "merkle_fold_leaves" : "merkle_leaves")
+                            : (kind == 3 ? "merkle_nodes_quad" : "merkle_nodes"),
+                 batch * ((level == 0 ? (fold_here ? 48 : 16) * count : 0) + 64 * digests), s);
     const uint64_t per_block = kind == 3 ? bs / 4 : bs;
     dim3 grid((unsigned)((count + per_block - 1) / per_block), batch);
     switch (kind) {
-      case 0: hipLaunchKernelGGL((k_merkle_levels<true, 256>), grid, dim3(bs), 0, s, a); break;
-      case 1: hipLaunchKernelGGL((k_merkle_levels<true, 1024>), grid, dim3(bs), 0, s, a); break;
+      case 0:
+        if (fold_here) hipLaunchKernelGGL((k_merkle_levels<true, 256, true>), grid, dim3(bs), 0, s, a);
+        else hipLaunchKernelGGL((k_merkle_levels<true, 256>), grid, dim3(bs), 0, s, a);
+        break;
+      case 1:
+        if (fold_here) hipLaunchKernelGGL((k_merkle_levels<true, 1024, true>), grid, dim3(bs), 0, s, a);
+        else hipLaunchKernelGGL((k_merkle_levels<true, 1024>), grid, dim3(bs), 0, s, a);
+        break;
       case 2: hipLaunchKernelGGL((k_merkle_levels<false, 256>), grid, dim3(bs), 0, s, a); break;
-      case 4: hipLaunchKernelGGL((k_merkle_levels<true, 512>), grid, dim3(bs), 0, s, a); break;
+      case 4:
+        if (fold_here) hipLaunchKernelGGL((k_merkle_levels<true, 512, true>), grid, dim3(bs), 0, s, a);
+        else hipLaunchKernelGGL((k_merkle_levels<true, 512>), grid, dim3(bs), 0, s, a);
+        break;
       default: hipLaunchKernelGGL(k_merkle_quad, grid, dim3(bs), 0, s, a); break;
     }
     hipError_t e = hipGetLastError();
@@ -991,27 +1016,6 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
   return hipSuccess;
 }
 
-hipError_t launch_fri_fold(fe* out, const fe* in, uint64_t half, const fe* Tlo, const fe* Thi, int shift,
-                           const fe& K, const fe& Wstride, unsigned grid, hipStream_t s) {
-  FoldArgs a;
-  a.out = out;
-  a.in = in;
-  a.half = half;
-  a.Tlo = Tlo;
-  a.Thi = Thi;
-  a.shift = shift;
-  a.K = K;
-  a.Wstride = Wstride;
-  ProfScope ps("fri_fold", 48 * half, s);
-  hipLaunchKernelGGL(k_fri_fold, dim3(grid), dim3(256), 0, s, a);
-  return hipGetLastError();
-}
-
-unsigned fri_fold_grid(uint64_t half) {
-  uint64_t blocks = (half + 255) / 256;
-  const uint64_t cap = 256 * 16;  // grid-stride beyond 16 blocks per CU
-  return (unsigned)(blocks < cap ? blocks : cap);
-}
 
 
 // ---------------------------------------------- row-sharded helpers: launchers

@@ -24,12 +24,20 @@ hipError_t launch_ntt_fused(fe* const* out, const fe* const* in, int batch, uint
 uint64_t merkle_tree_digests(uint64_t n);
 // root_host (optional, per tree; pointer mode only): host-coherent 64-byte slots that receive the root.
 // start_level 1: level 0 of `tree` already holds n digests (a tree over given digests).
+// FRI fold fused into the leaf level: leaves = fold(src) (fri.rs:151-159), also stored to dst
+struct FoldLeaves {
+  const fe* src;
+  fe* dst;
+  const fe* Tlo;
+  const fe* Thi;
+  int shift;
+  fe K;
+};
+// root_flag (optional, with root_host): set to root_seq after the root is visible to the host.
 hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, int batch, uint64_t n,
                               uint64_t* const* root_host, hipStream_t s, uint64_t leaves_ys = 0,
-                              uint64_t tree_ys = 0, int start_level = 0);
-hipError_t launch_fri_fold(fe* out, const fe* in, uint64_t half, const fe* Tlo, const fe* Thi, int shift,
-                           const fe& K, const fe& Wstride, unsigned grid, hipStream_t s);
-unsigned fri_fold_grid(uint64_t half);
+                              uint64_t tree_ys = 0, int start_level = 0, uint64_t* const* root_flag = nullptr,
+                              uint64_t root_seq = 0, const FoldLeaves* fold = nullptr);
 hipError_t launch_gather_digests(const uint64_t* tree, const uint64_t* idx, uint64_t* out, uint32_t count,
                                  hipStream_t s);
 hipError_t launch_gather_digest_ptrs(const uint64_t* addrs, uint64_t* out, uint32_t count, hipStream_t s);

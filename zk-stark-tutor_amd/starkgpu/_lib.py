@@ -58,6 +58,8 @@ PROTOTYPES = {
     "sg_last_error": (ctypes.c_char_p, [_vp]),
     "sg_ctx_stream": (_vp, [_vp]),
     "sg_ctx_trim": (ctypes.c_int, [_vp]),
+    "sg_ctx_set_async": (ctypes.c_int, [_vp, ctypes.c_int]),
+    "sg_ctx_synchronize": (ctypes.c_int, [_vp]),
     "sg_ctx_profile": (ctypes.c_int, [_vp, ctypes.c_int]),
     "sg_ctx_profile_only": (ctypes.c_int, [_vp, ctypes.c_char_p]),
     "sg_ctx_profile_report": (ctypes.c_int, [_vp, ctypes.c_char_p, _sz, _P(_sz)]),

@@ -105,6 +105,13 @@ class Context:
     def stream(self) -> int:
         return self._lib.sg_ctx_stream(self.handle) or 0
 
+    def set_async(self, enable: bool) -> None:
+        """_dev transforms return once enqueued (stream-ordered); call synchronize() before reading."""
+        self.check(self._lib.sg_ctx_set_async(self.handle, int(enable)))
+
+    def synchronize(self) -> None:
+        self.check(self._lib.sg_ctx_synchronize(self.handle))
+
     def profile(self, enable: bool) -> None:
         """Start (resetting totals) or stop per-kernel HIP-event timing."""
         self.check(self._lib.sg_ctx_profile(self.handle, 1 if enable else 0))
