@@ -215,6 +215,36 @@ int sg_fri_fold_runs_dev(sg_ctx* ctx, sg_fe omega, sg_fe offset, sg_fe alpha, co
                          size_t n_local, size_t run, size_t run_stride, size_t run_off,
                          size_t n_global, sg_fe* d_out);
 
+/* ------------------------------------------- polynomial algebra (fft/ntt_arithmetics.rs)
+ * A polynomial is a device-resident coefficient vector owned by the library
+ * (field/polynomial.rs Polynomial: never trimmed; degree() skips trailing zeros).
+ * Outputs are the reference's exact vectors (same length, same values). */
+typedef struct sg_poly sg_poly;
+int sg_poly_create(sg_ctx* ctx, const sg_fe* coeffs, size_t len, sg_poly** out);        /* Polynomial::new */
+int sg_poly_create_dev(sg_ctx* ctx, const sg_fe* d_coeffs, size_t len, sg_poly** out);
+size_t sg_poly_len(const sg_poly* p);                                                     /* coefficients.len() */
+const sg_fe* sg_poly_data_dev(const sg_poly* p);
+int sg_poly_read(sg_ctx* ctx, const sg_poly* p, sg_fe* out);                              /* len() elements */
+int sg_poly_degree(sg_ctx* ctx, const sg_poly* p, int64_t* out); /* polynomial.rs:41-58 (-1 = None) */
+void sg_poly_free(sg_poly* p);
+/* ntt_arithmetics.rs:5-64 fast_multiply(root, root_order, lhs, rhs) */
+int sg_fast_multiply(sg_ctx* ctx, sg_fe root, uint64_t root_order, const sg_poly* lhs, const sg_poly* rhs,
+                     sg_poly** out);
+/* ntt_arithmetics.rs:239-310 fast_coset_divide(root, root_order, offset, lhs, rhs);
+ * a zero divisor value fails like the reference's "divide by zero" panic */
+int sg_fast_coset_divide(sg_ctx* ctx, sg_fe root, uint64_t root_order, sg_fe offset, const sg_poly* lhs,
+                         const sg_poly* rhs, sg_poly** out);
+/* ntt_arithmetics.rs:66-113 fast_zerofier(root, root_order, domain): geometric domains
+ * (domain[i] = root^i) in closed form on the GPU, other domains up to 1024 points */
+int sg_fast_zerofier(sg_ctx* ctx, sg_fe root, uint64_t root_order, const sg_fe* domain, size_t n, sg_poly** out);
+/* ntt_arithmetics.rs:172-237 fast_interpolate_domain(root, root_order, domain, values) */
+int sg_fast_interpolate_domain(sg_ctx* ctx, sg_fe root, uint64_t root_order, const sg_fe* domain,
+                               const sg_fe* values, size_t n, sg_poly** out);
+/* the geometric-domain forms of the two above (domain root^0 .. root^(n-1), n <= root_order) */
+int sg_fast_zerofier_geometric(sg_ctx* ctx, sg_fe root, uint64_t root_order, size_t n, sg_poly** out);
+int sg_fast_interpolate_geometric_dev(sg_ctx* ctx, sg_fe root, uint64_t root_order, const sg_fe* d_values,
+                                      size_t n, sg_poly** out);
+
 #ifdef __cplusplus
 }
 #endif

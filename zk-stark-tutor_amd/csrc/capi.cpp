@@ -17,6 +17,7 @@
 #include "host_hash.hpp"
 #include "kernels.hpp"
 #include "transcript.hpp"
+#include "internal.hpp"
 
 using namespace sg;
 
@@ -126,39 +127,7 @@ const fe* sg_ctx::stage_twiddles(const fe& root, int logn) {
 
 // ======================================================================== helpers
 
-namespace {
-
-inline fe to_fe(sg_fe a) { return fe_make(a.lo, a.hi); }
-inline sg_fe from_fe(const fe& a) { return sg_fe{fe_lo(a), fe_hi(a)}; }
-
-template <class F>
-int guard(sg_ctx* ctx, F&& f) {
-  struct ProfBind {
-    KernelProfiler* prev;
-    explicit ProfBind(sg_ctx* c) : prev(g_prof) { g_prof = (c && c->profiling) ? &c->prof : nullptr; }
-    ~ProfBind() { g_prof = prev; }
-  } bind(ctx);
-  try {
-    f();
-    return SG_OK;
-  } catch (const Error& e) {
-    if (ctx) ctx->last_error = e.msg;
-    return e.code;
-  } catch (const std::bad_alloc&) {
-    if (ctx) ctx->last_error = "host allocation failed";
-    return SG_ERR_NOMEM;
-  } catch (...) {
-    if (ctx) ctx->last_error = "unknown error";
-    return SG_ERR_INVALID;
-  }
-}
-
-inline int ilog2_exact(uint64_t n) {
-  int l = 0;
-  while (((uint64_t)1 << l) < n) ++l;
-  return l;
-}
-inline uint64_t next_pow2(uint64_t n) { return n <= 1 ? 1 : (uint64_t)1 << ilog2_exact(n); }
+namespace sg {
 
 void check_canonical(const sg_fe* v, size_t n, const char* what) {
   for (size_t i = 0; i < n; ++i)
@@ -202,7 +171,7 @@ void ntt_dev(sg_ctx* ctx, const fe& root, const fe* d_in, uint64_t n_in, fe* d_o
   ntt_run(ctx, &d_out, &d_in, 1, n_in, logn, root, sA, sB, 0, post);
 }
 
-}  // namespace
+}  // namespace sg
 
 // ======================================================================== C ABI: context
 
@@ -238,6 +207,7 @@ extern "C" void sg_ctx_destroy(sg_ctx* ctx) {
   ctx->trim();
   for (auto& kv : ctx->pow_tables) (void)hipFree(kv.second.ptr);
   for (auto& kv : ctx->stage_tables) (void)hipFree(kv.second);
+  for (auto& kv : ctx->interp_tables) (void)hipFree(kv.second);
   if (ctx->pinned_roots) (void)hipHostFree(ctx->pinned_roots);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
@@ -297,6 +267,8 @@ extern "C" int sg_ctx_trim(sg_ctx* ctx) {
     ctx->pow_tables.clear();
     for (auto& kv : ctx->stage_tables) (void)hipFree(kv.second);
     ctx->stage_tables.clear();
+    for (auto& kv : ctx->interp_tables) (void)hipFree(kv.second);
+    ctx->interp_tables.clear();
   });
 }
 
@@ -346,7 +318,7 @@ extern "C" int sg_intt_dev(sg_ctx* ctx, sg_fe root, const sg_fe* d_in, size_t n_
   });
 }
 
-namespace {
+namespace sg {
 // fft/ntt_arithmetics.rs:161-170 for `batch` polynomials of equal length d (one launch per pass)
 void coset_evaluate_batch(sg_ctx* ctx, const fe& generator, uint64_t root_order, const fe& off,
                           const fe* const* in, size_t d, fe* const* out, int batch) {
@@ -366,7 +338,7 @@ void coset_evaluate_batch(sg_ctx* ctx, const fe& generator, uint64_t root_order,
     SG_REQUIRE(!ranges_overlap(in[b], d, out[b], n), "fast_coset_evaluate: output must not alias the input");
   ntt_run(ctx, out, in, batch, d, logn, generator, sA, sB, skip, nullptr);
 }
-}  // namespace
+}  // namespace sg
 
 extern "C" int sg_fast_coset_evaluate_dev(sg_ctx* ctx, sg_fe generator, uint64_t root_order, sg_fe offset,
                                           const sg_fe* d_coeffs, size_t d, sg_fe* d_out) {
@@ -441,15 +413,7 @@ extern "C" int sg_fast_coset_evaluate(sg_ctx* ctx, sg_fe generator, uint64_t roo
 
 // ======================================================================== C ABI: Merkle
 
-struct sg_tree {
-  uint64_t n = 0;
-  int logn = 0;
-  DevBuf buf;  // (2n - 1) digests x 8 u64
-  uint8_t root[64];
-};
-
-namespace {
-inline uint64_t level_offset(uint64_t n, int level) { return 2 * n - 2 * (n >> level); }
+namespace sg {
 
 // Spin until the tree kernels have published `batch` roots (flag == seq).  The
 // stream is queried now and then so a finished-without-flag stream or a kernel
@@ -503,7 +467,7 @@ void build_trees(sg_ctx* ctx, const fe* const* d_leaves, int batch, uint64_t n, 
 
 // build into a tree whose buffer is already allocated; with `fold`, the leaves are
 // the FRI fold of fold->src, computed by the leaf kernel and stored to d_leaves
-void fill_tree(sg_ctx* ctx, const fe* d_leaves, sg_tree* t, const FoldLeaves* fold = nullptr) {
+void fill_tree(sg_ctx* ctx, const fe* d_leaves, sg_tree* t, const FoldLeaves* fold) {
   uint64_t* buf = t->buf.as<uint64_t>();
   uint64_t* root_dev = ctx->pinned_roots_dev;
   uint64_t* flag_dev = ctx->pinned_roots_dev + 32;
@@ -533,7 +497,7 @@ void gather_digests(sg_ctx* ctx, const sg_tree* t, const std::vector<uint64_t>& 
   SG_HIP(hipMemcpyAsync(out, dout.get(), idx.size() * 64, hipMemcpyDeviceToHost, ctx->stream));
   SG_HIP(hipStreamSynchronize(ctx->stream));
 }
-}  // namespace
+}  // namespace sg
 
 extern "C" int sg_merkle_build_dev(sg_ctx* ctx, const sg_fe* d_leaves, size_t n, sg_tree** out) {
   return guard(ctx, [&] {
@@ -727,14 +691,7 @@ extern "C" int sg_stream_deserialize(const uint8_t* bytes, size_t len, sg_stream
 
 // ======================================================================== C ABI: FRI
 
-struct sg_fri_state {
-  std::vector<DevBuf> codewords;  // round r codeword (device); [0] empty when borrowed
-  std::vector<const sg::fe*> cw;  // round r codeword pointer (the caller's buffer for a borrowed round 0)
-  std::vector<uint64_t> lengths;
-  std::vector<std::unique_ptr<sg_tree>> trees;
-};
-
-namespace {
+namespace sg {
 
 size_t fri_num_rounds(const sg_fri* f) {
   // fri.rs:40-50
@@ -765,7 +722,7 @@ void put_u128_be(std::vector<uint8_t>& out, const fe& a) {
 
 // fri.rs:115-172.  Retains every round's codeword and tree in `st`.
 void fri_commit_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, const sg_proof_stream* ps,
-                    sg_fri_state& st, bool borrow_input = false) {
+                    sg_fri_state& st, bool borrow_input) {
   SG_REQUIRE(ps && ps->push && ps->fiat_shamir_prover, "proof stream callbacks required");
   size_t rounds = fri_num_rounds(f);
   SG_REQUIRE(rounds >= 1, "FRI: zero rounds for this domain");
@@ -982,7 +939,7 @@ void fri_prove_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, con
   }
 }
 
-}  // namespace
+}  // namespace sg
 
 extern "C" size_t sg_fri_num_rounds(const sg_fri* fri) { return fri ? fri_num_rounds(fri) : 0; }
 

@@ -85,6 +85,8 @@ struct sg_ctx {
   // stage-major NTT twiddles of `root` for a 2^logn transform (cached)
   const sg::fe* stage_twiddles(const sg::fe& root, int logn);
   std::map<std::pair<std::pair<uint64_t, uint64_t>, int>, void*> stage_tables;
+  // geometric interpolation kernels NTT_D(1 / (1 - q^-j)) keyed by (q limbs, D) (poly.cpp)
+  std::map<std::pair<std::pair<uint64_t, uint64_t>, uint64_t>, void*> interp_tables;
 };
 
 namespace sg {

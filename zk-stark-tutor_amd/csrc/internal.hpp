@@ -1,0 +1,94 @@
+// Library-internal helpers shared by the C-ABI translation units (capi.cpp,
+// poly.cpp, stark.cpp): error guard, element conversion, NTT/LDE drivers,
+// retained Merkle trees and the FRI driver.
+#pragma once
+#include <cstdint>
+#include <memory>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "../../include/stark_gpu.h"
+#include "context.hpp"
+#include "fe128.hpp"
+#include "kernels.hpp"
+
+// retained device tree: all 2n - 1 digests (merkle_root.rs:7-32 levels, leaf level first)
+struct sg_tree {
+  uint64_t n = 0;
+  int logn = 0;
+  sg::DevBuf buf;  // (2n - 1) digests x 8 u64
+  uint8_t root[64];
+};
+
+struct sg_fri_state {
+  std::vector<sg::DevBuf> codewords;  // round r codeword (device); [0] empty when borrowed
+  std::vector<const sg::fe*> cw;      // round r codeword pointer (the caller's buffer for a borrowed round 0)
+  std::vector<uint64_t> lengths;
+  std::vector<std::unique_ptr<sg_tree>> trees;
+};
+
+namespace sg {
+
+inline fe to_fe(sg_fe a) { return fe_make(a.lo, a.hi); }
+inline sg_fe from_fe(const fe& a) { return sg_fe{fe_lo(a), fe_hi(a)}; }
+
+// Runs f, mapping library errors to the C-ABI return code (+ ctx->last_error).
+template <class F>
+int guard(sg_ctx* ctx, F&& f) {
+  struct ProfBind {
+    KernelProfiler* prev;
+    explicit ProfBind(sg_ctx* c) : prev(g_prof) { g_prof = (c && c->profiling) ? &c->prof : nullptr; }
+    ~ProfBind() { g_prof = prev; }
+  } bind(ctx);
+  try {
+    f();
+    return SG_OK;
+  } catch (const Error& e) {
+    if (ctx) ctx->last_error = e.msg;
+    return e.code;
+  } catch (const std::bad_alloc&) {
+    if (ctx) ctx->last_error = "host allocation failed";
+    return SG_ERR_NOMEM;
+  } catch (...) {
+    if (ctx) ctx->last_error = "unknown error";
+    return SG_ERR_INVALID;
+  }
+}
+
+inline int ilog2_exact(uint64_t n) {
+  int l = 0;
+  while (((uint64_t)1 << l) < n) ++l;
+  return l;
+}
+inline uint64_t next_pow2(uint64_t n) { return n <= 1 ? 1 : (uint64_t)1 << ilog2_exact(n); }
+inline uint64_t level_offset(uint64_t n, int level) { return 2 * n - 2 * (n >> level); }
+
+void check_canonical(const sg_fe* v, size_t n, const char* what);
+bool ranges_overlap(const fe* a, uint64_t na, const fe* b, uint64_t nb);
+// bit-reversal gather + DIT stages of a 2^logn transform (optional offset^i scale via sA/sB, skip, post scale)
+void ntt_run(sg_ctx* ctx, fe* const* out, const fe* const* in, int batch, uint64_t n_in, int logn, const fe& root,
+             const fe* sA, const fe* sB, int skip, const fe* post_host);
+// out (next_pow2(n_in)) = ntt(root, in) (fft/ntt.rs:7-49); post: Montgomery constant applied to every output
+void ntt_dev(sg_ctx* ctx, const fe& root, const fe* d_in, uint64_t n_in, fe* d_out, const fe* post,
+             const fe* scale_offset);
+// fft/ntt_arithmetics.rs:161-170 for `batch` (1..4) polynomials of length d
+void coset_evaluate_batch(sg_ctx* ctx, const fe& generator, uint64_t root_order, const fe& off,
+                          const fe* const* in, size_t d, fe* const* out, int batch);
+
+void build_trees(sg_ctx* ctx, const fe* const* d_leaves, int batch, uint64_t n, std::unique_ptr<sg_tree>* out);
+sg_tree* build_tree(sg_ctx* ctx, const fe* d_leaves, uint64_t n);
+void fill_tree(sg_ctx* ctx, const fe* d_leaves, sg_tree* t, const FoldLeaves* fold = nullptr);
+void path_indices(const sg_tree* t, uint64_t index, std::vector<uint64_t>& idx);
+void gather_digests(sg_ctx* ctx, const sg_tree* t, const std::vector<uint64_t>& idx, uint8_t* out);
+
+size_t fri_num_rounds(const sg_fri* f);
+void push_obj(const sg_proof_stream* ps, uint8_t code, const uint8_t* p, size_t len);
+void put_u128_be_at(uint8_t* out, const fe& a);
+void put_u128_be(std::vector<uint8_t>& out, const fe& a);
+void fri_commit_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, const sg_proof_stream* ps,
+                    sg_fri_state& st, bool borrow_input = false);
+void fri_prove_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, const sg_proof_stream* ps,
+                   size_t* top);
+
+}  // namespace sg

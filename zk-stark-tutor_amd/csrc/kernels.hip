@@ -22,6 +22,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include "fe128.hpp"
+#include "dev_util.hpp"
 #include "blake2b.hpp"
 #include "leaf_decimal.hpp"
 #include "kernels.hpp"
@@ -35,14 +36,6 @@ constexpr int kMaxBatch = 4;  // transforms / trees per launch (blockIdx.y)
 
 // ------------------------------------------------------------------ helpers
 
-__device__ __forceinline__ fe ld_fe(const fe* p) {
-  uint4 v = *reinterpret_cast<const uint4*>(p);
-  fe r = {{v.x, v.y, v.z, v.w}};
-  return r;
-}
-__device__ __forceinline__ void st_fe(fe* p, const fe& a) {
-  *reinterpret_cast<uint4*>(p) = make_uint4(a.w[0], a.w[1], a.w[2], a.w[3]);
-}
 
 // (a + p) / 2 if a odd else a / 2 -- a * 2^-1 mod p for canonical a
 __device__ __forceinline__ fe fe_halve(const fe& a) {

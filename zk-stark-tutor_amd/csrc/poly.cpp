@@ -1,0 +1,588 @@
+// Device polynomial algebra (fft/ntt_arithmetics.rs) over the gfx950 NTT and
+// elementwise kernels, its C ABI (sg_poly_*, sg_fast_*), and small host
+// polynomials.  See poly.hpp.
+//
+// Bit-exactness: fast_multiply / fast_coset_divide follow the reference's own
+// algorithm step by step (order shrinking, padding, truncation, unscaling), so
+// they return its exact output even when a division is not exact.  Zerofiers
+// and interpolants are unique polynomials; on geometric domains (the only
+// large ones a STARK uses: omicron^0..omicron^(n-1)) they are computed in closed
+// form instead of through the reference's product / remainder trees:
+//   * prod_{i<n} (x - q^i) = sum_j (-1)^(n-j) q^((n-j)(n-j-1)/2) [n j]_q x^j
+//     (Gauss binomial theorem; [n j]_q from prefix products of (1 - q^l));
+//   * the interpolant through (q^i, y_i), i < n < D = ord(q), is the INTT_D of
+//     its values on the whole group: y_i for i < n and, for m >= n,
+//     Z(q^m) sum_i y_i / (Z'(q^i) (q^m - q^i)) -- one cyclic convolution with
+//     1 / (1 - q^-j) (3 NTTs), Z = the zerofier above.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <memory>
+#include <vector>
+
+#include "host_field.hpp"
+#include "internal.hpp"
+#include "poly.hpp"
+#include "poly_kernels.hpp"
+
+namespace sg {
+
+namespace {
+inline fe one_m() { return to_mont(fe_one()); }
+inline bool fe_is_zero_h(const fe& a) { return (a.w[0] | a.w[1] | a.w[2] | a.w[3]) == 0; }
+inline void sync_unless_async(sg_ctx* ctx) {
+  if (!ctx->async_dev) SG_HIP(hipStreamSynchronize(ctx->stream));
+}
+// two-level Montgomery power tables of f for exponents < count
+void pow_tables2(sg_ctx* ctx, const fe& f, uint64_t count, const fe** A, const fe** B) {
+  *A = ctx->pow_table(f, 4096);
+  *B = ctx->pow_table(fe_pow(f, 4096), std::max<uint64_t>((count + 4095) / 4096, 1));
+}
+}  // namespace
+
+// ------------------------------------------------------------------ buffers
+
+DPoly dpoly_alloc(sg_ctx* ctx, uint64_t len) {
+  DPoly d;
+  d.len = len;
+  if (len) d.buf = DevBuf(ctx, len * sizeof(fe));
+  return d;
+}
+
+DPoly dpoly_upload(sg_ctx* ctx, const fe* host, uint64_t len) {
+  DPoly d = dpoly_alloc(ctx, len);
+  if (len) SG_HIP(hipMemcpyAsync(d.p(), host, len * sizeof(fe), hipMemcpyHostToDevice, ctx->stream));
+  return d;
+}
+
+std::vector<fe> dpoly_download(sg_ctx* ctx, const fe* d, uint64_t len) {
+  std::vector<fe> out(len);
+  if (len) SG_HIP(hipMemcpyAsync(out.data(), d, len * sizeof(fe), hipMemcpyDeviceToHost, ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  return out;
+}
+
+DPoly dpoly_copy(sg_ctx* ctx, const fe* d, uint64_t len) {
+  DPoly o = dpoly_alloc(ctx, len);
+  if (len) SG_HIP(hipMemcpyAsync(o.p(), d, len * sizeof(fe), hipMemcpyDeviceToDevice, ctx->stream));
+  return o;
+}
+
+int64_t dev_degree(sg_ctx* ctx, const fe* d, uint64_t len) {
+  if (!len) return -1;
+  DevBuf last(ctx, 8);
+  SG_HIP(hipMemsetAsync(last.get(), 0, 8, ctx->stream));
+  SG_HIP(launch_last_nonzero(d, len, last.as<unsigned long long>(), ctx->stream));
+  unsigned long long h = 0;
+  SG_HIP(hipMemcpyAsync(&h, last.get(), 8, hipMemcpyDeviceToHost, ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  return (int64_t)h - 1;
+}
+
+// ------------------------------------------------------------------ roots
+
+fe root_of_order(uint64_t n) {
+  SG_REQUIRE(n && (n & (n - 1)) == 0, "Field does not have any roots where n > 2^119 or not a power of two.");
+  fe root = fe_generator();
+  unsigned __int128 order = (unsigned __int128)1 << 119;
+  while (order != n) {
+    root = fe_mul(root, root);
+    order >>= 1;
+  }
+  return root;
+}
+
+void check_root(const fe& root, uint64_t root_order) {
+  SG_REQUIRE(fe_eq(fe_pow(root, root_order), fe_one()), "supplied root does not have supplied root_order");
+  SG_REQUIRE(!fe_eq(fe_pow(root, root_order / 2), fe_one()), "supplied root is not a primitive of root_order");
+}
+
+// ------------------------------------------------------------------ transforms
+
+void ntt_sized(sg_ctx* ctx, const fe& root, const fe* in, uint64_t n_in, int logn, fe* out, const fe* scale_offset) {
+  const uint64_t n = (uint64_t)1 << logn;
+  SG_REQUIRE(n_in <= n, "ntt_sized: input longer than the transform");
+  SG_REQUIRE(!ranges_overlap(in, n_in, out, n), "ntt: output must not alias the input");
+  const fe* sA = nullptr;
+  const fe* sB = nullptr;
+  if (scale_offset) pow_tables2(ctx, *scale_offset, std::max<uint64_t>(n_in, 1), &sA, &sB);
+  if (n_in == 0) {
+    SG_HIP(hipMemsetAsync(out, 0, n * sizeof(fe), ctx->stream));
+    return;
+  }
+  ntt_run(ctx, &out, &in, 1, n_in, logn, root, sA, sB, 0, nullptr);
+}
+
+void intt_sized(sg_ctx* ctx, const fe& root, const fe* in, int logn, fe* out) {
+  const uint64_t n = (uint64_t)1 << logn;
+  if (n < 2) {  // fft/ntt.rs:56-58
+    SG_HIP(hipMemcpyAsync(out, in, n * sizeof(fe), hipMemcpyDeviceToDevice, ctx->stream));
+    return;
+  }
+  fe ninv_m = to_mont(fe_inv(fe_from_u64(n)));
+  ntt_run(ctx, &out, &in, 1, n, logn, fe_inv(root), nullptr, nullptr, 0, &ninv_m);
+}
+
+// ------------------------------------------------------------------ elementwise
+
+void dev_mul(sg_ctx* ctx, fe* out, const fe* a, const fe* b, uint64_t n) {
+  SG_HIP(launch_ew_mul(out, a, b, n, fe_r2(), ctx->stream));
+}
+
+void dev_div(sg_ctx* ctx, fe* out, const fe* a, const fe* b, uint64_t n) {
+  if (!n) return;
+  DevBuf flag(ctx, 4);
+  SG_HIP(hipMemsetAsync(flag.get(), 0, 4, ctx->stream));
+  SG_HIP(launch_batch_div(out, a, b, n, fe_r2(), one_m(), flag.as<unsigned>(), ctx->stream));
+  unsigned h = 0;
+  SG_HIP(hipMemcpyAsync(&h, flag.get(), 4, hipMemcpyDeviceToHost, ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  SG_REQUIRE(h == 0, "divide by zero");  // field_element.rs:82-90
+}
+
+void dev_scale_pow(sg_ctx* ctx, fe* out, const fe* in, uint64_t n, const fe& f, uint64_t start) {
+  if (!n) return;
+  const fe *A, *B;
+  pow_tables2(ctx, f, start + n, &A, &B);
+  SG_HIP(launch_mul_pow2(out, in, n, start, A, B, ctx->stream));
+}
+
+void dev_prefix_product(sg_ctx* ctx, fe* data, uint64_t n) {
+  if (!n) return;
+  uint64_t tiles = (n + 1023) / 1024;
+  if (tiles == 1) {
+    SG_HIP(launch_scan_tile(data, n, nullptr, fe_r2(), one_m(), ctx->stream));
+    return;
+  }
+  DevBuf tot(ctx, tiles * sizeof(fe));
+  SG_HIP(launch_scan_tile(data, n, tot.as<fe>(), fe_r2(), one_m(), ctx->stream));
+  dev_prefix_product(ctx, tot.as<fe>(), tiles);
+  SG_HIP(launch_scan_fix(data, n, tot.as<fe>(), fe_r2(), ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));  // tot returns to the pool
+}
+
+// ------------------------------------------------------------------ products
+
+DPoly poly_mul_exact(sg_ctx* ctx, const fe* a, uint64_t la, const fe* b, uint64_t lb) {
+  if (!la || !lb) return DPoly{};
+  const uint64_t lr = la + lb - 1;
+  DPoly out = dpoly_alloc(ctx, lr);
+  if (la * lb <= 64 || std::min(la, lb) == 1) {
+    // tiny: on the host
+    std::vector<fe> ha = dpoly_download(ctx, a, la), hb = dpoly_download(ctx, b, lb);
+    HPoly r = hp_mul(ha, hb);
+    SG_HIP(hipMemcpyAsync(out.p(), r.data(), lr * sizeof(fe), hipMemcpyHostToDevice, ctx->stream));
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+    return out;
+  }
+  const uint64_t n = next_pow2(lr);
+  const int logn = ilog2_exact(n);
+  const fe w = root_of_order(n);
+  DevBuf va(ctx, n * sizeof(fe)), vb(ctx, n * sizeof(fe)), c(ctx, n * sizeof(fe));
+  ntt_sized(ctx, w, a, la, logn, va.as<fe>());
+  ntt_sized(ctx, w, b, lb, logn, vb.as<fe>());
+  dev_mul(ctx, va.as<fe>(), va.as<fe>(), vb.as<fe>(), n);
+  intt_sized(ctx, w, va.as<fe>(), logn, c.as<fe>());
+  SG_HIP(hipMemcpyAsync(out.p(), c.get(), lr * sizeof(fe), hipMemcpyDeviceToDevice, ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  return out;
+}
+
+namespace {
+// the reference's inner(): pad to `order` (only when shorter), optional scale, ntt
+void ref_inner_ntt(sg_ctx* ctx, const fe& root, uint64_t order, const fe* p, uint64_t len, const fe* scale,
+                   DevBuf& out, uint64_t& out_len) {
+  out_len = std::max<uint64_t>(next_pow2(std::max<uint64_t>(len, 1)), order);
+  out = DevBuf(ctx, out_len * sizeof(fe));
+  ntt_sized(ctx, root, p, len, ilog2_exact(out_len), out.as<fe>(), scale);
+}
+}  // namespace
+
+DPoly fast_multiply_dev(sg_ctx* ctx, fe root, uint64_t root_order, const fe* a, uint64_t la, const fe* b,
+                        uint64_t lb) {
+  check_root(root, root_order);
+  int64_t da = dev_degree(ctx, a, la), db = dev_degree(ctx, b, lb);
+  if (da < 0 || db < 0) return DPoly{};
+  const uint64_t deg = (uint64_t)da + (uint64_t)db;
+  const uint64_t result_len = deg + 1;
+  uint64_t order = root_order;
+  while (deg < order / 2) {
+    root = fe_mul(root, root);
+    order /= 2;
+  }
+  DevBuf va, vb;
+  uint64_t na, nb;
+  ref_inner_ntt(ctx, root, order, a, la, nullptr, va, na);
+  ref_inner_ntt(ctx, root, order, b, lb, nullptr, vb, nb);
+  // Hadamard over the first `order` entries, intt over `order` entries
+  dev_mul(ctx, va.as<fe>(), va.as<fe>(), vb.as<fe>(), order);
+  DevBuf c(ctx, order * sizeof(fe));
+  intt_sized(ctx, root, va.as<fe>(), ilog2_exact(order), c.as<fe>());
+  uint64_t keep = std::min(result_len, order);
+  DPoly out = dpoly_copy(ctx, c.as<fe>(), keep);
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  return out;
+}
+
+DPoly fast_coset_divide_dev(sg_ctx* ctx, fe root, uint64_t root_order, const fe& offset, const fe* lhs, uint64_t ll,
+                            const fe* rhs, uint64_t lr) {
+  check_root(root, root_order);
+  int64_t dr = dev_degree(ctx, rhs, lr);
+  SG_REQUIRE(dr >= 0, "cannot divide by zero polynomial");
+  int64_t dl = dev_degree(ctx, lhs, ll);
+  if (dl < 0) return DPoly{};
+  SG_REQUIRE(dl >= dr, "cannot divide by polynomial of larger degree");
+  const uint64_t deg = (uint64_t)std::max(dl, dr);
+  const uint64_t result_len = (uint64_t)(dl - dr + 1);
+  uint64_t order = root_order;
+  while (deg < order / 2) {
+    root = fe_mul(root, root);
+    order /= 2;
+  }
+  DevBuf vl, vr;
+  uint64_t nl, nr;
+  ref_inner_ntt(ctx, root, order, lhs, ll, &offset, vl, nl);
+  ref_inner_ntt(ctx, root, order, rhs, lr, &offset, vr, nr);
+  dev_div(ctx, vl.as<fe>(), vl.as<fe>(), vr.as<fe>(), order);
+  DevBuf c(ctx, order * sizeof(fe));
+  intt_sized(ctx, root, vl.as<fe>(), ilog2_exact(order), c.as<fe>());
+  uint64_t keep = std::min(result_len, order);
+  DPoly out = dpoly_alloc(ctx, keep);
+  dev_scale_pow(ctx, out.p(), c.as<fe>(), keep, fe_inv(offset));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  return out;
+}
+
+// ------------------------------------------------------------------ geometric domains
+
+DPoly zerofier_geometric_dev(sg_ctx* ctx, const fe& q, uint64_t D, uint64_t n) {
+  SG_REQUIRE(n <= D, "zerofier: more points than the order of the root");
+  if (n == 0) return DPoly{};
+  if (n == D) {
+    // the whole group: the reference's last fast_multiply has degree D = order, so its
+    // size-D NTT wraps x^D - 1 onto x^0 - 1 = 0 and returns D zeros (not truncated)
+    DPoly z = dpoly_alloc(ctx, D);
+    SG_HIP(hipMemsetAsync(z.p(), 0, D * sizeof(fe), ctx->stream));
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+    return z;
+  }
+  const fe *qA, *qB;
+  pow_tables2(ctx, q, D, &qA, &qB);
+  DevBuf F(ctx, (n + 1) * sizeof(fe)), invF(ctx, (n + 1) * sizeof(fe));
+  const fe one = fe_one();
+  SG_HIP(hipMemcpyAsync(F.get(), &one, sizeof(fe), hipMemcpyHostToDevice, ctx->stream));
+  SG_HIP(launch_one_minus_pow(F.as<fe>() + 1, n, 1, qA, qB, ctx->stream));  // 1 - q^l, l = 1..n
+  dev_prefix_product(ctx, F.as<fe>(), n + 1);
+  dev_div(ctx, invF.as<fe>(), nullptr, F.as<fe>(), n + 1);
+  DPoly z = dpoly_alloc(ctx, n + 1);
+  SG_HIP(launch_qbinom(z.p(), F.as<fe>(), invF.as<fe>(), n, D, qA, qB, fe_r2(), ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  return z;
+}
+
+namespace {
+// NTT_D of b[j] = 1 / (1 - q^-j) (j >= 1), b[0] = 0; cached per (q, D)
+const fe* interp_kernel(sg_ctx* ctx, const fe& q, uint64_t D) {
+  auto key = std::make_pair(std::make_pair(fe_lo(q), fe_hi(q)), D);
+  auto it = ctx->interp_tables.find(key);
+  if (it != ctx->interp_tables.end()) return reinterpret_cast<const fe*>(it->second);
+  const fe qinv = fe_inv(q);
+  const fe *A, *B;
+  pow_tables2(ctx, qinv, D, &A, &B);
+  DevBuf b(ctx, D * sizeof(fe));
+  SG_HIP(hipMemsetAsync(b.get(), 0, sizeof(fe), ctx->stream));
+  SG_HIP(launch_one_minus_pow(b.as<fe>() + 1, D - 1, 1, A, B, ctx->stream));
+  dev_div(ctx, b.as<fe>() + 1, nullptr, b.as<fe>() + 1, D - 1);
+  void* t = nullptr;
+  SG_HIP(hipMalloc(&t, D * sizeof(fe)));
+  ntt_sized(ctx, q, b.as<fe>(), D, ilog2_exact(D), reinterpret_cast<fe*>(t));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  ctx->interp_tables[key] = t;
+  return reinterpret_cast<const fe*>(t);
+}
+}  // namespace
+
+DPoly interpolate_geometric_dev(sg_ctx* ctx, const fe& q, uint64_t D, const fe* y, uint64_t n) {
+  SG_REQUIRE(n <= D, "interpolate: more points than the order of the root");
+  SG_REQUIRE(D && (D & (D - 1)) == 0, "interpolate: root order must be a power of two");
+  if (n == 0) return DPoly{};
+  if (n == 1) return dpoly_copy(ctx, y, 1);
+  const int logD = ilog2_exact(D);
+  if (n == D) {
+    DPoly out = dpoly_alloc(ctx, D);
+    intt_sized(ctx, q, y, logD, out.p());
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+    return out;
+  }
+  // Z, Z(q^m) and Z'(q^i)
+  DPoly Z = zerofier_geometric_dev(ctx, q, D, n);
+  DevBuf Zv(ctx, D * sizeof(fe)), Zd(ctx, n * sizeof(fe)), Zdv(ctx, D * sizeof(fe));
+  ntt_sized(ctx, q, Z.p(), n + 1, logD, Zv.as<fe>());
+  SG_HIP(launch_deriv(Zd.as<fe>(), Z.p(), n, fe_r2(), ctx->stream));
+  ntt_sized(ctx, q, Zd.as<fe>(), n, logD, Zdv.as<fe>());
+  // a_i = y_i / Z'(q^i); S = a (*) b cyclically, b[j] = 1 / (1 - q^-j)
+  DevBuf a(ctx, n * sizeof(fe)), va(ctx, D * sizeof(fe)), S(ctx, D * sizeof(fe));
+  dev_div(ctx, a.as<fe>(), y, Zdv.as<fe>(), n);
+  ntt_sized(ctx, q, a.as<fe>(), n, logD, va.as<fe>());
+  dev_mul(ctx, va.as<fe>(), va.as<fe>(), interp_kernel(ctx, q, D), D);
+  intt_sized(ctx, q, va.as<fe>(), logD, S.as<fe>());
+  // values on the whole group, then the coefficients
+  const fe *iA, *iB;
+  pow_tables2(ctx, fe_inv(q), D, &iA, &iB);
+  SG_HIP(launch_interp_assemble(va.as<fe>(), y, Zv.as<fe>(), S.as<fe>(), n, D, iA, iB, fe_r2(), ctx->stream));
+  intt_sized(ctx, q, va.as<fe>(), logD, S.as<fe>());
+  DPoly out = dpoly_copy(ctx, S.as<fe>(), n);
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  return out;
+}
+
+void coset_interpolate_dev(sg_ctx* ctx, const fe* values, uint64_t L, const fe& offset, fe* out) {
+  const fe w = root_of_order(L);
+  DevBuf c(ctx, L * sizeof(fe));
+  intt_sized(ctx, w, values, ilog2_exact(L), c.as<fe>());
+  dev_scale_pow(ctx, out, c.as<fe>(), L, fe_inv(offset));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+}
+
+void coset_values_dev(sg_ctx* ctx, const fe* coeffs, uint64_t len, uint64_t L, const fe& offset, fe* out) {
+  SG_REQUIRE(len <= L, "coset values: polynomial longer than the domain");
+  ntt_sized(ctx, root_of_order(L), coeffs, len, ilog2_exact(L), out, &offset);
+}
+
+// ------------------------------------------------------------------ host polynomials
+
+int64_t hp_degree(const HPoly& a) {
+  for (int64_t i = (int64_t)a.size() - 1; i >= 0; --i)
+    if (!fe_is_zero_h(a[i])) return i;
+  return -1;
+}
+
+HPoly hp_add(const HPoly& a, const HPoly& b) {
+  if (hp_degree(a) < 0) return b;
+  if (hp_degree(b) < 0) return a;
+  HPoly r(std::max(a.size(), b.size()), fe_zero());
+  for (size_t i = 0; i < a.size(); ++i) r[i] = fe_add(r[i], a[i]);
+  for (size_t i = 0; i < b.size(); ++i) r[i] = fe_add(r[i], b[i]);
+  return r;
+}
+
+HPoly hp_neg(const HPoly& a) {
+  HPoly r(a.size());
+  for (size_t i = 0; i < a.size(); ++i) r[i] = fe_neg(a[i]);
+  return r;
+}
+
+HPoly hp_sub(const HPoly& a, const HPoly& b) { return hp_add(a, hp_neg(b)); }
+
+HPoly hp_mul(const HPoly& a, const HPoly& b) {
+  if (a.empty() || b.empty()) return {};
+  HPoly r(a.size() + b.size() - 1, fe_zero());
+  for (size_t i = 0; i < a.size(); ++i) {
+    if (fe_is_zero_h(a[i])) continue;
+    fe am = to_mont(a[i]);
+    for (size_t j = 0; j < b.size(); ++j) r[i + j] = fe_add(r[i + j], mont_mul(b[j], am));
+  }
+  return r;
+}
+
+HPoly hp_scale(const HPoly& a, const fe& f) {
+  HPoly r(a.size());
+  fe pw = fe_one();
+  for (size_t i = 0; i < a.size(); ++i) {
+    r[i] = fe_mul(pw, a[i]);
+    pw = fe_mul(pw, f);
+  }
+  return r;
+}
+
+fe hp_eval(const HPoly& a, const fe& x) {
+  fe acc = fe_zero();
+  fe xm = to_mont(x);
+  for (size_t i = a.size(); i-- > 0;) acc = fe_add(mont_mul(acc, xm), a[i]);
+  return acc;
+}
+
+HPoly hp_zerofier(const std::vector<fe>& domain) {
+  if (domain.empty()) return {};
+  HPoly acc = {fe_neg(domain[0]), fe_one()};
+  for (size_t i = 1; i < domain.size(); ++i) acc = hp_mul(acc, HPoly{fe_neg(domain[i]), fe_one()});
+  return acc;
+}
+
+HPoly hp_interpolate(const std::vector<fe>& domain, const std::vector<fe>& values) {
+  SG_REQUIRE(domain.size() == values.size(), "number of elements in domain does not match number of values");
+  const size_t n = domain.size();
+  if (n == 0) return {};
+  HPoly acc(n, fe_zero());
+  for (size_t i = 0; i < n; ++i) {
+    HPoly num = {fe_one()};
+    fe den = fe_one();
+    for (size_t j = 0; j < n; ++j) {
+      if (j == i) continue;
+      num = hp_mul(num, HPoly{fe_neg(domain[j]), fe_one()});
+      den = fe_mul(den, fe_sub(domain[i], domain[j]));
+    }
+    SG_REQUIRE(!fe_is_zero_h(den), "divide by zero");
+    fe c = fe_mul(values[i], fe_inv(den));
+    for (size_t k = 0; k < n; ++k) acc[k] = fe_add(acc[k], fe_mul(num[k], c));
+  }
+  return acc;
+}
+
+bool is_geometric(const fe* domain, uint64_t n, const fe& root) {
+  fe x = fe_one();
+  fe rm = to_mont(root);
+  for (uint64_t i = 0; i < n; ++i) {
+    if (!fe_eq(domain[i], x)) return false;
+    x = mont_mul(x, rm);
+  }
+  return true;
+}
+
+}  // namespace sg
+
+// ====================================================================== C ABI
+
+using namespace sg;
+
+namespace {
+sg_poly* wrap(DPoly&& d) {
+  sg_poly* p = new sg_poly();
+  p->d = std::move(d);
+  return p;
+}
+const fe* dptr(const sg_poly* p) { return p ? p->d.p() : nullptr; }
+uint64_t dlen(const sg_poly* p) { return p ? p->d.len : 0; }
+constexpr uint64_t kHostDomainMax = 1024;
+}  // namespace
+
+extern "C" int sg_poly_create(sg_ctx* ctx, const sg_fe* coeffs, size_t len, sg_poly** out) {
+  return guard(ctx, [&] {
+    SG_REQUIRE(out && (coeffs || !len), "null argument");
+    SG_HIP(hipSetDevice(ctx->device));
+    check_canonical(coeffs, len, "coefficients");
+    DPoly d = dpoly_upload(ctx, reinterpret_cast<const fe*>(coeffs), len);
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+    *out = wrap(std::move(d));
+  });
+}
+
+extern "C" int sg_poly_create_dev(sg_ctx* ctx, const sg_fe* d_coeffs, size_t len, sg_poly** out) {
+  return guard(ctx, [&] {
+    SG_REQUIRE(out && (d_coeffs || !len), "null argument");
+    SG_HIP(hipSetDevice(ctx->device));
+    DPoly d = dpoly_copy(ctx, reinterpret_cast<const fe*>(d_coeffs), len);
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+    *out = wrap(std::move(d));
+  });
+}
+
+extern "C" size_t sg_poly_len(const sg_poly* p) { return p ? p->d.len : 0; }
+extern "C" const sg_fe* sg_poly_data_dev(const sg_poly* p) {
+  return p ? reinterpret_cast<const sg_fe*>(p->d.p()) : nullptr;
+}
+
+extern "C" int sg_poly_read(sg_ctx* ctx, const sg_poly* p, sg_fe* out) {
+  return guard(ctx, [&] {
+    SG_REQUIRE(p && (out || !p->d.len), "null argument");
+    SG_HIP(hipSetDevice(ctx->device));
+    if (p->d.len)
+      SG_HIP(hipMemcpyAsync(out, p->d.p(), p->d.len * sizeof(fe), hipMemcpyDeviceToHost, ctx->stream));
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+  });
+}
+
+extern "C" int sg_poly_degree(sg_ctx* ctx, const sg_poly* p, int64_t* out) {
+  return guard(ctx, [&] {
+    SG_REQUIRE(p && out, "null argument");
+    SG_HIP(hipSetDevice(ctx->device));
+    *out = dev_degree(ctx, p->d.p(), p->d.len);
+  });
+}
+
+extern "C" void sg_poly_free(sg_poly* p) { delete p; }
+
+extern "C" int sg_fast_multiply(sg_ctx* ctx, sg_fe root, uint64_t root_order, const sg_poly* lhs, const sg_poly* rhs,
+                                sg_poly** out) {
+  return guard(ctx, [&] {
+    SG_REQUIRE(lhs && rhs && out, "null argument");
+    SG_HIP(hipSetDevice(ctx->device));
+    *out = wrap(fast_multiply_dev(ctx, to_fe(root), root_order, dptr(lhs), dlen(lhs), dptr(rhs), dlen(rhs)));
+  });
+}
+
+extern "C" int sg_fast_coset_divide(sg_ctx* ctx, sg_fe root, uint64_t root_order, sg_fe offset, const sg_poly* lhs,
+                                    const sg_poly* rhs, sg_poly** out) {
+  return guard(ctx, [&] {
+    SG_REQUIRE(lhs && rhs && out, "null argument");
+    SG_HIP(hipSetDevice(ctx->device));
+    *out = wrap(fast_coset_divide_dev(ctx, to_fe(root), root_order, to_fe(offset), dptr(lhs), dlen(lhs), dptr(rhs),
+                                      dlen(rhs)));
+  });
+}
+
+extern "C" int sg_fast_zerofier(sg_ctx* ctx, sg_fe root, uint64_t root_order, const sg_fe* domain, size_t n,
+                                sg_poly** out) {
+  return guard(ctx, [&] {
+    SG_REQUIRE(out && (domain || !n), "null argument");
+    SG_HIP(hipSetDevice(ctx->device));
+    check_canonical(domain, n, "domain");
+    const fe r = to_fe(root);
+    check_root(r, root_order);
+    const fe* dom = reinterpret_cast<const fe*>(domain);
+    if (n > 1 && is_geometric(dom, n, r) && n <= root_order) {
+      *out = wrap(zerofier_geometric_dev(ctx, r, root_order, n));
+      return;
+    }
+    SG_REQUIRE(n <= kHostDomainMax, "fast_zerofier: non-geometric domains above 1024 points are not supported");
+    HPoly z = hp_zerofier(std::vector<fe>(dom, dom + n));
+    DPoly d = dpoly_upload(ctx, z.data(), z.size());
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+    *out = wrap(std::move(d));
+  });
+}
+
+extern "C" int sg_fast_interpolate_domain(sg_ctx* ctx, sg_fe root, uint64_t root_order, const sg_fe* domain,
+                                          const sg_fe* values, size_t n, sg_poly** out) {
+  return guard(ctx, [&] {
+    SG_REQUIRE(out && ((domain && values) || !n), "null argument");
+    SG_HIP(hipSetDevice(ctx->device));
+    check_canonical(domain, n, "domain");
+    check_canonical(values, n, "values");
+    const fe r = to_fe(root);
+    check_root(r, root_order);
+    const fe* dom = reinterpret_cast<const fe*>(domain);
+    const fe* val = reinterpret_cast<const fe*>(values);
+    if (n > 1 && n <= root_order && is_geometric(dom, n, r)) {
+      DPoly y = dpoly_upload(ctx, val, n);
+      *out = wrap(interpolate_geometric_dev(ctx, r, root_order, y.p(), n));
+      return;
+    }
+    SG_REQUIRE(n <= kHostDomainMax,
+               "fast_interpolate_domain: non-geometric domains above 1024 points are not supported");
+    HPoly ip = hp_interpolate(std::vector<fe>(dom, dom + n), std::vector<fe>(val, val + n));
+    DPoly d = dpoly_upload(ctx, ip.data(), ip.size());
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+    *out = wrap(std::move(d));
+  });
+}
+
+extern "C" int sg_fast_zerofier_geometric(sg_ctx* ctx, sg_fe root, uint64_t root_order, size_t n, sg_poly** out) {
+  return guard(ctx, [&] {
+    SG_REQUIRE(out, "null argument");
+    SG_HIP(hipSetDevice(ctx->device));
+    check_root(to_fe(root), root_order);
+    *out = wrap(zerofier_geometric_dev(ctx, to_fe(root), root_order, n));
+  });
+}
+
+extern "C" int sg_fast_interpolate_geometric_dev(sg_ctx* ctx, sg_fe root, uint64_t root_order, const sg_fe* d_values,
+                                                 size_t n, sg_poly** out) {
+  return guard(ctx, [&] {
+    SG_REQUIRE(out && (d_values || !n), "null argument");
+    SG_HIP(hipSetDevice(ctx->device));
+    check_root(to_fe(root), root_order);
+    *out = wrap(interpolate_geometric_dev(ctx, to_fe(root), root_order, reinterpret_cast<const fe*>(d_values), n));
+  });
+}

@@ -1,0 +1,85 @@
+// Device polynomial algebra: fft/ntt_arithmetics.rs (fast_multiply, fast_zerofier,
+// fast_interpolate_domain, fast_coset_divide) on the gfx950 NTT, plus the small
+// host polynomials the STARK needs for boundary constraints.
+//
+// A polynomial is a coefficient vector that is never trimmed (field/polynomial.rs
+// keeps trailing zeros; degree() skips them).
+#pragma once
+#include <cstdint>
+#include <vector>
+
+#include "context.hpp"
+#include "fe128.hpp"
+
+struct sg_poly;
+
+namespace sg {
+
+struct DPoly {
+  DevBuf buf;
+  uint64_t len = 0;
+  fe* p() const { return buf.as<fe>(); }
+};
+
+DPoly dpoly_alloc(sg_ctx* ctx, uint64_t len);
+DPoly dpoly_upload(sg_ctx* ctx, const fe* host, uint64_t len);
+std::vector<fe> dpoly_download(sg_ctx* ctx, const fe* d, uint64_t len);
+DPoly dpoly_copy(sg_ctx* ctx, const fe* d, uint64_t len);
+
+// polynomial.rs:41-58 degree(): -1 for None (synchronizes)
+int64_t dev_degree(sg_ctx* ctx, const fe* d, uint64_t len);
+
+// primitive root of order n (field.rs:58-71)
+fe root_of_order(uint64_t n);
+// ntt_arithmetics.rs:11-24 assertions
+void check_root(const fe& root, uint64_t root_order);
+
+// size-2^logn transforms of the first n_in entries (zero beyond), optional offset^i input scale
+void ntt_sized(sg_ctx* ctx, const fe& root, const fe* in, uint64_t n_in, int logn, fe* out,
+               const fe* scale_offset = nullptr);
+void intt_sized(sg_ctx* ctx, const fe& root, const fe* in, int logn, fe* out);
+
+void dev_mul(sg_ctx* ctx, fe* out, const fe* a, const fe* b, uint64_t n);
+// out = a / b elementwise (a == nullptr: 1 / b); throws "divide by zero" on a zero divisor
+void dev_div(sg_ctx* ctx, fe* out, const fe* a, const fe* b, uint64_t n);
+// out[i] = in[i] * f^(start + i)
+void dev_scale_pow(sg_ctx* ctx, fe* out, const fe* in, uint64_t n, const fe& f, uint64_t start = 0);
+// in-place inclusive prefix product
+void dev_prefix_product(sg_ctx* ctx, fe* data, uint64_t n);
+
+// exact product (length la + lb - 1, empty if either is empty): polynomial.rs:285-308 semantics
+DPoly poly_mul_exact(sg_ctx* ctx, const fe* a, uint64_t la, const fe* b, uint64_t lb);
+// ntt_arithmetics.rs:5-64
+DPoly fast_multiply_dev(sg_ctx* ctx, fe root, uint64_t root_order, const fe* a, uint64_t la, const fe* b,
+                        uint64_t lb);
+// ntt_arithmetics.rs:239-310
+DPoly fast_coset_divide_dev(sg_ctx* ctx, fe root, uint64_t root_order, const fe& offset, const fe* lhs, uint64_t ll,
+                            const fe* rhs, uint64_t lr);
+// prod_{i<n} (x - q^i) for q of order D (ntt_arithmetics.rs:66-113 on the domain q^0..q^(n-1)), length n + 1;
+// n == D reproduces the reference's wrapped result (D zeros)
+DPoly zerofier_geometric_dev(sg_ctx* ctx, const fe& q, uint64_t D, uint64_t n);
+// the interpolant of degree < n through (q^i, y_i), i < n <= D (ntt_arithmetics.rs:172-237), length n
+DPoly interpolate_geometric_dev(sg_ctx* ctx, const fe& q, uint64_t D, const fe* y, uint64_t n);
+// coefficients (length L) of the polynomial of degree < L with P(offset w^k) = values[k], w of order L
+void coset_interpolate_dev(sg_ctx* ctx, const fe* values, uint64_t L, const fe& offset, fe* out);
+// out (length L, a power of two >= len) = [P(offset w^k)], w of order L
+void coset_values_dev(sg_ctx* ctx, const fe* coeffs, uint64_t len, uint64_t L, const fe& offset, fe* out);
+
+// ---- host polynomials (small: boundary interpolants / zerofiers, constants) ----
+using HPoly = std::vector<fe>;
+int64_t hp_degree(const HPoly& a);
+HPoly hp_add(const HPoly& a, const HPoly& b);  // polynomial.rs:251-276 (zero operand -> other)
+HPoly hp_neg(const HPoly& a);
+HPoly hp_sub(const HPoly& a, const HPoly& b);
+HPoly hp_mul(const HPoly& a, const HPoly& b);  // polynomial.rs:285-308
+HPoly hp_scale(const HPoly& a, const fe& f);
+fe hp_eval(const HPoly& a, const fe& x);
+HPoly hp_zerofier(const std::vector<fe>& domain);                                   // length n + 1 (n > 0)
+HPoly hp_interpolate(const std::vector<fe>& domain, const std::vector<fe>& values);  // length n
+bool is_geometric(const fe* domain, uint64_t n, const fe& root);                    // domain[i] == root^i
+
+}  // namespace sg
+
+struct sg_poly {
+  sg::DPoly d;
+};

@@ -1,0 +1,377 @@
+// gfx950 kernels for the polynomial algebra around the LDE:
+// pointwise products / quotients with batched inversion, prefix products, the
+// closed-form zerofier of a geometric domain, the assembly step of
+// geometric-domain interpolation, pointwise AIR evaluation and the weighted
+// combination of shifted polynomials.  All elementwise work is HBM-bound
+// integer VALU: packed 16-byte elements, one dwordx4 per lane, grid-strided.
+//
+// Conventions: data arrays are canonical; tables of constants (power tables,
+// weights) are Montgomery(x) = x R mod p, R = 2^128; `r2` = R^2 mod p turns a
+// canonical value into Montgomery form with one product.
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+#include "dev_util.hpp"
+#include "fe128.hpp"
+#include "poly_kernels.hpp"
+#include "profiler.hpp"
+
+namespace sg {
+
+namespace {
+
+constexpr unsigned kBlock = 256;
+
+__device__ __forceinline__ fe fe_one_c() { return fe_make(1, 0); }
+__device__ __forceinline__ bool fe_is_zero(const fe& a) { return (a.w[0] | a.w[1] | a.w[2] | a.w[3]) == 0; }
+
+// x^(p-2) * R for x_m = x R (Montgomery in, Montgomery out): Fermat inverse.
+// p - 2 = 0xCB7FFFFF_FFFFFFFF_FFFFFFFF_FFFFFFFF: 128-bit left-to-right square-and-multiply.
+__device__ __forceinline__ fe mont_inv(const fe& xm, const fe& one_m) {
+  fe acc = one_m;
+  const uint32_t e3 = P3 - 1u;  // top limb of p - 2 (low limbs: 0xFFFFFFFF.. except p0 - 2 wraps)
+#pragma unroll 1
+  for (int i = 127; i >= 0; --i) {
+    acc = mont_mul(acc, acc);
+    uint32_t limb = i >= 96 ? e3 : 0xFFFFFFFFu;
+    // p - 2 = (P3 << 96) + 2^96 - 1: limb 3 = P3 - 1, limbs 0..2 all ones
+    if ((limb >> (i & 31)) & 1u) acc = mont_mul(acc, xm);
+  }
+  return acc;
+}
+
+uint64_t grid_for(uint64_t n, uint64_t per_thread = 1) {
+  uint64_t threads = (n + per_thread - 1) / per_thread;
+  uint64_t b = (threads + kBlock - 1) / kBlock;
+  const uint64_t cap = 256 * 64;  // enough waves for 256 CUs; grid-stride beyond
+  return b < 1 ? 1 : (b > cap ? cap : b);
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------- elementwise
+
+// out[i] = a[i] * b[i]
+__global__ __launch_bounds__(kBlock) void k_ew_mul(fe* __restrict__ out, const fe* __restrict__ a,
+                                                   const fe* __restrict__ b, uint64_t n, fe r2) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    st_fe(out + i, mont_mul(mont_mul(ld_fe(a + i), ld_fe(b + i)), r2));
+}
+
+// out[i] = in[i] * f^(i + start) with Montgomery(f^e) = sA[e & 4095] * sB[e >> 12]
+__global__ __launch_bounds__(kBlock) void k_mul_pow2(fe* __restrict__ out, const fe* __restrict__ in, uint64_t n,
+                                                     uint64_t start, const fe* __restrict__ sA,
+                                                     const fe* __restrict__ sB) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t e = i + start;
+    fe f = mont_mul(ld_fe(sA + (e & 4095)), ld_fe(sB + (e >> 12)));
+    st_fe(out + i, mont_mul(ld_fe(in + i), f));
+  }
+}
+
+// out[i] = 1 - f^(i + start)  (f^e as above)
+__global__ __launch_bounds__(kBlock) void k_one_minus_pow(fe* __restrict__ out, uint64_t n, uint64_t start,
+                                                          const fe* __restrict__ sA, const fe* __restrict__ sB) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t e = i + start;
+    fe fm = mont_mul(ld_fe(sA + (e & 4095)), ld_fe(sB + (e >> 12)));
+    st_fe(out + i, fe_sub(fe_one_c(), mont_mul(fm, fe_one_c())));
+  }
+}
+
+// out[k] = (k + 1) * c[k + 1], k < n  (formal derivative)
+__global__ __launch_bounds__(kBlock) void k_deriv(fe* __restrict__ out, const fe* __restrict__ c, uint64_t n, fe r2) {
+  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (uint64_t)gridDim.x * blockDim.x)
+    st_fe(out + k, mont_mul(mont_mul(ld_fe(c + k + 1), fe_make(k + 1, 0)), r2));
+}
+
+// ------------------------------------------------------- batched inversion
+
+// out[i] = a[i] / b[i] (a == nullptr: 1 / b[i]).  Each lane owns K elements
+// i = t + k S (S = all lanes, coalesced), Montgomery's trick: K - 1 prefix
+// products, one Fermat inversion, 2 (K - 1) products back.  A zero divisor sets
+// *zero_flag (the reference panics: "divide by zero", field_element.rs:82-90).
+template <int K>
+__global__ __launch_bounds__(kBlock) void k_batch_div(fe* __restrict__ out, const fe* __restrict__ a,
+                                                      const fe* __restrict__ b, uint64_t n, fe r2, fe one_m,
+                                                      unsigned* __restrict__ zero_flag) {
+  const uint64_t S = (uint64_t)gridDim.x * blockDim.x;
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  fe pre[K];
+  fe acc = one_m;
+  bool zero = false;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    uint64_t i = t + k * S;
+    fe bm = one_m;
+    if (i < n) {
+      fe bv = ld_fe(b + i);
+      zero |= fe_is_zero(bv);
+      if (!fe_is_zero(bv)) bm = mont_mul(bv, r2);
+    }
+    pre[k] = acc;  // product of the elements before k
+    acc = mont_mul(acc, bm);
+  }
+  if (zero) atomicOr(zero_flag, 1u);
+  fe inv = mont_inv(acc, one_m);  // (prod b)^-1 R
+#pragma unroll
+  for (int k = K - 1; k >= 0; --k) {
+    uint64_t i = t + k * S;
+    if (i < n) {
+      fe bv = ld_fe(b + i);
+      fe bm = fe_is_zero(bv) ? one_m : mont_mul(bv, r2);
+      fe ik = mont_mul(inv, pre[k]);  // b_k^-1 R
+      inv = mont_mul(inv, bm);
+      fe av = a ? ld_fe(a + i) : fe_one_c();
+      st_fe(out + i, mont_mul(av, ik));  // a b^-1 (canonical)
+    }
+  }
+}
+
+// --------------------------------------------------------- prefix products
+
+// Inclusive prefix product over 1024-element tiles (256 lanes x 4): each lane
+// multiplies its 4 elements, the block scans the 256 lane totals in LDS
+// (Hillis-Steele), lanes rescale.  tile_tot[b] = product of tile b.
+__global__ __launch_bounds__(kBlock) void k_scan_tile(fe* __restrict__ data, uint64_t n, fe* __restrict__ tile_tot,
+                                                      fe r2, fe one_m) {
+  __shared__ fe sm[kBlock];
+  const uint64_t base = (uint64_t)blockIdx.x * 1024 + threadIdx.x * 4;
+  fe v[4];
+  fe run = one_m;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    fe x = base + k < n ? mont_mul(ld_fe(data + base + k), r2) : one_m;
+    run = mont_mul(run, x);
+    v[k] = run;
+  }
+  sm[threadIdx.x] = run;
+  __syncthreads();
+  for (unsigned off = 1; off < kBlock; off <<= 1) {
+    fe mine = sm[threadIdx.x];
+    fe other = threadIdx.x >= off ? sm[threadIdx.x - off] : one_m;
+    __syncthreads();
+    sm[threadIdx.x] = mont_mul(mine, other);
+    __syncthreads();
+  }
+  fe prefix = threadIdx.x ? sm[threadIdx.x - 1] : one_m;
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (base + k < n) st_fe(data + base + k, mont_mul(mont_mul(v[k], prefix), fe_one_c()));
+  if (threadIdx.x == kBlock - 1 && tile_tot) st_fe(tile_tot + blockIdx.x, mont_mul(sm[kBlock - 1], fe_one_c()));
+}
+
+// data[i] *= scanned_tot[tile(i) - 1] for tiles >= 1
+__global__ __launch_bounds__(kBlock) void k_scan_fix(fe* __restrict__ data, uint64_t n,
+                                                     const fe* __restrict__ scanned_tot, fe r2) {
+  for (uint64_t i = 1024 + (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+       i += (uint64_t)gridDim.x * blockDim.x) {
+    fe f = ld_fe(scanned_tot + (i / 1024) - 1);
+    st_fe(data + i, mont_mul(mont_mul(ld_fe(data + i), f), r2));
+  }
+}
+
+// ------------------------------------------- zerofier of a geometric domain
+
+// Z(x) = prod_{i<n} (x - q^i) = sum_j c_j x^j,
+// c_j = (-1)^(n-j) q^((n-j)(n-j-1)/2) F_n / (F_j F_(n-j)), F_k = prod_{l=1..k} (1 - q^l)
+// (Gauss binomial theorem).  F and invF hold F_0..F_n canonical; q^e from the
+// two-level Montgomery table (e reduced mod ord(q) = D, a power of two).
+__global__ __launch_bounds__(kBlock) void k_qbinom(fe* __restrict__ c, const fe* __restrict__ F,
+                                                   const fe* __restrict__ invF, uint64_t n, uint64_t D,
+                                                   const fe* __restrict__ qA, const fe* __restrict__ qB, fe r2) {
+  const fe Fn = ld_fe(F + n);
+  for (uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; j <= n; j += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t k = n - j;
+    unsigned __int128 tri = (unsigned __int128)k * (k ? k - 1 : 0) / 2;
+    uint64_t e = (uint64_t)(tri & (unsigned __int128)(D - 1));
+    fe qm = mont_mul(ld_fe(qA + (e & 4095)), ld_fe(qB + (e >> 12)));  // Montgomery(q^e)
+    fe v = mont_mul(mont_mul(Fn, ld_fe(invF + j)), r2);               // canonical F_n / F_j
+    v = mont_mul(mont_mul(v, ld_fe(invF + k)), r2);                    // / F_(n-j)
+    v = mont_mul(v, qm);                                               // * q^e
+    if (k & 1) v = fe_neg(v);
+    st_fe(c + j, v);
+  }
+}
+
+// V[m] = y[m] for m < n, else Zv[m] * q^-m * S[m]   (q^-m from the two-level table)
+__global__ __launch_bounds__(kBlock) void k_interp_assemble(fe* __restrict__ V, const fe* __restrict__ y,
+                                                            const fe* __restrict__ Zv, const fe* __restrict__ S,
+                                                            uint64_t n, uint64_t D, const fe* __restrict__ iA,
+                                                            const fe* __restrict__ iB, fe r2) {
+  for (uint64_t m = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; m < D; m += (uint64_t)gridDim.x * blockDim.x) {
+    fe v;
+    if (m < n) {
+      v = ld_fe(y + m);
+    } else {
+      fe im = mont_mul(ld_fe(iA + (m & 4095)), ld_fe(iB + (m >> 12)));  // Montgomery(q^-m)
+      v = mont_mul(ld_fe(Zv + m), im);                                   // Zv q^-m
+      v = mont_mul(mont_mul(v, ld_fe(S + m)), r2);                       // * S
+    }
+    st_fe(V + m, v);
+  }
+}
+
+// --------------------------------------------------------------- degree
+
+// *last = max{i + 1 : a[i] != 0} (0 when all zero): degree() = *last - 1 (polynomial.rs:41-58)
+__global__ __launch_bounds__(kBlock) void k_last_nonzero(const fe* __restrict__ a, uint64_t n,
+                                                         unsigned long long* __restrict__ last) {
+  unsigned long long best = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    if (!fe_is_zero(ld_fe(a + i))) best = i + 1;
+  // wave-level max, then one atomic per wave
+  for (int off = 32; off > 0; off >>= 1) {
+    unsigned long long o = __shfl_xor(best, off);
+    best = o > best ? o : best;
+  }
+  if ((threadIdx.x & 63) == 0 && best) atomicMax(last, best);
+}
+
+// ----------------------------------------------------------- AIR evaluation
+
+// out[y] = sum_g Q_g[y] * prod_j V_j[y]^exps[g][j]  (m_polynomial.rs:124-139 evaluated
+// pointwise on a coset: Q_g are the coset values of the x-polynomial of group g).
+__global__ __launch_bounds__(kBlock) void k_air_eval(AirEvalArgs a) {
+  for (uint64_t y = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; y < a.n; y += (uint64_t)gridDim.x * blockDim.x) {
+    fe vm[kAirMaxVars];
+#pragma unroll
+    for (int j = 0; j < kAirMaxVars; ++j)
+      vm[j] = j < a.nvars ? mont_mul(ld_fe(a.V[j] + y), a.r2) : a.one_m;
+    fe acc = fe_zero();
+    for (int g = 0; g < a.ngroups; ++g) {
+      fe prod = mont_mul(ld_fe(a.Q[g] + y), a.r2);
+      const uint32_t* e = a.exps + g * a.nvars;
+      for (int j = 0; j < a.nvars; ++j) {
+        uint32_t ej = e[j];
+        if (!ej) continue;
+        fe pw = a.one_m;
+        fe base = vm[0];
+#pragma unroll
+        for (int jj = 1; jj < kAirMaxVars; ++jj)
+          if (jj == j) base = vm[jj];
+        int top = 31 - __builtin_clz(ej);
+        for (int b = top; b >= 0; --b) {
+          pw = mont_mul(pw, pw);
+          if ((ej >> b) & 1u) pw = mont_mul(pw, base);
+        }
+        prod = mont_mul(prod, pw);
+      }
+      acc = fe_add(acc, prod);
+    }
+    st_fe(a.out + y, mont_mul(acc, fe_one_c()));
+  }
+}
+
+// ------------------------------------------------------- linear combination
+
+// out[k] = sum_t w_t * term_t[k - off_t] over off_t <= k < off_t + len_t (w_t Montgomery)
+__global__ __launch_bounds__(kBlock) void k_lincomb(LinCombArgs a) {
+  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < a.n; k += (uint64_t)gridDim.x * blockDim.x) {
+    fe acc = fe_zero();
+    for (int t = 0; t < a.nterms; ++t) {
+      uint64_t off = a.off[t];
+      if (k >= off && k - off < a.len[t]) acc = fe_add(acc, mont_mul(ld_fe(a.term[t] + (k - off)), a.w[t]));
+    }
+    st_fe(a.out + k, acc);
+  }
+}
+
+// ================================================================ launchers
+
+hipError_t launch_ew_mul(fe* out, const fe* a, const fe* b, uint64_t n, const fe& r2, hipStream_t s) {
+  if (!n) return hipSuccess;
+  ProfScope ps("ew_mul", 48 * n, s);
+  hipLaunchKernelGGL(k_ew_mul, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, s, out, a, b, n, r2);
+  return hipGetLastError();
+}
+
+hipError_t launch_mul_pow2(fe* out, const fe* in, uint64_t n, uint64_t start, const fe* sA, const fe* sB,
+                           hipStream_t s) {
+  if (!n) return hipSuccess;
+  ProfScope ps("mul_pow2", 32 * n, s);
+  hipLaunchKernelGGL(k_mul_pow2, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, s, out, in, n, start, sA, sB);
+  return hipGetLastError();
+}
+
+hipError_t launch_one_minus_pow(fe* out, uint64_t n, uint64_t start, const fe* sA, const fe* sB, hipStream_t s) {
+  if (!n) return hipSuccess;
+  ProfScope ps("one_minus_pow", 16 * n, s);
+  hipLaunchKernelGGL(k_one_minus_pow, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, s, out, n, start, sA, sB);
+  return hipGetLastError();
+}
+
+hipError_t launch_deriv(fe* out, const fe* c, uint64_t n, const fe& r2, hipStream_t s) {
+  if (!n) return hipSuccess;
+  ProfScope ps("deriv", 32 * n, s);
+  hipLaunchKernelGGL(k_deriv, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, s, out, c, n, r2);
+  return hipGetLastError();
+}
+
+hipError_t launch_batch_div(fe* out, const fe* a, const fe* b, uint64_t n, const fe& r2, const fe& one_m,
+                            unsigned* zero_flag, hipStream_t s) {
+  if (!n) return hipSuccess;
+  constexpr int K = 16;
+  ProfScope ps("batch_div", (a ? 48 : 32) * n, s);
+  // lanes = ceil(n / K), at least one full block
+  uint64_t lanes = (n + K - 1) / K;
+  uint64_t blocks = (lanes + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL((k_batch_div<K>), dim3((unsigned)blocks), dim3(kBlock), 0, s, out, a, b, n, r2, one_m,
+                     zero_flag);
+  return hipGetLastError();
+}
+
+hipError_t launch_scan_tile(fe* data, uint64_t n, fe* tile_tot, const fe& r2, const fe& one_m, hipStream_t s) {
+  if (!n) return hipSuccess;
+  ProfScope ps("scan_tile", 32 * n, s);
+  hipLaunchKernelGGL(k_scan_tile, dim3((unsigned)((n + 1023) / 1024)), dim3(kBlock), 0, s, data, n, tile_tot, r2,
+                     one_m);
+  return hipGetLastError();
+}
+
+hipError_t launch_scan_fix(fe* data, uint64_t n, const fe* scanned_tot, const fe& r2, hipStream_t s) {
+  if (n <= 1024) return hipSuccess;
+  ProfScope ps("scan_fix", 32 * n, s);
+  hipLaunchKernelGGL(k_scan_fix, dim3((unsigned)grid_for(n - 1024)), dim3(kBlock), 0, s, data, n, scanned_tot, r2);
+  return hipGetLastError();
+}
+
+hipError_t launch_qbinom(fe* c, const fe* F, const fe* invF, uint64_t n, uint64_t D, const fe* qA, const fe* qB,
+                         const fe& r2, hipStream_t s) {
+  ProfScope ps("qbinom", 48 * (n + 1), s);
+  hipLaunchKernelGGL(k_qbinom, dim3((unsigned)grid_for(n + 1)), dim3(kBlock), 0, s, c, F, invF, n, D, qA, qB, r2);
+  return hipGetLastError();
+}
+
+hipError_t launch_interp_assemble(fe* V, const fe* y, const fe* Zv, const fe* S, uint64_t n, uint64_t D,
+                                  const fe* iA, const fe* iB, const fe& r2, hipStream_t s) {
+  ProfScope ps("interp_assemble", 64 * D, s);
+  hipLaunchKernelGGL(k_interp_assemble, dim3((unsigned)grid_for(D)), dim3(kBlock), 0, s, V, y, Zv, S, n, D, iA,
+                     iB, r2);
+  return hipGetLastError();
+}
+
+hipError_t launch_last_nonzero(const fe* a, uint64_t n, unsigned long long* last, hipStream_t s) {
+  if (!n) return hipSuccess;
+  ProfScope ps("last_nonzero", 16 * n, s);
+  hipLaunchKernelGGL(k_last_nonzero, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, s, a, n, last);
+  return hipGetLastError();
+}
+
+hipError_t launch_air_eval(const AirEvalArgs& a, hipStream_t s) {
+  if (!a.n) return hipSuccess;
+  if (a.nvars > kAirMaxVars || a.nvars < 1) return hipErrorInvalidValue;
+  ProfScope ps("air_eval", 16 * a.n * (a.nvars + a.ngroups + 1), s);
+  hipLaunchKernelGGL(k_air_eval, dim3((unsigned)grid_for(a.n)), dim3(kBlock), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_lincomb(const LinCombArgs& a, hipStream_t s) {
+  if (!a.n) return hipSuccess;
+  if (a.nterms > kLinCombMaxTerms) return hipErrorInvalidValue;
+  ProfScope ps("lincomb", 16 * a.n * (a.nterms + 1), s);
+  hipLaunchKernelGGL(k_lincomb, dim3((unsigned)grid_for(a.n)), dim3(kBlock), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace sg

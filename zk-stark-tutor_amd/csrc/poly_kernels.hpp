@@ -1,0 +1,49 @@
+// Launchers for the polynomial-algebra kernels (poly_kernels.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include "fe128.hpp"
+
+namespace sg {
+
+constexpr int kAirMaxVars = 8;        // point variables besides x (2 m registers, m <= 4)
+constexpr int kLinCombMaxTerms = 48;  // terms of one weighted combination
+
+struct AirEvalArgs {
+  fe* out;
+  const fe* const* Q;    // device array [ngroups] of coset-value arrays (x-polynomial of each group)
+  const fe* const* V;    // device array [nvars] of coset-value arrays (point variables 1..)
+  const uint32_t* exps;  // device [ngroups][nvars]
+  int ngroups, nvars;
+  uint64_t n;
+  fe r2, one_m;
+};
+
+struct LinCombArgs {
+  fe* out;
+  uint64_t n;
+  int nterms;
+  const fe* term[kLinCombMaxTerms];
+  uint64_t off[kLinCombMaxTerms];
+  uint64_t len[kLinCombMaxTerms];
+  fe w[kLinCombMaxTerms];  // Montgomery
+};
+
+hipError_t launch_ew_mul(fe* out, const fe* a, const fe* b, uint64_t n, const fe& r2, hipStream_t s);
+hipError_t launch_mul_pow2(fe* out, const fe* in, uint64_t n, uint64_t start, const fe* sA, const fe* sB,
+                           hipStream_t s);
+hipError_t launch_one_minus_pow(fe* out, uint64_t n, uint64_t start, const fe* sA, const fe* sB, hipStream_t s);
+hipError_t launch_deriv(fe* out, const fe* c, uint64_t n, const fe& r2, hipStream_t s);
+hipError_t launch_batch_div(fe* out, const fe* a, const fe* b, uint64_t n, const fe& r2, const fe& one_m,
+                            unsigned* zero_flag, hipStream_t s);
+hipError_t launch_scan_tile(fe* data, uint64_t n, fe* tile_tot, const fe& r2, const fe& one_m, hipStream_t s);
+hipError_t launch_scan_fix(fe* data, uint64_t n, const fe* scanned_tot, const fe& r2, hipStream_t s);
+hipError_t launch_qbinom(fe* c, const fe* F, const fe* invF, uint64_t n, uint64_t D, const fe* qA, const fe* qB,
+                         const fe& r2, hipStream_t s);
+hipError_t launch_interp_assemble(fe* V, const fe* y, const fe* Zv, const fe* S, uint64_t n, uint64_t D,
+                                  const fe* iA, const fe* iB, const fe& r2, hipStream_t s);
+hipError_t launch_last_nonzero(const fe* a, uint64_t n, unsigned long long* last, hipStream_t s);
+hipError_t launch_air_eval(const AirEvalArgs& a, hipStream_t s);
+hipError_t launch_lincomb(const LinCombArgs& a, hipStream_t s);
+
+}  // namespace sg

@@ -8,4 +8,7 @@ from .api import (CODEWORD, FIELD_PRIME, LEAFS, PATH, PROOF_BYTES, ROOT, VALUE, 
                   fast_coset_evaluate_dev, fe_array, fe_inverse, fe_mul, fe_pow,
                   generator, intt, intt_dev, ntt, ntt_dev, primitive_nth_root, sample, to_ints)
 
+from .algebra import (Polynomial, fast_coset_divide, fast_interpolate_domain, fast_interpolate_geometric_dev,
+                      fast_multiply, fast_zerofier, fast_zerofier_geometric)
+
 __all__ = [n for n in dir() if not n.startswith("_")]

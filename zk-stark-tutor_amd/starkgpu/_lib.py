@@ -117,6 +117,20 @@ PROTOTYPES = {
     "sg_forest_free": (None, [_vp, _vp]),
     "sg_merkle_top_dev": (ctypes.c_int, [_vp, _vp, _sz, _P(_vp)]),
     "sg_fri_fold_runs_dev": (ctypes.c_int, [_vp, sg_fe, sg_fe, sg_fe, _vp, _sz, _sz, _sz, _sz, _sz, _vp]),
+    # polynomial algebra (fft/ntt_arithmetics.rs)
+    "sg_poly_create": (ctypes.c_int, [_vp, _vp, _sz, _P(_vp)]),
+    "sg_poly_create_dev": (ctypes.c_int, [_vp, _vp, _sz, _P(_vp)]),
+    "sg_poly_len": (_sz, [_vp]),
+    "sg_poly_data_dev": (_vp, [_vp]),
+    "sg_poly_read": (ctypes.c_int, [_vp, _vp, _vp]),
+    "sg_poly_degree": (ctypes.c_int, [_vp, _vp, _P(ctypes.c_int64)]),
+    "sg_poly_free": (None, [_vp]),
+    "sg_fast_multiply": (ctypes.c_int, [_vp, sg_fe, ctypes.c_uint64, _vp, _vp, _P(_vp)]),
+    "sg_fast_coset_divide": (ctypes.c_int, [_vp, sg_fe, ctypes.c_uint64, sg_fe, _vp, _vp, _P(_vp)]),
+    "sg_fast_zerofier": (ctypes.c_int, [_vp, sg_fe, ctypes.c_uint64, _vp, _sz, _P(_vp)]),
+    "sg_fast_interpolate_domain": (ctypes.c_int, [_vp, sg_fe, ctypes.c_uint64, _vp, _vp, _sz, _P(_vp)]),
+    "sg_fast_zerofier_geometric": (ctypes.c_int, [_vp, sg_fe, ctypes.c_uint64, _sz, _P(_vp)]),
+    "sg_fast_interpolate_geometric_dev": (ctypes.c_int, [_vp, sg_fe, ctypes.c_uint64, _vp, _sz, _P(_vp)]),
 }
 
 _lib = None
