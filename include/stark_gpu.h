@@ -245,6 +245,71 @@ int sg_fast_zerofier_geometric(sg_ctx* ctx, sg_fe root, uint64_t root_order, siz
 int sg_fast_interpolate_geometric_dev(sg_ctx* ctx, sg_fe root, uint64_t root_order, const sg_fe* d_values,
                                       size_t n, sg_poly** out);
 
+/* ------------------------------------------- multivariate polynomials (m_polynomial.rs)
+ * MPolynomial {exponent vector: coefficient}; zero coefficients are kept as keys (the
+ * STARK's degree bounds read the keys, stark.rs:117-160).  Stored grouped by the
+ * register exponents (variables 1..) with a dense coefficient vector in variable 0. */
+typedef struct sg_mpoly sg_mpoly;
+/* MPolynomial::new(dict): nterms keys of nvars exponents each (variable 0 first) */
+int sg_mpoly_create(sg_ctx* ctx, size_t nvars, size_t nterms, const uint32_t* exps, const sg_fe* coeffs,
+                    sg_mpoly** out);
+int sg_mpoly_constant(sg_ctx* ctx, sg_fe c, sg_mpoly** out);                            /* m_polynomial.rs:37-44 */
+int sg_mpoly_variable(sg_ctx* ctx, size_t num_variables, size_t index, sg_mpoly** out); /* :49-64 variables()[i] */
+int sg_mpoly_lift(sg_ctx* ctx, const sg_fe* coeffs, size_t len, size_t variable_index, sg_mpoly** out); /* :66-81 */
+int sg_mpoly_lift_poly(sg_ctx* ctx, const sg_poly* p, size_t variable_index, sg_mpoly** out);
+int sg_mpoly_neg(sg_ctx* ctx, const sg_mpoly* a, sg_mpoly** out);                          /* :170-181 */
+int sg_mpoly_add(sg_ctx* ctx, const sg_mpoly* a, const sg_mpoly* b, sg_mpoly** out);       /* :183-222 */
+int sg_mpoly_sub(sg_ctx* ctx, const sg_mpoly* a, const sg_mpoly* b, sg_mpoly** out);       /* :224-229 */
+int sg_mpoly_mul(sg_ctx* ctx, const sg_mpoly* a, const sg_mpoly* b, sg_mpoly** out);       /* :231-262 */
+int sg_mpoly_pow(sg_ctx* ctx, const sg_mpoly* a, sg_fe exponent, sg_mpoly** out);          /* :265-298 (u128) */
+int sg_mpoly_is_zero(const sg_mpoly* a);                                                   /* :83-93 (1/0) */
+int sg_mpoly_evaluate(sg_ctx* ctx, const sg_mpoly* a, const sg_fe* point, size_t n, sg_fe* out); /* :95-122 */
+/* grouped view: ngroups groups of (nvars - 1 register exponents, x-vector length, coefficients) */
+int sg_mpoly_shape(const sg_mpoly* a, size_t* nvars, size_t* ngroups, size_t* ncoeffs);
+int sg_mpoly_export(const sg_mpoly* a, uint32_t* exps, uint64_t* lens, sg_fe* coeffs);
+void sg_mpoly_free(sg_mpoly* a);
+
+/* ------------------------------------------- Rescue-Prime (rescue_prime/rescue_prime.rs) */
+typedef struct sg_rescue sg_rescue;
+typedef struct {
+  uint64_t cycle;
+  uint64_t reg;
+  sg_fe value;
+} sg_boundary; /* (cycle, register, value) boundary constraint (stark.rs:279) */
+int sg_rescue_create(sg_ctx* ctx, size_t m, size_t capacity, size_t security_level, size_t N,
+                     sg_rescue** out); /* rescue_prime.rs:111-128 RescuePrime::new */
+void sg_rescue_free(sg_rescue* rp);
+/* alpha / alpha_inv exponents (u128 in an sg_fe), MDS and MDS^-1 (m x m row-major), 2 m N round constants */
+int sg_rescue_info(const sg_rescue* rp, sg_fe* alpha, sg_fe* alpha_inv, sg_fe* mds, sg_fe* mds_inv,
+                   sg_fe* round_constants);
+int sg_rescue_hash(sg_ctx* ctx, const sg_rescue* rp, sg_fe input, sg_fe* out);   /* rescue_prime.rs:183-190 */
+int sg_rescue_trace(sg_ctx* ctx, const sg_rescue* rp, sg_fe input, sg_fe* trace); /* :192-204, (N+1) x m */
+/* rescue_prime.rs:206-283 transition_constraints(omicron, omicron_domain_length): m polynomials */
+int sg_rescue_transition_constraints(sg_ctx* ctx, const sg_rescue* rp, sg_fe omicron,
+                                     uint64_t omicron_domain_length, sg_mpoly** out);
+int sg_rescue_boundary_constraints(const sg_rescue* rp, sg_fe output, sg_boundary* out); /* :285-290, 2 */
+
+/* ------------------------------------------- STARK (stark/stark.rs) */
+typedef struct sg_stark sg_stark;
+/* stark.rs:71-114 Stark::new */
+int sg_stark_create(sg_ctx* ctx, size_t expansion_factor, size_t num_colinearity_checks, size_t security_level,
+                    size_t num_registers, size_t num_cycles, size_t transition_constraints_degree, sg_stark** out);
+void sg_stark_free(sg_stark* st);
+int sg_stark_params(const sg_stark* st, sg_fe* omicron, uint64_t* omicron_domain_length, sg_fri* fri,
+                    size_t* num_randomizers);
+/* stark.rs:171-186 max_degree (the randomizer polynomial has max_degree + 1 coefficients) */
+int sg_stark_max_degree(sg_ctx* ctx, const sg_stark* st, const sg_mpoly* const* tcs, size_t ntcs, uint64_t* out);
+/* stark.rs:117-160 transition_degree_bounds */
+int sg_stark_degree_bounds(sg_ctx* ctx, const sg_stark* st, const sg_mpoly* const* tcs, size_t ntcs,
+                           uint64_t* transition_bounds);
+/* stark.rs:276-562 Stark::prove.  The thread_rng draws are explicit: trace_randomizers =
+ * num_randomizers x num_registers field elements (stark.rs:285-301, row-major), then the
+ * randomizer polynomial's max_degree + 1 coefficients (stark.rs:425-433).  The proof is the
+ * stream's digest(); SG_ERR_INVALID with the reference's Err text where it returns Err. */
+int sg_stark_prove(sg_ctx* ctx, const sg_stark* st, const sg_fe* trace, size_t rows, const sg_mpoly* const* tcs,
+                   size_t ntcs, const sg_boundary* boundary, size_t nb, const sg_fe* trace_randomizers,
+                   const sg_fe* randomizer_coeffs, size_t n_rc, const sg_proof_stream* ps);
+
 #ifdef __cplusplus
 }
 #endif

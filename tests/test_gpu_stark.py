@@ -1,0 +1,164 @@
+"""GPU parity of MPolynomial, Rescue-Prime and the end-to-end Stark::prove (SURVEY.md 8(f)
+f3/f4, BASELINE config C4): libstarkgpu vs the CPU oracle (oracle/stark_prove_oracle.py),
+exact equality of group coefficient vectors and of the complete proof bytes."""
+import json
+import os
+import random
+
+import pytest
+
+import stark_oracle as o
+import stark_prove_oracle as e
+import starkgpu as sg
+
+pytestmark = pytest.mark.gpu
+P = o.P
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def grouped(d):
+    """oracle dict {(x, r1, ..): c} -> (nvars, {(r1, ..): dense x-coefficients})."""
+    if not d:
+        return 0, {}
+    nv = len(next(iter(d)))
+    out = {}
+    for k, c in d.items():
+        v = out.setdefault(tuple(k[1:]), [])
+        if len(v) <= k[0]:
+            v.extend([0] * (k[0] + 1 - len(v)))
+        v[k[0]] = (v[k[0]] + c) % P
+    return nv, out
+
+
+def same(mp, od):
+    assert mp.groups() == grouped(od.d)
+
+
+def test_rescue_matches_reference_kats():
+    with open(os.path.join(HERE, "golden", "reference_kats_e2e.json")) as f:
+        k = json.load(f)
+    r = k["rescue_new"]
+    rp = sg.RescuePrime(2, 1, 128, 27)
+    assert rp.alpha == r["alpha"] and rp.alpha_inv == int(r["alpha_inv"]), r["src"]
+    assert rp.MDS == [[int(x) for x in row] for row in r["mds"]], r["src"]
+    assert rp.MDS_inv == [[int(x) for x in row] for row in r["mds_inv"]], r["src"]
+    assert rp.round_constants == [int(x) for x in r["round_constants"]], r["src"]
+    h = k["rescue_hash"]
+    assert rp.hash(int(h["input"])) == int(h["output"]), h["src"]
+    t = k["rescue_trace"]
+    tr = rp.trace(int(t["input"]))
+    assert tr[0][0] == int(t["first_rate"]) and tr[-1][0] == int(t["last_rate"]), t["src"]
+    orp = e.RescuePrime(2, 1, 128, 27)
+    assert tr == orp.trace(int(t["input"]))
+    # other shapes vs the oracle
+    for (m, cap, sec, N) in ((3, 1, 2, 9), (2, 1, 2, 100)):
+        a, b = sg.RescuePrime(m, cap, sec, N), e.RescuePrime(m, cap, sec, N)
+        assert a.MDS == b.MDS and a.MDS_inv == b.MDS_inv and a.round_constants == b.round_constants
+        assert a.trace(12345) == b.trace(12345)
+
+
+def test_mpolynomial_ops_vs_oracle():
+    with open(os.path.join(HERE, "golden", "reference_kats_e2e.json")) as f:
+        k = json.load(f)
+    for name, op in (("mpoly_mul", lambda a, b: a * b), ("mpoly_add", lambda a, b: a + b),
+                     ("mpoly_sub", lambda a, b: a - b)):
+        v = k[name]
+        # the library needs keys of one length per polynomial; pad like the reference's Add/Mul
+        na = max(len(x[0]) for x in v["a"])
+        nb = max(len(x[0]) for x in v["b"])
+        da = {tuple(x[0]) + (0,) * (na - len(x[0])): int(x[1]) for x in v["a"]}
+        db = {tuple(x[0]) + (0,) * (nb - len(x[0])): int(x[1]) for x in v["b"]}
+        got = op(sg.MPolynomial.new(da), sg.MPolynomial.new(db))
+        want = op(e.MPolynomial(da), e.MPolynomial(db))
+        same(got, want)
+        assert grouped(want.d) == grouped({tuple(x[0]): int(x[1]) for x in v["out"]}), v["src"]
+    rng = random.Random(3)
+    for _ in range(5):
+        nv = rng.randrange(1, 4)
+        da = {tuple(rng.randrange(4) for _ in range(nv)): rng.choice([0, rng.randrange(P)]) for _ in range(6)}
+        db = {tuple(rng.randrange(3) for _ in range(nv)): rng.randrange(P) for _ in range(4)}
+        A, B = sg.MPolynomial.new(da), sg.MPolynomial.new(db)
+        oa, ob = e.MPolynomial(da), e.MPolynomial(db)
+        same(A * B, oa * ob)
+        same(A + B, oa + ob)
+        same(A - B, oa - ob)
+        same(A ** 3, oa ** 3)
+        same(A ** 0, oa ** 0)
+        pt = [rng.randrange(P) for _ in range(nv)]
+        assert A.evaluate(pt) == oa.evaluate(pt)
+    same(sg.MPolynomial.lift([3, 0, 5, 0], 0), e.MPolynomial.lift([3, 0, 5, 0], 0))
+    same(sg.MPolynomial.lift([3, 0, 5], 2), e.MPolynomial.lift([3, 0, 5], 2))
+    for a, b in zip(sg.MPolynomial.variables(3), e.MPolynomial.variables(3)):
+        same(a, b)
+
+
+def test_rescue_transition_constraints_vs_oracle():
+    st = e.Stark(4, 2, 2, 2, 28, 2)
+    air_o = e.RescuePrime(2, 1, 2, 27).transition_constraints(st.omicron, st.omicron_domain_length)
+    air_g = sg.RescuePrime(2, 1, 2, 27).transition_constraints(st.omicron, st.omicron_domain_length)
+    for a, b in zip(air_g, air_o):
+        same(a, b)
+
+
+def _case(N, exp, c, sec, tcd, seed, m=2):
+    rp_o, rp_g = e.RescuePrime(m, 1, sec, N), sg.RescuePrime(m, 1, sec, N)
+    st_o = e.Stark(exp, c, sec, m, N + 1, tcd)
+    st_g = sg.Stark(exp, c, sec, m, N + 1, tcd)
+    assert st_g.omicron == st_o.omicron and st_g.omicron_domain_length == st_o.omicron_domain_length
+    air_o = rp_o.transition_constraints(st_o.omicron, st_o.omicron_domain_length)
+    air_g = rp_g.transition_constraints(st_g.omicron, st_g.omicron_domain_length)
+    assert st_g.transition_degree_bounds(air_g) == st_o.transition_degree_bounds(air_o)
+    assert st_g.max_degree(air_g) == st_o.max_degree(air_o)
+    inp = o.sample(seed)
+    out = rp_o.hash(inp)
+    nrc = st_o.num_randomizer_coefficients(air_o)
+    r = e.randomness_from_seed(seed, m * st_o.num_randomizers + nrc)
+    tr = [r[m * i:m * i + m] for i in range(st_o.num_randomizers)]
+    rc = r[m * st_o.num_randomizers:]
+    return rp_o, st_o, st_g, air_o, air_g, rp_o.trace(inp), rp_o.boundary_constraints(out), tr, rc, out
+
+
+@pytest.mark.parametrize("N,exp,c,sec,tcd", [(27, 4, 2, 2, 2), (27, 8, 4, 8, 3), (40, 4, 3, 4, 2), (9, 16, 2, 4, 4)])
+def test_stark_prove_bytes_vs_oracle(N, exp, c, sec, tcd):
+    """stark.rs:276-562 proof bytes == the oracle's (randomizers injected identically)."""
+    rp, st_o, st_g, air_o, air_g, trace, bnd, tr, rc, out = _case(N, exp, c, sec, tcd, b"case-%d" % N)
+    ops = o.IndependentProofStream()
+    want = st_o.prove(trace, air_o, bnd, ops, tr, rc)
+    gps = sg.IndependentProofStream()
+    got = st_g.prove(trace, air_g, bnd, gps, tr, rc)
+    assert got == want
+    ok, err = st_o.verify(air_o, bnd, o.IndependentProofStream(ops.objects))
+    # with transition_constraints_degree too small for alpha = 3 (max_degree >= omicron order)
+    # the reference's NTT products wrap and its proof does not verify: same bytes, same verdict
+    assert ok == (st_o.max_degree(air_o) < st_o.omicron_domain_length), err
+
+
+def test_stark_false_witness_and_claim():
+    """stark.rs:845-880: a false witness gives the reference's (rejected) proof bytes; a false
+    claim is rejected by the verifier."""
+    rp, st_o, st_g, air_o, air_g, trace, bnd, tr, rc, out = _case(27, 4, 2, 2, 2, b"bad")
+    bad = [list(r) for r in trace]
+    bad[22][1] = o.add_mod(bad[22][1], 17274817952119230544216945715808633996)
+    ops, gps = o.IndependentProofStream(), sg.IndependentProofStream()
+    assert st_g.prove(bad, air_g, bnd, gps, tr, rc) == st_o.prove(bad, air_o, bnd, ops, tr, rc)
+    ok, _ = st_o.verify(air_o, bnd, o.IndependentProofStream(ops.objects))
+    assert not ok
+    honest = sg.IndependentProofStream()
+    st_g.prove(trace, air_g, bnd, honest, tr, rc)
+    objs = honest.objects()
+    ok, err = st_o.verify(air_o, bnd, o.IndependentProofStream(objs))
+    assert ok, err
+    ok, _ = st_o.verify(air_o, rp.boundary_constraints(o.add_mod(out, 1)), o.IndependentProofStream(objs))
+    assert not ok
+
+
+def test_stark_prove_callback_stream_and_errors():
+    rp, st_o, st_g, air_o, air_g, trace, bnd, tr, rc, out = _case(27, 4, 2, 2, 2, b"cb")
+    ops = o.IndependentProofStream()
+    want = st_o.prove(trace, air_o, bnd, ops, tr, rc)
+    # any ProofStream implementation through the callbacks
+    pys = o.IndependentProofStream()
+    st_g.prove(trace, air_g, bnd, pys, tr, rc)
+    assert pys.digest() == want
+    with pytest.raises(sg.StarkGpuError):
+        st_g.prove(trace, air_g, bnd, sg.IndependentProofStream(), tr, rc[:-1])

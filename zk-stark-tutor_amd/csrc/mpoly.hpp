@@ -1,0 +1,47 @@
+// Multivariate polynomials (m_polynomial.rs) grouped for the GPU.
+//
+// The reference stores {exponent vector: coefficient} and keeps zero
+// coefficients (Add/Mul never remove keys); the STARK's degree bounds are taken
+// over the KEYS (stark.rs:117-160).  Here a polynomial is grouped by the
+// exponents of variables 1.. (the registers) with a dense coefficient vector in
+// variable 0 (x) per group: F[x][v_1..v_k].  A group's vector length is its
+// largest x-exponent key + 1, which is exactly what the key-based degree bounds
+// read, and every reference operation maps onto groups:
+//   add  = union of groups, coefficient vectors added (length max)
+//   mul  = all pairs of groups, x-vectors multiplied (length la + lb - 1; large
+//          products on the GPU NTT)
+// Evaluation on a coset is pointwise: sum_g Q_g(y) prod_j V_j(y)^e_gj.
+#pragma once
+#include <cstdint>
+#include <map>
+#include <vector>
+
+#include "context.hpp"
+#include "fe128.hpp"
+#include "poly.hpp"
+
+namespace sg {
+
+struct MPoly {
+  uint32_t nvars = 0;                          // key length (0: empty dictionary)
+  std::map<std::vector<uint32_t>, HPoly> g;    // exponents of variables 1..nvars-1 -> x coefficients
+};
+
+MPoly mp_constant(const fe& c);
+std::vector<MPoly> mp_variables(uint32_t n);
+MPoly mp_lift(const HPoly& poly, uint32_t variable_index);
+bool mp_is_zero(const MPoly& a);
+MPoly mp_neg(const MPoly& a);
+MPoly mp_add(const MPoly& a, const MPoly& b);
+MPoly mp_sub(const MPoly& a, const MPoly& b);
+MPoly mp_mul(sg_ctx* ctx, const MPoly& a, const MPoly& b);
+MPoly mp_pow(sg_ctx* ctx, const MPoly& a, unsigned __int128 e);
+fe mp_evaluate(const MPoly& a, const std::vector<fe>& point);
+// exact product of two x-vectors (GPU NTT when large)
+HPoly x_mul(sg_ctx* ctx, const HPoly& a, const HPoly& b);
+
+}  // namespace sg
+
+struct sg_mpoly {
+  sg::MPoly m;
+};

@@ -1,1 +1,803 @@
-// placeholder (filled below)
+// Rescue-Prime (rescue_prime/rescue_prime.rs) and the end-to-end STARK prover
+// (stark/stark.rs:71-562) over the device kernels, and their C ABI.
+//
+// Stark::prove on the GPU (BASELINE config C4):
+//   trace columns --(geometric interpolation, poly.cpp)--> trace polynomials
+//   boundary quotients: fast_coset_divide (the reference's algorithm, bit-exact)
+//   boundary-quotient / randomizer LDEs + retained Merkle trees (kernels.hip)
+//   transition polynomials: the AIR (grouped MPolynomial) evaluated pointwise on
+//     a coset of size L > degree and interpolated back (the unique polynomial
+//     evaluate_symbolic returns), then fast_coset_divide by the transition zerofier
+//   combination polynomial (weighted, shifted terms) -> LDE -> FRI::prove
+//   openings of the boundary-quotient and randomizer codewords (batched gathers).
+// The thread_rng draws (trace randomizers, randomizer polynomial) are explicit inputs.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "host_field.hpp"
+#include "host_hash.hpp"
+#include "internal.hpp"
+#include "mpoly.hpp"
+#include "poly.hpp"
+#include "poly_kernels.hpp"
+
+namespace sg {
+
+namespace {
+
+unsigned __int128 u128_gcd(unsigned __int128 a, unsigned __int128 b) {
+  while (b) {
+    unsigned __int128 t = a % b;
+    a = b;
+    b = t;
+  }
+  return a;
+}
+
+int bitlen_count(unsigned __int128 x) {  // utils/bit_iter.rs BitIter::from(x).count()
+  int n = 0;
+  while (x) {
+    ++n;
+    x >>= 1;
+  }
+  return n ? n : 1;
+}
+
+std::string u128_decimal(unsigned __int128 v) {
+  if (v == 0) return "0";
+  std::string s;
+  while (v) {
+    s.push_back((char)('0' + (int)(v % 10)));
+    v /= 10;
+  }
+  std::reverse(s.begin(), s.end());
+  return s;
+}
+
+fe fe_div(const fe& a, const fe& b) {
+  SG_REQUIRE(!fe_eq(b, fe_zero()), "divide by zero");
+  return fe_mul(a, fe_inv(b));
+}
+
+using Mat = std::vector<std::vector<fe>>;
+
+// utils/matrix.rs:5-49
+void rref(Mat& m) {
+  size_t lead = 0;
+  const size_t rows = m.size(), cols = m[0].size();
+  for (size_t r = 0; r < rows; ++r) {
+    if (cols <= lead) break;
+    size_t i = r;
+    bool stop = false;
+    while (fe_eq(m[i][lead], fe_zero())) {
+      ++i;
+      if (rows == i) {
+        i = r;
+        ++lead;
+        if (cols == lead) {
+          stop = true;
+          break;
+        }
+      }
+    }
+    if (stop) break;
+    std::swap(m[i], m[r]);
+    if (!fe_eq(m[r][lead], fe_zero())) {
+      fe piv = m[r][lead];
+      for (auto& el : m[r]) el = fe_div(el, piv);
+    }
+    for (size_t ii = 0; ii < rows; ++ii) {
+      if (ii == r) continue;
+      fe hold = m[ii][lead];
+      for (size_t k = 0; k < cols; ++k) m[ii][k] = fe_sub(m[ii][k], fe_mul(hold, m[r][k]));
+    }
+    ++lead;
+  }
+}
+
+Mat transpose(const Mat& m) {
+  Mat t(m[0].size(), std::vector<fe>(m.size()));
+  for (size_t r = 0; r < m.size(); ++r)
+    for (size_t c = 0; c < m[0].size(); ++c) t[c][r] = m[r][c];
+  return t;
+}
+
+// utils/matrix.rs:68-110
+Mat inverse(const Mat& m) {
+  const size_t n = m.size();
+  Mat aug(n);
+  for (size_t i = 0; i < n; ++i) {
+    SG_REQUIRE(m[i].size() == n, "Inverse exists only for square matrices");
+    aug[i] = m[i];
+    aug[i].resize(2 * n, fe_zero());
+    aug[i][n + i] = fe_one();
+  }
+  rref(aug);
+  for (size_t i = 0; i < n; ++i)
+    for (size_t j = 0; j < n; ++j)
+      SG_REQUIRE(fe_eq(aug[i][j], i == j ? fe_one() : fe_zero()), "Couldnt construct identity matrix to find inverse");
+  Mat out(n);
+  for (size_t i = 0; i < n; ++i) out[i].assign(aug[i].begin() + n, aug[i].end());
+  return out;
+}
+
+}  // namespace
+}  // namespace sg
+
+using namespace sg;
+
+// ====================================================================== Rescue-Prime
+
+struct sg_rescue {
+  size_t m = 0, capacity = 0, security = 0, N = 0;
+  unsigned __int128 alpha = 0, alpha_inv = 0;  // exponents (rescue_prime.rs:120-123)
+  Mat mds, mds_inv;
+  std::vector<fe> rc;  // 2 m N round constants
+
+  // rescue_prime.rs:52-106, one round r
+  void round(std::vector<fe>& state, size_t r) const {
+    std::vector<fe> s(m), t(m, fe_zero());
+    for (size_t i = 0; i < m; ++i) s[i] = fe_pow(state[i], alpha);
+    for (size_t i = 0; i < m; ++i)
+      for (size_t j = 0; j < m; ++j) t[j] = fe_add(t[j], fe_mul(mds[j][i], s[i]));
+    for (size_t j = 0; j < m; ++j) t[j] = fe_pow(fe_add(t[j], rc[2 * r * m + j]), alpha_inv);
+    std::vector<fe> u(m, fe_zero());
+    for (size_t i = 0; i < m; ++i)
+      for (size_t j = 0; j < m; ++j) u[j] = fe_add(u[j], fe_mul(mds[j][i], t[i]));
+    for (size_t j = 0; j < m; ++j) state[j] = fe_add(u[j], rc[2 * r * m + m + j]);
+  }
+};
+
+namespace {
+
+void rescue_init(sg_rescue& rp, size_t m, size_t capacity, size_t security, size_t N) {
+  SG_REQUIRE(m >= 1 && capacity <= m, "invalid Rescue-Prime state size");
+  rp.m = m;
+  rp.capacity = capacity;
+  rp.security = security;
+  rp.N = N;
+  const unsigned __int128 p = fe_to_u128(fe_prime());
+  // field.rs:46-56 smallest_generator
+  unsigned __int128 k = 3;
+  while (u128_gcd(k, p - 1) != 1) ++k;
+  const fe g = fe_from_u128(k);
+  rp.alpha = k;
+  rp.alpha_inv = fe_to_u128(fe_inv(fe_neg(g)));
+  // rescue_prime.rs:130-148 get_mds
+  Mat mat(m, std::vector<fe>(2 * m));
+  for (size_t i = 0; i < m; ++i)
+    for (size_t j = 0; j < 2 * m; ++j) mat[i][j] = fe_pow(g, (unsigned __int128)(i * j));
+  rref(mat);
+  Mat right(m);
+  for (size_t i = 0; i < m; ++i) right[i].assign(mat[i].begin() + m, mat[i].end());
+  rp.mds = transpose(right);
+  rp.mds_inv = inverse(rp.mds);
+  // rescue_prime.rs:150-180 get_round_constants: 17-byte chunks of SHAKE256(seed), sum 256^j b_j
+  const size_t bytes_per_int = (size_t)(bitlen_count(p) + 7) / 8 + 1;
+  const size_t num = 2 * m * N;
+  char seed[256];
+  snprintf(seed, sizeof(seed), "Rescue-XLIX(%s,%zu,%zu,%zu)", u128_decimal(p).c_str(), m, capacity, security);
+  std::vector<uint8_t> raw(bytes_per_int * std::max<size_t>(num, 1));
+  shake256(reinterpret_cast<const uint8_t*>(seed), strlen(seed), raw.data(), bytes_per_int * num);
+  rp.rc.resize(num);
+  const fe f256 = fe_from_u64(256);
+  std::vector<fe> pw(bytes_per_int);
+  pw[0] = fe_one();
+  for (size_t j = 1; j < bytes_per_int; ++j) pw[j] = fe_mul(pw[j - 1], f256);
+  for (size_t i = 0; i < num; ++i) {
+    fe acc = fe_zero();
+    for (size_t j = 0; j < bytes_per_int; ++j)
+      acc = fe_add(acc, fe_mul(pw[j], fe_from_u64(raw[bytes_per_int * i + j])));
+    rp.rc[i] = acc;
+  }
+}
+
+std::vector<fe> rescue_trace(const sg_rescue& rp, const fe& input) {
+  std::vector<fe> state(rp.m, fe_zero());
+  state[0] = input;
+  std::vector<fe> out;
+  out.reserve((rp.N + 1) * rp.m);
+  out.insert(out.end(), state.begin(), state.end());
+  for (size_t r = 0; r < rp.N; ++r) {
+    rp.round(state, r);
+    out.insert(out.end(), state.begin(), state.end());
+  }
+  return out;
+}
+
+// rescue_prime.rs:206-283
+std::vector<MPoly> rescue_transition_constraints(sg_ctx* ctx, const sg_rescue& rp, const fe& omicron, uint64_t D) {
+  const size_t m = rp.m, N = rp.N;
+  check_root(omicron, D);
+  SG_REQUIRE(N <= D, "more rounds than the omicron domain");
+  // round-constant interpolants over omicron^r, r < N (geometric domain, on the GPU)
+  auto interp = [&](size_t which) {
+    std::vector<fe> vals(N);
+    for (size_t r = 0; r < N; ++r) vals[r] = rp.rc[2 * r * m + which];
+    DPoly y = dpoly_upload(ctx, vals.data(), N);
+    DPoly p = N > 1 ? interpolate_geometric_dev(ctx, omicron, D, y.p(), N) : std::move(y);
+    return mp_lift(dpoly_download(ctx, p.p(), p.len), 0);
+  };
+  std::vector<MPoly> first(m), second(m);
+  for (size_t i = 0; i < m; ++i) first[i] = interp(i);
+  for (size_t i = 0; i < m; ++i) second[i] = interp(m + i);
+  std::vector<MPoly> vars = mp_variables((uint32_t)(1 + 2 * m));
+  std::vector<MPoly> out;
+  for (size_t i = 0; i < m; ++i) {
+    MPoly lhs;
+    for (size_t k = 0; k < m; ++k) {
+      MPoly t = mp_mul(ctx, mp_constant(rp.mds[i][k]), mp_pow(ctx, vars[1 + k], rp.alpha));
+      lhs = k ? mp_add(lhs, t) : t;
+    }
+    lhs = mp_add(lhs, first[i]);
+    MPoly rhs;
+    for (size_t k = 0; k < m; ++k) {
+      MPoly t = mp_mul(ctx, mp_constant(rp.mds_inv[i][k]), mp_sub(vars[1 + m + k], second[k]));
+      rhs = k ? mp_add(rhs, t) : t;
+    }
+    rhs = mp_pow(ctx, rhs, rp.alpha);
+    out.push_back(mp_sub(lhs, rhs));
+  }
+  return out;
+}
+
+}  // namespace
+
+// ====================================================================== STARK
+
+struct sg_stark {
+  size_t expansion = 0, num_colinearity = 0, security = 0, m = 0, original_trace_length = 0, num_randomizers = 0;
+  uint64_t D = 0;  // omicron_domain_length
+  fe omicron, omega, generator;
+  sg_fri fri;
+};
+
+namespace {
+
+struct Boundary {
+  uint64_t cycle, reg;
+  fe value;
+};
+
+// stark.rs:117-160 (over the dictionary KEYS, i.e. group lengths here)
+std::vector<uint64_t> transition_degree_bounds(const sg_stark& st, const std::vector<const MPoly*>& tcs) {
+  std::vector<uint64_t> pd(2 * st.m + 1, (uint64_t)(st.original_trace_length + st.num_randomizers - 1));
+  pd[0] = 1;
+  std::vector<uint64_t> out;
+  for (const MPoly* a : tcs) {
+    SG_REQUIRE(!a->g.empty(), "cannot calculate max on empty vec a");
+    uint64_t mx = 0;
+    for (auto& kv : a->g) {
+      // zip(points_degree, key): x exponent, then registers
+      uint64_t s = 0;
+      if (a->nvars >= 1 && !pd.empty()) s += pd[0] * (uint64_t)(kv.second.size() - 1);
+      for (size_t j = 0; j < kv.first.size() && j + 1 < pd.size(); ++j) s += pd[j + 1] * kv.first[j];
+      mx = std::max(mx, s);
+    }
+    out.push_back(mx);
+  }
+  return out;
+}
+
+std::vector<uint64_t> transition_quotient_degree_bounds(const sg_stark& st, const std::vector<const MPoly*>& tcs) {
+  std::vector<uint64_t> b = transition_degree_bounds(st, tcs);
+  for (auto& d : b) d -= (uint64_t)(st.original_trace_length - 1);
+  return b;
+}
+
+uint64_t max_degree(const sg_stark& st, const std::vector<const MPoly*>& tcs) {
+  SG_REQUIRE(!tcs.empty(), "Cannot calculate max for empty transition_constraints vector");
+  std::vector<uint64_t> b = transition_degree_bounds(st, tcs);
+  uint64_t md = *std::max_element(b.begin(), b.end());
+  return ((uint64_t)1 << bitlen_count(md)) - 1;
+}
+
+fe omicron_pow(const sg_stark& st, uint64_t c) { return fe_pow(st.omicron, (unsigned __int128)c); }
+
+std::vector<HPoly> boundary_zerofiers(const sg_stark& st, const std::vector<Boundary>& bnd) {
+  std::vector<HPoly> out;
+  for (size_t s = 0; s < st.m; ++s) {
+    std::vector<fe> dom;
+    for (auto& b : bnd)
+      if (b.reg == s) dom.push_back(omicron_pow(st, b.cycle));
+    out.push_back(hp_zerofier(dom));
+  }
+  return out;
+}
+
+std::vector<HPoly> boundary_interpolants(const sg_stark& st, const std::vector<Boundary>& bnd) {
+  std::vector<HPoly> out;
+  for (size_t s = 0; s < st.m; ++s) {
+    std::vector<fe> dom, val;
+    for (auto& b : bnd)
+      if (b.reg == s) {
+        dom.push_back(omicron_pow(st, b.cycle));
+        val.push_back(b.value);
+      }
+    out.push_back(hp_interpolate(dom, val));
+  }
+  return out;
+}
+
+// x-exponent + (T'-1) * register-exponent sum over groups with a non-zero x vector:
+// the length - 1 of the vector evaluate_symbolic builds (m_polynomial.rs:124-139)
+uint64_t symbolic_degree_bound(const MPoly& a, uint64_t point_deg) {
+  uint64_t mx = 0;
+  for (auto& kv : a.g) {
+    int64_t dx = hp_degree(kv.second);
+    if (dx < 0) continue;
+    uint64_t s = (uint64_t)dx;
+    for (uint32_t e : kv.first) s += point_deg * e;
+    mx = std::max(mx, s);
+  }
+  return mx;
+}
+
+struct DevTerm {
+  const fe* p;
+  uint64_t off, len;
+  fe w;
+};
+
+// device linear combination sum_t w_t * x^off_t * term_t, output length max(off + len)
+DPoly lincomb(sg_ctx* ctx, const std::vector<DevTerm>& terms) {
+  uint64_t n = 0;
+  for (auto& t : terms) n = std::max(n, t.off + t.len);
+  DPoly out = dpoly_alloc(ctx, n);
+  if (!n) return out;
+  SG_REQUIRE(terms.size() <= (size_t)kLinCombMaxTerms, "too many combination terms");
+  LinCombArgs a{};
+  a.out = out.p();
+  a.n = n;
+  a.nterms = (int)terms.size();
+  for (size_t t = 0; t < terms.size(); ++t) {
+    a.term[t] = terms[t].p;
+    a.off[t] = terms[t].off;
+    a.len[t] = terms[t].p ? terms[t].len : 0;
+    a.w[t] = to_mont(terms[t].w);
+  }
+  SG_HIP(launch_lincomb(a, ctx->stream));
+  return out;
+}
+
+// the polynomial evaluate_symbolic returns, coefficient vector of length `len`
+DPoly transition_polynomial(sg_ctx* ctx, const MPoly& tc, const std::vector<DPoly>& trace_polys, uint64_t Tp,
+                            const fe& omicron, const fe& offset, uint64_t& len) {
+  const size_t m = trace_polys.size();
+  SG_REQUIRE(tc.nvars <= 1 + 2 * m, "transition constraint has more variables than the point");
+  SG_REQUIRE(2 * m <= (size_t)kAirMaxVars, "at most 4 registers are supported by the AIR kernel");
+  const uint64_t bound = symbolic_degree_bound(tc, Tp - 1);
+  len = bound + 1;
+  const uint64_t L = next_pow2(len);
+  // point values on the coset offset * <w_L>: P_s(y) and P_s(omicron y)
+  std::vector<DPoly> V;
+  const fe off_omicron = fe_mul(offset, omicron);
+  for (size_t s = 0; s < m; ++s) {
+    V.push_back(dpoly_alloc(ctx, L));
+    coset_values_dev(ctx, trace_polys[s].p(), trace_polys[s].len, L, offset, V.back().p());
+  }
+  for (size_t s = 0; s < m; ++s) {
+    V.push_back(dpoly_alloc(ctx, L));
+    coset_values_dev(ctx, trace_polys[s].p(), trace_polys[s].len, L, off_omicron, V.back().p());
+  }
+  // group x-polynomials on the same coset
+  std::vector<DPoly> Q;
+  std::vector<uint32_t> exps;
+  const int nv = 2 * (int)m;
+  for (auto& kv : tc.g) {
+    const int64_t dx = hp_degree(kv.second);
+    if (dx < 0) continue;  // an all-zero group adds nothing (its products are zero polynomials)
+    DPoly x = dpoly_upload(ctx, kv.second.data(), (uint64_t)dx + 1);
+    Q.push_back(dpoly_alloc(ctx, L));
+    coset_values_dev(ctx, x.p(), x.len, L, offset, Q.back().p());
+    for (int j = 0; j < nv; ++j) exps.push_back(j < (int)kv.first.size() ? kv.first[j] : 0u);
+  }
+  DPoly vals = dpoly_alloc(ctx, L);
+  if (Q.empty()) {
+    SG_HIP(hipMemsetAsync(vals.p(), 0, L * sizeof(fe), ctx->stream));
+  } else {
+    std::vector<const fe*> qp, vp;
+    for (auto& q : Q) qp.push_back(q.p());
+    for (auto& v : V) vp.push_back(v.p());
+    DevBuf dq(ctx, qp.size() * sizeof(void*)), dv(ctx, vp.size() * sizeof(void*)), de(ctx, exps.size() * 4);
+    SG_HIP(hipMemcpyAsync(dq.get(), qp.data(), qp.size() * sizeof(void*), hipMemcpyHostToDevice, ctx->stream));
+    SG_HIP(hipMemcpyAsync(dv.get(), vp.data(), vp.size() * sizeof(void*), hipMemcpyHostToDevice, ctx->stream));
+    SG_HIP(hipMemcpyAsync(de.get(), exps.data(), exps.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+    AirEvalArgs a{};
+    a.out = vals.p();
+    a.Q = dq.as<const fe*>();
+    a.V = dv.as<const fe*>();
+    a.exps = de.as<uint32_t>();
+    a.ngroups = (int)Q.size();
+    a.nvars = nv;
+    a.n = L;
+    a.r2 = fe_r2();
+    a.one_m = to_mont(fe_one());
+    SG_HIP(launch_air_eval(a, ctx->stream));
+    SG_HIP(hipStreamSynchronize(ctx->stream));  // pointer tables return to the pool
+  }
+  DPoly coeffs = dpoly_alloc(ctx, L);
+  coset_interpolate_dev(ctx, vals.p(), L, offset, coeffs.p());
+  coeffs.len = len;  // coefficients len..L-1 are zero
+  return coeffs;
+}
+
+// proof_stream pushes of (Value, Path) for `idx` in a retained codeword/tree (stark.rs:545-560)
+void push_openings(sg_ctx* ctx, const sg_proof_stream* ps, const fe* cw, const sg_tree* t,
+                   const std::vector<uint64_t>& idx) {
+  std::vector<uint64_t> fe_addr, dg_addr;
+  for (uint64_t i : idx) {
+    fe_addr.push_back((uint64_t)(uintptr_t)cw + 16 * i);
+    std::vector<uint64_t> p;
+    path_indices(t, i, p);
+    for (uint64_t d : p) dg_addr.push_back((uint64_t)(uintptr_t)t->buf.get() + 64 * d);
+  }
+  std::vector<fe> vals(fe_addr.size());
+  std::vector<uint8_t> digs(dg_addr.size() * 64);
+  DevBuf da(ctx, std::max<size_t>(fe_addr.size(), 1) * 8), dv(ctx, std::max<size_t>(fe_addr.size(), 1) * 16);
+  DevBuf db(ctx, std::max<size_t>(dg_addr.size(), 1) * 8), dd(ctx, std::max<size_t>(dg_addr.size(), 1) * 64);
+  SG_HIP(hipMemcpyAsync(da.get(), fe_addr.data(), fe_addr.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+  SG_HIP(launch_gather_fe_ptrs(da.as<uint64_t>(), dv.as<fe>(), (uint32_t)fe_addr.size(), ctx->stream));
+  if (!dg_addr.empty()) {
+    SG_HIP(hipMemcpyAsync(db.get(), dg_addr.data(), dg_addr.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+    SG_HIP(launch_gather_digest_ptrs(db.as<uint64_t>(), dd.as<uint64_t>(), (uint32_t)dg_addr.size(), ctx->stream));
+    SG_HIP(hipMemcpyAsync(digs.data(), dd.get(), digs.size(), hipMemcpyDeviceToHost, ctx->stream));
+  }
+  SG_HIP(hipMemcpyAsync(vals.data(), dv.get(), vals.size() * 16, hipMemcpyDeviceToHost, ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  const size_t depth = (size_t)t->logn;
+  std::vector<uint8_t> obj(depth * 72);
+  static const uint8_t len64[8] = {0, 0, 0, 0, 0, 0, 0, 64};
+  for (size_t k = 0; k < idx.size(); ++k) {
+    uint8_t v[16];
+    put_u128_be_at(v, vals[k]);
+    push_obj(ps, SG_OBJ_VALUE, v, 16);
+    uint8_t* p = obj.data();
+    for (size_t d = 0; d < depth; ++d, p += 72) {
+      memcpy(p, len64, 8);
+      memcpy(p + 8, digs.data() + (k * depth + d) * 64, 64);
+    }
+    push_obj(ps, SG_OBJ_PATH, obj.data(), obj.size());
+  }
+}
+
+std::vector<fe> sample_weights(size_t number, const uint8_t* randomness, size_t len) {
+  // stark.rs:268-274: sample(0^i || randomness)
+  std::vector<fe> out;
+  std::vector<uint8_t> buf;
+  for (size_t i = 0; i < number; ++i) {
+    buf.assign(i, 0);
+    buf.insert(buf.end(), randomness, randomness + len);
+    out.push_back(fe_sample(buf.data(), buf.size()));
+  }
+  return out;
+}
+
+struct AsyncScope {
+  sg_ctx* ctx;
+  bool prev;
+  explicit AsyncScope(sg_ctx* c) : ctx(c), prev(c->async_dev) { c->async_dev = true; }
+  ~AsyncScope() { ctx->async_dev = prev; }
+};
+
+// stark.rs:276-562
+void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* trace, size_t rows, const std::vector<const MPoly*>& tcs,
+                 const std::vector<Boundary>& bnd, const fe* trace_rand, const fe* rcoef, size_t nrc,
+                 const sg_proof_stream* ps) {
+  SG_REQUIRE(ps && ps->push && ps->fiat_shamir_prover, "proof stream callbacks required");
+  const size_t m = st.m;
+  const uint64_t D = st.D;
+  const fe g = st.generator;
+  const uint64_t Nf = st.fri.domain_length;
+  AsyncScope async_scope(ctx);
+  // randomized trace (stark.rs:285-301), columns on the device
+  const uint64_t Tp = rows + st.num_randomizers;
+  SG_REQUIRE(Tp <= D, "randomized trace longer than the omicron domain");
+  std::vector<DPoly> trace_polys;
+  {
+    std::vector<fe> col(Tp);
+    for (size_t s = 0; s < m; ++s) {
+      for (size_t r = 0; r < rows; ++r) col[r] = trace[r * m + s];
+      for (size_t r = 0; r < st.num_randomizers; ++r) col[rows + r] = trace_rand[r * m + s];
+      DPoly y = dpoly_upload(ctx, col.data(), Tp);
+      trace_polys.push_back(interpolate_geometric_dev(ctx, st.omicron, D, y.p(), Tp));
+    }
+  }
+  // boundary quotients (stark.rs:326-362)
+  std::vector<HPoly> bi = boundary_interpolants(st, bnd), bz = boundary_zerofiers(st, bnd);
+  std::vector<DPoly> bqs;
+  for (size_t s = 0; s < m; ++s) {
+    DPoly I = dpoly_upload(ctx, bi[s].data(), bi[s].size());
+    DPoly Z = dpoly_upload(ctx, bz[s].data(), bz[s].size());
+    DPoly diff = lincomb(ctx, {{trace_polys[s].p(), 0, trace_polys[s].len, fe_one()},
+                               {I.p(), 0, I.len, fe_neg(fe_one())}});
+    bqs.push_back(fast_coset_divide_dev(ctx, st.omicron, D, g, diff.p(), diff.len, Z.p(), Z.len));
+  }
+  // boundary-quotient codewords + roots (stark.rs:367-386)
+  std::vector<DPoly> bq_cw;
+  std::vector<std::unique_ptr<sg_tree>> bq_trees(m);
+  for (size_t s = 0; s < m; ++s) {
+    SG_REQUIRE(bqs[s].len <= Nf, "fast_coset_evaluate: polynomial longer than root_order");
+    bq_cw.push_back(dpoly_alloc(ctx, Nf));
+    const fe* in = bqs[s].p();
+    fe* out = bq_cw.back().p();
+    if (bqs[s].len)
+      coset_evaluate_batch(ctx, st.omega, Nf, g, &in, bqs[s].len, &out, 1);
+    else
+      SG_HIP(hipMemsetAsync(out, 0, Nf * sizeof(fe), ctx->stream));
+  }
+  for (size_t s = 0; s < m; s += 4) {
+    int b = (int)std::min<size_t>(4, m - s);
+    const fe* leaves[4];
+    for (int k = 0; k < b; ++k) leaves[k] = bq_cw[s + k].p();
+    build_trees(ctx, leaves, b, Nf, &bq_trees[s]);
+  }
+  for (size_t s = 0; s < m; ++s) push_obj(ps, SG_OBJ_ROOT, bq_trees[s]->root, 64);
+  // transition quotients (stark.rs:388-422)
+  const uint64_t T = st.original_trace_length;
+  SG_REQUIRE(T >= 2, "transition zerofier needs a trace of at least two rows");
+  DPoly tz = zerofier_geometric_dev(ctx, st.omicron, D, T - 1);
+  std::vector<DPoly> tqs;
+  for (const MPoly* tc : tcs) {
+    uint64_t len = 0;
+    DPoly tp = transition_polynomial(ctx, *tc, trace_polys, Tp, st.omicron, g, len);
+    tqs.push_back(fast_coset_divide_dev(ctx, st.omicron, D, g, tp.p(), len, tz.p(), tz.len));
+  }
+  // randomizer polynomial + codeword (stark.rs:424-445)
+  const uint64_t tcd = max_degree(st, tcs);
+  SG_REQUIRE(nrc == tcd + 1, "randomizer polynomial must have max_degree(transition_constraints) + 1 coefficients");
+  SG_REQUIRE(nrc <= Nf, "fast_coset_evaluate: polynomial longer than root_order");
+  DPoly rpoly = dpoly_upload(ctx, rcoef, nrc);
+  DPoly r_cw = dpoly_alloc(ctx, Nf);
+  {
+    const fe* in = rpoly.p();
+    fe* out = r_cw.p();
+    coset_evaluate_batch(ctx, st.omega, Nf, g, &in, nrc, &out, 1);
+  }
+  std::unique_ptr<sg_tree> r_tree(build_tree(ctx, r_cw.p(), Nf));
+  push_obj(ps, SG_OBJ_ROOT, r_tree->root, 64);
+  // weights (stark.rs:447-450)
+  uint8_t fs[32];
+  if (ps->fiat_shamir_prover(ps->user, 32, fs) != 0)
+    throw Error{SG_ERR_CALLBACK, "proof stream fiat_shamir callback failed"};
+  std::vector<fe> weights = sample_weights(1 + 2 * tqs.size() + 2 * bqs.size(), fs, 32);
+  // degree check (stark.rs:451-465)
+  std::vector<uint64_t> tqdb = transition_quotient_degree_bounds(st, tcs);
+  for (size_t i = 0; i < tqs.size(); ++i) {
+    int64_t d = dev_degree(ctx, tqs[i].p(), tqs[i].len);
+    SG_REQUIRE(d >= 0, "Failed to get degree of transition quotient");
+    SG_REQUIRE((uint64_t)d == tqdb[i], "transition quotient degrees do not match with expectation");
+  }
+  // terms + combination (stark.rs:467-512): x^shift * q via fast_multiply is the exact shift
+  std::vector<uint64_t> bqdb;
+  for (size_t s = 0; s < m; ++s) {
+    int64_t dz = hp_degree(bz[s]);
+    SG_REQUIRE(dz >= 0, "Couldnt get degree of boundary zerofier");
+    bqdb.push_back(Tp - 1 - (uint64_t)dz);
+  }
+  std::vector<DevTerm> terms;
+  std::vector<DPoly> wrapped;  // products that wrap the omicron domain (kept alive for the combination)
+  wrapped.reserve(2 * (tqs.size() + bqs.size()));
+  size_t wi = 0;
+  terms.push_back({rpoly.p(), 0, rpoly.len, weights[wi++]});
+  auto add_pair = [&](const DPoly& q, uint64_t shift) {
+    terms.push_back({q.p(), 0, q.len, weights[wi++]});
+    const fe w = weights[wi++];
+    int64_t d = dev_degree(ctx, q.p(), q.len);
+    if (d < 0) return;  // fast_multiply of a zero polynomial is the empty polynomial
+    if (shift + (uint64_t)d < D) {
+      // no wrap-around: fast_multiply(x^shift, q) is exactly q shifted, truncated at its degree
+      terms.push_back({q.p(), shift, (uint64_t)d + 1, w});
+    } else {
+      // degree >= omicron order: the reference's NTT product wraps; reproduce it step by step
+      std::vector<fe> xs(shift + 1, fe_zero());
+      xs[shift] = fe_one();
+      DPoly dx = dpoly_upload(ctx, xs.data(), xs.size());
+      wrapped.push_back(fast_multiply_dev(ctx, st.omicron, D, dx.p(), dx.len, q.p(), q.len));
+      terms.push_back({wrapped.back().p(), 0, wrapped.back().len, w});
+    }
+  };
+  for (size_t i = 0; i < tqs.size(); ++i) add_pair(tqs[i], tcd - tqdb[i]);
+  for (size_t s = 0; s < m; ++s) add_pair(bqs[s], tcd - bqdb[s]);
+  DPoly comb = lincomb(ctx, terms);
+  SG_REQUIRE(comb.len <= Nf, "fast_coset_evaluate: polynomial longer than root_order");
+  DPoly comb_cw = dpoly_alloc(ctx, Nf);
+  {
+    const fe* in = comb.p();
+    fe* out = comb_cw.p();
+    coset_evaluate_batch(ctx, st.omega, Nf, g, &in, comb.len, &out, 1);
+  }
+  // FRI (stark.rs:514-522)
+  std::vector<size_t> top(st.fri.num_colinearity_tests);
+  fri_prove_dev(ctx, &st.fri, comb_cw.p(), Nf, ps, top.data());
+  // openings (stark.rs:524-560)
+  std::vector<uint64_t> dup;
+  for (size_t i : top) dup.push_back(i);
+  for (size_t i : top) dup.push_back((i + st.expansion) % Nf);
+  std::vector<uint64_t> quad = dup;
+  for (uint64_t i : dup) quad.push_back((i + Nf / 2) % Nf);
+  std::sort(quad.begin(), quad.end());
+  for (size_t s = 0; s < m; ++s) push_openings(ctx, ps, bq_cw[s].p(), bq_trees[s].get(), quad);
+  push_openings(ctx, ps, r_cw.p(), r_tree.get(), quad);
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+}
+
+std::vector<const MPoly*> tc_list(const sg_mpoly* const* tcs, size_t n) {
+  std::vector<const MPoly*> v;
+  for (size_t i = 0; i < n; ++i) {
+    SG_REQUIRE(tcs[i], "null transition constraint");
+    v.push_back(&tcs[i]->m);
+  }
+  return v;
+}
+
+}  // namespace
+
+// ====================================================================== C ABI: Rescue-Prime
+
+extern "C" int sg_rescue_create(sg_ctx* ctx, size_t m, size_t capacity, size_t security_level, size_t N,
+                                sg_rescue** out) {
+  return guard(ctx, [&] {
+    SG_REQUIRE(out, "null argument");
+    std::unique_ptr<sg_rescue> rp(new sg_rescue());
+    rescue_init(*rp, m, capacity, security_level, N);
+    *out = rp.release();
+  });
+}
+
+extern "C" void sg_rescue_free(sg_rescue* rp) { delete rp; }
+
+extern "C" int sg_rescue_info(const sg_rescue* rp, sg_fe* alpha, sg_fe* alpha_inv, sg_fe* mds, sg_fe* mds_inv,
+                              sg_fe* round_constants) {
+  if (!rp) return SG_ERR_INVALID;
+  if (alpha) *alpha = from_fe(fe_from_u128(rp->alpha));
+  if (alpha_inv) *alpha_inv = from_fe(fe_from_u128(rp->alpha_inv));
+  for (size_t i = 0; i < rp->m; ++i)
+    for (size_t j = 0; j < rp->m; ++j) {
+      if (mds) mds[i * rp->m + j] = from_fe(rp->mds[i][j]);
+      if (mds_inv) mds_inv[i * rp->m + j] = from_fe(rp->mds_inv[i][j]);
+    }
+  if (round_constants)
+    for (size_t i = 0; i < rp->rc.size(); ++i) round_constants[i] = from_fe(rp->rc[i]);
+  return SG_OK;
+}
+
+extern "C" int sg_rescue_hash(sg_ctx* ctx, const sg_rescue* rp, sg_fe input, sg_fe* out) {
+  return guard(ctx, [&] {
+    SG_REQUIRE(rp && out, "null argument");
+    SG_REQUIRE(rp->capacity == 1, "Received wrong number of input elements");
+    check_canonical(&input, 1, "input");
+    std::vector<fe> state(rp->m, fe_zero());
+    state[0] = to_fe(input);
+    for (size_t r = 0; r < rp->N; ++r) rp->round(state, r);
+    *out = from_fe(state[0]);
+  });
+}
+
+extern "C" int sg_rescue_trace(sg_ctx* ctx, const sg_rescue* rp, sg_fe input, sg_fe* trace) {
+  return guard(ctx, [&] {
+    SG_REQUIRE(rp && trace, "null argument");
+    SG_REQUIRE(rp->capacity == 1, "Received wrong number of input elements");
+    check_canonical(&input, 1, "input");
+    std::vector<fe> t = rescue_trace(*rp, to_fe(input));
+    memcpy(trace, t.data(), t.size() * sizeof(fe));
+  });
+}
+
+extern "C" int sg_rescue_transition_constraints(sg_ctx* ctx, const sg_rescue* rp, sg_fe omicron,
+                                                uint64_t omicron_domain_length, sg_mpoly** out) {
+  return guard(ctx, [&] {
+    SG_REQUIRE(rp && out, "null argument");
+    SG_HIP(hipSetDevice(ctx->device));
+    std::vector<MPoly> tcs = rescue_transition_constraints(ctx, *rp, to_fe(omicron), omicron_domain_length);
+    for (size_t i = 0; i < tcs.size(); ++i) {
+      out[i] = new sg_mpoly();
+      out[i]->m = std::move(tcs[i]);
+    }
+  });
+}
+
+extern "C" int sg_rescue_boundary_constraints(const sg_rescue* rp, sg_fe output, sg_boundary* out) {
+  if (!rp || !out) return SG_ERR_INVALID;
+  // rescue_prime.rs:285-290
+  out[0] = sg_boundary{0, 1, sg_fe{0, 0}};
+  out[1] = sg_boundary{rp->N, 0, output};
+  return SG_OK;
+}
+
+// ====================================================================== C ABI: STARK
+
+extern "C" int sg_stark_create(sg_ctx* ctx, size_t expansion_factor, size_t num_colinearity_checks,
+                               size_t security_level, size_t num_registers, size_t num_cycles,
+                               size_t transition_constraints_degree, sg_stark** out) {
+  return guard(ctx, [&] {
+    SG_REQUIRE(out, "null argument");
+    // stark.rs:71-114
+    SG_REQUIRE((size_t)bitlen_count(fe_to_u128(fe_prime())) >= security_level, "field order has to be at least security_level bits");
+    SG_REQUIRE(expansion_factor && (expansion_factor & (expansion_factor - 1)) == 0,
+               "expansion_factor must be a power of 2");
+    SG_REQUIRE(expansion_factor >= 4, "expansion_factor must be at least 4");
+    SG_REQUIRE(num_colinearity_checks * 2 >= security_level,
+               "number of collinearity checks must be at least half of security_level");
+    std::unique_ptr<sg_stark> st(new sg_stark());
+    st->expansion = expansion_factor;
+    st->num_colinearity = num_colinearity_checks;
+    st->security = security_level;
+    st->m = num_registers;
+    st->original_trace_length = num_cycles;
+    st->num_randomizers = 4 * num_colinearity_checks;
+    const uint64_t randomized = num_cycles + st->num_randomizers;
+    const int bl = bitlen_count((unsigned __int128)randomized * transition_constraints_degree);
+    SG_REQUIRE(bl <= 40, "omicron domain too large");
+    st->D = (uint64_t)1 << bl;
+    const uint64_t Nf = st->D * expansion_factor;
+    st->generator = fe_generator();
+    st->omega = root_of_order(Nf);
+    st->omicron = root_of_order(st->D);
+    st->fri.offset = from_fe(st->generator);
+    st->fri.omega = from_fe(st->omega);
+    st->fri.domain_length = Nf;
+    st->fri.expansion_factor = expansion_factor;
+    st->fri.num_colinearity_tests = num_colinearity_checks;
+    *out = st.release();
+  });
+}
+
+extern "C" void sg_stark_free(sg_stark* st) { delete st; }
+
+extern "C" int sg_stark_params(const sg_stark* st, sg_fe* omicron, uint64_t* omicron_domain_length, sg_fri* fri,
+                               size_t* num_randomizers) {
+  if (!st) return SG_ERR_INVALID;
+  if (omicron) *omicron = from_fe(st->omicron);
+  if (omicron_domain_length) *omicron_domain_length = st->D;
+  if (fri) *fri = st->fri;
+  if (num_randomizers) *num_randomizers = st->num_randomizers;
+  return SG_OK;
+}
+
+extern "C" int sg_stark_max_degree(sg_ctx* ctx, const sg_stark* st, const sg_mpoly* const* tcs, size_t ntcs,
+                                   uint64_t* out) {
+  return guard(ctx, [&] {
+    SG_REQUIRE(st && out && (tcs || !ntcs), "null argument");
+    *out = max_degree(*st, tc_list(tcs, ntcs));
+  });
+}
+
+extern "C" int sg_stark_degree_bounds(sg_ctx* ctx, const sg_stark* st, const sg_mpoly* const* tcs, size_t ntcs,
+                                      uint64_t* transition_bounds) {
+  return guard(ctx, [&] {
+    SG_REQUIRE(st && transition_bounds && (tcs || !ntcs), "null argument");
+    std::vector<uint64_t> b = transition_degree_bounds(*st, tc_list(tcs, ntcs));
+    std::copy(b.begin(), b.end(), transition_bounds);
+  });
+}
+
+extern "C" int sg_stark_prove(sg_ctx* ctx, const sg_stark* st, const sg_fe* trace, size_t rows,
+                              const sg_mpoly* const* tcs, size_t ntcs, const sg_boundary* boundary, size_t nb,
+                              const sg_fe* trace_randomizers, const sg_fe* randomizer_coeffs, size_t n_rc,
+                              const sg_proof_stream* ps) {
+  return guard(ctx, [&] {
+    SG_REQUIRE(st && (trace || !rows) && (tcs || !ntcs) && (boundary || !nb), "null argument");
+    SG_REQUIRE(trace_randomizers || !st->num_randomizers, "null argument");
+    SG_HIP(hipSetDevice(ctx->device));
+    check_canonical(trace, rows * st->m, "trace");
+    check_canonical(trace_randomizers, st->num_randomizers * st->m, "trace randomizers");
+    check_canonical(randomizer_coeffs, n_rc, "randomizer coefficients");
+    std::vector<Boundary> bnd;
+    for (size_t i = 0; i < nb; ++i) {
+      check_canonical(&boundary[i].value, 1, "boundary value");
+      SG_REQUIRE(boundary[i].reg < st->m, "boundary register out of range");
+      bnd.push_back({boundary[i].cycle, boundary[i].reg, to_fe(boundary[i].value)});
+    }
+    stark_prove(ctx, *st, reinterpret_cast<const fe*>(trace), rows, tc_list(tcs, ntcs), bnd,
+                reinterpret_cast<const fe*>(trace_randomizers), reinterpret_cast<const fe*>(randomizer_coeffs), n_rc,
+                ps);
+  });
+}

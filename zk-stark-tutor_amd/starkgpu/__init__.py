@@ -10,5 +10,6 @@ from .api import (CODEWORD, FIELD_PRIME, LEAFS, PATH, PROOF_BYTES, ROOT, VALUE, 
 
 from .algebra import (Polynomial, fast_coset_divide, fast_interpolate_domain, fast_interpolate_geometric_dev,
                       fast_multiply, fast_zerofier, fast_zerofier_geometric)
+from .stark import MPolynomial, RescuePrime, Stark
 
 __all__ = [n for n in dir() if not n.startswith("_")]

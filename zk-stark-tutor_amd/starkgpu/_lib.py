@@ -131,6 +131,38 @@ PROTOTYPES = {
     "sg_fast_interpolate_domain": (ctypes.c_int, [_vp, sg_fe, ctypes.c_uint64, _vp, _vp, _sz, _P(_vp)]),
     "sg_fast_zerofier_geometric": (ctypes.c_int, [_vp, sg_fe, ctypes.c_uint64, _sz, _P(_vp)]),
     "sg_fast_interpolate_geometric_dev": (ctypes.c_int, [_vp, sg_fe, ctypes.c_uint64, _vp, _sz, _P(_vp)]),
+    # multivariate polynomials (m_polynomial.rs)
+    "sg_mpoly_create": (ctypes.c_int, [_vp, _sz, _sz, _vp, _vp, _P(_vp)]),
+    "sg_mpoly_constant": (ctypes.c_int, [_vp, sg_fe, _P(_vp)]),
+    "sg_mpoly_variable": (ctypes.c_int, [_vp, _sz, _sz, _P(_vp)]),
+    "sg_mpoly_lift": (ctypes.c_int, [_vp, _vp, _sz, _sz, _P(_vp)]),
+    "sg_mpoly_lift_poly": (ctypes.c_int, [_vp, _vp, _sz, _P(_vp)]),
+    "sg_mpoly_neg": (ctypes.c_int, [_vp, _vp, _P(_vp)]),
+    "sg_mpoly_add": (ctypes.c_int, [_vp, _vp, _vp, _P(_vp)]),
+    "sg_mpoly_sub": (ctypes.c_int, [_vp, _vp, _vp, _P(_vp)]),
+    "sg_mpoly_mul": (ctypes.c_int, [_vp, _vp, _vp, _P(_vp)]),
+    "sg_mpoly_pow": (ctypes.c_int, [_vp, _vp, sg_fe, _P(_vp)]),
+    "sg_mpoly_is_zero": (ctypes.c_int, [_vp]),
+    "sg_mpoly_evaluate": (ctypes.c_int, [_vp, _vp, _vp, _sz, _fep]),
+    "sg_mpoly_shape": (ctypes.c_int, [_vp, _P(_sz), _P(_sz), _P(_sz)]),
+    "sg_mpoly_export": (ctypes.c_int, [_vp, _vp, _vp, _vp]),
+    "sg_mpoly_free": (None, [_vp]),
+    # Rescue-Prime (rescue_prime/rescue_prime.rs)
+    "sg_rescue_create": (ctypes.c_int, [_vp, _sz, _sz, _sz, _sz, _P(_vp)]),
+    "sg_rescue_free": (None, [_vp]),
+    "sg_rescue_info": (ctypes.c_int, [_vp, _fep, _fep, _vp, _vp, _vp]),
+    "sg_rescue_hash": (ctypes.c_int, [_vp, _vp, sg_fe, _fep]),
+    "sg_rescue_trace": (ctypes.c_int, [_vp, _vp, sg_fe, _vp]),
+    "sg_rescue_transition_constraints": (ctypes.c_int, [_vp, _vp, sg_fe, ctypes.c_uint64, _P(_vp)]),
+    "sg_rescue_boundary_constraints": (ctypes.c_int, [_vp, sg_fe, _vp]),
+    # STARK (stark/stark.rs)
+    "sg_stark_create": (ctypes.c_int, [_vp, _sz, _sz, _sz, _sz, _sz, _sz, _P(_vp)]),
+    "sg_stark_free": (None, [_vp]),
+    "sg_stark_params": (ctypes.c_int, [_vp, _fep, _P(ctypes.c_uint64), _P(sg_fri), _P(_sz)]),
+    "sg_stark_max_degree": (ctypes.c_int, [_vp, _vp, _vp, _sz, _P(ctypes.c_uint64)]),
+    "sg_stark_degree_bounds": (ctypes.c_int, [_vp, _vp, _vp, _sz, _vp]),
+    "sg_stark_prove": (ctypes.c_int, [_vp, _vp, _vp, _sz, _vp, _sz, _vp, _sz, _vp, _vp, _sz,
+                                      _P(sg_proof_stream)]),
 }
 
 _lib = None
