@@ -90,14 +90,11 @@ def div(a: int, b: int) -> int:
 
 
 def fpow(x: int, e: int) -> int:
-    """field/field_element.rs:108-143: left-to-right square-and-multiply over bitlen(e)."""
-    acc = 1
-    nbits = max(e.bit_length(), 1)  # BitIter of 0 yields one (false) bit
-    for i in range(nbits - 1, -1, -1):
-        acc = mul_mod(acc, acc)
-        if (e >> i) & 1:
-            acc = mul_mod(acc, x)
-    return acc
+    """field/field_element.rs:108-143: left-to-right square-and-multiply over bitlen(e).
+
+    The loop computes x^e mod p (x^0 = 1, including 0^0); CPython's three-argument pow
+    returns the same value and is used for speed."""
+    return pow(x, e, P)
 
 
 def primitive_nth_root(n: int) -> int:

@@ -484,11 +484,12 @@ class RescuePrime:
         seed = "Rescue-XLIX({},{},{},{})".format(P, m, capacity, security_level).encode()
         raw = shake256(seed, bytes_per_int * num)
         out = []
+        f256 = [fpow(256, j) for j in range(bytes_per_int)]
         for i in range(num):
             chunk = raw[bytes_per_int * i: bytes_per_int * (i + 1)]
             acc = 0
             for j, b in enumerate(chunk):
-                acc = add_mod(acc, mul_mod(fpow(256, j), b))
+                acc = add_mod(acc, mul_mod(f256[j], b))
             out.append(acc)
         return out
 
@@ -760,7 +761,8 @@ class Stark:
         tcd = self.max_degree(tcs)
         tqdb = self.transition_quotient_degree_bounds(tcs)
         bqdb = self.boundary_quotient_degree_bounds(rtl, boundary)
-        tz = self.transition_zerofier()
+        # transition_zerofier().evaluate(x) == prod_{i < T-1} (x - omicron^i), evaluated directly
+        tdom = [self.omicron_pow(i) for i in range(self.original_trace_length - 1)]
         for ii, ic in enumerate(indices):
             x = mul_mod(self.fri.offset, fpow(self.fri.omega, ic))
             inx = (ic + self.expansion_factor) % N
@@ -772,7 +774,9 @@ class Stark:
             point = [x] + cur + nxt
             tvals = [tc.evaluate(point) for tc in tcs]
             terms = [rnd[ic]]
-            zx = p_evaluate(tz, x)
+            zx = 1
+            for d in tdom:
+                zx = zx * (x - d) % P
             for s, tv in enumerate(tvals):
                 q = div(tv, zx)
                 terms.append(q)
@@ -793,3 +797,106 @@ def fast_coset_evaluate_ref(generator: int, root_order: int, offset: int, coeffs
         raise ValueError("polynomial longer than root_order")
     c = p_scale(coeffs, offset) + [0] * (root_order - len(coeffs))
     return ntt(generator, c)
+
+
+# ------------------------------------------- Rescue AIR evaluated from its structure
+
+class RescueAirAtPoint:
+    """The value of RescuePrime.transition_constraints()[i] at a point, from the AIR's structure
+    (rescue_prime.rs:246-283): sum_k MDS[i][k] prev_k^alpha + C1_i(x) - (sum_k MDS^-1[i][k]
+    (next_k - C2_k(x)))^alpha, with the round-constant interpolants C1/C2 (degree < N over
+    omicron^r, r < N) evaluated by the barycentric formula in O(N) per point.  Used to verify
+    proofs at sizes where the expanded MPolynomial (O(N^2) to build) is out of reach; `d`
+    holds keys whose maximum equals the full key set's in stark.rs:117-160 (which only takes a
+    max): x^(3(N-1)), prev/next cubes and the mixed cubic terms."""
+
+    def __init__(self, rp: RescuePrime, i: int, bary: "GeometricBarycentric"):
+        self.rp, self.i, self.bary = rp, i, bary
+        m, N = rp.m, rp.N
+        nv = 1 + 2 * m
+        keys = {(3 * (N - 1),) + (0,) * (2 * m), (N - 1,) + (0,) * (2 * m)}
+        for k in range(m):
+            e = [0] * nv
+            e[1 + k] = 3
+            keys.add(tuple(e))
+            for a in range(4):
+                e = [0] * nv
+                e[1 + m + k] = a
+                e[0] = (3 - a) * (N - 1)
+                keys.add(tuple(e))
+        self.d = {k: 0 for k in keys}
+
+    @staticmethod
+    def for_rescue(rp: RescuePrime, omicron: int) -> List["RescueAirAtPoint"]:
+        m = rp.m
+        cols = {}
+        for i in range(m):
+            cols[("c1", i)] = [rp.round_constants[2 * r * m + i] for r in range(rp.N)]
+            cols[("c2", i)] = [rp.round_constants[2 * r * m + m + i] for r in range(rp.N)]
+        bary = GeometricBarycentric(omicron, rp.N, cols)
+        return [RescueAirAtPoint(rp, i, bary) for i in range(m)]
+
+    def evaluate(self, point):
+        rp, i, m = self.rp, self.i, self.rp.m
+        x = point[0]
+        prev, nxt = point[1:1 + m], point[1 + m:1 + 2 * m]
+        lhs = self.bary.value(x, ("c1", i))
+        for k in range(m):
+            lhs = (lhs + rp.MDS[i][k] * fpow(prev[k], rp.alpha)) % P
+        acc = 0
+        for k in range(m):
+            acc = (acc + rp.MDS_inv[i][k] * (nxt[k] - self.bary.value(x, ("c2", k)))) % P
+        return (lhs - fpow(acc, rp.alpha)) % P
+
+
+class GeometricBarycentric:
+    """Barycentric evaluation of the interpolants through (q^r, v_r), r < n, q of order >= n,
+    for a set of value columns: P(x) = Z(x) sum_r v_r w_r / (x - q^r),
+    1/w_r = q^(r(r-1)/2 + r(n-1-r)) A_r B_(n-1-r), A_k = prod_{i<=k} (q^i - 1),
+    B_k = prod_{i<=k} (1 - q^i).  Same values as the unique interpolant
+    fast_interpolate_domain returns (ntt_arithmetics.rs:172-237)."""
+
+    def __init__(self, q: int, n: int, columns):
+        self.q, self.n = q, n
+        self.dom = [1] * n
+        for r in range(1, n):
+            self.dom[r] = self.dom[r - 1] * q % P
+        A, B = [1] * n, [1] * n
+        for k in range(1, n):
+            qk = self.dom[k]
+            A[k] = A[k - 1] * (qk - 1) % P
+            B[k] = B[k - 1] * (1 - qk) % P
+        # q^(e_r), e_r = r(r-1)/2 + r(n-1-r); e_{r+1} - e_r = n - 2 - r
+        qinv = inv(q)
+        step = fpow(q, n - 2) if n >= 2 else 1
+        pe, winv = 1, []
+        for r in range(n):
+            winv.append(pe * A[r] % P * B[n - 1 - r] % P)
+            pe = pe * step % P
+            step = step * qinv % P
+        w = _batch_inv(winv)
+        self.cols = {k: [v * wr % P for v, wr in zip(vals, w)] for k, vals in columns.items()}
+        self.cache = {}
+
+    def value(self, x: int, key) -> int:
+        if x not in self.cache:
+            diffs = [(x - d) % P for d in self.dom]
+            z = 1
+            for dd in diffs:
+                z = z * dd % P
+            iv = _batch_inv(diffs)
+            self.cache[x] = {k: z * (sum(a * b for a, b in zip(col, iv)) % P) % P for k, col in self.cols.items()}
+        return self.cache[x][key]
+
+
+def _batch_inv(xs):
+    pre, acc = [], 1
+    for x in xs:
+        pre.append(acc)
+        acc = acc * x % P
+    inv_acc = inv(acc)
+    out = [0] * len(xs)
+    for i in range(len(xs) - 1, -1, -1):
+        out[i] = inv_acc * pre[i] % P
+        inv_acc = inv_acc * xs[i] % P
+    return out

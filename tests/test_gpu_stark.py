@@ -162,3 +162,40 @@ def test_stark_prove_callback_stream_and_errors():
     assert pys.digest() == want
     with pytest.raises(sg.StarkGpuError):
         st_g.prove(trace, air_g, bnd, sg.IndependentProofStream(), tr, rc[:-1])
+
+
+def test_stark_prove_c4_rescue_trace_2p16():
+    """BASELINE config C4 at full size: Rescue-Prime (m=2, N=65278 -> trace 2^16 rows with the 256
+    randomizer rows), expansion 8, 64 colinearity checks, security 128, transition degree 3
+    (omicron domain 2^18, FRI domain 2^21).  The oracle cannot rebuild the expanded AIR at this
+    size (O(N^2)), so the proof is checked by the oracle's verifier with the AIR evaluated from
+    its structure (RescueAirAtPoint), and a false claim must be rejected."""
+    import time
+    N = 65278
+    rp_g = sg.RescuePrime(2, 1, 128, N)
+    st_g = sg.Stark(8, 64, 128, 2, N + 1, 3)
+    assert st_g.omicron_domain_length == 1 << 18 and st_g.fri_domain_length == 1 << 21
+    air_g = rp_g.transition_constraints(st_g.omicron, st_g.omicron_domain_length)
+    rp_o = e.RescuePrime(2, 1, 128, N)
+    assert rp_g.round_constants == rp_o.round_constants
+    inp = o.sample(b"c4")
+    out = rp_o.hash(inp)
+    trace = rp_g.trace_array(inp)
+    assert sg.to_ints(trace[-2:-1])[0] == out
+    st_o = e.Stark(8, 64, 128, 2, N + 1, 3)
+    sair = e.RescueAirAtPoint.for_rescue(rp_o, st_o.omicron)
+    assert st_g.transition_degree_bounds(air_g) == st_o.transition_degree_bounds(sair)
+    nrc = st_g.num_randomizer_coefficients(air_g)
+    r = e.randomness_from_seed(b"c4", 2 * st_g.num_randomizers + nrc)
+    tr = sg.fe_array(r[:2 * st_g.num_randomizers])
+    rc = sg.fe_array(r[2 * st_g.num_randomizers:])
+    bnd = rp_o.boundary_constraints(out)
+    ps = sg.IndependentProofStream()
+    t0 = time.perf_counter()
+    st_g.prove(trace, air_g, bnd, ps, tr, rc)
+    print("C4 prove: %.1f ms" % ((time.perf_counter() - t0) * 1e3))
+    objs = ps.objects()
+    ok, err = st_o.verify(sair, bnd, o.IndependentProofStream(objs))
+    assert ok, err
+    ok, _ = st_o.verify(sair, rp_o.boundary_constraints(o.add_mod(out, 1)), o.IndependentProofStream(objs))
+    assert not ok
