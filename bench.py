@@ -1,18 +1,21 @@
 #!/usr/bin/env python3
-"""Benchmark: the STARK prover's LDE + Merkle + FRI hot block on MI355X.
+"""Benchmark: end-to-end Stark::prove on a Rescue-Prime trace of 2^20 rows, on MI355X.
 
-Workload (BASELINE.json metric "NTT Gelem/s + prove ms, Rescue-Prime trace 2^20",
-SURVEY.md §8(d) last row): per step, the Stark::prove LDE+commit block
-(stark/stark.rs:367-386, 425-445, 500-522) for a trace of 2^20 rows with
-m = 2 registers, expansion factor 8 (N = 2^23) and 64 colinearity tests:
-  * 2 boundary-quotient polynomials (2^20 coefficients): LDE -> Merkle commit -> push root
-  * 1 randomizer polynomial:  LDE -> Merkle commit -> push root
-  * Fiat-Shamir weights (stark.rs:447-450)
-  * 1 combination polynomial: LDE -> FRI::prove (commit: 15 folds + 16 Merkle trees; query phase)
-Polynomial coefficients are synthetic (seeded SHAKE256 stream);
-the O(T^2) trace interpolation / quotient algebra that produces them in the
-reference is out of scope.  Inputs are resident in HBM
-before timing starts.
+Workload (BASELINE.json metric "NTT Gelem/s + prove ms, Rescue-Prime trace 2^20"):
+one step = one complete `Stark::prove` (stark/stark.rs:276-562) of a Rescue-Prime
+(m = 2, capacity 1, security 128) execution trace with 2^20 - 1 randomized rows
+(N = 2^20 - 258 rounds + 256 randomizer rows; the same convention as BASELINE
+config C4 at 2^16), expansion factor 8, 64 colinearity checks, transition degree 3
+(omicron domain 2^22, FRI domain 2^25):
+  trace interpolation -> boundary quotients -> 2 LDEs + Merkle commits ->
+  transition polynomials (AIR on a coset) / zerofier division -> randomizer LDE +
+  commit -> Fiat-Shamir weights -> combination polynomial -> LDE -> FRI::prove ->
+  openings.
+The trace, the randomizers (thread_rng draws, injected from a seeded generator)
+and the transition constraints are resident in HBM before timing starts; every
+step writes a complete proof into a fresh proof stream.
+`value` = committed codeword elements per second ((m + 2) x 2^25 per proof);
+`prove_ms` = the proof time.
 
 One process per GPU (torchrun); each rank proves its own independent trace
 (weak scaling, no collective on the data path).  Rank 0 prints one JSON line.
@@ -63,7 +66,48 @@ def to_device(arr: np.ndarray, device) -> torch.Tensor:
     return torch.from_numpy(arr.view(np.int64).copy()).to(device)
 
 
-class Workload:
+class ProveWorkload:
+    """Stark::prove on a Rescue-Prime trace with 2^log_rows - 1 randomized rows (stark.rs:276-562)."""
+
+    def __init__(self, rank: int, device, ctx: sg.Context, log_rows=LOG_TRACE):
+        self.ctx = ctx
+        self.N = (1 << log_rows) - 2 - 4 * COLINEARITY  # Rescue rounds: trace N + 1 rows
+        self.rp = sg.RescuePrime(REGISTERS, 1, 128, self.N, ctx=ctx)
+        self.stark = sg.Stark(EXPANSION, COLINEARITY, 128, REGISTERS, self.N + 1, 3, ctx=ctx)
+        self.air = self.rp.transition_constraints(self.stark.omicron, self.stark.omicron_domain_length)
+        inp = int.from_bytes(hashlib_shake(b"sg-bench-input" + rank.to_bytes(8, "big"), 16), "big") % P
+        self.boundary = self.rp.boundary_constraints(self.rp.hash(inp))
+        self.trace = to_device(self.rp.trace_array(inp), device)
+        self.rows = self.N + 1
+        self.nrc = self.stark.num_randomizer_coefficients(self.air)
+        self.trace_rand = to_device(synthetic_fe(rank, b"trace-rand", REGISTERS * self.stark.num_randomizers), device)
+        self.rcoef = to_device(synthetic_fe(rank, b"rand-poly", self.nrc), device)
+        self.fri_len = self.stark.fri_domain_length
+        self.last_proof = None
+
+    def step(self, phases=None):
+        t0 = time.perf_counter()
+        stream = sg.IndependentProofStream()
+        self.stark.prove_dev(self.trace.data_ptr(), self.rows, self.air, self.boundary, stream,
+                             self.trace_rand.data_ptr(), self.rcoef.data_ptr(), self.nrc)
+        self.last_proof = stream
+        if phases is not None:
+            phases["prove"] = phases.get("prove", 0.0) + (time.perf_counter() - t0)
+        return stream
+
+    def elements_per_step(self) -> int:
+        return (REGISTERS + 2) * self.fri_len
+
+
+def hashlib_shake(data: bytes, n: int) -> bytes:
+    import hashlib
+    return hashlib.shake_256(data).digest(n)
+
+
+class BlockWorkload:
+    """The LDE + commit block of earlier rounds (side measurement): synthetic 2^20-coefficient
+    polynomials, N = 2^23 (stark.rs:367-386, 425-445, 500-522)."""
+
     def __init__(self, rank: int, device, ctx: sg.Context, log_trace=LOG_TRACE):
         self.ctx = ctx
         self.d = 1 << log_trace
@@ -175,6 +219,33 @@ def side_measurements(ctx: sg.Context, device, iters: int = 5) -> dict:
     return out
 
 
+def block_and_c4(ctx: sg.Context, device, iters: int = 5) -> dict:
+    """The LDE+commit block of earlier rounds (N = 2^23) and BASELINE config C4 (Stark::prove on a
+    Rescue-Prime trace of 2^16 - 1 randomized rows, FRI domain 2^21)."""
+    out = {}
+    blk = BlockWorkload(0, device, ctx)
+    blk.step()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        blk.step()
+    torch.cuda.synchronize(device)
+    out["lde_commit_block_2p23_ms"] = round((time.perf_counter() - t0) / iters * 1e3, 3)
+    del blk
+    c4 = ProveWorkload(0, device, ctx, 16)
+    c4.step()
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        c4.step()
+    torch.cuda.synchronize(device)
+    out["c4_prove_trace_2p16_ms"] = round((time.perf_counter() - t0) / iters * 1e3, 3)
+    out["c4_proof_bytes"] = len(c4.last_proof.digest())
+    del c4
+    ctx.trim()
+    return out
+
+
 def allreduce_max(value: float, device) -> float:
     """max over ranks (device tensor on RCCL, host tensor on gloo)."""
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
@@ -261,9 +332,11 @@ def side_sharded(ctx: sg.Context, device, world: int, rank: int, iters: int = 3)
 def cpu_baseline_leg(seconds_budget: float = 15.0):
     """The reference-faithful C restatement (oracle/ref_cpu.c) on one host core, on a bounded sample.
 
-    Same block as the GPU step (4 LDEs, 3 Merkle commits, FRI commit + query
-    with the reference's O(n)-per-opening Merkle::open), at trace 2^9
-    (N = 2^12), repeated until ~seconds_budget of CPU time.
+    The LDE + commit + FRI part of the prove (4 LDEs, 3 Merkle commits, FRI commit +
+    query with the reference's O(n)-per-opening Merkle::open) at trace 2^9
+    (N = 2^12), repeated until ~seconds_budget of CPU time.  The reference's
+    trace interpolation and quotient algebra are O(T^2) and are
+    timed separately through the Python restatement (cpu_baseline_e2e).
     """
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import ref_cpu as rc
@@ -310,14 +383,42 @@ def cpu_baseline_leg(seconds_budget: float = 15.0):
     }
 
 
+def cpu_baseline_e2e(seconds_budget: float = 6.0) -> dict:
+    """The whole Stark::prove through the oracle's restatement (oracle/stark_prove_oracle.py: the
+    reference's O(n^2) polynomial algebra, pure Python) at the reference test's size: Rescue-Prime
+    N = 27, expansion 4, c = 2 (stark.rs:823-840), one core."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import stark_oracle as o
+    import stark_prove_oracle as e
+    rp = e.RescuePrime(2, 1, 2, 27)
+    st = e.Stark(4, 2, 2, 2, 28, 2)
+    air = rp.transition_constraints(st.omicron, st.omicron_domain_length)
+    inp = o.sample(b"deadbeef")
+    trace, bnd = rp.trace(inp), rp.boundary_constraints(rp.hash(inp))
+    r = e.randomness_from_seed(b"cpu", 2 * st.num_randomizers + st.num_randomizer_coefficients(air))
+    tr = [r[2 * i:2 * i + 2] for i in range(st.num_randomizers)]
+    rc = r[2 * st.num_randomizers:]
+    n, t0 = 0, time.perf_counter()
+    while True:
+        st.prove(trace, air, bnd, o.IndependentProofStream(), tr, rc)
+        n += 1
+        el = time.perf_counter() - t0
+        if el >= seconds_budget or n >= 50:
+            break
+    per = el / n
+    return {"value": round(4 * st.fri.domain_length / per / 1e9, 9), "unit": "Gelem/s", "cores": 1, "kind": "port",
+            "sample": f"Stark::prove, Rescue-Prime N=27 (reference test size, FRI domain 512), {n} proofs, "
+                      f"{per * 1e3:.1f} ms/proof; Python restatement of the reference's algorithms"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--log-trace", type=int, default=LOG_TRACE)
+    ap.add_argument("--log-trace", type=int, default=LOG_TRACE, help="log2 of the randomized trace rows + 1")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-side", action="store_true", help="skip the C2 NTT and 2^24 north-star side measurements")
+    ap.add_argument("--no-side", action="store_true", help="skip the side measurements (C2, C4, C5, block, 2^24)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -335,7 +436,7 @@ def main():
             dist.init_process_group(backend, timeout=timedelta(seconds=600))
 
     ctx = sg.Context(gpu)
-    wl = Workload(rank, device, ctx, args.log_trace)
+    wl = ProveWorkload(rank, device, ctx, args.log_trace)
     # warmup; the last warmup step runs with every launch timed, which yields the
     # per-kernel breakdown and picks the dominant kernel for the roofline
     breakdown = {}
@@ -402,10 +503,15 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "u128 (F_p, p = 1 + 407*2^119)",
-        "data": "synthetic (seeded SHAKE256 coefficients, SURVEY.md 8(d))",
-        "config": {"workload": f"Stark LDE+commit block: trace 2^{args.log_trace}, {REGISTERS} registers, "
-                               f"expansion {EXPANSION} (N=2^{args.log_trace + 3}), FRI prove c={COLINEARITY}",
+        "data": "synthetic: Rescue-Prime execution trace of a seeded input; randomizers from a seeded "
+                "SHAKE256 stream (SURVEY.md 8(d))",
+        "config": {"workload": f"Stark::prove, Rescue-Prime m={REGISTERS} trace {wl.rows} rows "
+                               f"(+{wl.stark.num_randomizers} randomizers = 2^{args.log_trace} - 1), "
+                               f"expansion {EXPANSION}, c={COLINEARITY}, security 128, transition degree 3 "
+                               f"(omicron domain 2^{wl.stark.omicron_domain_length.bit_length() - 1}, "
+                               f"FRI domain 2^{wl.fri_len.bit_length() - 1})",
                    "codeword_elements_per_step_per_gpu": wl.elements_per_step(),
+                   "proof_bytes": len(wl.last_proof.digest()) if wl.last_proof is not None else None,
                    "parallelism": f"replicas x{world} (independent traces, no data-path collective)"},
         "roofline": {"kernel": name, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
@@ -418,7 +524,10 @@ def main():
         "host_phases_ms": {k: round(v / args.steps * 1e3, 3) for k, v in host_phases.items()},
     }
     if world == 1 and not args.no_side:
+        del wl
+        ctx.trim()
         result["side"] = side_measurements(ctx, device)
+        result["side"].update(block_and_c4(ctx, device))
         result["side"].update(c5_single_gpu(ctx, device))
     if world > 1 and not args.no_side:
         # a hang in a collective must not cost the main line: rank 0 prints it and exits
@@ -439,6 +548,7 @@ def main():
             watchdog.cancel()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline_leg()
+        result["cpu_baseline_e2e"] = cpu_baseline_e2e()
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -309,6 +309,11 @@ int sg_stark_degree_bounds(sg_ctx* ctx, const sg_stark* st, const sg_mpoly* cons
 int sg_stark_prove(sg_ctx* ctx, const sg_stark* st, const sg_fe* trace, size_t rows, const sg_mpoly* const* tcs,
                    size_t ntcs, const sg_boundary* boundary, size_t nb, const sg_fe* trace_randomizers,
                    const sg_fe* randomizer_coeffs, size_t n_rc, const sg_proof_stream* ps);
+/* the same with the trace, the trace randomizers and the randomizer coefficients in device memory */
+int sg_stark_prove_dev(sg_ctx* ctx, const sg_stark* st, const sg_fe* d_trace, size_t rows,
+                       const sg_mpoly* const* tcs, size_t ntcs, const sg_boundary* boundary, size_t nb,
+                       const sg_fe* d_trace_randomizers, const sg_fe* d_randomizer_coeffs, size_t n_rc,
+                       const sg_proof_stream* ps);
 
 #ifdef __cplusplus
 }

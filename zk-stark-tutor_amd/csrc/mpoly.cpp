@@ -95,6 +95,7 @@ MPoly mp_lift(const HPoly& poly, uint32_t vi) {
 
 MPoly mp_neg(const MPoly& a) {
   MPoly r = a;
+  r.dev.reset();
   for (auto& kv : r.g)
     for (auto& c : kv.second) c = fe_neg(c);
   return r;
@@ -146,6 +147,32 @@ MPoly mp_pow(sg_ctx* ctx, const MPoly& a, unsigned __int128 e) {
     if ((e >> i) & 1) acc = mp_mul(ctx, acc, a);
   }
   return acc;
+}
+
+MPolyDevice::~MPolyDevice() {
+  for (void* p : ptr)
+    if (p) (void)hipFree(p);
+}
+
+const MPolyDevice& mp_device(sg_ctx* ctx, const MPoly& a) {
+  if (a.dev && a.dev->device == ctx->device) return *a.dev;
+  auto d = std::make_shared<MPolyDevice>();
+  d->device = ctx->device;
+  for (auto& kv : a.g) {
+    const int64_t deg = hp_degree(kv.second);
+    void* p = nullptr;
+    if (deg >= 0) {
+      SG_HIP(hipMalloc(&p, (size_t)(deg + 1) * sizeof(fe)));
+      d->ptr.push_back(p);
+      SG_HIP(hipMemcpyAsync(p, kv.second.data(), (size_t)(deg + 1) * sizeof(fe), hipMemcpyHostToDevice, ctx->stream));
+    } else {
+      d->ptr.push_back(nullptr);
+    }
+    d->len.push_back((uint64_t)(deg + 1));
+  }
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  a.dev = d;
+  return *a.dev;
 }
 
 fe mp_evaluate(const MPoly& a, const std::vector<fe>& point) {

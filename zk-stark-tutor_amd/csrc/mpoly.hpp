@@ -14,6 +14,7 @@
 #pragma once
 #include <cstdint>
 #include <map>
+#include <memory>
 #include <vector>
 
 #include "context.hpp"
@@ -22,10 +23,22 @@
 
 namespace sg {
 
+// device-resident copies of the group x-vectors (trimmed at their degree), uploaded on first
+// use by the prover: the constraints are an input of every proof, like the trace
+struct MPolyDevice {
+  int device = -1;
+  std::vector<void*> ptr;      // per group (map order); nullptr for an all-zero group
+  std::vector<uint64_t> len;   // degree + 1 (0 for an all-zero group)
+  ~MPolyDevice();
+};
+
 struct MPoly {
   uint32_t nvars = 0;                          // key length (0: empty dictionary)
   std::map<std::vector<uint32_t>, HPoly> g;    // exponents of variables 1..nvars-1 -> x coefficients
+  mutable std::shared_ptr<MPolyDevice> dev;    // lazily built (polynomials are immutable once built)
 };
+
+const MPolyDevice& mp_device(sg_ctx* ctx, const MPoly& a);
 
 MPoly mp_constant(const fe& c);
 std::vector<MPoly> mp_variables(uint32_t n);

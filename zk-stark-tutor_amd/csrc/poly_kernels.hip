@@ -277,7 +277,21 @@ __global__ __launch_bounds__(kBlock) void k_lincomb(LinCombArgs a) {
   }
 }
 
+// out[i] = in[i * stride]  (one register column of a row-major trace)
+__global__ __launch_bounds__(kBlock) void k_gather_stride(fe* __restrict__ out, const fe* __restrict__ in, uint64_t n,
+                                                          uint64_t stride) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
+    st_fe(out + i, ld_fe(in + i * stride));
+}
+
 // ================================================================ launchers
+
+hipError_t launch_gather_stride(fe* out, const fe* in, uint64_t n, uint64_t stride, hipStream_t s) {
+  if (!n) return hipSuccess;
+  ProfScope ps("gather_stride", 32 * n, s);
+  hipLaunchKernelGGL(k_gather_stride, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, s, out, in, n, stride);
+  return hipGetLastError();
+}
 
 hipError_t launch_ew_mul(fe* out, const fe* a, const fe* b, uint64_t n, const fe& r2, hipStream_t s) {
   if (!n) return hipSuccess;

@@ -45,5 +45,6 @@ hipError_t launch_interp_assemble(fe* V, const fe* y, const fe* Zv, const fe* S,
 hipError_t launch_last_nonzero(const fe* a, uint64_t n, unsigned long long* last, hipStream_t s);
 hipError_t launch_air_eval(const AirEvalArgs& a, hipStream_t s);
 hipError_t launch_lincomb(const LinCombArgs& a, hipStream_t s);
+hipError_t launch_gather_stride(fe* out, const fe* in, uint64_t n, uint64_t stride, hipStream_t s);
 
 }  // namespace sg

@@ -187,15 +187,14 @@ void rescue_init(sg_rescue& rp, size_t m, size_t capacity, size_t security, size
   std::vector<uint8_t> raw(bytes_per_int * std::max<size_t>(num, 1));
   shake256(reinterpret_cast<const uint8_t*>(seed), strlen(seed), raw.data(), bytes_per_int * num);
   rp.rc.resize(num);
-  const fe f256 = fe_from_u64(256);
-  std::vector<fe> pw(bytes_per_int);
-  pw[0] = fe_one();
-  for (size_t j = 1; j < bytes_per_int; ++j) pw[j] = fe_mul(pw[j - 1], f256);
+  SG_REQUIRE(bytes_per_int == 17, "round constants: 17-byte chunks expected for this field");
+  // sum_j 256^j b_j = L + b16 2^128 with L the little-endian u128 of bytes 0..15
+  const fe two128 = fe_from_u128((unsigned __int128)0 - p);  // 2^128 mod p (2^128 < 2p)
   for (size_t i = 0; i < num; ++i) {
-    fe acc = fe_zero();
-    for (size_t j = 0; j < bytes_per_int; ++j)
-      acc = fe_add(acc, fe_mul(pw[j], fe_from_u64(raw[bytes_per_int * i + j])));
-    rp.rc[i] = acc;
+    const uint8_t* c = raw.data() + bytes_per_int * i;
+    unsigned __int128 L = 0;
+    for (int j = 15; j >= 0; --j) L = (L << 8) | c[j];
+    rp.rc[i] = fe_add(fe_from_u128(L % p), fe_mul(fe_from_u64(c[16]), two128));
   }
 }
 
@@ -387,17 +386,17 @@ DPoly transition_polynomial(sg_ctx* ctx, const MPoly& tc, const std::vector<DPol
     V.push_back(dpoly_alloc(ctx, L));
     coset_values_dev(ctx, trace_polys[s].p(), trace_polys[s].len, L, off_omicron, V.back().p());
   }
-  // group x-polynomials on the same coset
+  // group x-polynomials (device-resident, uploaded once per constraint) on the same coset
+  const MPolyDevice& xd = mp_device(ctx, tc);
   std::vector<DPoly> Q;
   std::vector<uint32_t> exps;
   const int nv = 2 * (int)m;
-  for (auto& kv : tc.g) {
-    const int64_t dx = hp_degree(kv.second);
-    if (dx < 0) continue;  // an all-zero group adds nothing (its products are zero polynomials)
-    DPoly x = dpoly_upload(ctx, kv.second.data(), (uint64_t)dx + 1);
+  size_t gi = 0;
+  for (auto it = tc.g.begin(); it != tc.g.end(); ++it, ++gi) {
+    if (!xd.len[gi]) continue;  // an all-zero group adds nothing (its products are zero polynomials)
     Q.push_back(dpoly_alloc(ctx, L));
-    coset_values_dev(ctx, x.p(), x.len, L, offset, Q.back().p());
-    for (int j = 0; j < nv; ++j) exps.push_back(j < (int)kv.first.size() ? kv.first[j] : 0u);
+    coset_values_dev(ctx, reinterpret_cast<const fe*>(xd.ptr[gi]), xd.len[gi], L, offset, Q.back().p());
+    for (int j = 0; j < nv; ++j) exps.push_back(j < (int)it->first.size() ? it->first[j] : 0u);
   }
   DPoly vals = dpoly_alloc(ctx, L);
   if (Q.empty()) {
@@ -488,9 +487,10 @@ struct AsyncScope {
 };
 
 // stark.rs:276-562
-void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* trace, size_t rows, const std::vector<const MPoly*>& tcs,
-                 const std::vector<Boundary>& bnd, const fe* trace_rand, const fe* rcoef, size_t nrc,
-                 const sg_proof_stream* ps) {
+// d_trace: rows x m (row-major), d_trace_rand: num_randomizers x m, d_rcoef: nrc -- all on the device
+void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows,
+                 const std::vector<const MPoly*>& tcs, const std::vector<Boundary>& bnd, const fe* d_trace_rand,
+                 const fe* d_rcoef, size_t nrc, const sg_proof_stream* ps) {
   SG_REQUIRE(ps && ps->push && ps->fiat_shamir_prover, "proof stream callbacks required");
   const size_t m = st.m;
   const uint64_t D = st.D;
@@ -502,12 +502,11 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* trace, size_t rows, 
   SG_REQUIRE(Tp <= D, "randomized trace longer than the omicron domain");
   std::vector<DPoly> trace_polys;
   {
-    std::vector<fe> col(Tp);
+    DPoly col = dpoly_alloc(ctx, Tp);
     for (size_t s = 0; s < m; ++s) {
-      for (size_t r = 0; r < rows; ++r) col[r] = trace[r * m + s];
-      for (size_t r = 0; r < st.num_randomizers; ++r) col[rows + r] = trace_rand[r * m + s];
-      DPoly y = dpoly_upload(ctx, col.data(), Tp);
-      trace_polys.push_back(interpolate_geometric_dev(ctx, st.omicron, D, y.p(), Tp));
+      SG_HIP(launch_gather_stride(col.p(), d_trace + s, rows, m, ctx->stream));
+      SG_HIP(launch_gather_stride(col.p() + rows, d_trace_rand + s, st.num_randomizers, m, ctx->stream));
+      trace_polys.push_back(interpolate_geometric_dev(ctx, st.omicron, D, col.p(), Tp));
     }
   }
   // boundary quotients (stark.rs:326-362)
@@ -554,10 +553,9 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* trace, size_t rows, 
   const uint64_t tcd = max_degree(st, tcs);
   SG_REQUIRE(nrc == tcd + 1, "randomizer polynomial must have max_degree(transition_constraints) + 1 coefficients");
   SG_REQUIRE(nrc <= Nf, "fast_coset_evaluate: polynomial longer than root_order");
-  DPoly rpoly = dpoly_upload(ctx, rcoef, nrc);
   DPoly r_cw = dpoly_alloc(ctx, Nf);
   {
-    const fe* in = rpoly.p();
+    const fe* in = d_rcoef;
     fe* out = r_cw.p();
     coset_evaluate_batch(ctx, st.omega, Nf, g, &in, nrc, &out, 1);
   }
@@ -586,7 +584,7 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* trace, size_t rows, 
   std::vector<DPoly> wrapped;  // products that wrap the omicron domain (kept alive for the combination)
   wrapped.reserve(2 * (tqs.size() + bqs.size()));
   size_t wi = 0;
-  terms.push_back({rpoly.p(), 0, rpoly.len, weights[wi++]});
+  terms.push_back({d_rcoef, 0, nrc, weights[wi++]});
   auto add_pair = [&](const DPoly& q, uint64_t shift) {
     terms.push_back({q.p(), 0, q.len, weights[wi++]});
     const fe w = weights[wi++];
@@ -796,8 +794,30 @@ extern "C" int sg_stark_prove(sg_ctx* ctx, const sg_stark* st, const sg_fe* trac
       SG_REQUIRE(boundary[i].reg < st->m, "boundary register out of range");
       bnd.push_back({boundary[i].cycle, boundary[i].reg, to_fe(boundary[i].value)});
     }
-    stark_prove(ctx, *st, reinterpret_cast<const fe*>(trace), rows, tc_list(tcs, ntcs), bnd,
-                reinterpret_cast<const fe*>(trace_randomizers), reinterpret_cast<const fe*>(randomizer_coeffs), n_rc,
-                ps);
+    DPoly dt = dpoly_upload(ctx, reinterpret_cast<const fe*>(trace), rows * st->m);
+    DPoly dr = dpoly_upload(ctx, reinterpret_cast<const fe*>(trace_randomizers), st->num_randomizers * st->m);
+    DPoly dc = dpoly_upload(ctx, reinterpret_cast<const fe*>(randomizer_coeffs), n_rc);
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+    stark_prove(ctx, *st, dt.p(), rows, tc_list(tcs, ntcs), bnd, dr.p(), dc.p(), n_rc, ps);
+  });
+}
+
+extern "C" int sg_stark_prove_dev(sg_ctx* ctx, const sg_stark* st, const sg_fe* d_trace, size_t rows,
+                                  const sg_mpoly* const* tcs, size_t ntcs, const sg_boundary* boundary, size_t nb,
+                                  const sg_fe* d_trace_randomizers, const sg_fe* d_randomizer_coeffs, size_t n_rc,
+                                  const sg_proof_stream* ps) {
+  return guard(ctx, [&] {
+    SG_REQUIRE(st && (d_trace || !rows) && (tcs || !ntcs) && (boundary || !nb), "null argument");
+    SG_REQUIRE(d_trace_randomizers || !st->num_randomizers, "null argument");
+    SG_HIP(hipSetDevice(ctx->device));
+    std::vector<Boundary> bnd;
+    for (size_t i = 0; i < nb; ++i) {
+      check_canonical(&boundary[i].value, 1, "boundary value");
+      SG_REQUIRE(boundary[i].reg < st->m, "boundary register out of range");
+      bnd.push_back({boundary[i].cycle, boundary[i].reg, to_fe(boundary[i].value)});
+    }
+    stark_prove(ctx, *st, reinterpret_cast<const fe*>(d_trace), rows, tc_list(tcs, ntcs), bnd,
+                reinterpret_cast<const fe*>(d_trace_randomizers), reinterpret_cast<const fe*>(d_randomizer_coeffs),
+                n_rc, ps);
   });
 }

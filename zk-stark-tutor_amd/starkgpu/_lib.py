@@ -163,6 +163,8 @@ PROTOTYPES = {
     "sg_stark_degree_bounds": (ctypes.c_int, [_vp, _vp, _vp, _sz, _vp]),
     "sg_stark_prove": (ctypes.c_int, [_vp, _vp, _vp, _sz, _vp, _sz, _vp, _sz, _vp, _vp, _sz,
                                       _P(sg_proof_stream)]),
+    "sg_stark_prove_dev": (ctypes.c_int, [_vp, _vp, _vp, _sz, _vp, _sz, _vp, _sz, _vp, _vp, _sz,
+                                          _P(sg_proof_stream)]),
 }
 
 _lib = None

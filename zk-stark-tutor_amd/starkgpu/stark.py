@@ -248,6 +248,26 @@ class Stark:
         self.ctx.check(rcode)
         return proof_stream.digest()
 
+    def prove_dev(self, d_trace: int, rows: int, transition_constraints: Sequence[MPolynomial],
+                  boundary: Sequence[Tuple[int, int, int]], proof_stream, d_trace_randomizers: int,
+                  d_randomizer_coefficients: int, n_randomizer_coefficients: int) -> None:
+        """prove() with the trace (rows x registers, row-major), the trace randomizers and the
+        randomizer coefficients already in device memory (e.g. torch tensor data_ptr())."""
+        bnd = (sg_boundary * max(len(boundary), 1))(*[sg_boundary(c, r, _fe(v)) for (c, r, v) in boundary])
+        if isinstance(proof_stream, IndependentProofStream):
+            cb, adapter = proof_stream.callbacks(), None
+        else:
+            adapter = CallbackProofStream(proof_stream)
+            cb = adapter.callbacks()
+        rcode = self.ctx._lib.sg_stark_prove_dev(self.ctx.handle, self.handle, ctypes.c_void_p(d_trace), rows,
+                                                 self._tcs(transition_constraints), len(transition_constraints), bnd,
+                                                 len(boundary), ctypes.c_void_p(d_trace_randomizers),
+                                                 ctypes.c_void_p(d_randomizer_coefficients),
+                                                 n_randomizer_coefficients, ctypes.byref(cb))
+        if adapter is not None and adapter.error is not None:
+            raise adapter.error
+        self.ctx.check(rcode)
+
     def __del__(self):
         try:
             if self.handle:
