@@ -158,19 +158,52 @@ const MPolyDevice& mp_device(sg_ctx* ctx, const MPoly& a) {
   if (a.dev && a.dev->device == ctx->device) return *a.dev;
   auto d = std::make_shared<MPolyDevice>();
   d->device = ctx->device;
+  // normalize every group's x-vector (trimmed at its degree) by its first non-zero
+  // coefficient: proportional groups (e.g. the C^j (next)^e terms of a cubed AIR row) share
+  // one device copy and one coset LDE per proof
+  std::map<std::vector<uint64_t>, std::vector<int32_t>> by_hash;  // (len, a few limbs) -> candidates
+  std::vector<HPoly> normed;
   for (auto& kv : a.g) {
     const int64_t deg = hp_degree(kv.second);
-    void* p = nullptr;
-    if (deg >= 0) {
-      SG_HIP(hipMalloc(&p, (size_t)(deg + 1) * sizeof(fe)));
-      d->ptr.push_back(p);
-      SG_HIP(hipMemcpyAsync(p, kv.second.data(), (size_t)(deg + 1) * sizeof(fe), hipMemcpyHostToDevice, ctx->stream));
-    } else {
-      d->ptr.push_back(nullptr);
+    if (deg < 0) {
+      d->qidx.push_back(-1);
+      d->scale.push_back(fe_zero());
+      continue;
     }
-    d->len.push_back((uint64_t)(deg + 1));
+    size_t first = 0;
+    while (is_zero_fe(kv.second[first])) ++first;
+    const fe s = kv.second[first];
+    const fe sinv_m = to_mont(fe_inv(s));
+    HPoly v((size_t)deg + 1);
+    for (size_t i = 0; i < v.size(); ++i) v[i] = mont_mul(kv.second[i], sinv_m);
+    std::vector<uint64_t> key = {v.size(), first};
+    for (size_t i = v.size() - std::min<size_t>(v.size(), 4); i < v.size(); ++i) {
+      key.push_back(fe_lo(v[i]));
+      key.push_back(fe_hi(v[i]));
+    }
+    int32_t found = -1;
+    for (int32_t c : by_hash[key])
+      if (normed[(size_t)c].size() == v.size() &&
+          memcmp(normed[(size_t)c].data(), v.data(), v.size() * sizeof(fe)) == 0) {
+        found = c;
+        break;
+      }
+    if (found < 0) {
+      found = (int32_t)normed.size();
+      by_hash[key].push_back(found);
+      normed.push_back(std::move(v));
+    }
+    d->qidx.push_back(found);
+    d->scale.push_back(s);
   }
-  SG_HIP(hipStreamSynchronize(ctx->stream));
+  for (auto& v : normed) {
+    void* p = nullptr;
+    SG_HIP(hipMalloc(&p, v.size() * sizeof(fe)));
+    d->ptr.push_back(p);
+    d->len.push_back(v.size());
+    SG_HIP(hipMemcpyAsync(p, v.data(), v.size() * sizeof(fe), hipMemcpyHostToDevice, ctx->stream));
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+  }
   a.dev = d;
   return *a.dev;
 }

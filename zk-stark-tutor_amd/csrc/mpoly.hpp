@@ -27,8 +27,10 @@ namespace sg {
 // use by the prover: the constraints are an input of every proof, like the trace
 struct MPolyDevice {
   int device = -1;
-  std::vector<void*> ptr;      // per group (map order); nullptr for an all-zero group
-  std::vector<uint64_t> len;   // degree + 1 (0 for an all-zero group)
+  std::vector<void*> ptr;       // distinct x-polynomials up to a scalar (first non-zero coefficient 1)
+  std::vector<uint64_t> len;    // their degree + 1
+  std::vector<int32_t> qidx;    // per group (map order): index into ptr, -1 for an all-zero group
+  std::vector<fe> scale;        // per group: x-polynomial = scale * ptr[qidx]
   ~MPolyDevice();
 };
 

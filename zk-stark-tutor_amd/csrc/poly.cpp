@@ -186,15 +186,43 @@ DPoly poly_mul_exact(sg_ctx* ctx, const fe* a, uint64_t la, const fe* b, uint64_
   return out;
 }
 
-namespace {
-// the reference's inner(): pad to `order` (only when shorter), optional scale, ntt
 void ref_inner_ntt(sg_ctx* ctx, const fe& root, uint64_t order, const fe* p, uint64_t len, const fe* scale,
                    DevBuf& out, uint64_t& out_len) {
+  // the reference's inner(): pad to `order` only when shorter, optional scale, ntt
   out_len = std::max<uint64_t>(next_pow2(std::max<uint64_t>(len, 1)), order);
   out = DevBuf(ctx, out_len * sizeof(fe));
   ntt_sized(ctx, root, p, len, ilog2_exact(out_len), out.as<fe>(), scale);
 }
-}  // namespace
+
+DivPlan coset_divide_plan(fe root, uint64_t root_order, int64_t dl, int64_t dr) {
+  SG_REQUIRE(dr >= 0, "cannot divide by zero polynomial");
+  DivPlan pl;
+  pl.zero_lhs = dl < 0;
+  if (pl.zero_lhs) return pl;
+  SG_REQUIRE(dl >= dr, "cannot divide by polynomial of larger degree");
+  const uint64_t deg = (uint64_t)std::max(dl, dr);
+  pl.result_len = (uint64_t)(dl - dr + 1);
+  uint64_t order = root_order;
+  while (deg < order / 2) {
+    root = fe_mul(root, root);
+    order /= 2;
+  }
+  pl.root = root;
+  pl.order = order;
+  return pl;
+}
+
+DPoly coset_divide_finish(sg_ctx* ctx, const DivPlan& pl, const fe& offset, fe* lhs_v, const fe* rhs_v) {
+  if (pl.zero_lhs) return DPoly{};
+  dev_div(ctx, lhs_v, lhs_v, rhs_v, pl.order);
+  DevBuf c(ctx, pl.order * sizeof(fe));
+  intt_sized(ctx, pl.root, lhs_v, ilog2_exact(pl.order), c.as<fe>());
+  uint64_t keep = std::min(pl.result_len, pl.order);
+  DPoly out = dpoly_alloc(ctx, keep);
+  dev_scale_pow(ctx, out.p(), c.as<fe>(), keep, fe_inv(offset));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  return out;
+}
 
 DPoly fast_multiply_dev(sg_ctx* ctx, fe root, uint64_t root_order, const fe* a, uint64_t la, const fe* b,
                         uint64_t lb) {
@@ -225,30 +253,15 @@ DPoly fast_multiply_dev(sg_ctx* ctx, fe root, uint64_t root_order, const fe* a, 
 DPoly fast_coset_divide_dev(sg_ctx* ctx, fe root, uint64_t root_order, const fe& offset, const fe* lhs, uint64_t ll,
                             const fe* rhs, uint64_t lr) {
   check_root(root, root_order);
-  int64_t dr = dev_degree(ctx, rhs, lr);
+  const int64_t dr = dev_degree(ctx, rhs, lr);
   SG_REQUIRE(dr >= 0, "cannot divide by zero polynomial");
-  int64_t dl = dev_degree(ctx, lhs, ll);
-  if (dl < 0) return DPoly{};
-  SG_REQUIRE(dl >= dr, "cannot divide by polynomial of larger degree");
-  const uint64_t deg = (uint64_t)std::max(dl, dr);
-  const uint64_t result_len = (uint64_t)(dl - dr + 1);
-  uint64_t order = root_order;
-  while (deg < order / 2) {
-    root = fe_mul(root, root);
-    order /= 2;
-  }
+  const DivPlan pl = coset_divide_plan(root, root_order, dev_degree(ctx, lhs, ll), dr);
+  if (pl.zero_lhs) return DPoly{};
   DevBuf vl, vr;
   uint64_t nl, nr;
-  ref_inner_ntt(ctx, root, order, lhs, ll, &offset, vl, nl);
-  ref_inner_ntt(ctx, root, order, rhs, lr, &offset, vr, nr);
-  dev_div(ctx, vl.as<fe>(), vl.as<fe>(), vr.as<fe>(), order);
-  DevBuf c(ctx, order * sizeof(fe));
-  intt_sized(ctx, root, vl.as<fe>(), ilog2_exact(order), c.as<fe>());
-  uint64_t keep = std::min(result_len, order);
-  DPoly out = dpoly_alloc(ctx, keep);
-  dev_scale_pow(ctx, out.p(), c.as<fe>(), keep, fe_inv(offset));
-  SG_HIP(hipStreamSynchronize(ctx->stream));
-  return out;
+  ref_inner_ntt(ctx, pl.root, pl.order, lhs, ll, &offset, vl, nl);
+  ref_inner_ntt(ctx, pl.root, pl.order, rhs, lr, &offset, vr, nr);
+  return coset_divide_finish(ctx, pl, offset, vl.as<fe>(), vr.as<fe>());
 }
 
 // ------------------------------------------------------------------ geometric domains

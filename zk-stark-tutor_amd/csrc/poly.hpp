@@ -52,6 +52,19 @@ DPoly poly_mul_exact(sg_ctx* ctx, const fe* a, uint64_t la, const fe* b, uint64_
 // ntt_arithmetics.rs:5-64
 DPoly fast_multiply_dev(sg_ctx* ctx, fe root, uint64_t root_order, const fe* a, uint64_t la, const fe* b,
                         uint64_t lb);
+// fast_coset_divide in pieces (so a caller holding the lhs coset values can reuse them):
+// the order / root / result length the reference derives from the degrees, its padded
+// (optionally offset-scaled) NTT, and the pointwise quotient -> INTT -> truncate -> unscale
+struct DivPlan {
+  fe root;
+  uint64_t order = 0;
+  uint64_t result_len = 0;
+  bool zero_lhs = false;
+};
+DivPlan coset_divide_plan(fe root, uint64_t root_order, int64_t deg_lhs, int64_t deg_rhs);
+void ref_inner_ntt(sg_ctx* ctx, const fe& root, uint64_t order, const fe* p, uint64_t len, const fe* scale,
+                   DevBuf& out, uint64_t& out_len);
+DPoly coset_divide_finish(sg_ctx* ctx, const DivPlan& pl, const fe& offset, fe* lhs_v, const fe* rhs_v);
 // ntt_arithmetics.rs:239-310
 DPoly fast_coset_divide_dev(sg_ctx* ctx, fe root, uint64_t root_order, const fe& offset, const fe* lhs, uint64_t ll,
                             const fe* rhs, uint64_t lr);

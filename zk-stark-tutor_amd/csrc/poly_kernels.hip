@@ -217,21 +217,28 @@ __global__ __launch_bounds__(kBlock) void k_interp_assemble(fe* __restrict__ V, 
 // *last = max{i + 1 : a[i] != 0} (0 when all zero): degree() = *last - 1 (polynomial.rs:41-58)
 __global__ __launch_bounds__(kBlock) void k_last_nonzero(const fe* __restrict__ a, uint64_t n,
                                                          unsigned long long* __restrict__ last) {
+  __shared__ unsigned long long wmax[kBlock / 64];
   unsigned long long best = 0;
   for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
     if (!fe_is_zero(ld_fe(a + i))) best = i + 1;
-  // wave-level max, then one atomic per wave
+  // wave max, block max, one atomic per block (a per-wave atomic on one address serializes)
   for (int off = 32; off > 0; off >>= 1) {
     unsigned long long o = __shfl_xor(best, off);
     best = o > best ? o : best;
   }
-  if ((threadIdx.x & 63) == 0 && best) atomicMax(last, best);
+  if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = best;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (unsigned w = 1; w < kBlock / 64; ++w) best = wmax[w] > best ? wmax[w] : best;
+    if (best) atomicMax(last, best);
+  }
 }
 
 // ----------------------------------------------------------- AIR evaluation
 
-// out[y] = sum_g Q_g[y] * prod_j V_j[y]^exps[g][j]  (m_polynomial.rs:124-139 evaluated
-// pointwise on a coset: Q_g are the coset values of the x-polynomial of group g).
+// out[y] = sum_g s_g Q_q(g)[y] * prod_j V_j[y]^exps[g][j]  (m_polynomial.rs:124-139 evaluated
+// pointwise on a coset: s_g Q_q(g) are the coset values of the x-polynomial of group g; groups
+// whose x-polynomials are proportional share one LDE).
 __global__ __launch_bounds__(kBlock) void k_air_eval(AirEvalArgs a) {
   for (uint64_t y = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; y < a.n; y += (uint64_t)gridDim.x * blockDim.x) {
     fe vm[kAirMaxVars];
@@ -240,7 +247,7 @@ __global__ __launch_bounds__(kBlock) void k_air_eval(AirEvalArgs a) {
       vm[j] = j < a.nvars ? mont_mul(ld_fe(a.V[j] + y), a.r2) : a.one_m;
     fe acc = fe_zero();
     for (int g = 0; g < a.ngroups; ++g) {
-      fe prod = mont_mul(ld_fe(a.Q[g] + y), a.r2);
+      fe prod = mont_mul(ld_fe(a.Q[a.qidx[g]] + y), ld_fe(a.qscale + g));  // Montgomery(scale * Q)
       const uint32_t* e = a.exps + g * a.nvars;
       for (int j = 0; j < a.nvars; ++j) {
         uint32_t ej = e[j];
@@ -368,7 +375,9 @@ hipError_t launch_interp_assemble(fe* V, const fe* y, const fe* Zv, const fe* S,
 hipError_t launch_last_nonzero(const fe* a, uint64_t n, unsigned long long* last, hipStream_t s) {
   if (!n) return hipSuccess;
   ProfScope ps("last_nonzero", 16 * n, s);
-  hipLaunchKernelGGL(k_last_nonzero, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, s, a, n, last);
+  uint64_t blocks = (n + kBlock * 8 - 1) / (kBlock * 8);  // >= 8 elements per lane, <= 1024 atomics
+  if (blocks > 1024) blocks = 1024;
+  hipLaunchKernelGGL(k_last_nonzero, dim3((unsigned)blocks), dim3(kBlock), 0, s, a, n, last);
   return hipGetLastError();
 }
 

@@ -11,9 +11,11 @@ constexpr int kLinCombMaxTerms = 48;  // terms of one weighted combination
 
 struct AirEvalArgs {
   fe* out;
-  const fe* const* Q;    // device array [ngroups] of coset-value arrays (x-polynomial of each group)
-  const fe* const* V;    // device array [nvars] of coset-value arrays (point variables 1..)
-  const uint32_t* exps;  // device [ngroups][nvars]
+  const fe* const* Q;     // device array of coset-value arrays (the distinct x-polynomials)
+  const uint32_t* qidx;   // device [ngroups]: group g's x-polynomial = qscale[g] * Q[qidx[g]]
+  const fe* qscale;       // device [ngroups]: Montgomery(Montgomery(scale)) = scale * R^2
+  const fe* const* V;     // device array [nvars] of coset-value arrays (point variables 1..)
+  const uint32_t* exps;   // device [ngroups][nvars]
   int ngroups, nvars;
   uint64_t n;
   fe r2, one_m;

@@ -15,6 +15,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <map>
 #include <cstring>
 #include <memory>
 #include <numeric>
@@ -366,66 +367,82 @@ DPoly lincomb(sg_ctx* ctx, const std::vector<DevTerm>& terms) {
   return out;
 }
 
-// the polynomial evaluate_symbolic returns, coefficient vector of length `len`
-DPoly transition_polynomial(sg_ctx* ctx, const MPoly& tc, const std::vector<DPoly>& trace_polys, uint64_t Tp,
-                            const fe& omicron, const fe& offset, uint64_t& len) {
-  const size_t m = trace_polys.size();
-  SG_REQUIRE(tc.nvars <= 1 + 2 * m, "transition constraint has more variables than the point");
-  SG_REQUIRE(2 * m <= (size_t)kAirMaxVars, "at most 4 registers are supported by the AIR kernel");
-  const uint64_t bound = symbolic_degree_bound(tc, Tp - 1);
-  len = bound + 1;
-  const uint64_t L = next_pow2(len);
-  // point values on the coset offset * <w_L>: P_s(y) and P_s(omicron y)
+// point values on the coset offset * <w_L>: P_s(y) and P_s(omicron y) (the point
+// [x, P_s(x), P_s(omicron x)] of stark.rs:388-400), shared by every constraint
+struct AirCoset {
+  uint64_t L = 0;
   std::vector<DPoly> V;
+};
+
+AirCoset air_coset(sg_ctx* ctx, const std::vector<DPoly>& trace_polys, uint64_t L, const fe& omicron,
+                   const fe& offset) {
+  AirCoset c;
+  c.L = L;
   const fe off_omicron = fe_mul(offset, omicron);
-  for (size_t s = 0; s < m; ++s) {
-    V.push_back(dpoly_alloc(ctx, L));
-    coset_values_dev(ctx, trace_polys[s].p(), trace_polys[s].len, L, offset, V.back().p());
-  }
-  for (size_t s = 0; s < m; ++s) {
-    V.push_back(dpoly_alloc(ctx, L));
-    coset_values_dev(ctx, trace_polys[s].p(), trace_polys[s].len, L, off_omicron, V.back().p());
-  }
-  // group x-polynomials (device-resident, uploaded once per constraint) on the same coset
+  for (int pass = 0; pass < 2; ++pass)
+    for (auto& tp : trace_polys) {
+      c.V.push_back(dpoly_alloc(ctx, L));
+      const fe* in = tp.p();
+      fe* out = c.V.back().p();
+      coset_evaluate_batch(ctx, root_of_order(L), L, pass ? off_omicron : offset, &in, tp.len, &out, 1);
+    }
+  return c;
+}
+
+// values on the coset of the polynomial evaluate_symbolic returns (m_polynomial.rs:124-139)
+DPoly transition_values(sg_ctx* ctx, const MPoly& tc, const AirCoset& co, const fe& offset) {
+  const uint64_t L = co.L;
+  const int nv = (int)co.V.size();
+  SG_REQUIRE(tc.nvars <= 1 + (uint32_t)nv, "transition constraint has more variables than the point");
+  SG_REQUIRE(nv <= kAirMaxVars, "at most 4 registers are supported by the AIR kernel");
+  // distinct group x-polynomials (device-resident, uploaded once per constraint) on the coset
   const MPolyDevice& xd = mp_device(ctx, tc);
   std::vector<DPoly> Q;
-  std::vector<uint32_t> exps;
-  const int nv = 2 * (int)m;
+  for (size_t q = 0; q < xd.ptr.size(); ++q) {
+    Q.push_back(dpoly_alloc(ctx, L));
+    const fe* in = reinterpret_cast<const fe*>(xd.ptr[q]);
+    fe* out = Q.back().p();
+    coset_evaluate_batch(ctx, root_of_order(L), L, offset, &in, xd.len[q], &out, 1);
+  }
+  std::vector<uint32_t> exps, qidx;
+  std::vector<fe> qscale;
   size_t gi = 0;
   for (auto it = tc.g.begin(); it != tc.g.end(); ++it, ++gi) {
-    if (!xd.len[gi]) continue;  // an all-zero group adds nothing (its products are zero polynomials)
-    Q.push_back(dpoly_alloc(ctx, L));
-    coset_values_dev(ctx, reinterpret_cast<const fe*>(xd.ptr[gi]), xd.len[gi], L, offset, Q.back().p());
+    if (xd.qidx[gi] < 0) continue;  // an all-zero group adds nothing (its products are zero polynomials)
+    qidx.push_back((uint32_t)xd.qidx[gi]);
+    qscale.push_back(to_mont(to_mont(xd.scale[gi])));
     for (int j = 0; j < nv; ++j) exps.push_back(j < (int)it->first.size() ? it->first[j] : 0u);
   }
   DPoly vals = dpoly_alloc(ctx, L);
-  if (Q.empty()) {
+  if (qidx.empty()) {
     SG_HIP(hipMemsetAsync(vals.p(), 0, L * sizeof(fe), ctx->stream));
-  } else {
-    std::vector<const fe*> qp, vp;
-    for (auto& q : Q) qp.push_back(q.p());
-    for (auto& v : V) vp.push_back(v.p());
-    DevBuf dq(ctx, qp.size() * sizeof(void*)), dv(ctx, vp.size() * sizeof(void*)), de(ctx, exps.size() * 4);
-    SG_HIP(hipMemcpyAsync(dq.get(), qp.data(), qp.size() * sizeof(void*), hipMemcpyHostToDevice, ctx->stream));
-    SG_HIP(hipMemcpyAsync(dv.get(), vp.data(), vp.size() * sizeof(void*), hipMemcpyHostToDevice, ctx->stream));
-    SG_HIP(hipMemcpyAsync(de.get(), exps.data(), exps.size() * 4, hipMemcpyHostToDevice, ctx->stream));
-    AirEvalArgs a{};
-    a.out = vals.p();
-    a.Q = dq.as<const fe*>();
-    a.V = dv.as<const fe*>();
-    a.exps = de.as<uint32_t>();
-    a.ngroups = (int)Q.size();
-    a.nvars = nv;
-    a.n = L;
-    a.r2 = fe_r2();
-    a.one_m = to_mont(fe_one());
-    SG_HIP(launch_air_eval(a, ctx->stream));
-    SG_HIP(hipStreamSynchronize(ctx->stream));  // pointer tables return to the pool
+    return vals;
   }
-  DPoly coeffs = dpoly_alloc(ctx, L);
-  coset_interpolate_dev(ctx, vals.p(), L, offset, coeffs.p());
-  coeffs.len = len;  // coefficients len..L-1 are zero
-  return coeffs;
+  std::vector<const fe*> qp, vp;
+  for (auto& q : Q) qp.push_back(q.p());
+  for (auto& v : co.V) vp.push_back(v.p());
+  DevBuf dq(ctx, qp.size() * sizeof(void*)), dv(ctx, vp.size() * sizeof(void*)), de(ctx, exps.size() * 4);
+  DevBuf di(ctx, qidx.size() * 4), ds(ctx, qscale.size() * sizeof(fe));
+  SG_HIP(hipMemcpyAsync(dq.get(), qp.data(), qp.size() * sizeof(void*), hipMemcpyHostToDevice, ctx->stream));
+  SG_HIP(hipMemcpyAsync(dv.get(), vp.data(), vp.size() * sizeof(void*), hipMemcpyHostToDevice, ctx->stream));
+  SG_HIP(hipMemcpyAsync(de.get(), exps.data(), exps.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+  SG_HIP(hipMemcpyAsync(di.get(), qidx.data(), qidx.size() * 4, hipMemcpyHostToDevice, ctx->stream));
+  SG_HIP(hipMemcpyAsync(ds.get(), qscale.data(), qscale.size() * sizeof(fe), hipMemcpyHostToDevice, ctx->stream));
+  AirEvalArgs a{};
+  a.out = vals.p();
+  a.Q = dq.as<const fe*>();
+  a.qidx = di.as<uint32_t>();
+  a.qscale = ds.as<fe>();
+  a.V = dv.as<const fe*>();
+  a.exps = de.as<uint32_t>();
+  a.ngroups = (int)qidx.size();
+  a.nvars = nv;
+  a.n = L;
+  a.r2 = fe_r2();
+  a.one_m = to_mont(fe_one());
+  SG_HIP(launch_air_eval(a, ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));  // pointer tables return to the pool
+  return vals;
 }
 
 // proof_stream pushes of (Value, Path) for `idx` in a retained codeword/tree (stark.rs:545-560)
@@ -539,15 +556,44 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
     build_trees(ctx, leaves, b, Nf, &bq_trees[s]);
   }
   for (size_t s = 0; s < m; ++s) push_obj(ps, SG_OBJ_ROOT, bq_trees[s]->root, 64);
-  // transition quotients (stark.rs:388-422)
+  // transition quotients (stark.rs:388-422): evaluate_symbolic's polynomial from its values on a
+  // coset of size L > its length, then fast_coset_divide by the transition zerofier.  When the
+  // division's order equals L its lhs NTT IS those coset values (same offset, same root), so
+  // they are reused; the zerofier's NTT is shared by all constraints.
   const uint64_t T = st.original_trace_length;
   SG_REQUIRE(T >= 2, "transition zerofier needs a trace of at least two rows");
   DPoly tz = zerofier_geometric_dev(ctx, st.omicron, D, T - 1);
+  const int64_t dtz = dev_degree(ctx, tz.p(), tz.len);
+  std::map<uint64_t, AirCoset> cosets;
+  std::map<uint64_t, std::pair<DevBuf, uint64_t>> tz_ntt;  // order -> NTT of scale(tz, g)
   std::vector<DPoly> tqs;
   for (const MPoly* tc : tcs) {
-    uint64_t len = 0;
-    DPoly tp = transition_polynomial(ctx, *tc, trace_polys, Tp, st.omicron, g, len);
-    tqs.push_back(fast_coset_divide_dev(ctx, st.omicron, D, g, tp.p(), len, tz.p(), tz.len));
+    const uint64_t len = symbolic_degree_bound(*tc, Tp - 1) + 1;
+    const uint64_t L = next_pow2(len);
+    auto cit = cosets.find(L);
+    if (cit == cosets.end()) cit = cosets.emplace(L, air_coset(ctx, trace_polys, L, st.omicron, g)).first;
+    DPoly vals = transition_values(ctx, *tc, cit->second, g);
+    DPoly coeffs = dpoly_alloc(ctx, L);
+    coset_interpolate_dev(ctx, vals.p(), L, g, coeffs.p());  // coefficients len..L-1 are zero
+    const DivPlan pl = coset_divide_plan(st.omicron, D, dev_degree(ctx, coeffs.p(), len), dtz);
+    if (pl.zero_lhs) {
+      tqs.push_back(DPoly{});
+      continue;
+    }
+    DevBuf lhs_own;
+    fe* lhs_v = vals.p();
+    if (!(pl.order == L && len <= pl.order)) {
+      uint64_t nl;
+      ref_inner_ntt(ctx, pl.root, pl.order, coeffs.p(), len, &g, lhs_own, nl);
+      lhs_v = lhs_own.as<fe>();
+    }
+    auto zit = tz_ntt.find(pl.order);
+    if (zit == tz_ntt.end()) {
+      std::pair<DevBuf, uint64_t> z;
+      ref_inner_ntt(ctx, pl.root, pl.order, tz.p(), tz.len, &g, z.first, z.second);
+      zit = tz_ntt.emplace(pl.order, std::move(z)).first;
+    }
+    tqs.push_back(coset_divide_finish(ctx, pl, g, lhs_v, zit->second.first.as<fe>()));
   }
   // randomizer polynomial + codeword (stark.rs:424-445)
   const uint64_t tcd = max_degree(st, tcs);
