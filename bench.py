@@ -45,6 +45,9 @@ EXPANSION = 8       # N = 2^23
 COLINEARITY = 64
 REGISTERS = 2       # Rescue-Prime m = 2
 HBM_PEAK_GBS = 8000.0
+# PMC HBM bytes of this workload's kernels (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes on
+# `bench.py --steps 3 --warmup 1 --no-side`, tools/_gpu_full_e2e.sh + tools/pmc_traffic.py)
+PMC_TRAFFIC_FILE = "r01_pmc_traffic_e2e.json"
 
 
 def synthetic_fe(seed: int, tag: bytes, n: int) -> np.ndarray:
@@ -480,12 +483,12 @@ def main():
     # measured HBM bytes per launch of that kernel (rocprofv3 PMC passes on this code, committed under
     # profiles/; the live bench cannot collect PMC counters itself)
     traffic, traffic_src = None, None
-    pmc_file = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
-    if os.path.exists(pmc_file):
+    pmc_file = os.path.join(ROOT, "profiles", PMC_TRAFFIC_FILE)
+    if os.path.exists(pmc_file) and args.log_trace == LOG_TRACE:
         pmc = json.load(open(pmc_file))["kernels"].get(name)
         if pmc:
             traffic = int(pmc["hbm_bytes_per_launch"])
-            traffic_src = "profiles/r01_pmc_traffic.json (FETCH_SIZE x2 + WRITE_SIZE per launch)"
+            traffic_src = f"profiles/{PMC_TRAFFIC_FILE} (FETCH_SIZE x2 + WRITE_SIZE per launch, same workload)"
     phases = {k: {"launches": v["launches"], "ms_per_step": round(v["ms"], 4),
                   "GBps": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["ms"] > 0 else None}
               for k, v in sorted(breakdown.items(), key=lambda kv: -kv[1]["ms"])}
