@@ -111,6 +111,19 @@ const fe* sg_ctx::pow_table(const fe& root, uint64_t count) {
   return reinterpret_cast<const fe*>(table);
 }
 
+void* sg_ctx::staging(int slot, size_t bytes) {
+  if (staging_bytes[slot] < bytes) {
+    SG_HIP(hipStreamSynchronize(stream));  // the old buffer may still be in flight
+    if (staging_ptr[slot]) (void)hipHostFree(staging_ptr[slot]);
+    staging_ptr[slot] = nullptr;
+    staging_bytes[slot] = 0;
+    size_t r = pool_round(bytes);
+    SG_HIP(hipHostMalloc(&staging_ptr[slot], r, hipHostMallocDefault));
+    staging_bytes[slot] = r;
+  }
+  return staging_ptr[slot];
+}
+
 const fe* sg_ctx::stage_twiddles(const fe& root, int logn) {
   auto key = std::make_pair(std::make_pair(fe_lo(root), fe_hi(root)), logn);
   auto it = stage_tables.find(key);
@@ -208,6 +221,8 @@ extern "C" void sg_ctx_destroy(sg_ctx* ctx) {
   for (auto& kv : ctx->pow_tables) (void)hipFree(kv.second.ptr);
   for (auto& kv : ctx->stage_tables) (void)hipFree(kv.second);
   for (auto& kv : ctx->interp_tables) (void)hipFree(kv.second);
+  for (void* p : ctx->staging_ptr)
+    if (p) (void)hipHostFree(p);
   if (ctx->pinned_roots) (void)hipHostFree(ctx->pinned_roots);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
@@ -847,6 +862,25 @@ void sample_indices(const uint8_t* seed, size_t seed_len, size_t size, size_t re
 }
 
 // fri.rs:174-208 for every round, then returns top-level indices (fri.rs:210-248)
+void gather_openings(sg_ctx* ctx, const std::vector<uint64_t>& fe_addr, const std::vector<uint64_t>& dg_addr,
+                     const fe** vals, const uint8_t** digs) {
+  const size_t nf = fe_addr.size(), nd = dg_addr.size();
+  uint8_t* up = static_cast<uint8_t*>(ctx->staging(0, (nf + nd) * 8 + 8));
+  uint8_t* down = static_cast<uint8_t*>(ctx->staging(1, nf * 16 + nd * 64 + 16));
+  memcpy(up, fe_addr.data(), nf * 8);
+  memcpy(up + nf * 8, dg_addr.data(), nd * 8);
+  DevBuf da(ctx, (nf + nd) * 8 + 8), dv(ctx, nf * 16 + nd * 64 + 16);
+  SG_HIP(hipMemcpyAsync(da.get(), up, (nf + nd) * 8, hipMemcpyHostToDevice, ctx->stream));
+  if (nf) SG_HIP(launch_gather_fe_ptrs(da.as<uint64_t>(), dv.as<fe>(), (uint32_t)nf, ctx->stream));
+  if (nd)
+    SG_HIP(launch_gather_digest_ptrs(da.as<uint64_t>() + nf, reinterpret_cast<uint64_t*>(dv.as<uint8_t>() + nf * 16),
+                                     (uint32_t)nd, ctx->stream));
+  SG_HIP(hipMemcpyAsync(down, dv.get(), nf * 16 + nd * 64, hipMemcpyDeviceToHost, ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  *vals = reinterpret_cast<const fe*>(down);
+  *digs = down + nf * 16;
+}
+
 void fri_prove_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, const sg_proof_stream* ps,
                    size_t* top) {
   sg_fri_state st;
@@ -897,19 +931,9 @@ void fri_prove_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, con
       for (uint64_t d : p) dg_addr.push_back(bn + 64 * d);
     }
   }
-  std::vector<fe> vals(fe_addr.size());
-  std::vector<uint8_t> digs(dg_addr.size() * 64);
-  {
-    DevBuf da(ctx, std::max<size_t>(fe_addr.size(), 1) * 8), dv(ctx, std::max<size_t>(fe_addr.size(), 1) * 16);
-    DevBuf db(ctx, std::max<size_t>(dg_addr.size(), 1) * 8), dd(ctx, std::max<size_t>(dg_addr.size(), 1) * 64);
-    SG_HIP(hipMemcpyAsync(da.get(), fe_addr.data(), fe_addr.size() * 8, hipMemcpyHostToDevice, ctx->stream));
-    SG_HIP(hipMemcpyAsync(db.get(), dg_addr.data(), dg_addr.size() * 8, hipMemcpyHostToDevice, ctx->stream));
-    SG_HIP(launch_gather_fe_ptrs(da.as<uint64_t>(), dv.as<fe>(), (uint32_t)fe_addr.size(), ctx->stream));
-    SG_HIP(launch_gather_digest_ptrs(db.as<uint64_t>(), dd.as<uint64_t>(), (uint32_t)dg_addr.size(), ctx->stream));
-    SG_HIP(hipMemcpyAsync(vals.data(), dv.get(), vals.size() * 16, hipMemcpyDeviceToHost, ctx->stream));
-    SG_HIP(hipMemcpyAsync(digs.data(), dd.get(), digs.size(), hipMemcpyDeviceToHost, ctx->stream));
-    SG_HIP(hipStreamSynchronize(ctx->stream));
-  }
+  const fe* vals = nullptr;
+  const uint8_t* digs = nullptr;
+  gather_openings(ctx, fe_addr, dg_addr, &vals, &digs);
   // payloads are written in place (memcpy) into one reused buffer per object kind
   size_t fpos = 0, dpos = 0;
   uint8_t leafs[48];
@@ -930,7 +954,7 @@ void fri_prove_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, con
         for (size_t k = 0; k < lens[which]; ++k, p += 72) {
           static const uint8_t len64[8] = {0, 0, 0, 0, 0, 0, 0, 64};
           memcpy(p, len64, 8);
-          memcpy(p + 8, digs.data() + (dpos + k) * 64, 64);
+          memcpy(p + 8, digs + (dpos + k) * 64, 64);
         }
         dpos += lens[which];
         push_obj(ps, SG_OBJ_PATH, obj.data(), obj.size());

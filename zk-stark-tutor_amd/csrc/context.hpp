@@ -87,6 +87,11 @@ struct sg_ctx {
   std::map<std::pair<std::pair<uint64_t, uint64_t>, int>, void*> stage_tables;
   // geometric interpolation kernels NTT_D(1 / (1 - q^-j)) keyed by (q limbs, D) (poly.cpp)
   std::map<std::pair<std::pair<uint64_t, uint64_t>, uint64_t>, void*> interp_tables;
+  // pinned host staging buffers (grown on demand): slot 0 uploads gather addresses,
+  // slot 1 receives gathered openings -- pageable copies of MBs cost ~10x more
+  void* staging_ptr[2] = {nullptr, nullptr};
+  size_t staging_bytes[2] = {0, 0};
+  void* staging(int slot, size_t bytes);
 };
 
 namespace sg {

@@ -90,5 +90,9 @@ void fri_commit_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, co
                     sg_fri_state& st, bool borrow_input = false);
 void fri_prove_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, const sg_proof_stream* ps,
                    size_t* top);
+// one launch each: field elements and digests at the given device addresses, into pinned
+// staging memory (valid until the next call on this context)
+void gather_openings(sg_ctx* ctx, const std::vector<uint64_t>& fe_addr, const std::vector<uint64_t>& dg_addr,
+                     const fe** vals, const uint8_t** digs);
 
 }  // namespace sg

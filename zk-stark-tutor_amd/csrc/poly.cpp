@@ -191,6 +191,17 @@ void ref_inner_ntt(sg_ctx* ctx, const fe& root, uint64_t order, const fe* p, uin
   // the reference's inner(): pad to `order` only when shorter, optional scale, ntt
   out_len = std::max<uint64_t>(next_pow2(std::max<uint64_t>(len, 1)), order);
   out = DevBuf(ctx, out_len * sizeof(fe));
+  if (len >= 1 && len <= (uint64_t)kSmallPolyMax && out_len == order && order >= 2) {
+    // a tiny polynomial (a boundary zerofier): its NTT is its values at offset root^k -- Horner
+    SmallPoly sp{};
+    sp.len = (int)len;
+    SG_HIP(hipMemcpyAsync(sp.c, p, len * sizeof(fe), hipMemcpyDeviceToHost, ctx->stream));
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+    const fe *A, *B;
+    pow_tables2(ctx, root, order, &A, &B);
+    SG_HIP(launch_eval_small(out.as<fe>(), sp, order, A, B, to_mont(scale ? *scale : fe_one()), ctx->stream));
+    return;
+  }
   ntt_sized(ctx, root, p, len, ilog2_exact(out_len), out.as<fe>(), scale);
 }
 
@@ -313,7 +324,7 @@ const fe* interp_kernel(sg_ctx* ctx, const fe& q, uint64_t D) {
 }
 }  // namespace
 
-DPoly interpolate_geometric_dev(sg_ctx* ctx, const fe& q, uint64_t D, const fe* y, uint64_t n) {
+DPoly interpolate_geometric_dev(sg_ctx* ctx, const fe& q, uint64_t D, const fe* y, uint64_t n, GeoInterpCache* cache) {
   SG_REQUIRE(n <= D, "interpolate: more points than the order of the root");
   SG_REQUIRE(D && (D & (D - 1)) == 0, "interpolate: root order must be a power of two");
   if (n == 0) return DPoly{};
@@ -325,12 +336,24 @@ DPoly interpolate_geometric_dev(sg_ctx* ctx, const fe& q, uint64_t D, const fe* 
     SG_HIP(hipStreamSynchronize(ctx->stream));
     return out;
   }
-  // Z, Z(q^m) and Z'(q^i)
-  DPoly Z = zerofier_geometric_dev(ctx, q, D, n);
-  DevBuf Zv(ctx, D * sizeof(fe)), Zd(ctx, n * sizeof(fe)), Zdv(ctx, D * sizeof(fe));
-  ntt_sized(ctx, q, Z.p(), n + 1, logD, Zv.as<fe>());
-  SG_HIP(launch_deriv(Zd.as<fe>(), Z.p(), n, fe_r2(), ctx->stream));
-  ntt_sized(ctx, q, Zd.as<fe>(), n, logD, Zdv.as<fe>());
+  // Z, Z(q^m) and Z'(q^i) (cached per domain)
+  GeoInterpCache local;
+  GeoInterpCache& zc = cache ? *cache : local;
+  if (!(zc.n == n && zc.D == D && fe_eq(zc.q, q))) {
+    DPoly Z = zerofier_geometric_dev(ctx, q, D, n);
+    DevBuf Zd(ctx, n * sizeof(fe));
+    zc.Zv = DevBuf(ctx, D * sizeof(fe));
+    zc.Zdv = DevBuf(ctx, D * sizeof(fe));
+    ntt_sized(ctx, q, Z.p(), n + 1, logD, zc.Zv.as<fe>());
+    SG_HIP(launch_deriv(Zd.as<fe>(), Z.p(), n, fe_r2(), ctx->stream));
+    ntt_sized(ctx, q, Zd.as<fe>(), n, logD, zc.Zdv.as<fe>());
+    SG_HIP(hipStreamSynchronize(ctx->stream));  // Z and Zd return to the pool
+    zc.q = q;
+    zc.D = D;
+    zc.n = n;
+  }
+  const DevBuf& Zv = zc.Zv;
+  const DevBuf& Zdv = zc.Zdv;
   // a_i = y_i / Z'(q^i); S = a (*) b cyclically, b[j] = 1 / (1 - q^-j)
   DevBuf a(ctx, n * sizeof(fe)), va(ctx, D * sizeof(fe)), S(ctx, D * sizeof(fe));
   dev_div(ctx, a.as<fe>(), y, Zdv.as<fe>(), n);

@@ -71,8 +71,15 @@ DPoly fast_coset_divide_dev(sg_ctx* ctx, fe root, uint64_t root_order, const fe&
 // prod_{i<n} (x - q^i) for q of order D (ntt_arithmetics.rs:66-113 on the domain q^0..q^(n-1)), length n + 1;
 // n == D reproduces the reference's wrapped result (D zeros)
 DPoly zerofier_geometric_dev(sg_ctx* ctx, const fe& q, uint64_t D, uint64_t n);
+// Z(q^m) and Z'(q^i) of the domain q^0..q^(n-1), reusable across interpolations on one domain
+struct GeoInterpCache {
+  fe q;
+  uint64_t D = 0, n = 0;
+  DevBuf Zv, Zdv;
+};
 // the interpolant of degree < n through (q^i, y_i), i < n <= D (ntt_arithmetics.rs:172-237), length n
-DPoly interpolate_geometric_dev(sg_ctx* ctx, const fe& q, uint64_t D, const fe* y, uint64_t n);
+DPoly interpolate_geometric_dev(sg_ctx* ctx, const fe& q, uint64_t D, const fe* y, uint64_t n,
+                                GeoInterpCache* cache = nullptr);
 // coefficients (length L) of the polynomial of degree < L with P(offset w^k) = values[k], w of order L
 void coset_interpolate_dev(sg_ctx* ctx, const fe* values, uint64_t L, const fe& offset, fe* out);
 // out (length L, a power of two >= len) = [P(offset w^k)], w of order L

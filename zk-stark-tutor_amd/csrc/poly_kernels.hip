@@ -291,7 +291,29 @@ __global__ __launch_bounds__(kBlock) void k_gather_stride(fe* __restrict__ out, 
     st_fe(out + i, ld_fe(in + i * stride));
 }
 
+// out[k] = P(offset w^k), k < n, for a polynomial of at most kSmallPolyMax coefficients (Horner):
+// the NTT of the zero-padded, offset-scaled coefficient vector, without the transform
+__global__ __launch_bounds__(kBlock) void k_eval_small(fe* __restrict__ out, SmallPoly p, uint64_t n,
+                                                       const fe* __restrict__ wA, const fe* __restrict__ wB,
+                                                       fe off_m) {
+  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < n; k += (uint64_t)gridDim.x * blockDim.x) {
+    fe xm = mont_mul(mont_mul(ld_fe(wA + (k & 4095)), ld_fe(wB + (k >> 12))), off_m);  // Montgomery(offset w^k)
+    fe acc = p.c[p.len - 1];
+    for (int j = (int)p.len - 2; j >= 0; --j) acc = fe_add(mont_mul(acc, xm), p.c[j]);
+    st_fe(out + k, acc);
+  }
+}
+
 // ================================================================ launchers
+
+hipError_t launch_eval_small(fe* out, const SmallPoly& p, uint64_t n, const fe* wA, const fe* wB, const fe& off_m,
+                             hipStream_t s) {
+  if (!n) return hipSuccess;
+  if (p.len < 1 || p.len > kSmallPolyMax) return hipErrorInvalidValue;
+  ProfScope ps("eval_small", 16 * n, s);
+  hipLaunchKernelGGL(k_eval_small, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, s, out, p, n, wA, wB, off_m);
+  return hipGetLastError();
+}
 
 hipError_t launch_gather_stride(fe* out, const fe* in, uint64_t n, uint64_t stride, hipStream_t s) {
   if (!n) return hipSuccess;

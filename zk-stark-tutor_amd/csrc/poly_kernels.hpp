@@ -21,6 +21,12 @@ struct AirEvalArgs {
   fe r2, one_m;
 };
 
+constexpr int kSmallPolyMax = 16;
+struct SmallPoly {
+  fe c[kSmallPolyMax];  // canonical coefficients
+  int len;
+};
+
 struct LinCombArgs {
   fe* out;
   uint64_t n;
@@ -47,6 +53,8 @@ hipError_t launch_interp_assemble(fe* V, const fe* y, const fe* Zv, const fe* S,
 hipError_t launch_last_nonzero(const fe* a, uint64_t n, unsigned long long* last, hipStream_t s);
 hipError_t launch_air_eval(const AirEvalArgs& a, hipStream_t s);
 hipError_t launch_lincomb(const LinCombArgs& a, hipStream_t s);
+hipError_t launch_eval_small(fe* out, const SmallPoly& p, uint64_t n, const fe* wA, const fe* wB, const fe& off_m,
+                             hipStream_t s);
 hipError_t launch_gather_stride(fe* out, const fe* in, uint64_t n, uint64_t stride, hipStream_t s);
 
 }  // namespace sg

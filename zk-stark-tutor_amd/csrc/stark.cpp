@@ -445,42 +445,37 @@ DPoly transition_values(sg_ctx* ctx, const MPoly& tc, const AirCoset& co, const 
   return vals;
 }
 
-// proof_stream pushes of (Value, Path) for `idx` in a retained codeword/tree (stark.rs:545-560)
-void push_openings(sg_ctx* ctx, const sg_proof_stream* ps, const fe* cw, const sg_tree* t,
+// proof_stream pushes of (Value, Path) for `idx` in each retained codeword/tree, in order
+// (stark.rs:545-560); every opening of every tree is gathered with one launch each
+void push_openings(sg_ctx* ctx, const sg_proof_stream* ps, const std::vector<std::pair<const fe*, const sg_tree*>>& cts,
                    const std::vector<uint64_t>& idx) {
-  std::vector<uint64_t> fe_addr, dg_addr;
-  for (uint64_t i : idx) {
-    fe_addr.push_back((uint64_t)(uintptr_t)cw + 16 * i);
-    std::vector<uint64_t> p;
-    path_indices(t, i, p);
-    for (uint64_t d : p) dg_addr.push_back((uint64_t)(uintptr_t)t->buf.get() + 64 * d);
-  }
-  std::vector<fe> vals(fe_addr.size());
-  std::vector<uint8_t> digs(dg_addr.size() * 64);
-  DevBuf da(ctx, std::max<size_t>(fe_addr.size(), 1) * 8), dv(ctx, std::max<size_t>(fe_addr.size(), 1) * 16);
-  DevBuf db(ctx, std::max<size_t>(dg_addr.size(), 1) * 8), dd(ctx, std::max<size_t>(dg_addr.size(), 1) * 64);
-  SG_HIP(hipMemcpyAsync(da.get(), fe_addr.data(), fe_addr.size() * 8, hipMemcpyHostToDevice, ctx->stream));
-  SG_HIP(launch_gather_fe_ptrs(da.as<uint64_t>(), dv.as<fe>(), (uint32_t)fe_addr.size(), ctx->stream));
-  if (!dg_addr.empty()) {
-    SG_HIP(hipMemcpyAsync(db.get(), dg_addr.data(), dg_addr.size() * 8, hipMemcpyHostToDevice, ctx->stream));
-    SG_HIP(launch_gather_digest_ptrs(db.as<uint64_t>(), dd.as<uint64_t>(), (uint32_t)dg_addr.size(), ctx->stream));
-    SG_HIP(hipMemcpyAsync(digs.data(), dd.get(), digs.size(), hipMemcpyDeviceToHost, ctx->stream));
-  }
-  SG_HIP(hipMemcpyAsync(vals.data(), dv.get(), vals.size() * 16, hipMemcpyDeviceToHost, ctx->stream));
-  SG_HIP(hipStreamSynchronize(ctx->stream));
-  const size_t depth = (size_t)t->logn;
-  std::vector<uint8_t> obj(depth * 72);
-  static const uint8_t len64[8] = {0, 0, 0, 0, 0, 0, 0, 64};
-  for (size_t k = 0; k < idx.size(); ++k) {
-    uint8_t v[16];
-    put_u128_be_at(v, vals[k]);
-    push_obj(ps, SG_OBJ_VALUE, v, 16);
-    uint8_t* p = obj.data();
-    for (size_t d = 0; d < depth; ++d, p += 72) {
-      memcpy(p, len64, 8);
-      memcpy(p + 8, digs.data() + (k * depth + d) * 64, 64);
+  std::vector<uint64_t> fe_addr, dg_addr, p;
+  for (auto& ct : cts)
+    for (uint64_t i : idx) {
+      fe_addr.push_back((uint64_t)(uintptr_t)ct.first + 16 * i);
+      p.clear();
+      path_indices(ct.second, i, p);
+      for (uint64_t d : p) dg_addr.push_back((uint64_t)(uintptr_t)ct.second->buf.get() + 64 * d);
     }
-    push_obj(ps, SG_OBJ_PATH, obj.data(), obj.size());
+  const fe* vals = nullptr;
+  const uint8_t* digs = nullptr;
+  gather_openings(ctx, fe_addr, dg_addr, &vals, &digs);
+  static const uint8_t len64[8] = {0, 0, 0, 0, 0, 0, 0, 64};
+  size_t vk = 0, dk = 0;
+  for (auto& ct : cts) {
+    const size_t depth = (size_t)ct.second->logn;
+    std::vector<uint8_t> obj(depth * 72);
+    for (size_t k = 0; k < idx.size(); ++k, ++vk) {
+      uint8_t v[16];
+      put_u128_be_at(v, vals[vk]);
+      push_obj(ps, SG_OBJ_VALUE, v, 16);
+      uint8_t* q = obj.data();
+      for (size_t d = 0; d < depth; ++d, q += 72, ++dk) {
+        memcpy(q, len64, 8);
+        memcpy(q + 8, digs + dk * 64, 64);
+      }
+      push_obj(ps, SG_OBJ_PATH, obj.data(), obj.size());
+    }
   }
 }
 
@@ -520,10 +515,11 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
   std::vector<DPoly> trace_polys;
   {
     DPoly col = dpoly_alloc(ctx, Tp);
+    GeoInterpCache zc;  // Z(omicron^m), Z'(omicron^i) shared by the register columns
     for (size_t s = 0; s < m; ++s) {
       SG_HIP(launch_gather_stride(col.p(), d_trace + s, rows, m, ctx->stream));
       SG_HIP(launch_gather_stride(col.p() + rows, d_trace_rand + s, st.num_randomizers, m, ctx->stream));
-      trace_polys.push_back(interpolate_geometric_dev(ctx, st.omicron, D, col.p(), Tp));
+      trace_polys.push_back(interpolate_geometric_dev(ctx, st.omicron, D, col.p(), Tp, &zc));
     }
   }
   // boundary quotients (stark.rs:326-362)
@@ -573,6 +569,36 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
     auto cit = cosets.find(L);
     if (cit == cosets.end()) cit = cosets.emplace(L, air_coset(ctx, trace_polys, L, st.omicron, g)).first;
     DPoly vals = transition_values(ctx, *tc, cit->second, g);
+    auto tz_values = [&](const DivPlan& pl) -> const fe* {
+      auto zit = tz_ntt.find(pl.order);
+      if (zit == tz_ntt.end()) {
+        std::pair<DevBuf, uint64_t> z;
+        ref_inner_ntt(ctx, pl.root, pl.order, tz.p(), tz.len, &g, z.first, z.second);
+        zit = tz_ntt.emplace(pl.order, std::move(z)).first;
+      }
+      return zit->second.first.as<fe>();
+    };
+    // Fast path: if the division by Z is exact, q = INTT(vals / Z) has degree dl - dr <= len - 1 - dr
+    // and then dl = deg(q) + dr exactly (q Z agrees with the transition polynomial on L > its
+    // degree points); with dl >= L/2 the reference's order is L, its lhs NTT is `vals` and its
+    // truncated quotient is q -- no coefficient transform of the lhs is needed.
+    if (L <= D && (uint64_t)dtz < len) {
+      DivPlan pl;
+      pl.root = root_of_order(L);
+      pl.order = L;
+      DevBuf qv(ctx, L * sizeof(fe)), qc(ctx, L * sizeof(fe));
+      dev_div(ctx, qv.as<fe>(), vals.p(), tz_values(pl), L);
+      intt_sized(ctx, pl.root, qv.as<fe>(), ilog2_exact(L), qc.as<fe>());
+      const int64_t dq = dev_degree(ctx, qc.as<fe>(), L);
+      const uint64_t dl = (uint64_t)dq + (uint64_t)dtz;
+      if (dq >= 0 && dl <= len - 1 && std::max<uint64_t>(dl, (uint64_t)dtz) >= L / 2) {
+        DPoly out = dpoly_alloc(ctx, (uint64_t)dq + 1);
+        dev_scale_pow(ctx, out.p(), qc.as<fe>(), out.len, fe_inv(g));
+        tqs.push_back(std::move(out));
+        continue;
+      }
+    }
+    // general path (inexact division or a degree below L/2): the reference's steps
     DPoly coeffs = dpoly_alloc(ctx, L);
     coset_interpolate_dev(ctx, vals.p(), L, g, coeffs.p());  // coefficients len..L-1 are zero
     const DivPlan pl = coset_divide_plan(st.omicron, D, dev_degree(ctx, coeffs.p(), len), dtz);
@@ -587,13 +613,7 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
       ref_inner_ntt(ctx, pl.root, pl.order, coeffs.p(), len, &g, lhs_own, nl);
       lhs_v = lhs_own.as<fe>();
     }
-    auto zit = tz_ntt.find(pl.order);
-    if (zit == tz_ntt.end()) {
-      std::pair<DevBuf, uint64_t> z;
-      ref_inner_ntt(ctx, pl.root, pl.order, tz.p(), tz.len, &g, z.first, z.second);
-      zit = tz_ntt.emplace(pl.order, std::move(z)).first;
-    }
-    tqs.push_back(coset_divide_finish(ctx, pl, g, lhs_v, zit->second.first.as<fe>()));
+    tqs.push_back(coset_divide_finish(ctx, pl, g, lhs_v, tz_values(pl)));
   }
   // randomizer polynomial + codeword (stark.rs:424-445)
   const uint64_t tcd = max_degree(st, tcs);
@@ -668,8 +688,10 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
   std::vector<uint64_t> quad = dup;
   for (uint64_t i : dup) quad.push_back((i + Nf / 2) % Nf);
   std::sort(quad.begin(), quad.end());
-  for (size_t s = 0; s < m; ++s) push_openings(ctx, ps, bq_cw[s].p(), bq_trees[s].get(), quad);
-  push_openings(ctx, ps, r_cw.p(), r_tree.get(), quad);
+  std::vector<std::pair<const fe*, const sg_tree*>> cts;
+  for (size_t s = 0; s < m; ++s) cts.emplace_back(bq_cw[s].p(), bq_trees[s].get());
+  cts.emplace_back(r_cw.p(), r_tree.get());
+  push_openings(ctx, ps, cts, quad);
   SG_HIP(hipStreamSynchronize(ctx->stream));
 }
 
