@@ -200,8 +200,8 @@ extern "C" int sg_ctx_create(int device, sg_ctx** out) {
   }
   void* pinned = nullptr;
   void* pinned_dev = nullptr;
-  // 4 root slots (64 B) + 4 ready flags (u64), host-coherent
-  if (hipHostMalloc(&pinned, 4 * 64 + 4 * 8, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+  // 4 root slots (64 B) + 4 ready flags (u64) + the division zero flag (u32, padded), host-coherent
+  if (hipHostMalloc(&pinned, 4 * 64 + 4 * 8 + 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
       hipHostGetDevicePointer(&pinned_dev, pinned, 0) != hipSuccess) {
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -209,7 +209,9 @@ extern "C" int sg_ctx_create(int device, sg_ctx** out) {
   }
   ctx->pinned_roots = reinterpret_cast<uint64_t*>(pinned);
   ctx->pinned_roots_dev = reinterpret_cast<uint64_t*>(pinned_dev);
-  memset(pinned, 0, 4 * 64 + 4 * 8);
+  memset(pinned, 0, 4 * 64 + 4 * 8 + 64);
+  ctx->div_zero_flag = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(pinned) + 4 * 64 + 4 * 8);
+  ctx->div_zero_flag_dev = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(pinned_dev) + 4 * 64 + 4 * 8);
   *out = ctx;
   return SG_OK;
 }

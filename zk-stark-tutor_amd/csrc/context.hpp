@@ -72,6 +72,10 @@ struct sg_ctx {
   uint64_t* pinned_roots = nullptr;      // host view, 4 x 64 bytes, then 4 x u64 ready flags
   uint64_t* pinned_roots_dev = nullptr;  // device view of the same memory
   uint64_t root_seq = 0;                 // last sequence number handed to a tree build
+  // host-coherent u32 raised (system-scope atomic) by k_batch_div on a zero divisor; read by
+  // the host at points where the stream has already drained past the divisions
+  uint32_t* div_zero_flag = nullptr;      // host view (inside the pinned_roots allocation)
+  uint32_t* div_zero_flag_dev = nullptr;  // device view
   bool async_dev = false;                // sg_ctx_set_async: _dev transforms return once enqueued
   // per-kernel event timing (sg_ctx_profile)
   bool profiling = false;

@@ -45,7 +45,12 @@ int guard(sg_ctx* ctx, F&& f) {
     f();
     return SG_OK;
   } catch (const Error& e) {
-    if (ctx) ctx->last_error = e.msg;
+    if (ctx) {
+      ctx->last_error = e.msg;
+      // a failed call may leave divisions in flight: drain and clear the zero-divisor flag
+      (void)hipStreamSynchronize(ctx->stream);
+      if (ctx->div_zero_flag) *reinterpret_cast<volatile uint32_t*>(ctx->div_zero_flag) = 0;
+    }
     return e.code;
   } catch (const std::bad_alloc&) {
     if (ctx) ctx->last_error = "host allocation failed";

@@ -129,13 +129,16 @@ void dev_mul(sg_ctx* ctx, fe* out, const fe* a, const fe* b, uint64_t n) {
 
 void dev_div(sg_ctx* ctx, fe* out, const fe* a, const fe* b, uint64_t n) {
   if (!n) return;
-  DevBuf flag(ctx, 4);
-  SG_HIP(hipMemsetAsync(flag.get(), 0, 4, ctx->stream));
-  SG_HIP(launch_batch_div(out, a, b, n, fe_r2(), one_m(), flag.as<unsigned>(), ctx->stream));
-  unsigned h = 0;
-  SG_HIP(hipMemcpyAsync(&h, flag.get(), 4, hipMemcpyDeviceToHost, ctx->stream));
-  SG_HIP(hipStreamSynchronize(ctx->stream));
-  SG_REQUIRE(h == 0, "divide by zero");  // field_element.rs:82-90
+  // a zero divisor raises ctx->div_zero_flag; check_div_zero() reports it once the stream
+  // has drained (no round trip per division)
+  SG_HIP(launch_batch_div(out, a, b, n, fe_r2(), one_m(), ctx->div_zero_flag_dev, ctx->stream));
+}
+
+void check_div_zero(sg_ctx* ctx) {
+  if (*reinterpret_cast<volatile uint32_t*>(ctx->div_zero_flag)) {
+    *reinterpret_cast<volatile uint32_t*>(ctx->div_zero_flag) = 0;
+    throw Error{SG_ERR_INVALID, "divide by zero"};  // field_element.rs:82-90
+  }
 }
 
 void dev_scale_pow(sg_ctx* ctx, fe* out, const fe* in, uint64_t n, const fe& f, uint64_t start) {
@@ -156,7 +159,6 @@ void dev_prefix_product(sg_ctx* ctx, fe* data, uint64_t n) {
   SG_HIP(launch_scan_tile(data, n, tot.as<fe>(), fe_r2(), one_m(), ctx->stream));
   dev_prefix_product(ctx, tot.as<fe>(), tiles);
   SG_HIP(launch_scan_fix(data, n, tot.as<fe>(), fe_r2(), ctx->stream));
-  SG_HIP(hipStreamSynchronize(ctx->stream));  // tot returns to the pool
 }
 
 // ------------------------------------------------------------------ products
@@ -182,7 +184,6 @@ DPoly poly_mul_exact(sg_ctx* ctx, const fe* a, uint64_t la, const fe* b, uint64_
   dev_mul(ctx, va.as<fe>(), va.as<fe>(), vb.as<fe>(), n);
   intt_sized(ctx, w, va.as<fe>(), logn, c.as<fe>());
   SG_HIP(hipMemcpyAsync(out.p(), c.get(), lr * sizeof(fe), hipMemcpyDeviceToDevice, ctx->stream));
-  SG_HIP(hipStreamSynchronize(ctx->stream));
   return out;
 }
 
@@ -231,7 +232,6 @@ DPoly coset_divide_finish(sg_ctx* ctx, const DivPlan& pl, const fe& offset, fe* 
   uint64_t keep = std::min(pl.result_len, pl.order);
   DPoly out = dpoly_alloc(ctx, keep);
   dev_scale_pow(ctx, out.p(), c.as<fe>(), keep, fe_inv(offset));
-  SG_HIP(hipStreamSynchronize(ctx->stream));
   return out;
 }
 
@@ -257,7 +257,6 @@ DPoly fast_multiply_dev(sg_ctx* ctx, fe root, uint64_t root_order, const fe* a, 
   intt_sized(ctx, root, va.as<fe>(), ilog2_exact(order), c.as<fe>());
   uint64_t keep = std::min(result_len, order);
   DPoly out = dpoly_copy(ctx, c.as<fe>(), keep);
-  SG_HIP(hipStreamSynchronize(ctx->stream));
   return out;
 }
 
@@ -285,8 +284,7 @@ DPoly zerofier_geometric_dev(sg_ctx* ctx, const fe& q, uint64_t D, uint64_t n) {
     // size-D NTT wraps x^D - 1 onto x^0 - 1 = 0 and returns D zeros (not truncated)
     DPoly z = dpoly_alloc(ctx, D);
     SG_HIP(hipMemsetAsync(z.p(), 0, D * sizeof(fe), ctx->stream));
-    SG_HIP(hipStreamSynchronize(ctx->stream));
-    return z;
+      return z;
   }
   const fe *qA, *qB;
   pow_tables2(ctx, q, D, &qA, &qB);
@@ -298,7 +296,6 @@ DPoly zerofier_geometric_dev(sg_ctx* ctx, const fe& q, uint64_t D, uint64_t n) {
   dev_div(ctx, invF.as<fe>(), nullptr, F.as<fe>(), n + 1);
   DPoly z = dpoly_alloc(ctx, n + 1);
   SG_HIP(launch_qbinom(z.p(), F.as<fe>(), invF.as<fe>(), n, D, qA, qB, fe_r2(), ctx->stream));
-  SG_HIP(hipStreamSynchronize(ctx->stream));
   return z;
 }
 
@@ -318,7 +315,6 @@ const fe* interp_kernel(sg_ctx* ctx, const fe& q, uint64_t D) {
   void* t = nullptr;
   SG_HIP(hipMalloc(&t, D * sizeof(fe)));
   ntt_sized(ctx, q, b.as<fe>(), D, ilog2_exact(D), reinterpret_cast<fe*>(t));
-  SG_HIP(hipStreamSynchronize(ctx->stream));
   ctx->interp_tables[key] = t;
   return reinterpret_cast<const fe*>(t);
 }
@@ -333,8 +329,7 @@ DPoly interpolate_geometric_dev(sg_ctx* ctx, const fe& q, uint64_t D, const fe* 
   if (n == D) {
     DPoly out = dpoly_alloc(ctx, D);
     intt_sized(ctx, q, y, logD, out.p());
-    SG_HIP(hipStreamSynchronize(ctx->stream));
-    return out;
+      return out;
   }
   // Z, Z(q^m) and Z'(q^i) (cached per domain)
   GeoInterpCache local;
@@ -347,7 +342,6 @@ DPoly interpolate_geometric_dev(sg_ctx* ctx, const fe& q, uint64_t D, const fe* 
     ntt_sized(ctx, q, Z.p(), n + 1, logD, zc.Zv.as<fe>());
     SG_HIP(launch_deriv(Zd.as<fe>(), Z.p(), n, fe_r2(), ctx->stream));
     ntt_sized(ctx, q, Zd.as<fe>(), n, logD, zc.Zdv.as<fe>());
-    SG_HIP(hipStreamSynchronize(ctx->stream));  // Z and Zd return to the pool
     zc.q = q;
     zc.D = D;
     zc.n = n;
@@ -366,7 +360,6 @@ DPoly interpolate_geometric_dev(sg_ctx* ctx, const fe& q, uint64_t D, const fe* 
   SG_HIP(launch_interp_assemble(va.as<fe>(), y, Zv.as<fe>(), S.as<fe>(), n, D, iA, iB, fe_r2(), ctx->stream));
   intt_sized(ctx, q, va.as<fe>(), logD, S.as<fe>());
   DPoly out = dpoly_copy(ctx, S.as<fe>(), n);
-  SG_HIP(hipStreamSynchronize(ctx->stream));
   return out;
 }
 
@@ -375,7 +368,6 @@ void coset_interpolate_dev(sg_ctx* ctx, const fe* values, uint64_t L, const fe& 
   DevBuf c(ctx, L * sizeof(fe));
   intt_sized(ctx, w, values, ilog2_exact(L), c.as<fe>());
   dev_scale_pow(ctx, out, c.as<fe>(), L, fe_inv(offset));
-  SG_HIP(hipStreamSynchronize(ctx->stream));
 }
 
 void coset_values_dev(sg_ctx* ctx, const fe* coeffs, uint64_t len, uint64_t L, const fe& offset, fe* out) {
@@ -486,6 +478,11 @@ sg_poly* wrap(DPoly&& d) {
   return p;
 }
 const fe* dptr(const sg_poly* p) { return p ? p->d.p() : nullptr; }
+// ABI calls return after their device work: drain the stream, then report a zero divisor
+void done(sg_ctx* ctx) {
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  check_div_zero(ctx);
+}
 uint64_t dlen(const sg_poly* p) { return p ? p->d.len : 0; }
 constexpr uint64_t kHostDomainMax = 1024;
 }  // namespace
@@ -541,7 +538,9 @@ extern "C" int sg_fast_multiply(sg_ctx* ctx, sg_fe root, uint64_t root_order, co
   return guard(ctx, [&] {
     SG_REQUIRE(lhs && rhs && out, "null argument");
     SG_HIP(hipSetDevice(ctx->device));
-    *out = wrap(fast_multiply_dev(ctx, to_fe(root), root_order, dptr(lhs), dlen(lhs), dptr(rhs), dlen(rhs)));
+    DPoly r = fast_multiply_dev(ctx, to_fe(root), root_order, dptr(lhs), dlen(lhs), dptr(rhs), dlen(rhs));
+    done(ctx);
+    *out = wrap(std::move(r));
   });
 }
 
@@ -550,8 +549,10 @@ extern "C" int sg_fast_coset_divide(sg_ctx* ctx, sg_fe root, uint64_t root_order
   return guard(ctx, [&] {
     SG_REQUIRE(lhs && rhs && out, "null argument");
     SG_HIP(hipSetDevice(ctx->device));
-    *out = wrap(fast_coset_divide_dev(ctx, to_fe(root), root_order, to_fe(offset), dptr(lhs), dlen(lhs), dptr(rhs),
-                                      dlen(rhs)));
+    DPoly r = fast_coset_divide_dev(ctx, to_fe(root), root_order, to_fe(offset), dptr(lhs), dlen(lhs), dptr(rhs),
+                                    dlen(rhs));
+    done(ctx);
+    *out = wrap(std::move(r));
   });
 }
 
@@ -565,7 +566,9 @@ extern "C" int sg_fast_zerofier(sg_ctx* ctx, sg_fe root, uint64_t root_order, co
     check_root(r, root_order);
     const fe* dom = reinterpret_cast<const fe*>(domain);
     if (n > 1 && is_geometric(dom, n, r) && n <= root_order) {
-      *out = wrap(zerofier_geometric_dev(ctx, r, root_order, n));
+      DPoly z = zerofier_geometric_dev(ctx, r, root_order, n);
+      done(ctx);
+      *out = wrap(std::move(z));
       return;
     }
     SG_REQUIRE(n <= kHostDomainMax, "fast_zerofier: non-geometric domains above 1024 points are not supported");
@@ -589,7 +592,9 @@ extern "C" int sg_fast_interpolate_domain(sg_ctx* ctx, sg_fe root, uint64_t root
     const fe* val = reinterpret_cast<const fe*>(values);
     if (n > 1 && n <= root_order && is_geometric(dom, n, r)) {
       DPoly y = dpoly_upload(ctx, val, n);
-      *out = wrap(interpolate_geometric_dev(ctx, r, root_order, y.p(), n));
+      DPoly ip = interpolate_geometric_dev(ctx, r, root_order, y.p(), n);
+      done(ctx);
+      *out = wrap(std::move(ip));
       return;
     }
     SG_REQUIRE(n <= kHostDomainMax,
@@ -606,7 +611,9 @@ extern "C" int sg_fast_zerofier_geometric(sg_ctx* ctx, sg_fe root, uint64_t root
     SG_REQUIRE(out, "null argument");
     SG_HIP(hipSetDevice(ctx->device));
     check_root(to_fe(root), root_order);
-    *out = wrap(zerofier_geometric_dev(ctx, to_fe(root), root_order, n));
+    DPoly z = zerofier_geometric_dev(ctx, to_fe(root), root_order, n);
+    done(ctx);
+    *out = wrap(std::move(z));
   });
 }
 
@@ -616,6 +623,8 @@ extern "C" int sg_fast_interpolate_geometric_dev(sg_ctx* ctx, sg_fe root, uint64
     SG_REQUIRE(out && (d_values || !n), "null argument");
     SG_HIP(hipSetDevice(ctx->device));
     check_root(to_fe(root), root_order);
-    *out = wrap(interpolate_geometric_dev(ctx, to_fe(root), root_order, reinterpret_cast<const fe*>(d_values), n));
+    DPoly ip = interpolate_geometric_dev(ctx, to_fe(root), root_order, reinterpret_cast<const fe*>(d_values), n);
+    done(ctx);
+    *out = wrap(std::move(ip));
   });
 }

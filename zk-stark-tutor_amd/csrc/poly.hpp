@@ -40,8 +40,11 @@ void ntt_sized(sg_ctx* ctx, const fe& root, const fe* in, uint64_t n_in, int log
 void intt_sized(sg_ctx* ctx, const fe& root, const fe* in, int logn, fe* out);
 
 void dev_mul(sg_ctx* ctx, fe* out, const fe* a, const fe* b, uint64_t n);
-// out = a / b elementwise (a == nullptr: 1 / b); throws "divide by zero" on a zero divisor
+// out = a / b elementwise (a == nullptr: 1 / b); a zero divisor is reported by check_div_zero
 void dev_div(sg_ctx* ctx, fe* out, const fe* a, const fe* b, uint64_t n);
+// throws "divide by zero" if a division since the last check saw a zero divisor; call only
+// after the stream has drained past those divisions (a synchronize or a tree-root wait)
+void check_div_zero(sg_ctx* ctx);
 // out[i] = in[i] * f^(start + i)
 void dev_scale_pow(sg_ctx* ctx, fe* out, const fe* in, uint64_t n, const fe& f, uint64_t start = 0);
 // in-place inclusive prefix product

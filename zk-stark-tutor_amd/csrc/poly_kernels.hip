@@ -112,7 +112,7 @@ __global__ __launch_bounds__(kBlock) void k_batch_div(fe* __restrict__ out, cons
     pre[k] = acc;  // product of the elements before k
     acc = mont_mul(acc, bm);
   }
-  if (zero) atomicOr(zero_flag, 1u);
+  if (zero) __hip_atomic_fetch_or(zero_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   fe inv = mont_inv(acc, one_m);  // (prod b)^-1 R
 #pragma unroll
   for (int k = K - 1; k >= 0; --k) {

@@ -551,6 +551,7 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
     for (int k = 0; k < b; ++k) leaves[k] = bq_cw[s + k].p();
     build_trees(ctx, leaves, b, Nf, &bq_trees[s]);
   }
+  check_div_zero(ctx);  // the root wait drained the stream past the boundary divisions
   for (size_t s = 0; s < m; ++s) push_obj(ps, SG_OBJ_ROOT, bq_trees[s]->root, 64);
   // transition quotients (stark.rs:388-422): evaluate_symbolic's polynomial from its values on a
   // coset of size L > its length, then fast_coset_divide by the transition zerofier.  When the
@@ -626,6 +627,7 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
     coset_evaluate_batch(ctx, st.omega, Nf, g, &in, nrc, &out, 1);
   }
   std::unique_ptr<sg_tree> r_tree(build_tree(ctx, r_cw.p(), Nf));
+  check_div_zero(ctx);  // ... and past the transition divisions
   push_obj(ps, SG_OBJ_ROOT, r_tree->root, 64);
   // weights (stark.rs:447-450)
   uint8_t fs[32];
@@ -693,6 +695,7 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
   cts.emplace_back(r_cw.p(), r_tree.get());
   push_openings(ctx, ps, cts, quad);
   SG_HIP(hipStreamSynchronize(ctx->stream));
+  check_div_zero(ctx);
 }
 
 std::vector<const MPoly*> tc_list(const sg_mpoly* const* tcs, size_t n) {
@@ -763,6 +766,8 @@ extern "C" int sg_rescue_transition_constraints(sg_ctx* ctx, const sg_rescue* rp
     SG_REQUIRE(rp && out, "null argument");
     SG_HIP(hipSetDevice(ctx->device));
     std::vector<MPoly> tcs = rescue_transition_constraints(ctx, *rp, to_fe(omicron), omicron_domain_length);
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+    check_div_zero(ctx);
     for (size_t i = 0; i < tcs.size(); ++i) {
       out[i] = new sg_mpoly();
       out[i]->m = std::move(tcs[i]);
