@@ -75,3 +75,67 @@ def test_host_transcript_matches_oracle():
     assert back.objects() == objs
     # an empty IndependentProofStream digests to a 16-byte zero field header
     assert sg.IndependentProofStream().digest() == bytes(16)
+
+
+# ---------------------------------------------------------------- host-only native logic
+
+def test_host_rescue_prime_matches_reference_kats():
+    """RescuePrime::new / hash / trace through the library's host path (no device)."""
+    import json
+    import stark_prove_oracle as e
+    with open(os.path.join(ROOT, "tests", "golden", "reference_kats_e2e.json")) as f:
+        k = json.load(f)
+    h = sg.HostContext()
+    rp = sg.RescuePrime(2, 1, 128, 27, ctx=h)
+    r = k["rescue_new"]
+    assert rp.alpha == r["alpha"] and rp.alpha_inv == int(r["alpha_inv"]), r["src"]
+    assert rp.MDS == [[int(x) for x in row] for row in r["mds"]], r["src"]
+    assert rp.MDS_inv == [[int(x) for x in row] for row in r["mds_inv"]], r["src"]
+    assert rp.round_constants == [int(x) for x in r["round_constants"]], r["src"]
+    assert rp.hash(int(k["rescue_hash"]["input"])) == int(k["rescue_hash"]["output"])
+    t = rp.trace(int(k["rescue_trace"]["input"]))
+    assert t[-1][0] == int(k["rescue_trace"]["last_rate"])
+    for (m, N) in ((3, 7), (2, 60)):
+        a, b = sg.RescuePrime(m, 1, 2, N, ctx=h), e.RescuePrime(m, 1, 2, N)
+        assert a.MDS == b.MDS and a.MDS_inv == b.MDS_inv and a.round_constants == b.round_constants
+        assert a.trace(99) == b.trace(99)
+    import pytest
+    with pytest.raises(sg.StarkGpuError, match="GPU context"):
+        rp.transition_constraints(1, 2)
+
+
+def test_host_mpolynomial_and_degree_bounds_match_oracle():
+    """MPolynomial arithmetic (small, host) and Stark's key-based degree bounds vs the oracle."""
+    import random
+    import stark_prove_oracle as e
+    h = sg.HostContext()
+
+    def grouped(d):
+        out = {}
+        for key, c in d.items():
+            v = out.setdefault(tuple(key[1:]), [])
+            v.extend([0] * (key[0] + 1 - len(v)))
+            v[key[0]] = (v[key[0]] + c) % o.P
+        return (len(next(iter(d))) if d else 0), out
+
+    rng = random.Random(11)
+    for _ in range(6):
+        nv = rng.randrange(1, 5)
+        da = {tuple(rng.randrange(4) for _ in range(nv)): rng.choice([0, rng.randrange(o.P)]) for _ in range(5)}
+        db = {tuple(rng.randrange(3) for _ in range(nv)): rng.randrange(o.P) for _ in range(4)}
+        A, B = sg.MPolynomial.new(da, ctx=h), sg.MPolynomial.new(db, ctx=h)
+        oa, ob = e.MPolynomial(da), e.MPolynomial(db)
+        assert (A * B).groups() == grouped((oa * ob).d)
+        assert (A - B).groups() == grouped((oa - ob).d)
+        assert (A ** 3).groups() == grouped((oa ** 3).d)
+        pt = [rng.randrange(o.P) for _ in range(nv)]
+        assert A.evaluate(pt) == oa.evaluate(pt)
+    # the oracle's Rescue AIR, handed to the library as dictionaries: same key-based bounds
+    st_o = e.Stark(4, 2, 2, 2, 28, 2)
+    st_h = sg.Stark(4, 2, 2, 2, 28, 2, ctx=h)
+    assert (st_h.omicron, st_h.omicron_domain_length, st_h.num_randomizers, st_h.fri_domain_length) == \
+        (st_o.omicron, st_o.omicron_domain_length, st_o.num_randomizers, st_o.fri.domain_length)
+    air_o = e.RescuePrime(2, 1, 2, 27).transition_constraints(st_o.omicron, st_o.omicron_domain_length)
+    air_h = [sg.MPolynomial.new(a.d, ctx=h) for a in air_o]
+    assert st_h.transition_degree_bounds(air_h) == st_o.transition_degree_bounds(air_o)
+    assert st_h.max_degree(air_h) == st_o.max_degree(air_o)

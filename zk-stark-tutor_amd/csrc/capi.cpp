@@ -275,7 +275,9 @@ extern "C" int sg_ctx_profile_report(sg_ctx* ctx, char* buf, size_t cap, size_t*
   });
 }
 
-extern "C" const char* sg_last_error(const sg_ctx* ctx) { return ctx ? ctx->last_error.c_str() : "null context"; }
+extern "C" const char* sg_last_error(const sg_ctx* ctx) {
+  return ctx ? ctx->last_error.c_str() : host_last_error().c_str();
+}
 extern "C" void* sg_ctx_stream(sg_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
 extern "C" int sg_ctx_trim(sg_ctx* ctx) {
   return guard(ctx, [&] {
@@ -313,7 +315,7 @@ extern "C" sg_fe sg_fe_pow(sg_fe a, uint64_t e) { return from_fe(fe_pow(to_fe(a)
 
 extern "C" int sg_ntt_dev(sg_ctx* ctx, sg_fe root, const sg_fe* d_in, size_t n_in, sg_fe* d_out) {
   return guard(ctx, [&] {
-    SG_HIP(hipSetDevice(ctx->device));
+    set_device(ctx);
     ntt_dev(ctx, to_fe(root), reinterpret_cast<const fe*>(d_in), n_in, reinterpret_cast<fe*>(d_out), nullptr,
             nullptr);
   });
@@ -321,7 +323,7 @@ extern "C" int sg_ntt_dev(sg_ctx* ctx, sg_fe root, const sg_fe* d_in, size_t n_i
 
 extern "C" int sg_intt_dev(sg_ctx* ctx, sg_fe root, const sg_fe* d_in, size_t n_in, sg_fe* d_out) {
   return guard(ctx, [&] {
-    SG_HIP(hipSetDevice(ctx->device));
+    set_device(ctx);
     if (n_in < 2) {
       // fft/ntt.rs:56-58: returned unchanged
       if (n_in) SG_HIP(hipMemcpyAsync(d_out, d_in, n_in * sizeof(fe), hipMemcpyDeviceToDevice, ctx->stream));
@@ -360,7 +362,7 @@ void coset_evaluate_batch(sg_ctx* ctx, const fe& generator, uint64_t root_order,
 extern "C" int sg_fast_coset_evaluate_dev(sg_ctx* ctx, sg_fe generator, uint64_t root_order, sg_fe offset,
                                           const sg_fe* d_coeffs, size_t d, sg_fe* d_out) {
   return guard(ctx, [&] {
-    SG_HIP(hipSetDevice(ctx->device));
+    set_device(ctx);
     const fe* in = reinterpret_cast<const fe*>(d_coeffs);
     fe* out = reinterpret_cast<fe*>(d_out);
     coset_evaluate_batch(ctx, to_fe(generator), root_order, to_fe(offset), &in, d, &out, 1);
@@ -371,7 +373,7 @@ extern "C" int sg_fast_coset_evaluate_batch_dev(sg_ctx* ctx, sg_fe generator, ui
                                                 const sg_fe* const* d_coeffs, size_t d, sg_fe* const* d_out,
                                                 size_t batch) {
   return guard(ctx, [&] {
-    SG_HIP(hipSetDevice(ctx->device));
+    set_device(ctx);
     SG_REQUIRE(d_coeffs && d_out && batch >= 1 && batch <= 4, "batch must be 1..4");
     coset_evaluate_batch(ctx, to_fe(generator), root_order, to_fe(offset),
                          reinterpret_cast<const fe* const*>(d_coeffs), d, reinterpret_cast<fe* const*>(d_out),
@@ -518,14 +520,14 @@ void gather_digests(sg_ctx* ctx, const sg_tree* t, const std::vector<uint64_t>& 
 
 extern "C" int sg_merkle_build_dev(sg_ctx* ctx, const sg_fe* d_leaves, size_t n, sg_tree** out) {
   return guard(ctx, [&] {
-    SG_HIP(hipSetDevice(ctx->device));
+    set_device(ctx);
     *out = build_tree(ctx, reinterpret_cast<const fe*>(d_leaves), n);
   });
 }
 extern "C" int sg_merkle_build_batch_dev(sg_ctx* ctx, const sg_fe* const* d_leaves, size_t n, size_t batch,
                                          sg_tree** out) {
   return guard(ctx, [&] {
-    SG_HIP(hipSetDevice(ctx->device));
+    set_device(ctx);
     SG_REQUIRE(d_leaves && out && batch >= 1 && batch <= 4, "batch must be 1..4");
     std::unique_ptr<sg_tree> t[4];
     build_trees(ctx, reinterpret_cast<const fe* const*>(d_leaves), (int)batch, n, t);
@@ -556,7 +558,7 @@ extern "C" void sg_tree_free(sg_ctx* ctx, sg_tree* t) {
 
 extern "C" int sg_merkle_commit(sg_ctx* ctx, const sg_fe* leaves, size_t n, uint8_t root[64]) {
   return guard(ctx, [&] {
-    SG_HIP(hipSetDevice(ctx->device));
+    set_device(ctx);
     SG_REQUIRE(n > 0 && (n & (n - 1)) == 0, "Leafs len must be power of two");
     check_canonical(leaves, n, "leaf");
     DevBuf d(ctx, n * sizeof(fe));
@@ -569,7 +571,7 @@ extern "C" int sg_merkle_commit(sg_ctx* ctx, const sg_fe* leaves, size_t n, uint
 extern "C" int sg_merkle_open(sg_ctx* ctx, size_t index, const sg_fe* leaves, size_t n, uint8_t* path,
                               size_t* path_len) {
   return guard(ctx, [&] {
-    SG_HIP(hipSetDevice(ctx->device));
+    set_device(ctx);
     SG_REQUIRE(n > 0 && (n & (n - 1)) == 0, "length must be power of two");
     SG_REQUIRE(index < n, "cannot open invalid index");
     check_canonical(leaves, n, "leaf");
@@ -972,7 +974,7 @@ extern "C" size_t sg_fri_num_rounds(const sg_fri* fri) { return fri ? fri_num_ro
 extern "C" int sg_fri_commit_dev(sg_ctx* ctx, const sg_fri* fri, const sg_fe* d_cw, size_t n,
                                  const sg_proof_stream* ps, sg_fri_state** keep) {
   return guard(ctx, [&] {
-    SG_HIP(hipSetDevice(ctx->device));
+    set_device(ctx);
     std::unique_ptr<sg_fri_state> st(new sg_fri_state());
     fri_commit_dev(ctx, fri, reinterpret_cast<const fe*>(d_cw), n, ps, *st, /*borrow_input=*/keep == nullptr);
     if (keep) *keep = st.release();
@@ -982,7 +984,7 @@ extern "C" int sg_fri_commit_dev(sg_ctx* ctx, const sg_fri* fri, const sg_fe* d_
 extern "C" int sg_fri_commit(sg_ctx* ctx, const sg_fri* fri, const sg_fe* cw, size_t n, const sg_proof_stream* ps,
                              sg_fri_state** keep) {
   return guard(ctx, [&] {
-    SG_HIP(hipSetDevice(ctx->device));
+    set_device(ctx);
     check_canonical(cw, n, "codeword");
     DevBuf d(ctx, std::max<size_t>(n, 1) * sizeof(fe));
     if (n) SG_HIP(hipMemcpyAsync(d.get(), cw, n * sizeof(fe), hipMemcpyHostToDevice, ctx->stream));
@@ -995,7 +997,7 @@ extern "C" int sg_fri_commit(sg_ctx* ctx, const sg_fri* fri, const sg_fe* cw, si
 extern "C" int sg_fri_prove_dev(sg_ctx* ctx, const sg_fri* fri, const sg_fe* d_cw, size_t n, const sg_proof_stream* ps,
                                 size_t* top) {
   return guard(ctx, [&] {
-    SG_HIP(hipSetDevice(ctx->device));
+    set_device(ctx);
     fri_prove_dev(ctx, fri, reinterpret_cast<const fe*>(d_cw), n, ps, top);
   });
 }
@@ -1003,7 +1005,7 @@ extern "C" int sg_fri_prove_dev(sg_ctx* ctx, const sg_fri* fri, const sg_fe* d_c
 extern "C" int sg_fri_prove(sg_ctx* ctx, const sg_fri* fri, const sg_fe* cw, size_t n, const sg_proof_stream* ps,
                             size_t* top) {
   return guard(ctx, [&] {
-    SG_HIP(hipSetDevice(ctx->device));
+    set_device(ctx);
     check_canonical(cw, n, "codeword");
     DevBuf d(ctx, std::max<size_t>(n, 1) * sizeof(fe));
     if (n) SG_HIP(hipMemcpyAsync(d.get(), cw, n * sizeof(fe), hipMemcpyHostToDevice, ctx->stream));
@@ -1049,7 +1051,7 @@ constexpr uint64_t kRowsPerLaunch = 65535;  // grid.y limit
 extern "C" int sg_ntt_rows_dev(sg_ctx* ctx, sg_fe root, const sg_fe* d_in, size_t n_in, size_t rows, sg_fe* d_out,
                                size_t n) {
   return guard(ctx, [&] {
-    SG_HIP(hipSetDevice(ctx->device));
+    set_device(ctx);
     SG_REQUIRE(d_in && d_out, "null buffer");
     SG_REQUIRE(n > 0 && (n & (n - 1)) == 0, "ntt rows: n must be a power of two");
     SG_REQUIRE(n_in > 0 && n_in <= n, "ntt rows: need 0 < n_in <= n");
@@ -1076,7 +1078,7 @@ extern "C" int sg_ntt_rows_dev(sg_ctx* ctx, sg_fe root, const sg_fe* d_in, size_
 
 extern "C" int sg_scale_dev(sg_ctx* ctx, sg_fe* d_data, size_t n, sg_fe c) {
   return guard(ctx, [&] {
-    SG_HIP(hipSetDevice(ctx->device));
+    set_device(ctx);
     SG_REQUIRE(fe_is_canonical(to_fe(c)), "scale: constant must be canonical");
     if (n == 0) return;
     fe cm = to_mont(to_fe(c));
@@ -1090,7 +1092,7 @@ extern "C" int sg_scale_dev(sg_ctx* ctx, sg_fe* d_data, size_t n, sg_fe c) {
 extern "C" int sg_mul_pow_dev(sg_ctx* ctx, sg_fe base, sg_fe* d_data, size_t rows, size_t cols, uint64_t a0,
                               uint64_t a1, uint64_t b0, uint64_t b1) {
   return guard(ctx, [&] {
-    SG_HIP(hipSetDevice(ctx->device));
+    set_device(ctx);
     const fe b = to_fe(base);
     SG_REQUIRE(fe_is_canonical(b), "mul_pow: base must be canonical");
     if (rows == 0 || cols == 0) return;
@@ -1107,7 +1109,7 @@ extern "C" int sg_mul_pow_dev(sg_ctx* ctx, sg_fe base, sg_fe* d_data, size_t row
 
 extern "C" int sg_transpose_dev(sg_ctx* ctx, const sg_fe* d_in, sg_fe* d_out, size_t A, size_t B, size_t C) {
   return guard(ctx, [&] {
-    SG_HIP(hipSetDevice(ctx->device));
+    set_device(ctx);
     const uint64_t total = (uint64_t)A * B * C;
     if (total == 0) return;
     SG_REQUIRE(!ranges_overlap(reinterpret_cast<const fe*>(d_in), total, reinterpret_cast<const fe*>(d_out), total),
@@ -1119,7 +1121,7 @@ extern "C" int sg_transpose_dev(sg_ctx* ctx, const sg_fe* d_in, sg_fe* d_out, si
 
 extern "C" int sg_merkle_forest_dev(sg_ctx* ctx, const sg_fe* d_leaves, size_t run, size_t runs, sg_forest** out) {
   return guard(ctx, [&] {
-    SG_HIP(hipSetDevice(ctx->device));
+    set_device(ctx);
     SG_REQUIRE(out && d_leaves, "null argument");
     SG_REQUIRE(run > 0 && (run & (run - 1)) == 0, "Leafs len must be power of two");
     SG_REQUIRE(runs >= 1, "forest: zero runs");
@@ -1143,7 +1145,7 @@ extern "C" int sg_merkle_forest_dev(sg_ctx* ctx, const sg_fe* d_leaves, size_t r
 
 extern "C" int sg_forest_roots_dev(sg_ctx* ctx, const sg_forest* f, uint8_t* d_roots) {
   return guard(ctx, [&] {
-    SG_HIP(hipSetDevice(ctx->device));
+    set_device(ctx);
     SG_REQUIRE(f && d_roots, "null argument");
     const uint64_t per = merkle_tree_digests(f->run) * 8;
     const uint64_t root_off = (2 * f->run - 2) * 8;
@@ -1179,7 +1181,7 @@ extern "C" void sg_forest_free(sg_ctx* ctx, sg_forest* f) {
 
 extern "C" int sg_merkle_top_dev(sg_ctx* ctx, const uint8_t* d_digests, size_t n, sg_tree** out) {
   return guard(ctx, [&] {
-    SG_HIP(hipSetDevice(ctx->device));
+    set_device(ctx);
     SG_REQUIRE(out && d_digests, "null argument");
     SG_REQUIRE(n > 0 && (n & (n - 1)) == 0, "Leafs len must be power of two");
     std::unique_ptr<sg_tree> t(new sg_tree());
@@ -1203,7 +1205,7 @@ extern "C" int sg_fri_fold_runs_dev(sg_ctx* ctx, sg_fe omega, sg_fe offset, sg_f
                                     size_t n_local, size_t run, size_t run_stride, size_t run_off, size_t n_global,
                                     sg_fe* d_out) {
   return guard(ctx, [&] {
-    SG_HIP(hipSetDevice(ctx->device));
+    set_device(ctx);
     SG_REQUIRE(d_in && d_out, "null buffer");
     SG_REQUIRE(n_global >= 2 && (n_global & (n_global - 1)) == 0, "fold: global length must be a power of two >= 2");
     SG_REQUIRE(n_local >= 2 && n_local % 2 == 0 && run > 0, "fold: bad local shape");

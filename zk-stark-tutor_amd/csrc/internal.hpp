@@ -33,6 +33,12 @@ namespace sg {
 inline fe to_fe(sg_fe a) { return fe_make(a.lo, a.hi); }
 inline sg_fe from_fe(const fe& a) { return sg_fe{fe_lo(a), fe_hi(a)}; }
 
+// error text of calls made without a context (host-only entry points accept ctx == NULL)
+inline std::string& host_last_error() {
+  static thread_local std::string s;
+  return s;
+}
+
 // Runs f, mapping library errors to the C-ABI return code (+ ctx->last_error).
 template <class F>
 int guard(sg_ctx* ctx, F&& f) {
@@ -50,15 +56,23 @@ int guard(sg_ctx* ctx, F&& f) {
       // a failed call may leave divisions in flight: drain and clear the zero-divisor flag
       (void)hipStreamSynchronize(ctx->stream);
       if (ctx->div_zero_flag) *reinterpret_cast<volatile uint32_t*>(ctx->div_zero_flag) = 0;
+    } else {
+      host_last_error() = e.msg;
     }
     return e.code;
   } catch (const std::bad_alloc&) {
-    if (ctx) ctx->last_error = "host allocation failed";
+    (ctx ? ctx->last_error : host_last_error()) = "host allocation failed";
     return SG_ERR_NOMEM;
   } catch (...) {
-    if (ctx) ctx->last_error = "unknown error";
+    (ctx ? ctx->last_error : host_last_error()) = "unknown error";
     return SG_ERR_INVALID;
   }
+}
+
+// device entry points: a context is required (host-only ones accept NULL)
+inline void set_device(sg_ctx* ctx) {
+  if (!ctx) throw Error{SG_ERR_INVALID, "a GPU context is required"};
+  SG_HIP(hipSetDevice(ctx->device));
 }
 
 inline int ilog2_exact(uint64_t n) {

@@ -280,7 +280,7 @@ extern "C" int sg_mpoly_lift(sg_ctx* ctx, const sg_fe* coeffs, size_t len, size_
 
 extern "C" int sg_mpoly_lift_poly(sg_ctx* ctx, const sg_poly* p, size_t variable_index, sg_mpoly** out) {
   return guard(ctx, [&] {
-    SG_REQUIRE(out && p, "null argument");
+    SG_REQUIRE(ctx && out && p, "a GPU context and a polynomial are required");
     *out = wrapm(mp_lift(dpoly_download(ctx, p->d.p(), p->d.len), (uint32_t)variable_index));
   });
 }
@@ -309,7 +309,7 @@ extern "C" int sg_mpoly_sub(sg_ctx* ctx, const sg_mpoly* a, const sg_mpoly* b, s
 extern "C" int sg_mpoly_mul(sg_ctx* ctx, const sg_mpoly* a, const sg_mpoly* b, sg_mpoly** out) {
   return guard(ctx, [&] {
     SG_REQUIRE(a && b && out, "null argument");
-    SG_HIP(hipSetDevice(ctx->device));
+    if (ctx) SG_HIP(hipSetDevice(ctx->device));  // ctx == NULL: host-only (small products)
     *out = wrapm(mp_mul(ctx, a->m, b->m));
   });
 }
@@ -317,7 +317,7 @@ extern "C" int sg_mpoly_mul(sg_ctx* ctx, const sg_mpoly* a, const sg_mpoly* b, s
 extern "C" int sg_mpoly_pow(sg_ctx* ctx, const sg_mpoly* a, sg_fe exponent, sg_mpoly** out) {
   return guard(ctx, [&] {
     SG_REQUIRE(a && out, "null argument");
-    SG_HIP(hipSetDevice(ctx->device));
+    if (ctx) SG_HIP(hipSetDevice(ctx->device));  // ctx == NULL: host-only (small products)
     *out = wrapm(mp_pow(ctx, a->m, ((unsigned __int128)exponent.hi << 64) | exponent.lo));
   });
 }

@@ -490,7 +490,7 @@ constexpr uint64_t kHostDomainMax = 1024;
 extern "C" int sg_poly_create(sg_ctx* ctx, const sg_fe* coeffs, size_t len, sg_poly** out) {
   return guard(ctx, [&] {
     SG_REQUIRE(out && (coeffs || !len), "null argument");
-    SG_HIP(hipSetDevice(ctx->device));
+    set_device(ctx);
     check_canonical(coeffs, len, "coefficients");
     DPoly d = dpoly_upload(ctx, reinterpret_cast<const fe*>(coeffs), len);
     SG_HIP(hipStreamSynchronize(ctx->stream));
@@ -501,7 +501,7 @@ extern "C" int sg_poly_create(sg_ctx* ctx, const sg_fe* coeffs, size_t len, sg_p
 extern "C" int sg_poly_create_dev(sg_ctx* ctx, const sg_fe* d_coeffs, size_t len, sg_poly** out) {
   return guard(ctx, [&] {
     SG_REQUIRE(out && (d_coeffs || !len), "null argument");
-    SG_HIP(hipSetDevice(ctx->device));
+    set_device(ctx);
     DPoly d = dpoly_copy(ctx, reinterpret_cast<const fe*>(d_coeffs), len);
     SG_HIP(hipStreamSynchronize(ctx->stream));
     *out = wrap(std::move(d));
@@ -516,7 +516,7 @@ extern "C" const sg_fe* sg_poly_data_dev(const sg_poly* p) {
 extern "C" int sg_poly_read(sg_ctx* ctx, const sg_poly* p, sg_fe* out) {
   return guard(ctx, [&] {
     SG_REQUIRE(p && (out || !p->d.len), "null argument");
-    SG_HIP(hipSetDevice(ctx->device));
+    set_device(ctx);
     if (p->d.len)
       SG_HIP(hipMemcpyAsync(out, p->d.p(), p->d.len * sizeof(fe), hipMemcpyDeviceToHost, ctx->stream));
     SG_HIP(hipStreamSynchronize(ctx->stream));
@@ -526,7 +526,7 @@ extern "C" int sg_poly_read(sg_ctx* ctx, const sg_poly* p, sg_fe* out) {
 extern "C" int sg_poly_degree(sg_ctx* ctx, const sg_poly* p, int64_t* out) {
   return guard(ctx, [&] {
     SG_REQUIRE(p && out, "null argument");
-    SG_HIP(hipSetDevice(ctx->device));
+    set_device(ctx);
     *out = dev_degree(ctx, p->d.p(), p->d.len);
   });
 }
@@ -537,7 +537,7 @@ extern "C" int sg_fast_multiply(sg_ctx* ctx, sg_fe root, uint64_t root_order, co
                                 sg_poly** out) {
   return guard(ctx, [&] {
     SG_REQUIRE(lhs && rhs && out, "null argument");
-    SG_HIP(hipSetDevice(ctx->device));
+    set_device(ctx);
     DPoly r = fast_multiply_dev(ctx, to_fe(root), root_order, dptr(lhs), dlen(lhs), dptr(rhs), dlen(rhs));
     done(ctx);
     *out = wrap(std::move(r));
@@ -548,7 +548,7 @@ extern "C" int sg_fast_coset_divide(sg_ctx* ctx, sg_fe root, uint64_t root_order
                                     const sg_poly* rhs, sg_poly** out) {
   return guard(ctx, [&] {
     SG_REQUIRE(lhs && rhs && out, "null argument");
-    SG_HIP(hipSetDevice(ctx->device));
+    set_device(ctx);
     DPoly r = fast_coset_divide_dev(ctx, to_fe(root), root_order, to_fe(offset), dptr(lhs), dlen(lhs), dptr(rhs),
                                     dlen(rhs));
     done(ctx);
@@ -560,7 +560,7 @@ extern "C" int sg_fast_zerofier(sg_ctx* ctx, sg_fe root, uint64_t root_order, co
                                 sg_poly** out) {
   return guard(ctx, [&] {
     SG_REQUIRE(out && (domain || !n), "null argument");
-    SG_HIP(hipSetDevice(ctx->device));
+    set_device(ctx);
     check_canonical(domain, n, "domain");
     const fe r = to_fe(root);
     check_root(r, root_order);
@@ -583,7 +583,7 @@ extern "C" int sg_fast_interpolate_domain(sg_ctx* ctx, sg_fe root, uint64_t root
                                           const sg_fe* values, size_t n, sg_poly** out) {
   return guard(ctx, [&] {
     SG_REQUIRE(out && ((domain && values) || !n), "null argument");
-    SG_HIP(hipSetDevice(ctx->device));
+    set_device(ctx);
     check_canonical(domain, n, "domain");
     check_canonical(values, n, "values");
     const fe r = to_fe(root);
@@ -609,7 +609,7 @@ extern "C" int sg_fast_interpolate_domain(sg_ctx* ctx, sg_fe root, uint64_t root
 extern "C" int sg_fast_zerofier_geometric(sg_ctx* ctx, sg_fe root, uint64_t root_order, size_t n, sg_poly** out) {
   return guard(ctx, [&] {
     SG_REQUIRE(out, "null argument");
-    SG_HIP(hipSetDevice(ctx->device));
+    set_device(ctx);
     check_root(to_fe(root), root_order);
     DPoly z = zerofier_geometric_dev(ctx, to_fe(root), root_order, n);
     done(ctx);
@@ -621,7 +621,7 @@ extern "C" int sg_fast_interpolate_geometric_dev(sg_ctx* ctx, sg_fe root, uint64
                                                  size_t n, sg_poly** out) {
   return guard(ctx, [&] {
     SG_REQUIRE(out && (d_values || !n), "null argument");
-    SG_HIP(hipSetDevice(ctx->device));
+    set_device(ctx);
     check_root(to_fe(root), root_order);
     DPoly ip = interpolate_geometric_dev(ctx, to_fe(root), root_order, reinterpret_cast<const fe*>(d_values), n);
     done(ctx);

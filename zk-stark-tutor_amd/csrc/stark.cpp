@@ -763,8 +763,8 @@ extern "C" int sg_rescue_trace(sg_ctx* ctx, const sg_rescue* rp, sg_fe input, sg
 extern "C" int sg_rescue_transition_constraints(sg_ctx* ctx, const sg_rescue* rp, sg_fe omicron,
                                                 uint64_t omicron_domain_length, sg_mpoly** out) {
   return guard(ctx, [&] {
-    SG_REQUIRE(rp && out, "null argument");
-    SG_HIP(hipSetDevice(ctx->device));
+    SG_REQUIRE(ctx && rp && out, "a GPU context is required (interpolation on the device)");
+    set_device(ctx);
     std::vector<MPoly> tcs = rescue_transition_constraints(ctx, *rp, to_fe(omicron), omicron_domain_length);
     SG_HIP(hipStreamSynchronize(ctx->stream));
     check_div_zero(ctx);
@@ -855,9 +855,9 @@ extern "C" int sg_stark_prove(sg_ctx* ctx, const sg_stark* st, const sg_fe* trac
                               const sg_fe* trace_randomizers, const sg_fe* randomizer_coeffs, size_t n_rc,
                               const sg_proof_stream* ps) {
   return guard(ctx, [&] {
-    SG_REQUIRE(st && (trace || !rows) && (tcs || !ntcs) && (boundary || !nb), "null argument");
+    SG_REQUIRE(ctx && st && (trace || !rows) && (tcs || !ntcs) && (boundary || !nb), "null argument");
     SG_REQUIRE(trace_randomizers || !st->num_randomizers, "null argument");
-    SG_HIP(hipSetDevice(ctx->device));
+    set_device(ctx);
     check_canonical(trace, rows * st->m, "trace");
     check_canonical(trace_randomizers, st->num_randomizers * st->m, "trace randomizers");
     check_canonical(randomizer_coeffs, n_rc, "randomizer coefficients");
@@ -880,9 +880,9 @@ extern "C" int sg_stark_prove_dev(sg_ctx* ctx, const sg_stark* st, const sg_fe* 
                                   const sg_fe* d_trace_randomizers, const sg_fe* d_randomizer_coeffs, size_t n_rc,
                                   const sg_proof_stream* ps) {
   return guard(ctx, [&] {
-    SG_REQUIRE(st && (d_trace || !rows) && (tcs || !ntcs) && (boundary || !nb), "null argument");
+    SG_REQUIRE(ctx && st && (d_trace || !rows) && (tcs || !ntcs) && (boundary || !nb), "null argument");
     SG_REQUIRE(d_trace_randomizers || !st->num_randomizers, "null argument");
-    SG_HIP(hipSetDevice(ctx->device));
+    set_device(ctx);
     std::vector<Boundary> bnd;
     for (size_t i = 0; i < nb; ++i) {
       check_canonical(&boundary[i].value, 1, "boundary value");

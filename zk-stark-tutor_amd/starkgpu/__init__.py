@@ -2,7 +2,7 @@
 "Anatomy of a STARK" prover (SpekalsG3/zk-stark-tutor), behind the C ABI in
 include/stark_gpu.h.  See DESIGN.md."""
 from ._lib import LIB_PATH, StarkGpuError, lib
-from .api import (CODEWORD, FIELD_PRIME, LEAFS, PATH, PROOF_BYTES, ROOT, VALUE, CallbackProofStream, Context,
+from .api import (CODEWORD, FIELD_PRIME, LEAFS, PATH, PROOF_BYTES, ROOT, VALUE, CallbackProofStream, Context, HostContext,
                   DeviceTree, FRI, IndependentProofStream, MerkleRoot, SignatureProofStream, decode_object,
                   encode_object, fast_coset_evaluate, fast_coset_evaluate_batch_dev,
                   fast_coset_evaluate_dev, fe_array, fe_inverse, fe_mul, fe_pow,

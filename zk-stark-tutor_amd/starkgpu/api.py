@@ -144,6 +144,20 @@ class Context:
             pass
 
 
+class HostContext(Context):
+    """No device: a NULL context for the host-only entry points (Rescue-Prime constants /
+    hash / trace, MPolynomial arithmetic on small polynomials, Stark sizing and degree
+    bounds).  Device entry points reject it with "a GPU context is required"."""
+
+    def __init__(self):  # noqa: super().__init__ would open a device
+        self._lib = lib()
+        self.handle = None
+        self.device = -1
+
+    def close(self) -> None:
+        pass
+
+
 def _ctx(ctx: Optional[Context]) -> Context:
     return ctx if ctx is not None else Context.default()
 
