@@ -48,6 +48,7 @@ HBM_PEAK_GBS = 8000.0
 # PMC HBM bytes of this workload's kernels (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes on
 # `bench.py --steps 3 --warmup 1 --no-side`, tools/_gpu_full_e2e.sh + tools/pmc_traffic.py)
 PMC_TRAFFIC_FILE = "r01_pmc_traffic_e2e.json"
+PMC_VALU_FILE = "r01_pmc_valu_e2e.json"  # SQ_INSTS_VALU pass (tools/_pmc_valu_e2e.sh + tools/pmc_valu.py)
 
 
 def synthetic_fe(seed: int, tag: bytes, n: int) -> np.ndarray:
@@ -489,6 +490,20 @@ def main():
         if pmc:
             traffic = int(pmc["hbm_bytes_per_launch"])
             traffic_src = f"profiles/{PMC_TRAFFIC_FILE} (FETCH_SIZE x2 + WRITE_SIZE per launch, same workload)"
+    # VALU issue of the dominant kernel (rocprofv3 SQ_INSTS_VALU pass on this workload): the
+    # kernels are integer-VALU-bound, so this is the roof that actually binds them
+    valu = None
+    valu_file = os.path.join(ROOT, "profiles", PMC_VALU_FILE)
+    if os.path.exists(valu_file) and args.log_trace == LOG_TRACE:
+        vk = json.load(open(valu_file))["kernels"].get(name)
+        if vk:
+            inst = vk["valu_wave_instr_per_launch"] * st["launches"] / max(st["launches"], 1)
+            live = inst / (st["ms"] / st["launches"] * 1e-3)
+            valu = {"unit": "wave64 VALU instr/s", "instr_per_launch": int(inst),
+                    "achieved": round(live, -6), "peak": round(vk["peak_wave_instr_per_s"], -6),
+                    "frac": round(live / vk["peak_wave_instr_per_s"], 4), "clock_ghz": round(vk["clock_ghz"], 3),
+                    "source": f"profiles/{PMC_VALU_FILE} (SQ_INSTS_VALU per launch; roof = 1 instr/SIMD/4 clk, "
+                              f"1024 SIMDs, measured clock); achieved uses the live launch time"}
     phases = {k: {"launches": v["launches"], "ms_per_step": round(v["ms"], 4),
                   "GBps": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["ms"] > 0 else None}
               for k, v in sorted(breakdown.items(), key=lambda kv: -kv[1]["ms"])}
@@ -522,7 +537,9 @@ def main():
                      "avg_launch_ms": round(st["ms"] / st["launches"], 4),
                      "launches": st["launches"],
                      "alg_bytes_per_launch": int(st["bytes"] / st["launches"]),
-                     "note": "integer-VALU-bound (BLAKE2b / 128-bit Montgomery); see DESIGN.md section 4"},
+                     "note": "integer-VALU-bound (BLAKE2b / 128-bit Montgomery): see roofline.valu and DESIGN.md "
+                             "section 4",
+                     "valu": valu},
         "kernels_one_step": phases,  # every launch timed, last warmup step
         "host_phases_ms": {k: round(v / args.steps * 1e3, 3) for k, v in host_phases.items()},
     }
