@@ -24,7 +24,8 @@ def main():
     for _ in range(2):
         sg.ntt_dev(w, x.data_ptr(), n, y.data_ptr(), ctx=ctx)
         sg.intt_dev(w, y.data_ptr(), n, z.data_ptr(), ctx=ctx)
-    assert torch.equal(x, z)
+    if not os.environ.get("SG_NO_CHECK"):
+        assert torch.equal(x, z)
     ctx.profile(True)
     it = 5
     t0 = time.perf_counter()

@@ -8,6 +8,7 @@
 #include "host_field.hpp"
 #include "internal.hpp"
 #include "mpoly.hpp"
+#include "poly_kernels.hpp"
 
 namespace sg {
 
@@ -201,6 +202,7 @@ const MPolyDevice& mp_device(sg_ctx* ctx, const MPoly& a) {
     SG_HIP(hipMalloc(&p, v.size() * sizeof(fe)));
     d->ptr.push_back(p);
     d->len.push_back(v.size());
+    d->small.push_back(v.size() <= (size_t)kSmallPolyMax ? v : HPoly{});
     SG_HIP(hipMemcpyAsync(p, v.data(), v.size() * sizeof(fe), hipMemcpyHostToDevice, ctx->stream));
     SG_HIP(hipStreamSynchronize(ctx->stream));
   }

@@ -29,6 +29,7 @@ struct MPolyDevice {
   int device = -1;
   std::vector<void*> ptr;       // distinct x-polynomials up to a scalar (first non-zero coefficient 1)
   std::vector<uint64_t> len;    // their degree + 1
+  std::vector<HPoly> small;     // host copy of those with len <= kSmallPolyMax (else empty)
   std::vector<int32_t> qidx;    // per group (map order): index into ptr, -1 for an all-zero group
   std::vector<fe> scale;        // per group: x-polynomial = scale * ptr[qidx]
   ~MPolyDevice();

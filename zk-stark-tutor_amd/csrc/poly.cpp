@@ -31,12 +31,13 @@ namespace sg {
 namespace {
 inline fe one_m() { return to_mont(fe_one()); }
 inline bool fe_is_zero_h(const fe& a) { return (a.w[0] | a.w[1] | a.w[2] | a.w[3]) == 0; }
+}  // namespace
+
 // two-level Montgomery power tables of f for exponents < count
 void pow_tables2(sg_ctx* ctx, const fe& f, uint64_t count, const fe** A, const fe** B) {
   *A = ctx->pow_table(f, 4096);
   *B = ctx->pow_table(fe_pow(f, 4096), std::max<uint64_t>((count + 4095) / 4096, 1));
 }
-}  // namespace
 
 // ------------------------------------------------------------------ buffers
 

@@ -33,6 +33,8 @@ int64_t dev_degree(sg_ctx* ctx, const fe* d, uint64_t len);
 fe root_of_order(uint64_t n);
 // ntt_arithmetics.rs:11-24 assertions
 void check_root(const fe& root, uint64_t root_order);
+// Montgomery(f^e) = A[e & 4095] * B[e >> 12] for e < count (cached per context)
+void pow_tables2(sg_ctx* ctx, const fe& f, uint64_t count, const fe** A, const fe** B);
 
 // size-2^logn transforms of the first n_in entries (zero beyond), optional offset^i input scale
 void ntt_sized(sg_ctx* ctx, const fe& root, const fe* in, uint64_t n_in, int logn, fe* out,

@@ -26,16 +26,29 @@ __device__ __forceinline__ fe fe_one_c() { return fe_make(1, 0); }
 __device__ __forceinline__ bool fe_is_zero(const fe& a) { return (a.w[0] | a.w[1] | a.w[2] | a.w[3]) == 0; }
 
 // x^(p-2) * R for x_m = x R (Montgomery in, Montgomery out): Fermat inverse.
-// p - 2 = 0xCB7FFFFF_FFFFFFFF_FFFFFFFF_FFFFFFFF: 128-bit left-to-right square-and-multiply.
+// p - 2 = 407 * 2^119 - 1 = (203 << 120) + (0 << 119) + (2^119 - 1): x^203, one
+// squaring for the zero bit, then the 119 trailing ones as 17 windows of 7 bits
+// (7 squarings and one product by x^127 each): 158 products instead of 252 for
+// bitwise square-and-multiply.
 __device__ __forceinline__ fe mont_inv(const fe& xm, const fe& one_m) {
-  fe acc = one_m;
-  const uint32_t e3 = P3 - 1u;  // top limb of p - 2 (low limbs: 0xFFFFFFFF.. except p0 - 2 wraps)
+  (void)one_m;
+  fe x3 = mont_mul(mont_mul(xm, xm), xm);
+  fe w = x3;  // x^(2^k - 1), k = 2..7
+#pragma unroll
+  for (int k = 3; k <= 7; ++k) w = mont_mul(mont_mul(w, w), xm);
+  // x^203: 203 = 0b11001011, from x^3 = 0b11
+  fe acc = mont_mul(x3, x3);                  // x^6
+  acc = mont_mul(acc, acc);                   // x^12
+  acc = mont_mul(mont_mul(acc, acc), xm);     // x^25
+  acc = mont_mul(acc, acc);                   // x^50
+  acc = mont_mul(mont_mul(acc, acc), xm);     // x^101
+  acc = mont_mul(mont_mul(acc, acc), xm);     // x^203
+  acc = mont_mul(acc, acc);                   // x^406
 #pragma unroll 1
-  for (int i = 127; i >= 0; --i) {
-    acc = mont_mul(acc, acc);
-    uint32_t limb = i >= 96 ? e3 : 0xFFFFFFFFu;
-    // p - 2 = (P3 << 96) + 2^96 - 1: limb 3 = P3 - 1, limbs 0..2 all ones
-    if ((limb >> (i & 31)) & 1u) acc = mont_mul(acc, xm);
+  for (int win = 0; win < 17; ++win) {
+#pragma unroll
+    for (int s = 0; s < 7; ++s) acc = mont_mul(acc, acc);
+    acc = mont_mul(acc, w);
   }
   return acc;
 }
@@ -100,7 +113,7 @@ __global__ __launch_bounds__(kBlock) void k_batch_div(fe* __restrict__ out, cons
   fe pre[K];
   fe acc = one_m;
   bool zero = false;
-#pragma unroll
+#pragma clang loop unroll(full)
   for (int k = 0; k < K; ++k) {
     uint64_t i = t + k * S;
     fe bm = one_m;
@@ -114,7 +127,7 @@ __global__ __launch_bounds__(kBlock) void k_batch_div(fe* __restrict__ out, cons
   }
   if (zero) __hip_atomic_fetch_or(zero_flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   fe inv = mont_inv(acc, one_m);  // (prod b)^-1 R
-#pragma unroll
+#pragma clang loop unroll(full)
   for (int k = K - 1; k >= 0; --k) {
     uint64_t i = t + k * S;
     if (i < n) {
@@ -239,34 +252,58 @@ __global__ __launch_bounds__(kBlock) void k_last_nonzero(const fe* __restrict__ 
 // out[y] = sum_g s_g Q_q(g)[y] * prod_j V_j[y]^exps[g][j]  (m_polynomial.rs:124-139 evaluated
 // pointwise on a coset: s_g Q_q(g) are the coset values of the x-polynomial of group g; groups
 // whose x-polynomials are proportional share one LDE).
+// sum_q Q_q(y) * sum_{g in q} scale_g prod_j V_j(y)^e_gj: groups sorted by their
+// distinct x-polynomial, so each point loads every value array once (the next Q is
+// prefetched while the current group sum is formed) and a group costs one product
+// per variable it holds.
+template <int NV>
 __global__ __launch_bounds__(kBlock) void k_air_eval(AirEvalArgs a) {
   for (uint64_t y = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; y < a.n; y += (uint64_t)gridDim.x * blockDim.x) {
-    fe vm[kAirMaxVars];
+    // V_j, V_j^2, V_j^3 once per point: the Rescue AIR's monomials have per-variable
+    // exponents <= alpha = 3
+    fe p1[NV], p2[NV], p3[NV];
 #pragma unroll
-    for (int j = 0; j < kAirMaxVars; ++j)
-      vm[j] = j < a.nvars ? mont_mul(ld_fe(a.V[j] + y), a.r2) : a.one_m;
-    fe acc = fe_zero();
-    for (int g = 0; g < a.ngroups; ++g) {
-      fe prod = mont_mul(ld_fe(a.Q[a.qidx[g]] + y), ld_fe(a.qscale + g));  // Montgomery(scale * Q)
-      const uint32_t* e = a.exps + g * a.nvars;
-      for (int j = 0; j < a.nvars; ++j) {
-        uint32_t ej = e[j];
-        if (!ej) continue;
-        fe pw = a.one_m;
-        fe base = vm[0];
+    for (int j = 0; j < NV; ++j) p1[j] = ld_fe(a.V[j] + ((y + a.vshift[j]) & (a.n - 1)));
+    fe qnext = ld_fe(a.Q[0] + y);
 #pragma unroll
-        for (int jj = 1; jj < kAirMaxVars; ++jj)
-          if (jj == j) base = vm[jj];
-        int top = 31 - __builtin_clz(ej);
-        for (int b = top; b >= 0; --b) {
-          pw = mont_mul(pw, pw);
-          if ((ej >> b) & 1u) pw = mont_mul(pw, base);
-        }
-        prod = mont_mul(prod, pw);
-      }
-      acc = fe_add(acc, prod);
+    for (int j = 0; j < NV; ++j) {
+      p1[j] = mont_mul(p1[j], a.r2);
+      p2[j] = mont_mul(p1[j], p1[j]);
+      p3[j] = mont_mul(p2[j], p1[j]);
     }
-    st_fe(a.out + y, mont_mul(acc, fe_one_c()));
+    fe acc = fe_zero();
+    for (int q = 0; q < a.nq; ++q) {
+      const fe qv = qnext;
+      if (q + 1 < a.nq) qnext = ld_fe(a.Q[q + 1] + y);
+      fe sum = fe_zero();  // Montgomery
+      for (uint32_t g = a.qstart[q]; g < a.qstart[q + 1]; ++g) {
+        fe term = ld_fe(a.qscale + g);  // Montgomery(scale)
+        const uint32_t* e = a.exps + g * NV;
+#pragma unroll
+        for (int j = 0; j < NV; ++j) {
+          const uint32_t ej = e[j];  // uniform across the wave
+          if (!ej) continue;
+          fe pw;
+          if (ej == 1) {
+            pw = p1[j];
+          } else if (ej == 2) {
+            pw = p2[j];
+          } else if (ej == 3) {
+            pw = p3[j];
+          } else {  // general exponent: square-and-multiply from V_j
+            pw = p1[j];
+            for (int b = 30 - __builtin_clz(ej); b >= 0; --b) {
+              pw = mont_mul(pw, pw);
+              if ((ej >> b) & 1u) pw = mont_mul(pw, p1[j]);
+            }
+          }
+          term = mont_mul(term, pw);
+        }
+        sum = fe_add(sum, term);
+      }
+      acc = fe_add(acc, mont_mul(qv, sum));  // canonical Q times Montgomery sum: canonical
+    }
+    st_fe(a.out + y, acc);
   }
 }
 
@@ -405,9 +442,19 @@ hipError_t launch_last_nonzero(const fe* a, uint64_t n, unsigned long long* last
 
 hipError_t launch_air_eval(const AirEvalArgs& a, hipStream_t s) {
   if (!a.n) return hipSuccess;
-  if (a.nvars > kAirMaxVars || a.nvars < 1) return hipErrorInvalidValue;
-  ProfScope ps("air_eval", 16 * a.n * (a.nvars + a.ngroups + 1), s);
-  hipLaunchKernelGGL(k_air_eval, dim3((unsigned)grid_for(a.n)), dim3(kBlock), 0, s, a);
+  if (a.nvars > kAirMaxVars || a.nvars < 1 || a.nq < 1 || (a.n & (a.n - 1))) return hipErrorInvalidValue;
+  ProfScope ps("air_eval", 16 * a.n * (a.nvars + a.nq + 1), s);
+  const dim3 grid((unsigned)grid_for(a.n));
+  switch (a.nvars) {
+    case 1: hipLaunchKernelGGL(k_air_eval<1>, grid, dim3(kBlock), 0, s, a); break;
+    case 2: hipLaunchKernelGGL(k_air_eval<2>, grid, dim3(kBlock), 0, s, a); break;
+    case 3: hipLaunchKernelGGL(k_air_eval<3>, grid, dim3(kBlock), 0, s, a); break;
+    case 4: hipLaunchKernelGGL(k_air_eval<4>, grid, dim3(kBlock), 0, s, a); break;
+    case 5: hipLaunchKernelGGL(k_air_eval<5>, grid, dim3(kBlock), 0, s, a); break;
+    case 6: hipLaunchKernelGGL(k_air_eval<6>, grid, dim3(kBlock), 0, s, a); break;
+    case 7: hipLaunchKernelGGL(k_air_eval<7>, grid, dim3(kBlock), 0, s, a); break;
+    default: hipLaunchKernelGGL(k_air_eval<8>, grid, dim3(kBlock), 0, s, a); break;
+  }
   return hipGetLastError();
 }
 

@@ -11,13 +11,15 @@ constexpr int kLinCombMaxTerms = 48;  // terms of one weighted combination
 
 struct AirEvalArgs {
   fe* out;
-  const fe* const* Q;     // device array of coset-value arrays (the distinct x-polynomials)
-  const uint32_t* qidx;   // device [ngroups]: group g's x-polynomial = qscale[g] * Q[qidx[g]]
-  const fe* qscale;       // device [ngroups]: Montgomery(Montgomery(scale)) = scale * R^2
+  const fe* const* Q;     // device array [nq] of coset-value arrays (the distinct x-polynomials)
+  const uint32_t* qstart; // device [nq + 1]: groups qstart[q] .. qstart[q+1]-1 have x-polynomial
+                          // qscale[g] * Q[q] (groups sorted by q)
+  const fe* qscale;       // device [ngroups]: Montgomery(scale)
   const fe* const* V;     // device array [nvars] of coset-value arrays (point variables 1..)
   const uint32_t* exps;   // device [ngroups][nvars]
-  int ngroups, nvars;
-  uint64_t n;
+  int ngroups, nvars, nq;
+  uint64_t n;             // a power of two
+  uint64_t vshift[kAirMaxVars];  // variable j at point y reads V[j][(y + vshift[j]) mod n]
   fe r2, one_m;
 };
 

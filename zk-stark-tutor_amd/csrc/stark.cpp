@@ -368,23 +368,38 @@ DPoly lincomb(sg_ctx* ctx, const std::vector<DevTerm>& terms) {
 }
 
 // point values on the coset offset * <w_L>: P_s(y) and P_s(omicron y) (the point
-// [x, P_s(x), P_s(omicron x)] of stark.rs:388-400), shared by every constraint
+// [x, P_s(x), P_s(omicron x)] of stark.rs:388-400), shared by every constraint.  When
+// omicron lies in <w_L> (its order divides L: omicron = w_L^(L / order)), P_s(omicron y)
+// at y = offset w_L^i is P_s at offset w_L^(i + L / order): the same values rotated, read
+// with an index shift instead of a second transform.
 struct AirCoset {
   uint64_t L = 0;
-  std::vector<DPoly> V;
+  std::vector<DPoly> V;         // distinct value arrays
+  std::vector<int> var;         // point variable j -> index into V
+  std::vector<uint64_t> shift;  // point variable j reads V[var[j]][(i + shift[j]) mod L]
 };
 
 AirCoset air_coset(sg_ctx* ctx, const std::vector<DPoly>& trace_polys, uint64_t L, const fe& omicron,
-                   const fe& offset) {
+                   const fe& offset, uint64_t omicron_order) {
   AirCoset c;
   c.L = L;
+  const fe wL = root_of_order(L);
+  const bool rotate = omicron_order <= L && fe_eq(fe_pow(wL, L / omicron_order), omicron);
   const fe off_omicron = fe_mul(offset, omicron);
   for (int pass = 0; pass < 2; ++pass)
-    for (auto& tp : trace_polys) {
+    for (size_t s = 0; s < trace_polys.size(); ++s) {
+      if (pass && rotate) {
+        c.var.push_back((int)s);
+        c.shift.push_back(L / omicron_order);
+        continue;
+      }
+      const DPoly& tp = trace_polys[s];
       c.V.push_back(dpoly_alloc(ctx, L));
       const fe* in = tp.p();
       fe* out = c.V.back().p();
-      coset_evaluate_batch(ctx, root_of_order(L), L, pass ? off_omicron : offset, &in, tp.len, &out, 1);
+      coset_evaluate_batch(ctx, wL, L, pass ? off_omicron : offset, &in, tp.len, &out, 1);
+      c.var.push_back((int)c.V.size() - 1);
+      c.shift.push_back(0);
     }
   return c;
 }
@@ -392,7 +407,7 @@ AirCoset air_coset(sg_ctx* ctx, const std::vector<DPoly>& trace_polys, uint64_t 
 // values on the coset of the polynomial evaluate_symbolic returns (m_polynomial.rs:124-139)
 DPoly transition_values(sg_ctx* ctx, const MPoly& tc, const AirCoset& co, const fe& offset) {
   const uint64_t L = co.L;
-  const int nv = (int)co.V.size();
+  const int nv = (int)co.var.size();
   SG_REQUIRE(tc.nvars <= 1 + (uint32_t)nv, "transition constraint has more variables than the point");
   SG_REQUIRE(nv <= kAirMaxVars, "at most 4 registers are supported by the AIR kernel");
   // distinct group x-polynomials (device-resident, uploaded once per constraint) on the coset
@@ -400,46 +415,74 @@ DPoly transition_values(sg_ctx* ctx, const MPoly& tc, const AirCoset& co, const 
   std::vector<DPoly> Q;
   for (size_t q = 0; q < xd.ptr.size(); ++q) {
     Q.push_back(dpoly_alloc(ctx, L));
-    const fe* in = reinterpret_cast<const fe*>(xd.ptr[q]);
     fe* out = Q.back().p();
+    if (!xd.small[q].empty()) {  // a tiny polynomial (e.g. the constant 1): Horner at offset w_L^k
+      SmallPoly sp{};
+      sp.len = (int)xd.small[q].size();
+      for (int i = 0; i < sp.len; ++i) sp.c[i] = xd.small[q][(size_t)i];
+      const fe *A, *B;
+      pow_tables2(ctx, root_of_order(L), L, &A, &B);
+      SG_HIP(launch_eval_small(out, sp, L, A, B, to_mont(offset), ctx->stream));
+      continue;
+    }
+    const fe* in = reinterpret_cast<const fe*>(xd.ptr[q]);
     coset_evaluate_batch(ctx, root_of_order(L), L, offset, &in, xd.len[q], &out, 1);
   }
-  std::vector<uint32_t> exps, qidx;
+  // non-zero groups bucketed by their distinct x-polynomial (an all-zero group adds nothing:
+  // its products are zero polynomials)
+  const size_t nq = xd.ptr.size();
+  std::vector<std::vector<size_t>> by_q(nq);
+  std::vector<const std::vector<uint32_t>*> keys;
+  for (auto it = tc.g.begin(); it != tc.g.end(); ++it) keys.push_back(&it->first);
+  for (size_t gi = 0; gi < keys.size(); ++gi)
+    if (xd.qidx[gi] >= 0) by_q[(size_t)xd.qidx[gi]].push_back(gi);
+  std::vector<uint32_t> exps, qstart{0};
   std::vector<fe> qscale;
-  size_t gi = 0;
-  for (auto it = tc.g.begin(); it != tc.g.end(); ++it, ++gi) {
-    if (xd.qidx[gi] < 0) continue;  // an all-zero group adds nothing (its products are zero polynomials)
-    qidx.push_back((uint32_t)xd.qidx[gi]);
-    qscale.push_back(to_mont(to_mont(xd.scale[gi])));
-    for (int j = 0; j < nv; ++j) exps.push_back(j < (int)it->first.size() ? it->first[j] : 0u);
+  for (size_t q = 0; q < nq; ++q) {
+    for (size_t gi : by_q[q]) {
+      qscale.push_back(to_mont(xd.scale[gi]));
+      for (int j = 0; j < nv; ++j) exps.push_back(j < (int)keys[gi]->size() ? (*keys[gi])[j] : 0u);
+    }
+    qstart.push_back((uint32_t)qscale.size());
   }
   DPoly vals = dpoly_alloc(ctx, L);
-  if (qidx.empty()) {
+  if (qscale.empty()) {
     SG_HIP(hipMemsetAsync(vals.p(), 0, L * sizeof(fe), ctx->stream));
     return vals;
   }
+  // one upload of the tables: [Q pointers][V pointers][qscale][qstart][exps]
+  std::vector<uint8_t> tab;
+  auto put = [&](const void* p, size_t bytes) {
+    size_t o = (tab.size() + 15) & ~(size_t)15;
+    tab.resize(o + bytes);
+    memcpy(tab.data() + o, p, bytes);
+    return o;
+  };
   std::vector<const fe*> qp, vp;
   for (auto& q : Q) qp.push_back(q.p());
-  for (auto& v : co.V) vp.push_back(v.p());
-  DevBuf dq(ctx, qp.size() * sizeof(void*)), dv(ctx, vp.size() * sizeof(void*)), de(ctx, exps.size() * 4);
-  DevBuf di(ctx, qidx.size() * 4), ds(ctx, qscale.size() * sizeof(fe));
-  SG_HIP(hipMemcpyAsync(dq.get(), qp.data(), qp.size() * sizeof(void*), hipMemcpyHostToDevice, ctx->stream));
-  SG_HIP(hipMemcpyAsync(dv.get(), vp.data(), vp.size() * sizeof(void*), hipMemcpyHostToDevice, ctx->stream));
-  SG_HIP(hipMemcpyAsync(de.get(), exps.data(), exps.size() * 4, hipMemcpyHostToDevice, ctx->stream));
-  SG_HIP(hipMemcpyAsync(di.get(), qidx.data(), qidx.size() * 4, hipMemcpyHostToDevice, ctx->stream));
-  SG_HIP(hipMemcpyAsync(ds.get(), qscale.data(), qscale.size() * sizeof(fe), hipMemcpyHostToDevice, ctx->stream));
+  for (int j = 0; j < nv; ++j) vp.push_back(co.V[co.var[j]].p());
+  const size_t oq = put(qp.data(), qp.size() * sizeof(void*));
+  const size_t ov = put(vp.data(), vp.size() * sizeof(void*));
+  const size_t os = put(qscale.data(), qscale.size() * sizeof(fe));
+  const size_t ot = put(qstart.data(), qstart.size() * 4);
+  const size_t oe = put(exps.data(), exps.size() * 4);
+  DevBuf dt(ctx, tab.size());
+  SG_HIP(hipMemcpyAsync(dt.get(), tab.data(), tab.size(), hipMemcpyHostToDevice, ctx->stream));
+  uint8_t* base = dt.as<uint8_t>();
   AirEvalArgs a{};
   a.out = vals.p();
-  a.Q = dq.as<const fe*>();
-  a.qidx = di.as<uint32_t>();
-  a.qscale = ds.as<fe>();
-  a.V = dv.as<const fe*>();
-  a.exps = de.as<uint32_t>();
-  a.ngroups = (int)qidx.size();
+  a.Q = reinterpret_cast<const fe* const*>(base + oq);
+  a.V = reinterpret_cast<const fe* const*>(base + ov);
+  a.qscale = reinterpret_cast<const fe*>(base + os);
+  a.qstart = reinterpret_cast<const uint32_t*>(base + ot);
+  a.exps = reinterpret_cast<const uint32_t*>(base + oe);
+  a.ngroups = (int)qscale.size();
   a.nvars = nv;
+  a.nq = (int)nq;
   a.n = L;
   a.r2 = fe_r2();
   a.one_m = to_mont(fe_one());
+  for (int j = 0; j < nv; ++j) a.vshift[j] = co.shift[j];
   SG_HIP(launch_air_eval(a, ctx->stream));
   SG_HIP(hipStreamSynchronize(ctx->stream));  // pointer tables return to the pool
   return vals;
@@ -568,7 +611,7 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
     const uint64_t len = symbolic_degree_bound(*tc, Tp - 1) + 1;
     const uint64_t L = next_pow2(len);
     auto cit = cosets.find(L);
-    if (cit == cosets.end()) cit = cosets.emplace(L, air_coset(ctx, trace_polys, L, st.omicron, g)).first;
+    if (cit == cosets.end()) cit = cosets.emplace(L, air_coset(ctx, trace_polys, L, st.omicron, g, st.D)).first;
     DPoly vals = transition_values(ctx, *tc, cit->second, g);
     auto tz_values = [&](const DivPlan& pl) -> const fe* {
       auto zit = tz_ntt.find(pl.order);
