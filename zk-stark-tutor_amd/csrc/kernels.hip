@@ -108,6 +108,23 @@ __global__ void k_bitrev_gather(GatherArgs ga, uint64_t n_in, int logn, const fe
 
 // ------------------------------------------------------------- NTT passes
 
+// An LDS slot of one element, 16-byte aligned so every tile access is one
+// ds_read_b128 / ds_write_b128 (fe itself is 4-byte aligned: the compiler would
+// split it into two ds_read2_b32, twice the LDS cycles and 4-way bank conflicts
+// on the C = 16-column tiles that b128 banking serves conflict-free).
+struct alignas(16) fe_lds {
+  uint32_t w[4];
+  __device__ __forceinline__ operator fe() const {
+    const uint4 v = *reinterpret_cast<const uint4*>(w);
+    fe r = {{v.x, v.y, v.z, v.w}};
+    return r;
+  }
+  __device__ __forceinline__ fe_lds& operator=(const fe& a) {
+    *reinterpret_cast<uint4*>(w) = make_uint4(a.w[0], a.w[1], a.w[2], a.w[3]);
+    return *this;
+  }
+};
+
 struct PassArgs {
   fe* data[kMaxBatch];  // one transform per blockIdx.y
   const fe* tw;        // stage-major twiddles (see ntt_stage_twiddles), Montgomery form
@@ -122,7 +139,7 @@ struct PassArgs {
 // COLK: the tile's columns are consecutive low index bits (they enter the twiddle
 // index k); false when the columns are independent transforms' tiles (first pass).
 template <int R, bool COLK = true>
-__device__ __forceinline__ void radix_step(fe* lds, const PassArgs& a, int t, uint64_t lowbase) {
+__device__ __forceinline__ void radix_step(fe_lds* lds, const PassArgs& a, int t, uint64_t lowbase) {
   const int logC = a.logC;
   const uint32_t C = 1u << logC;
   const uint32_t groups = (1u << (a.L + logC)) >> R;
@@ -167,7 +184,7 @@ __device__ __forceinline__ void radix_step(fe* lds, const PassArgs& a, int t, ui
 #endif
 template <int TL>
 __global__ __launch_bounds__(256, SG_NTT_WPE) void k_ntt_pass(PassArgs a) {
-  extern __shared__ fe lds[];
+  extern __shared__ fe_lds lds[];
   const int logC = a.logC;
   const uint32_t C = 1u << logC;
   const uint32_t tile = 1u << (a.L + logC);
@@ -249,7 +266,7 @@ struct FirstArgs {
 
 template <int TL>
 __global__ __launch_bounds__(256, SG_NTT_WPE) void k_ntt_first(FirstArgs a) {
-  extern __shared__ fe lds[];
+  extern __shared__ fe_lds lds[];
   const int L = a.L, logC = a.logC, m = a.logn;
   const uint32_t C = 1u << logC;
   const int skip = a.skip < L ? a.skip : L;
