@@ -1,0 +1,10 @@
+# full GPU check of the current tree: parity suite, default bench, kernel stats of the E2E step
+set -e
+R=$GRAFT_REPO_ROOT
+cd $R
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pt.log 2>&1
+timeout -k 10 500 python bench.py > gpurun_out/bench.log 2>&1
+cd /tmp && export TMPDIR=/tmp
+rm -rf $R/gpurun_out/prof
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/prof -o run -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-side > $R/gpurun_out/prof.log 2>&1
