@@ -93,6 +93,56 @@ __host__ __device__ __forceinline__ fe fe_neg(const fe& a) {
   return fe_sub(fe_zero(), a);
 }
 
+// Lazy forms for the NTT butterflies: values anywhere in [0, 2^128) (< 2p), the
+// second operand canonical (a Montgomery product).  Only the 129th bit / the
+// borrow is corrected, by adding or subtracting p = 1 + (P3 << 96) under one
+// mask: 9 instructions instead of the 13 of a full reduction.  The residue is
+// the same, so a transform that canonicalizes on its last store is bit-exact.
+//   a + b  < 2^128 + p: on carry subtract p  -> [2^128 - p, 2^128)
+//   a - b >= -p:        on borrow add p      -> [0, p)
+__host__ __device__ __forceinline__ fe fe_add_lazy(const fe& a, const fe& b) {
+  unsigned c, g;
+  uint32_t s0 = __builtin_addc(a.w[0], b.w[0], 0u, &c);
+  uint32_t s1 = __builtin_addc(a.w[1], b.w[1], c, &c);
+  uint32_t s2 = __builtin_addc(a.w[2], b.w[2], c, &c);
+  uint32_t s3 = __builtin_addc(a.w[3], b.w[3], c, &c);
+  // a + b - p = (a + b - 2^128) + (2^128 - p): add 2^128 - p under the carry mask
+  const uint32_t m = c ? 0xFFFFFFFFu : 0u;
+  const uint32_t m3 = c ? SG_NEG_P3 : 0u;
+  fe r;
+  r.w[0] = __builtin_addc(s0, m, 0u, &g);
+  r.w[1] = __builtin_addc(s1, m, g, &g);
+  r.w[2] = __builtin_addc(s2, m, g, &g);
+  r.w[3] = __builtin_addc(s3, m3, g, &g);
+  return r;
+}
+
+__host__ __device__ __forceinline__ fe fe_sub_lazy(const fe& a, const fe& b) {
+  unsigned br, c;
+  uint32_t d0 = __builtin_subc(a.w[0], b.w[0], 0u, &br);
+  uint32_t d1 = __builtin_subc(a.w[1], b.w[1], br, &br);
+  uint32_t d2 = __builtin_subc(a.w[2], b.w[2], br, &br);
+  uint32_t d3 = __builtin_subc(a.w[3], b.w[3], br, &br);
+  const uint32_t m3 = br ? P3 : 0u;
+  fe r;
+  r.w[0] = __builtin_addc(d0, 0u, br, &c);
+  r.w[1] = __builtin_addc(d1, 0u, c, &c);
+  r.w[2] = __builtin_addc(d2, 0u, c, &c);
+  r.w[3] = __builtin_addc(d3, m3, c, &c);
+  return r;
+}
+
+// [0, 2^128) -> [0, p): subtract p once if a >= p
+__host__ __device__ __forceinline__ fe fe_canon(const fe& a) {
+  unsigned g;
+  uint32_t d0 = __builtin_addc(a.w[0], 0xFFFFFFFFu, 0u, &g);
+  uint32_t d1 = __builtin_addc(a.w[1], 0xFFFFFFFFu, g, &g);
+  uint32_t d2 = __builtin_addc(a.w[2], 0xFFFFFFFFu, g, &g);
+  uint32_t d3 = __builtin_addc(a.w[3], 0x347FFFFFu, g, &g);
+  fe r = {{g ? d0 : a.w[0], g ? d1 : a.w[1], g ? d2 : a.w[2], g ? d3 : a.w[3]}};
+  return r;
+}
+
 // ---------------------------------------------------------------------------
 // 32x32+64 -> 64 multiply-accumulate with carry-out into a 32-bit third word.
 #if defined(__HIP_DEVICE_COMPILE__)
@@ -101,11 +151,28 @@ __device__ __forceinline__ void mac3(uint32_t a, uint32_t b, uint64_t& acc, uint
   uint64_t cc;
   asm("v_mad_u64_u32 %0, %1, %3, %4, %5\n\t"
       "v_addc_co_u32 %2, %1, %2, 0, %1"
-      : "=&v"(r), "=&s"(cc), "+v"(acc2)
+      : "=v"(r), "=s"(cc), "+v"(acc2)
+      : "v"(a), "v"(b), "v"(acc));
+  acc = r;
+}
+// first product of a column: the carry-out initializes the third word
+// (one v_cndmask instead of zeroing it and adding the carry)
+__device__ __forceinline__ void mac3_first(uint32_t a, uint32_t b, uint64_t& acc, uint32_t& acc2) {
+  uint64_t r;
+  uint64_t cc;
+  asm("v_mad_u64_u32 %0, %1, %3, %4, %5\n\t"
+      "v_cndmask_b32_e64 %2, 0, 1, %1"
+      : "=v"(r), "=s"(cc), "=v"(acc2)
       : "v"(a), "v"(b), "v"(acc));
   acc = r;
 }
 #else
+__host__ inline void mac3_first(uint32_t a, uint32_t b, uint64_t& acc, uint32_t& acc2) {
+  uint64_t p = (uint64_t)a * b;
+  uint64_t s = acc + p;
+  acc2 = (s < p);
+  acc = s;
+}
 __host__ inline void mac3(uint32_t a, uint32_t b, uint64_t& acc, uint32_t& acc2) {
   uint64_t p = (uint64_t)a * b;
   uint64_t s = acc + p;
@@ -117,24 +184,23 @@ __host__ inline void mac3(uint32_t a, uint32_t b, uint64_t& acc, uint32_t& acc2)
 // 128x128 -> 256-bit product, product scanning (Comba) with a 96-bit column accumulator.
 __host__ __device__ __forceinline__ void mul_wide(const fe& a, const fe& b, uint32_t t[8]) {
   uint64_t acc = (uint64_t)a.w[0] * b.w[0];
-  uint32_t acc2 = 0;
+  uint32_t acc2;
 #define SG_COL_SHIFT(k)                                   \
   t[k] = (uint32_t)acc;                                   \
-  acc = (acc >> 32) | ((uint64_t)acc2 << 32);             \
-  acc2 = 0;
+  acc = (acc >> 32) | ((uint64_t)acc2 << 32);
   t[0] = (uint32_t)acc;
   acc >>= 32;
   acc += (uint64_t)a.w[0] * b.w[1];  // < 2^32 + (2^32-1)^2: no carry
-  mac3(a.w[1], b.w[0], acc, acc2);
+  mac3_first(a.w[1], b.w[0], acc, acc2);
   SG_COL_SHIFT(1)
-  mac3(a.w[0], b.w[2], acc, acc2); mac3(a.w[1], b.w[1], acc, acc2); mac3(a.w[2], b.w[0], acc, acc2);
+  mac3_first(a.w[0], b.w[2], acc, acc2); mac3(a.w[1], b.w[1], acc, acc2); mac3(a.w[2], b.w[0], acc, acc2);
   SG_COL_SHIFT(2)
-  mac3(a.w[0], b.w[3], acc, acc2); mac3(a.w[1], b.w[2], acc, acc2); mac3(a.w[2], b.w[1], acc, acc2);
+  mac3_first(a.w[0], b.w[3], acc, acc2); mac3(a.w[1], b.w[2], acc, acc2); mac3(a.w[2], b.w[1], acc, acc2);
   mac3(a.w[3], b.w[0], acc, acc2);
   SG_COL_SHIFT(3)
-  mac3(a.w[1], b.w[3], acc, acc2); mac3(a.w[2], b.w[2], acc, acc2); mac3(a.w[3], b.w[1], acc, acc2);
+  mac3_first(a.w[1], b.w[3], acc, acc2); mac3(a.w[2], b.w[2], acc, acc2); mac3(a.w[3], b.w[1], acc, acc2);
   SG_COL_SHIFT(4)
-  mac3(a.w[2], b.w[3], acc, acc2); mac3(a.w[3], b.w[2], acc, acc2);
+  mac3_first(a.w[2], b.w[3], acc, acc2); mac3(a.w[3], b.w[2], acc, acc2);
   t[5] = (uint32_t)acc;
   acc = (acc >> 32) | ((uint64_t)acc2 << 32);
   acc += (uint64_t)a.w[3] * b.w[3];  // the top column cannot overflow: T < 2^256

@@ -165,8 +165,8 @@ __device__ __forceinline__ void radix_step(fe_lds* lds, const PassArgs& a, int t
         fe w = ld_fe(a.tw + (((uint64_t)1 << (S - 1)) - 1) + k);
         fe o = mont_mul(x[m + (1 << u)], w);
         fe ev = x[m];
-        x[m] = fe_add(ev, o);
-        x[m + (1 << u)] = fe_sub(ev, o);
+        x[m] = fe_add_lazy(ev, o);  // tile values stay in [0, 2^128) until the last store
+        x[m + (1 << u)] = fe_sub_lazy(ev, o);
       }
     }
 #pragma unroll
@@ -220,6 +220,7 @@ __global__ __launch_bounds__(256, SG_NTT_WPE) void k_ntt_pass(PassArgs a) {
     else { radix_step<1>(lds, a, t, cb * C); t += 1; }
   }
   const bool post = a.post != nullptr;
+  const bool last = a.b0 + a.L == a.logn;  // the transform's last pass stores canonical values
   fe pc = post ? ld_fe(a.post) : fe_zero();
   if constexpr (TL > 0) {
     constexpr int PER = (1 << TL) / 256;
@@ -229,6 +230,7 @@ __global__ __launch_bounds__(256, SG_NTT_WPE) void k_ntt_pass(PassArgs a) {
       uint32_t g = l >> logC, c = l & (C - 1);
       fe v = lds[l];
       if (post) v = mont_mul(v, pc);
+      else if (last) v = fe_canon(v);
       st_fe(data + base + ((uint64_t)g << a.b0) + c, v);
     }
   } else {
@@ -236,6 +238,7 @@ __global__ __launch_bounds__(256, SG_NTT_WPE) void k_ntt_pass(PassArgs a) {
       uint32_t g = l >> logC, c = l & (C - 1);
       fe v = lds[l];
       if (post) v = mont_mul(v, pc);
+      else if (last) v = fe_canon(v);
       st_fe(data + base + ((uint64_t)g << a.b0) + c, v);
     }
   }
@@ -838,7 +841,11 @@ hipError_t launch_ntt_dit(fe* const* data, int batch, const fe* tw, int logn, co
     }
     return hipSuccess;
   }
+  // Balanced plan: as few passes as the tile allows (columns >= 8, i.e. 128-byte
+  // runs), then the stages spread evenly, e.g. 2^25 after a 9-stage first pass
+  // runs 8 + 8 instead of 7 + 7 + 2 (a whole HBM round trip for two stages).
   int b0 = first_b0;
+  int pi = 0;
   while (b0 < logn) {
     PassArgs a;
     for (int b = 0; b < kMaxBatch; ++b) a.data[b] = b < np ? data[b] : nullptr;
@@ -847,8 +854,9 @@ hipError_t launch_ntt_dit(fe* const* data, int batch, const fe* tw, int logn, co
     a.logn = logn;
     a.b0 = b0;
     int rem = logn - b0;
-    int lc_min = b0 < 4 ? b0 : 4;
-    a.L = rem < tile_log - lc_min ? rem : tile_log - lc_min;
+    int lmax = tile_log - (b0 < 3 ? b0 : 3);
+    int passes = (rem + lmax - 1) / lmax;
+    a.L = (rem + passes - 1) / passes;
     a.logC = b0 < tile_log - a.L ? b0 : tile_log - a.L;
     a.post = (b0 + a.L == logn) ? post : nullptr;
     uint64_t tile = (uint64_t)1 << (a.L + a.logC);
@@ -856,9 +864,8 @@ hipError_t launch_ntt_dit(fe* const* data, int batch, const fe* tw, int logn, co
     unsigned threads = tile >= 2048 ? 256 : (unsigned)(tile / 8 > 64 ? tile / 8 : 64);
     size_t lds = tile * sizeof(fe);
     static const char* names[] = {"ntt_pass1", "ntt_pass2", "ntt_pass3", "ntt_pass4", "ntt_pass5"};
-    int pi = 0;
-    for (int bb = first_b0, q = 0; bb < b0; ++q) { int r2 = logn - bb; int lm = bb < 4 ? bb : 4; bb += r2 < tile_log - lm ? r2 : tile_log - lm; pi = q + 1; }
     ProfScope ps(names[pi < 4 ? pi : 4], batch * 32 * ((uint64_t)1 << logn), s);
+    ++pi;
     dim3 grid((unsigned)ntiles, batch);
     if (tile == 4096 && threads == 256)
       hipLaunchKernelGGL(k_ntt_pass<12>, grid, dim3(256), lds, s, a);
