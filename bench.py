@@ -94,6 +94,8 @@ class ProveWorkload:
         stream = sg.IndependentProofStream()
         self.stark.prove_dev(self.trace.data_ptr(), self.rows, self.air, self.boundary, stream,
                              self.trace_rand.data_ptr(), self.rcoef.data_ptr(), self.nrc)
+        # Stark::prove returns the serialized proof (stark.rs:562): part of the step
+        self.last_proof_bytes = stream.digest()
         self.last_proof = stream
         if phases is not None:
             phases["prove"] = phases.get("prove", 0.0) + (time.perf_counter() - t0)

@@ -200,18 +200,26 @@ extern "C" int sg_ctx_create(int device, sg_ctx** out) {
   }
   void* pinned = nullptr;
   void* pinned_dev = nullptr;
-  // 4 root slots (64 B) + 4 ready flags (u64) + the division zero flag (u32, padded), host-coherent
-  if (hipHostMalloc(&pinned, 4 * 64 + 4 * 8 + 64, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
+  // root slots (64 B) + ready flags (u64) + the division zero flag (u32, padded), host-coherent
+  constexpr size_t kSlots = sg_ctx::kRootSlots;
+  constexpr size_t kPinned = kSlots * 64 + kSlots * 8 + 64;
+  if (hipStreamCreateWithFlags(&ctx->side, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming) != hipSuccess ||
+      hipHostMalloc(&pinned, kPinned, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
       hipHostGetDevicePointer(&pinned_dev, pinned, 0) != hipSuccess) {
+    if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
+    if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
+    if (ctx->side) (void)hipStreamDestroy(ctx->side);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return SG_ERR_HIP;
   }
   ctx->pinned_roots = reinterpret_cast<uint64_t*>(pinned);
   ctx->pinned_roots_dev = reinterpret_cast<uint64_t*>(pinned_dev);
-  memset(pinned, 0, 4 * 64 + 4 * 8 + 64);
-  ctx->div_zero_flag = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(pinned) + 4 * 64 + 4 * 8);
-  ctx->div_zero_flag_dev = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(pinned_dev) + 4 * 64 + 4 * 8);
+  memset(pinned, 0, kPinned);
+  ctx->div_zero_flag = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(pinned) + kSlots * 72);
+  ctx->div_zero_flag_dev = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(pinned_dev) + kSlots * 72);
   *out = ctx;
   return SG_OK;
 }
@@ -226,6 +234,9 @@ extern "C" void sg_ctx_destroy(sg_ctx* ctx) {
   for (void* p : ctx->staging_ptr)
     if (p) (void)hipHostFree(p);
   if (ctx->pinned_roots) (void)hipHostFree(ctx->pinned_roots);
+  (void)hipEventDestroy(ctx->ev_fork);
+  (void)hipEventDestroy(ctx->ev_join);
+  (void)hipStreamDestroy(ctx->side);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
 }
@@ -434,16 +445,16 @@ extern "C" int sg_fast_coset_evaluate(sg_ctx* ctx, sg_fe generator, uint64_t roo
 
 namespace sg {
 
-// Spin until the tree kernels have published `batch` roots (flag == seq).  The
-// stream is queried now and then so a finished-without-flag stream or a kernel
-// error surfaces instead of spinning forever.
-void wait_roots(sg_ctx* ctx, int batch, uint64_t seq) {
-  volatile uint64_t* flags = ctx->pinned_roots + 32;
+// Spin until the tree kernels have published `batch` roots (flag == seq) in slots
+// slot0.. .  `s` (the stream the trees run on) is queried now and then so a
+// finished-without-flag stream or a kernel error surfaces instead of spinning forever.
+void wait_roots(sg_ctx* ctx, int batch, uint64_t seq, int slot0, hipStream_t s) {
+  volatile uint64_t* flags = ctx->pinned_roots + sg_ctx::kFlagIndex + slot0;
   for (int b = 0; b < batch; ++b) {
     uint32_t spins = 0;
     while (flags[b] != seq) {
       if ((++spins & 255) == 0) {
-        hipError_t q = hipStreamQuery(ctx->stream);
+        hipError_t q = hipStreamQuery(s);
         if (q == hipSuccess) {
           if (flags[b] != seq) throw Error{SG_ERR_HIP, "tree root was not published"};
           break;
@@ -456,32 +467,54 @@ void wait_roots(sg_ctx* ctx, int batch, uint64_t seq) {
   std::atomic_thread_fence(std::memory_order_acquire);
 }
 
-// merkle_root.rs:21-32 for `batch` equal-size trees in one launch sequence
-void build_trees(sg_ctx* ctx, const fe* const* d_leaves, int batch, uint64_t n, std::unique_ptr<sg_tree>* out) {
+std::unique_ptr<sg_tree> new_tree(sg_ctx* ctx, uint64_t n) {
   SG_REQUIRE(n > 0 && (n & (n - 1)) == 0, "Leafs len must be power of two");
-  SG_REQUIRE(batch >= 1 && batch <= 4, "batch must be 1..4");
+  std::unique_ptr<sg_tree> t(new sg_tree());
+  t->n = n;
+  t->logn = ilog2_exact(n);
+  t->buf = DevBuf(ctx, merkle_tree_digests(n) * 64);
+  return t;
+}
+
+// merkle_root.rs:21-32 for `batch` equal-size trees (buffers already allocated) in one
+// launch sequence on stream `s`; the roots land in pinned slots slot0.. .  Returns the
+// sequence number finish_trees waits for.
+//
+// The kernel that computes each root also stores it into pinned host memory and
+// then raises a ready flag: the host spins on the flags instead of a blocking
+// stream synchronisation, so its next launches (Fiat-Shamir -> fold -> next
+// tree) follow the root within microseconds.
+uint64_t launch_trees(sg_ctx* ctx, const fe* const* d_leaves, int batch, sg_tree* const* trees, int slot0,
+                      hipStream_t s) {
+  SG_REQUIRE(batch >= 1 && batch <= 4 && slot0 >= 0 && slot0 + batch <= sg_ctx::kRootSlots, "batch must be 1..4");
   uint64_t* bufs[4] = {nullptr, nullptr, nullptr, nullptr};
-  for (int b = 0; b < batch; ++b) {
-    out[b].reset(new sg_tree());
-    out[b]->n = n;
-    out[b]->logn = ilog2_exact(n);
-    out[b]->buf = DevBuf(ctx, merkle_tree_digests(n) * 64);
-    bufs[b] = out[b]->buf.as<uint64_t>();
-  }
-  // the kernel that computes each root also stores it into pinned host memory and
-  // then raises a ready flag: the host spins on the flags instead of a blocking
-  // stream synchronisation, so its next launches (Fiat-Shamir -> fold -> next
-  // tree) follow the root within microseconds
   uint64_t* roots_dev[4] = {nullptr, nullptr, nullptr, nullptr};
   uint64_t* flags_dev[4] = {nullptr, nullptr, nullptr, nullptr};
   for (int b = 0; b < batch; ++b) {
-    roots_dev[b] = ctx->pinned_roots_dev + 8 * b;
-    flags_dev[b] = ctx->pinned_roots_dev + 32 + b;
+    SG_REQUIRE(trees[b]->n == trees[0]->n, "trees of one launch must have equal sizes");
+    bufs[b] = trees[b]->buf.as<uint64_t>();
+    roots_dev[b] = ctx->pinned_roots_dev + 8 * (slot0 + b);
+    flags_dev[b] = ctx->pinned_roots_dev + sg_ctx::kFlagIndex + slot0 + b;
   }
   const uint64_t seq = ++ctx->root_seq;
-  SG_HIP(launch_merkle_tree(d_leaves, bufs, batch, n, roots_dev, ctx->stream, 0, 0, 0, flags_dev, seq));
-  wait_roots(ctx, batch, seq);
-  for (int b = 0; b < batch; ++b) memcpy(out[b]->root, ctx->pinned_roots + 8 * b, 64);
+  SG_HIP(launch_merkle_tree(d_leaves, bufs, batch, trees[0]->n, roots_dev, s, 0, 0, 0, flags_dev, seq));
+  return seq;
+}
+
+void finish_trees(sg_ctx* ctx, sg_tree* const* trees, int batch, uint64_t seq, int slot0, hipStream_t s) {
+  wait_roots(ctx, batch, seq, slot0, s);
+  for (int b = 0; b < batch; ++b) memcpy(trees[b]->root, ctx->pinned_roots + 8 * (slot0 + b), 64);
+}
+
+void build_trees(sg_ctx* ctx, const fe* const* d_leaves, int batch, uint64_t n, std::unique_ptr<sg_tree>* out) {
+  SG_REQUIRE(batch >= 1 && batch <= 4, "batch must be 1..4");
+  sg_tree* t[4];
+  for (int b = 0; b < batch; ++b) {
+    out[b] = new_tree(ctx, n);
+    t[b] = out[b].get();
+  }
+  const uint64_t seq = launch_trees(ctx, d_leaves, batch, t, 0, ctx->stream);
+  finish_trees(ctx, t, batch, seq, 0, ctx->stream);
 }
 
 // build into a tree whose buffer is already allocated; with `fold`, the leaves are
@@ -489,10 +522,10 @@ void build_trees(sg_ctx* ctx, const fe* const* d_leaves, int batch, uint64_t n, 
 void fill_tree(sg_ctx* ctx, const fe* d_leaves, sg_tree* t, const FoldLeaves* fold) {
   uint64_t* buf = t->buf.as<uint64_t>();
   uint64_t* root_dev = ctx->pinned_roots_dev;
-  uint64_t* flag_dev = ctx->pinned_roots_dev + 32;
+  uint64_t* flag_dev = ctx->pinned_roots_dev + sg_ctx::kFlagIndex;
   const uint64_t seq = ++ctx->root_seq;
   SG_HIP(launch_merkle_tree(&d_leaves, &buf, 1, t->n, &root_dev, ctx->stream, 0, 0, 0, &flag_dev, seq, fold));
-  wait_roots(ctx, 1, seq);
+  wait_roots(ctx, 1, seq, 0, ctx->stream);
   memcpy(t->root, ctx->pinned_roots, 64);
 }
 
@@ -667,11 +700,11 @@ extern "C" int sg_stream_push(sg_stream* s, uint8_t code, const uint8_t* payload
 extern "C" size_t sg_stream_count(const sg_stream* s) { return s ? s->s.objects.size() : 0; }
 extern "C" int sg_stream_digest(const sg_stream* s, uint8_t* out, size_t cap, size_t* len) {
   if (!s) return SG_ERR_INVALID;
-  std::vector<uint8_t> d = s->s.digest();
-  if (len) *len = d.size();
+  const size_t n = serialized_size(s->s.objects, s->s.objects.size());
+  if (len) *len = n;
   if (out) {
-    if (cap < d.size()) return SG_ERR_INVALID;
-    memcpy(out, d.data(), d.size());
+    if (cap < n) return SG_ERR_INVALID;
+    serialize_into(s->s.objects, s->s.objects.size(), out);
   }
   return SG_OK;
 }

@@ -62,6 +62,9 @@ struct PowTable {
 struct sg_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  // second stream: Merkle trees overlapped with the main stream's algebra (stark_prove)
+  hipStream_t side = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   std::string last_error;
   // pool: rounded size -> free pointers
   std::multimap<size_t, void*> free_bufs;
@@ -69,7 +72,9 @@ struct sg_ctx {
   // power tables keyed by (root limbs, count)
   std::map<std::pair<std::pair<uint64_t, uint64_t>, uint64_t>, sg::PowTable> pow_tables;
   // host-coherent pinned slots for tree roots (written by the kernel that computes them)
-  uint64_t* pinned_roots = nullptr;      // host view, 4 x 64 bytes, then 4 x u64 ready flags
+  static constexpr int kRootSlots = 8;   // concurrent trees: stark_prove uses 0..m-1 and 4
+  static constexpr int kFlagIndex = 8 * kRootSlots;  // u64 index of the first ready flag
+  uint64_t* pinned_roots = nullptr;      // host view, kRootSlots x 64 bytes, then kRootSlots x u64 ready flags
   uint64_t* pinned_roots_dev = nullptr;  // device view of the same memory
   uint64_t root_seq = 0;                 // last sequence number handed to a tree build
   // host-coherent u32 raised (system-scope atomic) by k_batch_div on a zero divisor; read by

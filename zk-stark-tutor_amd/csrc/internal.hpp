@@ -96,6 +96,12 @@ void coset_evaluate_batch(sg_ctx* ctx, const fe& generator, uint64_t root_order,
                           const fe* const* in, size_t d, fe* const* out, int batch);
 
 void build_trees(sg_ctx* ctx, const fe* const* d_leaves, int batch, uint64_t n, std::unique_ptr<sg_tree>* out);
+// split form for trees built on another stream: allocate, launch (roots into pinned slots
+// slot0..slot0+batch-1), then wait for the published roots
+std::unique_ptr<sg_tree> new_tree(sg_ctx* ctx, uint64_t n);
+uint64_t launch_trees(sg_ctx* ctx, const fe* const* d_leaves, int batch, sg_tree* const* trees, int slot0,
+                      hipStream_t s);
+void finish_trees(sg_ctx* ctx, sg_tree* const* trees, int batch, uint64_t seq, int slot0, hipStream_t s);
 sg_tree* build_tree(sg_ctx* ctx, const fe* d_leaves, uint64_t n);
 void fill_tree(sg_ctx* ctx, const fe* d_leaves, sg_tree* t, const FoldLeaves* fold = nullptr);
 void path_indices(const sg_tree* t, uint64_t index, std::vector<uint64_t>& idx);

@@ -78,6 +78,20 @@ int64_t dev_degree(sg_ctx* ctx, const fe* d, uint64_t len) {
   return (int64_t)h - 1;
 }
 
+std::vector<int64_t> dev_degrees(sg_ctx* ctx, const std::vector<std::pair<const fe*, uint64_t>>& polys) {
+  std::vector<int64_t> out(polys.size(), -1);
+  if (polys.empty()) return out;
+  DevBuf last(ctx, 8 * polys.size());
+  SG_HIP(hipMemsetAsync(last.get(), 0, 8 * polys.size(), ctx->stream));
+  for (size_t i = 0; i < polys.size(); ++i)
+    SG_HIP(launch_last_nonzero(polys[i].first, polys[i].second, last.as<unsigned long long>() + i, ctx->stream));
+  std::vector<unsigned long long> h(polys.size());
+  SG_HIP(hipMemcpyAsync(h.data(), last.get(), 8 * polys.size(), hipMemcpyDeviceToHost, ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));  // one round trip for the whole batch
+  for (size_t i = 0; i < polys.size(); ++i) out[i] = (int64_t)h[i] - 1;
+  return out;
+}
+
 // ------------------------------------------------------------------ roots
 
 fe root_of_order(uint64_t n) {
@@ -262,11 +276,19 @@ DPoly fast_multiply_dev(sg_ctx* ctx, fe root, uint64_t root_order, const fe* a, 
 }
 
 DPoly fast_coset_divide_dev(sg_ctx* ctx, fe root, uint64_t root_order, const fe& offset, const fe* lhs, uint64_t ll,
-                            const fe* rhs, uint64_t lr) {
+                            const fe* rhs, uint64_t lr, int64_t rhs_degree) {
   check_root(root, root_order);
-  const int64_t dr = dev_degree(ctx, rhs, lr);
+  int64_t dl, dr;
+  if (rhs_degree >= -1) {
+    dr = rhs_degree;
+    dl = dev_degree(ctx, lhs, ll);
+  } else {
+    std::vector<int64_t> d = dev_degrees(ctx, {{lhs, ll}, {rhs, lr}});
+    dl = d[0];
+    dr = d[1];
+  }
   SG_REQUIRE(dr >= 0, "cannot divide by zero polynomial");
-  const DivPlan pl = coset_divide_plan(root, root_order, dev_degree(ctx, lhs, ll), dr);
+  const DivPlan pl = coset_divide_plan(root, root_order, dl, dr);
   if (pl.zero_lhs) return DPoly{};
   DevBuf vl, vr;
   uint64_t nl, nr;

@@ -11,6 +11,9 @@
 //   combination polynomial (weighted, shifted terms) -> LDE -> FRI::prove
 //   openings of the boundary-quotient and randomizer codewords (batched gathers).
 // The thread_rng draws (trace randomizers, randomizer polynomial) are explicit inputs.
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -534,6 +537,29 @@ std::vector<fe> sample_weights(size_t number, const uint8_t* randomness, size_t 
   return out;
 }
 
+// SG_PROVE_TIMING=1: host-clock phase marks of stark_prove on stderr (diagnostics only)
+struct PhaseMarks {
+  bool on;
+  std::chrono::steady_clock::time_point t0, last;
+  PhaseMarks() : on(getenv("SG_PROVE_TIMING") != nullptr), t0(std::chrono::steady_clock::now()), last(t0) {}
+  void operator()(const char* name) {
+    if (!on) return;
+    auto now = std::chrono::steady_clock::now();
+    fprintf(stderr, "sg-phase %-22s %8.3f ms (at %8.3f)\n", name,
+            std::chrono::duration<double, std::milli>(now - last).count(),
+            std::chrono::duration<double, std::milli>(now - t0).count());
+    last = now;
+  }
+};
+
+// Drains the side stream when the prover's scope ends (normally already joined; on an
+// error it keeps the pool from handing out buffers a side-stream kernel still uses).
+// Declared after the buffers the side stream touches, so it runs before they are released.
+struct SideDrain {
+  sg_ctx* ctx;
+  ~SideDrain() { (void)hipStreamSynchronize(ctx->side); }
+};
+
 struct AsyncScope {
   sg_ctx* ctx;
   bool prev;
@@ -552,9 +578,46 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
   const fe g = st.generator;
   const uint64_t Nf = st.fri.domain_length;
   AsyncScope async_scope(ctx);
-  // randomized trace (stark.rs:285-301), columns on the device
+  PhaseMarks mark;
   const uint64_t Tp = rows + st.num_randomizers;
   SG_REQUIRE(Tp <= D, "randomized trace longer than the omicron domain");
+  const uint64_t tcd = max_degree(st, tcs);
+  SG_REQUIRE(nrc == tcd + 1, "randomizer polynomial must have max_degree(transition_constraints) + 1 coefficients");
+  SG_REQUIRE(nrc <= Nf, "fast_coset_evaluate: polynomial longer than root_order");
+  // The Merkle trees of the boundary-quotient and randomizer codewords (VALU-bound BLAKE2b)
+  // run on the side stream, overlapped with the main stream's transforms and quotients
+  // (which mostly wait on memory).  Everything a side-stream kernel touches is allocated
+  // here, with the main stream drained: a pool buffer released by queued main-stream work
+  // can then never be handed to a side-stream kernel.
+  const bool overlap = m <= 4;  // root slots 0..m-1 (boundary quotients) and 4 (randomizer)
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  std::vector<DPoly> bq_cw;
+  std::vector<std::unique_ptr<sg_tree>> bq_trees(m);
+  for (size_t s = 0; s < m; ++s) bq_cw.push_back(dpoly_alloc(ctx, Nf));
+  DPoly r_cw = dpoly_alloc(ctx, Nf);
+  std::unique_ptr<sg_tree> r_tree;
+  if (overlap) {
+    for (size_t s = 0; s < m; ++s) bq_trees[s] = new_tree(ctx, Nf);
+    r_tree = new_tree(ctx, Nf);
+  }
+  SideDrain side_drain{ctx};
+  // randomizer codeword (stark.rs:424-445) first: it depends on nothing else, and its tree
+  // then hashes on the side stream while the main stream interpolates the trace
+  {
+    const fe* in = d_rcoef;
+    fe* out = r_cw.p();
+    coset_evaluate_batch(ctx, st.omega, Nf, g, &in, nrc, &out, 1);
+  }
+  uint64_t r_seq = 0, bq_seq = 0;
+  constexpr int kRandSlot = 4;
+  if (overlap) {
+    SG_HIP(hipEventRecord(ctx->ev_fork, ctx->stream));
+    SG_HIP(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
+    const fe* leaves = r_cw.p();
+    sg_tree* t = r_tree.get();
+    r_seq = launch_trees(ctx, &leaves, 1, &t, kRandSlot, ctx->side);
+  }
+  // randomized trace (stark.rs:285-301), columns on the device
   std::vector<DPoly> trace_polys;
   {
     DPoly col = dpoly_alloc(ctx, Tp);
@@ -565,6 +628,7 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
       trace_polys.push_back(interpolate_geometric_dev(ctx, st.omicron, D, col.p(), Tp, &zc));
     }
   }
+  mark("trace_interpolation");
   // boundary quotients (stark.rs:326-362)
   std::vector<HPoly> bi = boundary_interpolants(st, bnd), bz = boundary_zerofiers(st, bnd);
   std::vector<DPoly> bqs;
@@ -573,29 +637,40 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
     DPoly Z = dpoly_upload(ctx, bz[s].data(), bz[s].size());
     DPoly diff = lincomb(ctx, {{trace_polys[s].p(), 0, trace_polys[s].len, fe_one()},
                                {I.p(), 0, I.len, fe_neg(fe_one())}});
-    bqs.push_back(fast_coset_divide_dev(ctx, st.omicron, D, g, diff.p(), diff.len, Z.p(), Z.len));
+    bqs.push_back(fast_coset_divide_dev(ctx, st.omicron, D, g, diff.p(), diff.len, Z.p(), Z.len, hp_degree(bz[s])));
   }
-  // boundary-quotient codewords + roots (stark.rs:367-386)
-  std::vector<DPoly> bq_cw;
-  std::vector<std::unique_ptr<sg_tree>> bq_trees(m);
+  mark("boundary_quotients");
+  // boundary-quotient codewords (stark.rs:367-386); their trees hash on the side stream
+  // while the main stream computes the transition quotients
   for (size_t s = 0; s < m; ++s) {
     SG_REQUIRE(bqs[s].len <= Nf, "fast_coset_evaluate: polynomial longer than root_order");
-    bq_cw.push_back(dpoly_alloc(ctx, Nf));
     const fe* in = bqs[s].p();
-    fe* out = bq_cw.back().p();
+    fe* out = bq_cw[s].p();
     if (bqs[s].len)
       coset_evaluate_batch(ctx, st.omega, Nf, g, &in, bqs[s].len, &out, 1);
     else
       SG_HIP(hipMemsetAsync(out, 0, Nf * sizeof(fe), ctx->stream));
   }
-  for (size_t s = 0; s < m; s += 4) {
-    int b = (int)std::min<size_t>(4, m - s);
+  if (overlap) {
+    SG_HIP(hipEventRecord(ctx->ev_fork, ctx->stream));
+    SG_HIP(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
     const fe* leaves[4];
-    for (int k = 0; k < b; ++k) leaves[k] = bq_cw[s + k].p();
-    build_trees(ctx, leaves, b, Nf, &bq_trees[s]);
+    sg_tree* t[4];
+    for (size_t s = 0; s < m; ++s) {
+      leaves[s] = bq_cw[s].p();
+      t[s] = bq_trees[s].get();
+    }
+    bq_seq = launch_trees(ctx, leaves, (int)m, t, 0, ctx->side);
+    SG_HIP(hipEventRecord(ctx->ev_join, ctx->side));
+  } else {
+    for (size_t s = 0; s < m; s += 4) {
+      int b = (int)std::min<size_t>(4, m - s);
+      const fe* leaves[4];
+      for (int k = 0; k < b; ++k) leaves[k] = bq_cw[s + k].p();
+      build_trees(ctx, leaves, b, Nf, &bq_trees[s]);
+    }
   }
-  check_div_zero(ctx);  // the root wait drained the stream past the boundary divisions
-  for (size_t s = 0; s < m; ++s) push_obj(ps, SG_OBJ_ROOT, bq_trees[s]->root, 64);
+  mark("bq_lde");
   // transition quotients (stark.rs:388-422): evaluate_symbolic's polynomial from its values on a
   // coset of size L > its length, then fast_coset_divide by the transition zerofier.  When the
   // division's order equals L its lhs NTT IS those coset values (same offset, same root), so
@@ -659,19 +734,29 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
     }
     tqs.push_back(coset_divide_finish(ctx, pl, g, lhs_v, tz_values(pl)));
   }
-  // randomizer polynomial + codeword (stark.rs:424-445)
-  const uint64_t tcd = max_degree(st, tcs);
-  SG_REQUIRE(nrc == tcd + 1, "randomizer polynomial must have max_degree(transition_constraints) + 1 coefficients");
-  SG_REQUIRE(nrc <= Nf, "fast_coset_evaluate: polynomial longer than root_order");
-  DPoly r_cw = dpoly_alloc(ctx, Nf);
-  {
-    const fe* in = d_rcoef;
-    fe* out = r_cw.p();
-    coset_evaluate_batch(ctx, st.omega, Nf, g, &in, nrc, &out, 1);
+  mark("transition_quotients");
+  // every quotient's degree with one host round trip (checked after the weights, as the
+  // reference does, and used again by the terms below); it drains the main stream past
+  // every division, so a zero divisor is reported before any root is pushed
+  std::vector<std::pair<const fe*, uint64_t>> qpolys;
+  for (const DPoly& q : tqs) qpolys.emplace_back(q.p(), q.len);
+  for (const DPoly& q : bqs) qpolys.emplace_back(q.p(), q.len);
+  const std::vector<int64_t> qdeg = dev_degrees(ctx, qpolys);
+  check_div_zero(ctx);
+  // roots in the reference's order: boundary quotients (stark.rs:373-386), randomizer (:443)
+  if (overlap) {
+    sg_tree* t[4];
+    for (size_t s = 0; s < m; ++s) t[s] = bq_trees[s].get();
+    finish_trees(ctx, t, (int)m, bq_seq, 0, ctx->side);
+    sg_tree* rt = r_tree.get();
+    finish_trees(ctx, &rt, 1, r_seq, kRandSlot, ctx->side);
+    SG_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));  // openings read the trees
+  } else {
+    r_tree.reset(build_tree(ctx, r_cw.p(), Nf));
   }
-  std::unique_ptr<sg_tree> r_tree(build_tree(ctx, r_cw.p(), Nf));
-  check_div_zero(ctx);  // ... and past the transition divisions
+  for (size_t s = 0; s < m; ++s) push_obj(ps, SG_OBJ_ROOT, bq_trees[s]->root, 64);
   push_obj(ps, SG_OBJ_ROOT, r_tree->root, 64);
+  mark("trees_joined");
   // weights (stark.rs:447-450)
   uint8_t fs[32];
   if (ps->fiat_shamir_prover(ps->user, 32, fs) != 0)
@@ -680,7 +765,7 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
   // degree check (stark.rs:451-465)
   std::vector<uint64_t> tqdb = transition_quotient_degree_bounds(st, tcs);
   for (size_t i = 0; i < tqs.size(); ++i) {
-    int64_t d = dev_degree(ctx, tqs[i].p(), tqs[i].len);
+    int64_t d = qdeg[i];
     SG_REQUIRE(d >= 0, "Failed to get degree of transition quotient");
     SG_REQUIRE((uint64_t)d == tqdb[i], "transition quotient degrees do not match with expectation");
   }
@@ -696,10 +781,9 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
   wrapped.reserve(2 * (tqs.size() + bqs.size()));
   size_t wi = 0;
   terms.push_back({d_rcoef, 0, nrc, weights[wi++]});
-  auto add_pair = [&](const DPoly& q, uint64_t shift) {
+  auto add_pair = [&](const DPoly& q, uint64_t shift, int64_t d) {
     terms.push_back({q.p(), 0, q.len, weights[wi++]});
     const fe w = weights[wi++];
-    int64_t d = dev_degree(ctx, q.p(), q.len);
     if (d < 0) return;  // fast_multiply of a zero polynomial is the empty polynomial
     if (shift + (uint64_t)d < D) {
       // no wrap-around: fast_multiply(x^shift, q) is exactly q shifted, truncated at its degree
@@ -713,8 +797,8 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
       terms.push_back({wrapped.back().p(), 0, wrapped.back().len, w});
     }
   };
-  for (size_t i = 0; i < tqs.size(); ++i) add_pair(tqs[i], tcd - tqdb[i]);
-  for (size_t s = 0; s < m; ++s) add_pair(bqs[s], tcd - bqdb[s]);
+  for (size_t i = 0; i < tqs.size(); ++i) add_pair(tqs[i], tcd - tqdb[i], qdeg[i]);
+  for (size_t s = 0; s < m; ++s) add_pair(bqs[s], tcd - bqdb[s], qdeg[tqs.size() + s]);
   DPoly comb = lincomb(ctx, terms);
   SG_REQUIRE(comb.len <= Nf, "fast_coset_evaluate: polynomial longer than root_order");
   DPoly comb_cw = dpoly_alloc(ctx, Nf);
@@ -723,9 +807,11 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
     fe* out = comb_cw.p();
     coset_evaluate_batch(ctx, st.omega, Nf, g, &in, comb.len, &out, 1);
   }
+  mark("combination_lde");
   // FRI (stark.rs:514-522)
   std::vector<size_t> top(st.fri.num_colinearity_tests);
   fri_prove_dev(ctx, &st.fri, comb_cw.p(), Nf, ps, top.data());
+  mark("fri_prove");
   // openings (stark.rs:524-560)
   std::vector<uint64_t> dup;
   for (size_t i : top) dup.push_back(i);
@@ -739,6 +825,7 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
   push_openings(ctx, ps, cts, quad);
   SG_HIP(hipStreamSynchronize(ctx->stream));
   check_div_zero(ctx);
+  mark("openings");
 }
 
 std::vector<const MPoly*> tc_list(const sg_mpoly* const* tcs, size_t n) {

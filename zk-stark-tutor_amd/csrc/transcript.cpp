@@ -24,21 +24,34 @@ static bool carries_field(uint8_t code, size_t len) {
   return code == 3 || code == 4;
 }
 
-std::vector<uint8_t> serialize_objects(const std::vector<StreamObject>& objs, size_t count) {
-  std::vector<uint8_t> out(16, 0);
+size_t serialized_size(const std::vector<StreamObject>& objs, size_t count) {
+  size_t n = 16;
+  for (size_t i = 0; i < count; ++i) n += 9 + objs[i].payload.size();
+  return n;
+}
+
+// one pass over the objects straight into `out` (serialized_size bytes)
+void serialize_into(const std::vector<StreamObject>& objs, size_t count, uint8_t* out) {
+  uint8_t* q = out + 16;
   bool field = false;
   for (size_t i = 0; i < count; ++i) {
     const StreamObject& o = objs[i];
-    field = field || carries_field(o.code, o.payload.size());
-    out.push_back(o.code);
-    put_be64(out, (uint64_t)o.payload.size());
-    out.insert(out.end(), o.payload.begin(), o.payload.end());
+    const uint64_t len = o.payload.size();
+    field = field || carries_field(o.code, len);
+    *q++ = o.code;
+    for (int k = 7; k >= 0; --k) *q++ = (uint8_t)(len >> (8 * k));
+    if (len) memcpy(q, o.payload.data(), len);
+    q += len;
   }
-  if (field) {
-    // p = 1 + 407 * 2^119 big-endian: 0x0cb8 << 116 | 1
-    static const uint8_t pbe[16] = {0xcb, 0x80, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0x01};
-    memcpy(out.data(), pbe, 16);
-  }
+  // p = 1 + 407 * 2^119 big-endian: 0x0cb8 << 116 | 1
+  static const uint8_t pbe[16] = {0xcb, 0x80, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0x01};
+  if (field) memcpy(out, pbe, 16);
+  else memset(out, 0, 16);
+}
+
+std::vector<uint8_t> serialize_objects(const std::vector<StreamObject>& objs, size_t count) {
+  std::vector<uint8_t> out(serialized_size(objs, count));
+  serialize_into(objs, count, out.data());
   return out;
 }
 

@@ -36,6 +36,8 @@ struct Stream {
 };
 
 std::vector<uint8_t> serialize_objects(const std::vector<StreamObject>& objs, size_t count);
+size_t serialized_size(const std::vector<StreamObject>& objs, size_t count);
+void serialize_into(const std::vector<StreamObject>& objs, size_t count, uint8_t* out);
 bool deserialize_stream(const uint8_t* b, size_t len, Stream& s, std::string& err);
 
 }  // namespace sg

@@ -394,6 +394,11 @@ def decode_object(code: int, payload: bytes):
     raise ValueError("Unknown code")
 
 
+_new_bytes = ctypes.pythonapi.PyBytes_FromStringAndSize
+_new_bytes.restype = ctypes.py_object
+_new_bytes.argtypes = [ctypes.c_void_p, ctypes.c_ssize_t]
+
+
 class IndependentProofStream:
     """proof_stream.rs:15-78, held natively by the library (byte-exact digest)."""
 
@@ -435,11 +440,13 @@ class IndependentProofStream:
         rc = self._lib.sg_stream_digest(self.handle, None, 0, ctypes.byref(n))
         if rc != 0:
             raise StarkGpuError(rc, "digest")
-        buf = (ctypes.c_uint8 * n.value)()
-        rc = self._lib.sg_stream_digest(self.handle, buf, n.value, ctypes.byref(n))
+        # serialize straight into a fresh bytes object (one allocation, one pass)
+        out = _new_bytes(None, n.value)
+        rc = self._lib.sg_stream_digest(self.handle, ctypes.cast(ctypes.c_char_p(out), ctypes.c_void_p), n.value,
+                                        ctypes.byref(n))
         if rc != 0:
             raise StarkGpuError(rc, "digest")
-        return bytes(buf)
+        return out
 
     def fiat_shamir_prover(self, num_bytes: int) -> bytes:
         buf = (ctypes.c_uint8 * max(num_bytes, 1))()
