@@ -138,6 +138,29 @@ struct PassArgs {
 
 // COLK: the tile's columns are consecutive low index bits (they enter the twiddle
 // index k); false when the columns are independent transforms' tiles (first pass).
+// R radix-2 stages (tile-local stages t+1 .. t+R) on the 2^R elements of one group held
+// in registers: x[m] is tile row g0 + m * 2^t with g_low = g0 mod 2^t; `low` = the index
+// bits below b0 (cb*C + c; 0 when the columns are independent transforms).
+template <int R>
+__device__ __forceinline__ void radix_regs(fe* x, const PassArgs& a, int t, uint32_t g_low, uint64_t low) {
+#pragma unroll
+  for (int u = 0; u < R; ++u) {
+    const int S = a.b0 + t + u + 1;  // global stage, 1-based
+#pragma unroll
+    for (int m = 0; m < (1 << R); ++m) {
+      if (m & (1 << u)) continue;
+      uint64_t gmod = (uint64_t)g_low + ((uint64_t)(m & ((1 << u) - 1)) << t);
+      uint64_t k = (gmod << a.b0) + low;
+      // stage-major table: stage S's twiddles root^(k * n/2^S), k < 2^(S-1), start at 2^(S-1) - 1
+      fe w = ld_fe(a.tw + (((uint64_t)1 << (S - 1)) - 1) + k);
+      fe o = mont_mul(x[m + (1 << u)], w);
+      fe ev = x[m];
+      x[m] = fe_add_lazy(ev, o);  // tile values stay in [0, 2^128) until the last store
+      x[m + (1 << u)] = fe_sub_lazy(ev, o);
+    }
+  }
+}
+
 template <int R, bool COLK = true>
 __device__ __forceinline__ void radix_step(fe_lds* lds, const PassArgs& a, int t, uint64_t lowbase) {
   const int logC = a.logC;
@@ -152,23 +175,7 @@ __device__ __forceinline__ void radix_step(fe_lds* lds, const PassArgs& a, int t
     fe x[1 << R];
 #pragma unroll
     for (int m = 0; m < (1 << R); ++m) x[m] = lds[((g0 + ((uint32_t)m << t)) << logC) + c];
-    const uint64_t low = COLK ? lowbase + c : 0;  // cb*C + c: index bits below b0
-#pragma unroll
-    for (int u = 0; u < R; ++u) {
-      const int S = a.b0 + t + u + 1;  // global stage, 1-based
-#pragma unroll
-      for (int m = 0; m < (1 << R); ++m) {
-        if (m & (1 << u)) continue;
-        uint64_t gmod = (uint64_t)g_low + ((uint64_t)(m & ((1 << u) - 1)) << t);
-        uint64_t k = (gmod << a.b0) + low;
-        // stage-major table: stage S's twiddles root^(k * n/2^S), k < 2^(S-1), start at 2^(S-1) - 1
-        fe w = ld_fe(a.tw + (((uint64_t)1 << (S - 1)) - 1) + k);
-        fe o = mont_mul(x[m + (1 << u)], w);
-        fe ev = x[m];
-        x[m] = fe_add_lazy(ev, o);  // tile values stay in [0, 2^128) until the last store
-        x[m + (1 << u)] = fe_sub_lazy(ev, o);
-      }
-    }
+    radix_regs<R>(x, a, t, g_low, COLK ? lowbase + c : 0);
 #pragma unroll
     for (int m = 0; m < (1 << R); ++m) lds[((g0 + ((uint32_t)m << t)) << logC) + c] = x[m];
   }
@@ -244,6 +251,54 @@ __global__ __launch_bounds__(256, SG_NTT_WPE) void k_ntt_pass(PassArgs a) {
   }
 }
 
+// A 2048-element pass (256 threads, L >= 6 stages) whose first and last radix-8 steps
+// run straight out of / into HBM: each thread loads the 8 rows of its first-step group
+// (rows 8 qq + m of column c), and stores the 8 rows of its last-step group (rows
+// qq + m 2^(L-3)).  Only the middle stages go through LDS: one LDS write + one read per
+// element plus a round trip per middle step, and L/3 barriers fewer than k_ntt_pass.
+template <int TL>
+__global__ __launch_bounds__(256, SG_NTT_WPE) void k_ntt_pass_rr(PassArgs a) {
+  static_assert(TL == 11, "2048-element tiles, 256 threads");
+  extern __shared__ fe_lds lds[];
+  const int logC = a.logC, L = a.L;
+  const uint32_t C = 1u << logC;
+  const uint64_t ncb = (uint64_t)1 << (a.b0 - logC);
+  const uint64_t h = blockIdx.x / ncb;
+  const uint64_t cb = blockIdx.x % ncb;
+  const uint64_t base = (h << (a.b0 + L)) + cb * C;
+  fe* __restrict__ data = a.ys ? a.data[0] + (uint64_t)blockIdx.y * a.ys : a.data[blockIdx.y];
+  const uint32_t c = threadIdx.x & (C - 1), qq = threadIdx.x >> logC;  // qq < 2^(L-3)
+  const uint64_t low = cb * C + c;
+  fe x[8];
+#pragma unroll
+  for (int m = 0; m < 8; ++m) x[m] = ld_fe(data + base + ((uint64_t)(8 * qq + m) << a.b0) + c);
+  radix_regs<3>(x, a, 0, 0, low);
+#pragma unroll
+  for (int m = 0; m < 8; ++m) lds[((8 * qq + m) << logC) + c] = x[m];
+  __syncthreads();
+  int t = 3;
+  while (t < L - 3) {
+    int rem = L - 3 - t;
+    if (rem >= 3) { radix_step<3>(lds, a, t, cb * C); t += 3; }
+    else if (rem == 2) { radix_step<2>(lds, a, t, cb * C); t += 2; }
+    else { radix_step<1>(lds, a, t, cb * C); t += 1; }
+  }
+  const int tl = L - 3;
+#pragma unroll
+  for (int m = 0; m < 8; ++m) x[m] = lds[((qq + ((uint32_t)m << tl)) << logC) + c];
+  radix_regs<3>(x, a, tl, qq, low);
+  const bool post = a.post != nullptr;
+  const bool last = a.b0 + L == a.logn;  // the transform's last pass stores canonical values
+  const fe pc = post ? ld_fe(a.post) : fe_zero();
+#pragma unroll
+  for (int m = 0; m < 8; ++m) {
+    fe v = x[m];
+    if (post) v = mont_mul(v, pc);
+    else if (last) v = fe_canon(v);
+    st_fe(data + base + ((uint64_t)(qq + ((uint32_t)m << tl)) << a.b0) + c, v);
+  }
+}
+
 // First pass with the bit-reversal fused in (fft/ntt.rs:14 bit_reverse_copy).
 // Positions j = h*2^L + t of the bit-reversed array hold x[rev_m(j)] =
 // x[rev_{m-L}(h) + rev_L(t) * 2^(m-L)], so the C = 2^logC tiles whose
@@ -280,20 +335,6 @@ __global__ __launch_bounds__(256, SG_NTT_WPE) void k_ntt_first(FirstArgs a) {
   const uint64_t c0 = (uint64_t)bx << logC;
   const fe* __restrict__ in = a.in_ys ? a.in[0] + (uint64_t)blockIdx.y * a.in_ys : a.in[blockIdx.y];
   fe* __restrict__ out = a.out_ys ? a.out[0] + (uint64_t)blockIdx.y * a.out_ys : a.out[blockIdx.y];
-  const uint32_t rows = 1u << (L - skip);
-  const uint32_t rep = 1u << skip;
-  for (uint32_t l = threadIdx.x; l < rows * C; l += blockDim.x) {
-    const uint32_t k = l & (C - 1), u = l >> logC;
-    const uint64_t idx = c0 + k + ((uint64_t)u << (m - L));
-    fe v = fe_zero();
-    if (idx < a.n_in) {
-      v = ld_fe(in + idx);
-      if (a.sA) v = mont_mul(v, mont_mul(ld_fe(a.sA + (idx & 4095)), ld_fe(a.sB + (idx >> 12))));
-    }
-    const uint32_t t = __builtin_bitreverse32(u) >> (32 - L);
-    for (uint32_t r = 0; r < rep; ++r) lds[((t + r) << logC) + k] = v;
-  }
-  __syncthreads();
   PassArgs pa;
   pa.tw = a.tw;
   pa.post = nullptr;
@@ -301,7 +342,61 @@ __global__ __launch_bounds__(256, SG_NTT_WPE) void k_ntt_first(FirstArgs a) {
   pa.b0 = 0;
   pa.L = L;
   pa.logC = logC;
+  // one radix-8 group per thread in the first and last steps (column c, group qq)
+  const bool regs = L >= 6 && ((1u << (L - 3)) << logC) == blockDim.x;
   int t = skip;
+  if (regs && skip == 0) {
+    // first radix-8 step straight from HBM: tile row 8 qq + j holds x[rev_L(8 qq + j)]
+    const uint32_t c = threadIdx.x & (C - 1), qq = threadIdx.x >> logC;
+    fe x[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const uint32_t u = __builtin_bitreverse32(8 * qq + j) >> (32 - L);
+      const uint64_t idx = c0 + c + ((uint64_t)u << (m - L));
+      x[j] = fe_zero();
+      if (idx < a.n_in) {
+        x[j] = ld_fe(in + idx);
+        if (a.sA) x[j] = mont_mul(x[j], mont_mul(ld_fe(a.sA + (idx & 4095)), ld_fe(a.sB + (idx >> 12))));
+      }
+    }
+    radix_regs<3>(x, pa, 0, 0, 0);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) lds[((8 * qq + j) << logC) + c] = x[j];
+    t = 3;
+  } else {
+    const uint32_t rows = 1u << (L - skip);
+    const uint32_t rep = 1u << skip;
+    for (uint32_t l = threadIdx.x; l < rows * C; l += blockDim.x) {
+      const uint32_t k = l & (C - 1), u = l >> logC;
+      const uint64_t idx = c0 + k + ((uint64_t)u << (m - L));
+      fe v = fe_zero();
+      if (idx < a.n_in) {
+        v = ld_fe(in + idx);
+        if (a.sA) v = mont_mul(v, mont_mul(ld_fe(a.sA + (idx & 4095)), ld_fe(a.sB + (idx >> 12))));
+      }
+      const uint32_t tr = __builtin_bitreverse32(u) >> (32 - L);
+      for (uint32_t r = 0; r < rep; ++r) lds[((tr + r) << logC) + k] = v;
+    }
+  }
+  __syncthreads();
+  if (regs && L - t >= 3) {
+    // remainder step first, radix-8 steps, and the last radix-8 step (rows qq + m 2^(L-3)
+    // of column c) straight from registers to HBM: out[(h << L) + row]
+    const int r0 = (L - t) % 3;
+    if (r0 == 2) { radix_step<2, false>(lds, pa, t, 0); t += 2; }
+    else if (r0 == 1) { radix_step<1, false>(lds, pa, t, 0); t += 1; }
+    while (t < L - 3) { radix_step<3, false>(lds, pa, t, 0); t += 3; }
+    const uint32_t c = threadIdx.x & (C - 1), qq = threadIdx.x >> logC;
+    const int tl = L - 3;
+    fe x[8];
+#pragma unroll
+    for (int mm = 0; mm < 8; ++mm) x[mm] = lds[((qq + ((uint32_t)mm << tl)) << logC) + c];
+    radix_regs<3>(x, pa, tl, qq, 0);
+    const uint64_t h = __builtin_bitreverse64(c0 + c) >> (64 - (m - L));
+#pragma unroll
+    for (int mm = 0; mm < 8; ++mm) st_fe(out + (h << L) + qq + ((uint32_t)mm << tl), x[mm]);
+    return;
+  }
   while (t < L) {
     int rem = L - t;
     if (rem >= 3) { radix_step<3, false>(lds, pa, t, 0); t += 3; }
@@ -827,9 +922,11 @@ hipError_t launch_ntt_dit(fe* const* data, int batch, const fe* tw, int logn, co
     hipError_t e = hipFuncSetAttribute((const void*)k_ntt_pass<0>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
     if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_ntt_pass<12>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
     if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_ntt_pass<11>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_ntt_pass_rr<11>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
     if (e != hipSuccess) return e;
     lds_attr = true;
   }
+  static const bool use_rr = env_int("SG_NTT_RR", 1) != 0;  // register-direct first/last steps
   static const int tile_log = [] {
     int t = env_int("SG_NTT_TILE_LOG", 11);
     return (t == 11 || t == 12) ? t : 11;
@@ -869,6 +966,8 @@ hipError_t launch_ntt_dit(fe* const* data, int batch, const fe* tw, int logn, co
     dim3 grid((unsigned)ntiles, batch);
     if (tile == 4096 && threads == 256)
       hipLaunchKernelGGL(k_ntt_pass<12>, grid, dim3(256), lds, s, a);
+    else if (tile == 2048 && threads == 256 && a.L >= 6 && use_rr)
+      hipLaunchKernelGGL(k_ntt_pass_rr<11>, grid, dim3(256), lds, s, a);
     else if (tile == 2048 && threads == 256)
       hipLaunchKernelGGL(k_ntt_pass<11>, grid, dim3(256), lds, s, a);
     else
