@@ -691,20 +691,21 @@ extern "C" sg_proof_stream sg_stream_callbacks(sg_stream* s) {
 }
 extern "C" int sg_stream_push(sg_stream* s, uint8_t code, const uint8_t* payload, size_t len) {
   if (!s || code > 4 || (len && !payload)) return SG_ERR_INVALID;
-  StreamObject o;
-  o.code = code;
-  o.payload.assign(payload, payload + len);
-  s->s.objects.push_back(std::move(o));
+  try {
+    s->s.push(code, payload, len);
+  } catch (const std::bad_alloc&) {
+    return SG_ERR_NOMEM;
+  }
   return SG_OK;
 }
-extern "C" size_t sg_stream_count(const sg_stream* s) { return s ? s->s.objects.size() : 0; }
+extern "C" size_t sg_stream_count(const sg_stream* s) { return s ? s->s.count() : 0; }
 extern "C" int sg_stream_digest(const sg_stream* s, uint8_t* out, size_t cap, size_t* len) {
   if (!s) return SG_ERR_INVALID;
-  const size_t n = serialized_size(s->s.objects, s->s.objects.size());
+  const size_t n = s->s.digest_size(s->s.count());
   if (len) *len = n;
   if (out) {
     if (cap < n) return SG_ERR_INVALID;
-    serialize_into(s->s.objects, s->s.objects.size(), out);
+    s->s.digest_into(s->s.count(), out);
   }
   return SG_OK;
 }
@@ -721,11 +722,11 @@ extern "C" int sg_stream_fiat_shamir_verifier(const sg_stream* s, size_t num_byt
 }
 extern "C" int sg_stream_pull(sg_stream* s, uint8_t* code, const uint8_t** payload, size_t* len) {
   if (!s) return SG_ERR_INVALID;
-  if (s->s.read_index >= s->s.objects.size()) return SG_ERR_INVALID;  // "Cannot pull, queue is empty"
-  const StreamObject& o = s->s.objects[s->s.read_index++];
-  if (code) *code = o.code;
-  if (payload) *payload = o.payload.data();
-  if (len) *len = o.payload.size();
+  if (s->s.read_index >= s->s.count()) return SG_ERR_INVALID;  // "Cannot pull, queue is empty"
+  const size_t i = s->s.read_index++;
+  if (code) *code = s->s.code(i);
+  if (payload) *payload = s->s.payload(i);
+  if (len) *len = s->s.payload_len(i);
   return SG_OK;
 }
 extern "C" int sg_stream_deserialize(const uint8_t* bytes, size_t len, sg_stream** out) {
@@ -758,6 +759,21 @@ size_t fri_num_rounds(const sg_fri* f) {
 
 void push_obj(const sg_proof_stream* ps, uint8_t code, const uint8_t* p, size_t len) {
   if (ps->push(ps->user, code, p, len) != 0) throw Error{SG_ERR_CALLBACK, "proof stream push callback failed"};
+}
+
+uint8_t* ObjWriter::begin(uint8_t code_, size_t len) {
+  code = code_;
+  if (ps->push == stream_push_cb) {  // a native stream: write the payload in place
+    direct = true;
+    return reinterpret_cast<sg_stream*>(ps->user)->s.push_reserve(code, len);
+  }
+  direct = false;
+  scratch.resize(len);
+  return scratch.data();
+}
+
+void ObjWriter::commit() {
+  if (!direct) push_obj(ps, code, scratch.data(), scratch.size());
 }
 
 void put_u128_be_at(uint8_t* out, const fe& a) {
@@ -971,10 +987,11 @@ void fri_prove_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, con
   const fe* vals = nullptr;
   const uint8_t* digs = nullptr;
   gather_openings(ctx, fe_addr, dg_addr, &vals, &digs);
-  // payloads are written in place (memcpy) into one reused buffer per object kind
+  // payloads are written in place: straight into a native stream's body, else into
+  // one reused buffer handed to the push callback
   size_t fpos = 0, dpos = 0;
   uint8_t leafs[48];
-  std::vector<uint8_t> obj;
+  ObjWriter w{ps};
   for (size_t r = 0; r < R; ++r) {
     for (size_t s = 0; s < c; ++s) {
       for (int k = 0; k < 3; ++k) put_u128_be_at(leafs + 16 * k, vals[fpos + 3 * s + k]);
@@ -986,15 +1003,14 @@ void fri_prove_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, con
       const size_t lens[3] = {lc, lc, ln};
       for (int which = 0; which < 3; ++which) {
         // Path payload: per digest [len u64 BE = 64][64 bytes] (proof_stream_enum.rs:95-110)
-        obj.resize(lens[which] * 72);
-        uint8_t* p = obj.data();
+        uint8_t* p = w.begin(SG_OBJ_PATH, lens[which] * 72);
         for (size_t k = 0; k < lens[which]; ++k, p += 72) {
           static const uint8_t len64[8] = {0, 0, 0, 0, 0, 0, 0, 64};
           memcpy(p, len64, 8);
           memcpy(p + 8, digs + (dpos + k) * 64, 64);
         }
         dpos += lens[which];
-        push_obj(ps, SG_OBJ_PATH, obj.data(), obj.size());
+        w.commit();
       }
     }
   }

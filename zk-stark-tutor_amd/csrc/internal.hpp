@@ -109,6 +109,16 @@ void gather_digests(sg_ctx* ctx, const sg_tree* t, const std::vector<uint64_t>& 
 
 size_t fri_num_rounds(const sg_fri* f);
 void push_obj(const sg_proof_stream* ps, uint8_t code, const uint8_t* p, size_t len);
+// one object's payload, written in place into a native stream (sg_stream_callbacks) or staged
+// for the push callback of any other stream: p = begin(code, len); fill p[0..len); commit()
+struct ObjWriter {
+  const sg_proof_stream* ps;
+  std::vector<uint8_t> scratch{};
+  uint8_t code = 0;
+  bool direct = false;
+  uint8_t* begin(uint8_t code, size_t len);
+  void commit();
+};
 void put_u128_be_at(uint8_t* out, const fe& a);
 void put_u128_be(std::vector<uint8_t>& out, const fe& a);
 void fri_commit_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, const sg_proof_stream* ps,

@@ -508,19 +508,19 @@ void push_openings(sg_ctx* ctx, const sg_proof_stream* ps, const std::vector<std
   gather_openings(ctx, fe_addr, dg_addr, &vals, &digs);
   static const uint8_t len64[8] = {0, 0, 0, 0, 0, 0, 0, 64};
   size_t vk = 0, dk = 0;
+  ObjWriter w{ps};
   for (auto& ct : cts) {
     const size_t depth = (size_t)ct.second->logn;
-    std::vector<uint8_t> obj(depth * 72);
     for (size_t k = 0; k < idx.size(); ++k, ++vk) {
       uint8_t v[16];
       put_u128_be_at(v, vals[vk]);
       push_obj(ps, SG_OBJ_VALUE, v, 16);
-      uint8_t* q = obj.data();
+      uint8_t* q = w.begin(SG_OBJ_PATH, depth * 72);
       for (size_t d = 0; d < depth; ++d, q += 72, ++dk) {
         memcpy(q, len64, 8);
         memcpy(q + 8, digs + dk * 64, 64);
       }
-      push_obj(ps, SG_OBJ_PATH, obj.data(), obj.size());
+      w.commit();
     }
   }
 }
@@ -589,17 +589,14 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
   // (which mostly wait on memory).  Everything a side-stream kernel touches is allocated
   // here, with the main stream drained: a pool buffer released by queued main-stream work
   // can then never be handed to a side-stream kernel.
-  const bool overlap = m <= 4;  // root slots 0..m-1 (boundary quotients) and 4 (randomizer)
+  SG_REQUIRE(m <= 4, "at most 4 registers are supported by the AIR kernel");  // root slots 0..m-1, 4
   SG_HIP(hipStreamSynchronize(ctx->stream));
   std::vector<DPoly> bq_cw;
   std::vector<std::unique_ptr<sg_tree>> bq_trees(m);
   for (size_t s = 0; s < m; ++s) bq_cw.push_back(dpoly_alloc(ctx, Nf));
   DPoly r_cw = dpoly_alloc(ctx, Nf);
-  std::unique_ptr<sg_tree> r_tree;
-  if (overlap) {
-    for (size_t s = 0; s < m; ++s) bq_trees[s] = new_tree(ctx, Nf);
-    r_tree = new_tree(ctx, Nf);
-  }
+  for (size_t s = 0; s < m; ++s) bq_trees[s] = new_tree(ctx, Nf);
+  std::unique_ptr<sg_tree> r_tree = new_tree(ctx, Nf);
   SideDrain side_drain{ctx};
   // randomizer codeword (stark.rs:424-445) first: it depends on nothing else, and its tree
   // then hashes on the side stream while the main stream interpolates the trace
@@ -608,9 +605,9 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
     fe* out = r_cw.p();
     coset_evaluate_batch(ctx, st.omega, Nf, g, &in, nrc, &out, 1);
   }
-  uint64_t r_seq = 0, bq_seq = 0;
   constexpr int kRandSlot = 4;
-  if (overlap) {
+  uint64_t r_seq, bq_seq;
+  {
     SG_HIP(hipEventRecord(ctx->ev_fork, ctx->stream));
     SG_HIP(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
     const fe* leaves = r_cw.p();
@@ -651,7 +648,7 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
     else
       SG_HIP(hipMemsetAsync(out, 0, Nf * sizeof(fe), ctx->stream));
   }
-  if (overlap) {
+  {
     SG_HIP(hipEventRecord(ctx->ev_fork, ctx->stream));
     SG_HIP(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
     const fe* leaves[4];
@@ -662,13 +659,6 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
     }
     bq_seq = launch_trees(ctx, leaves, (int)m, t, 0, ctx->side);
     SG_HIP(hipEventRecord(ctx->ev_join, ctx->side));
-  } else {
-    for (size_t s = 0; s < m; s += 4) {
-      int b = (int)std::min<size_t>(4, m - s);
-      const fe* leaves[4];
-      for (int k = 0; k < b; ++k) leaves[k] = bq_cw[s + k].p();
-      build_trees(ctx, leaves, b, Nf, &bq_trees[s]);
-    }
   }
   mark("bq_lde");
   // transition quotients (stark.rs:388-422): evaluate_symbolic's polynomial from its values on a
@@ -744,15 +734,13 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
   const std::vector<int64_t> qdeg = dev_degrees(ctx, qpolys);
   check_div_zero(ctx);
   // roots in the reference's order: boundary quotients (stark.rs:373-386), randomizer (:443)
-  if (overlap) {
+  {
     sg_tree* t[4];
     for (size_t s = 0; s < m; ++s) t[s] = bq_trees[s].get();
     finish_trees(ctx, t, (int)m, bq_seq, 0, ctx->side);
     sg_tree* rt = r_tree.get();
     finish_trees(ctx, &rt, 1, r_seq, kRandSlot, ctx->side);
     SG_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));  // openings read the trees
-  } else {
-    r_tree.reset(build_tree(ctx, r_cw.p(), Nf));
   }
   for (size_t s = 0; s < m; ++s) push_obj(ps, SG_OBJ_ROOT, bq_trees[s]->root, 64);
   push_obj(ps, SG_OBJ_ROOT, r_tree->root, 64);

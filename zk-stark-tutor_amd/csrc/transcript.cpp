@@ -8,103 +8,174 @@
 //   deserialize              stark/stark.rs:30-67
 #include "transcript.hpp"
 
+#include <cstdlib>
 #include <cstring>
+#include <mutex>
+#include <new>
 
 #include "host_hash.hpp"
 
 namespace sg {
 
-static void put_be64(std::vector<uint8_t>& out, uint64_t v) {
+// ---------------------------------------------------------------- byte buffer
+
+ByteBuf::~ByteBuf() { free(p); }
+
+uint8_t* ByteBuf::grow(size_t add) {
+  if (n + add > cap) {
+    size_t c = cap ? cap : 4096;
+    while (c < n + add) c *= 2;
+    void* q = realloc(p, c);
+    if (!q) throw std::bad_alloc();
+    p = static_cast<uint8_t*>(q);
+    cap = c;
+  }
+  uint8_t* at = p + n;
+  n += add;
+  return at;
+}
+
+void ByteBuf::swap(ByteBuf& o) {
+  std::swap(p, o.p);
+  std::swap(n, o.n);
+  std::swap(cap, o.cap);
+}
+
+namespace {
+
+// released bodies keep their (warm) pages for the next stream: one proof stream per proof
+std::mutex g_body_mu;
+constexpr int kBodyCache = 2;
+ByteBuf g_bodies[kBodyCache];
+int g_nbodies = 0;
+constexpr size_t kBodyMaxCached = (size_t)256 << 20;
+
+void put_be64(std::vector<uint8_t>& out, uint64_t v) {
   for (int i = 7; i >= 0; --i) out.push_back((uint8_t)(v >> (8 * i)));
 }
 
-static bool carries_field(uint8_t code, size_t len) {
+uint64_t get_be64(const uint8_t* b) {
+  uint64_t v = 0;
+  for (int i = 0; i < 8; ++i) v = (v << 8) | b[i];
+  return v;
+}
+
+bool carries_field(uint8_t code, size_t len) {
   // Codeword with >= 1 element, Leafs, Value set the field (proof_stream_enum.rs:75-126, 164-174)
   if (code == 1) return len > 0;
   return code == 3 || code == 4;
 }
 
-size_t serialized_size(const std::vector<StreamObject>& objs, size_t count) {
-  size_t n = 16;
-  for (size_t i = 0; i < count; ++i) n += 9 + objs[i].payload.size();
-  return n;
+// p = 1 + 407 * 2^119 big-endian: 0x0cb8 << 116 | 1
+const uint8_t kPrimeBE[16] = {0xcb, 0x80, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0x01};
+
+}  // namespace
+
+// ---------------------------------------------------------------- stream
+
+Stream::Stream() {
+  std::lock_guard<std::mutex> lk(g_body_mu);
+  if (g_nbodies > 0) body.swap(g_bodies[--g_nbodies]);
+  body.n = 0;
 }
 
-// one pass over the objects straight into `out` (serialized_size bytes)
-void serialize_into(const std::vector<StreamObject>& objs, size_t count, uint8_t* out) {
-  uint8_t* q = out + 16;
-  bool field = false;
-  for (size_t i = 0; i < count; ++i) {
-    const StreamObject& o = objs[i];
-    const uint64_t len = o.payload.size();
-    field = field || carries_field(o.code, len);
-    *q++ = o.code;
-    for (int k = 7; k >= 0; --k) *q++ = (uint8_t)(len >> (8 * k));
-    if (len) memcpy(q, o.payload.data(), len);
-    q += len;
+Stream::~Stream() {
+  if (!body.cap || body.cap > kBodyMaxCached) return;
+  std::lock_guard<std::mutex> lk(g_body_mu);
+  if (g_nbodies < kBodyCache) body.swap(g_bodies[g_nbodies++]);
+}
+
+size_t Stream::payload_len(size_t i) const { return (size_t)get_be64(body.data() + offs[i] + 1); }
+
+uint8_t* Stream::push_reserve(uint8_t code, size_t len) {
+  offs.push_back(body.n);
+  uint8_t* h = body.grow(9 + len);
+  h[0] = code;
+  for (int i = 0; i < 8; ++i) h[1 + i] = (uint8_t)((uint64_t)len >> (8 * (7 - i)));
+  field = field || carries_field(code, len);
+  return h + 9;
+}
+
+void Stream::push(uint8_t code, const uint8_t* p, size_t len) {
+  uint8_t* d = push_reserve(code, len);
+  if (len) memcpy(d, p, len);
+}
+
+size_t Stream::digest_size(size_t cnt) const { return 16 + (cnt >= count() ? body.n : offs[cnt]); }
+
+void Stream::digest_into(size_t cnt, uint8_t* out) const {
+  bool f = field;
+  if (cnt < count()) {
+    f = false;
+    for (size_t i = 0; i < cnt && !f; ++i) f = carries_field(code(i), payload_len(i));
   }
-  // p = 1 + 407 * 2^119 big-endian: 0x0cb8 << 116 | 1
-  static const uint8_t pbe[16] = {0xcb, 0x80, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0x01};
-  if (field) memcpy(out, pbe, 16);
+  if (f) memcpy(out, kPrimeBE, 16);
   else memset(out, 0, 16);
+  const size_t len = digest_size(cnt) - 16;
+  if (len) memcpy(out + 16, body.data(), len);
 }
 
-std::vector<uint8_t> serialize_objects(const std::vector<StreamObject>& objs, size_t count) {
-  std::vector<uint8_t> out(serialized_size(objs, count));
-  serialize_into(objs, count, out.data());
-  return out;
+std::vector<uint8_t> Stream::digest(size_t cnt) const {
+  std::vector<uint8_t> d(digest_size(cnt));
+  digest_into(cnt, d.data());
+  return d;
 }
 
-std::vector<uint8_t> Stream::digest(size_t count) const { return serialize_objects(objects, count); }
-
-void Stream::fiat_shamir_all(size_t num_bytes, uint8_t* out) {
-  // header state if all objects are included
-  bool field = fs_field;
-  for (size_t i = fs_objects; i < objects.size(); ++i) field = field || carries_field(objects[i].code, objects[i].payload.size());
-  if (fs_objects == 0 || field != fs_field) {
-    // (re)build: [len u64 BE || prefix] for a signature stream, then header, then objects
-    fs_input.clear();
-    if (signature) {
-      put_be64(fs_input, (uint64_t)prefix.size());
-      fs_input.insert(fs_input.end(), prefix.begin(), prefix.end());
-    }
-    std::vector<uint8_t> d = serialize_objects(objects, objects.size());
-    fs_input.insert(fs_input.end(), d.begin(), d.end());
-    fs_objects = objects.size();
-    fs_field = field;
-    fs_sponge = ShakeSponge();
-    fs_absorbed = 0;
-  } else {
-    for (size_t i = fs_objects; i < objects.size(); ++i) {
-      const StreamObject& o = objects[i];
-      fs_input.push_back(o.code);
-      put_be64(fs_input, (uint64_t)o.payload.size());
-      fs_input.insert(fs_input.end(), o.payload.begin(), o.payload.end());
-    }
-    fs_objects = objects.size();
-  }
-  const size_t rate = 136;
-  size_t full = fs_input.size() / rate;
-  size_t done = fs_absorbed / rate;
-  if (full > done) {
-    fs_sponge.absorb_blocks(fs_input.data() + done * rate, full - done);
-    fs_absorbed = full * rate;
-  }
-  fs_sponge.finish(fs_input.data() + fs_absorbed, fs_input.size() - fs_absorbed, out, num_bytes);
-}
-
-void Stream::fiat_shamir(size_t count, size_t num_bytes, uint8_t* out) const {
-  std::vector<uint8_t> d = digest(count);
+void Stream::fiat_shamir(size_t cnt, size_t num_bytes, uint8_t* out) const {
+  std::vector<uint8_t> in;
   if (signature) {
     // shake256(len(prefix) u64 BE || prefix || digest)
-    std::vector<uint8_t> in;
     put_be64(in, (uint64_t)prefix.size());
     in.insert(in.end(), prefix.begin(), prefix.end());
-    in.insert(in.end(), d.begin(), d.end());
-    shake256(in.data(), in.size(), out, num_bytes);
-  } else {
-    shake256(d.data(), d.size(), out, num_bytes);
   }
+  const size_t pre = in.size();
+  in.resize(pre + digest_size(cnt));
+  digest_into(cnt, in.data() + pre);
+  shake256(in.data(), in.size(), out, num_bytes);
+}
+
+void Stream::fiat_shamir_all(size_t num_bytes, uint8_t* out) {
+  const size_t R = 136;  // SHAKE256 rate
+  if (!fs_valid || fs_field != field) {
+    fs_head.clear();
+    if (signature) {
+      put_be64(fs_head, (uint64_t)prefix.size());
+      fs_head.insert(fs_head.end(), prefix.begin(), prefix.end());
+    }
+    const uint8_t zero[16] = {0};
+    fs_head.insert(fs_head.end(), field ? kPrimeBE : zero, (field ? kPrimeBE : zero) + 16);
+    fs_sponge = ShakeSponge();
+    fs_absorbed = 0;
+    fs_field = field;
+    fs_valid = true;
+  }
+  const size_t H = fs_head.size(), total = H + body.n;
+  // bytes [off, off + len) of fs_head || body
+  auto gather = [&](size_t off, size_t len, uint8_t* dst) {
+    if (off < H) {
+      const size_t a = len < H - off ? len : H - off;
+      memcpy(dst, fs_head.data() + off, a);
+      dst += a;
+      off += a;
+      len -= a;
+    }
+    if (len) memcpy(dst, body.data() + (off - H), len);
+  };
+  uint8_t tmp[R];
+  size_t b = fs_absorbed / R;
+  const size_t full = total / R;
+  for (; b < full && b * R < H; ++b) {  // blocks that start in the head
+    gather(b * R, R, tmp);
+    fs_sponge.absorb_blocks(tmp, 1);
+  }
+  if (b < full) {  // the rest straight from the body
+    fs_sponge.absorb_blocks(body.data() + (b * R - H), full - b);
+    b = full;
+  }
+  fs_absorbed = full * R;
+  const size_t tail = total - fs_absorbed;
+  gather(fs_absorbed, tail, tmp);
+  fs_sponge.finish(tmp, tail, out, num_bytes);
 }
 
 bool deserialize_stream(const uint8_t* b, size_t len, Stream& s, std::string& err) {
@@ -112,16 +183,12 @@ bool deserialize_stream(const uint8_t* b, size_t len, Stream& s, std::string& er
   size_t pos = 16;
   while (pos < len) {
     if (len - pos < 9) { err = "truncated object header"; return false; }
-    uint8_t code = b[pos];
-    uint64_t sz = 0;
-    for (int i = 0; i < 8; ++i) sz = (sz << 8) | b[pos + 1 + i];
+    const uint8_t code = b[pos];
+    const uint64_t sz = get_be64(b + pos + 1);
     pos += 9;
     if (sz > len - pos) { err = "truncated object payload"; return false; }
     if (code > 4) { err = "Unknown code"; return false; }
-    StreamObject o;
-    o.code = code;
-    o.payload.assign(b + pos, b + pos + sz);
-    s.objects.push_back(std::move(o));
+    s.push(code, b + pos, (size_t)sz);
     pos += sz;
   }
   return true;
