@@ -936,14 +936,17 @@ void gather_openings(sg_ctx* ctx, const std::vector<uint64_t>& fe_addr, const st
 
 void fri_prove_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, const sg_proof_stream* ps,
                    size_t* top) {
+  PhaseMarks mark;
   sg_fri_state st;
   fri_commit_dev(ctx, f, d_cw, n, ps, st, /*borrow_input=*/true);
+  mark("fri_commit");
   SG_REQUIRE(st.codewords.size() >= 2, "FRI prove needs at least two rounds (reference indexes codewords[1])");
   uint8_t seed[32];
   if (ps->fiat_shamir_prover(ps->user, 32, seed) != 0)
     throw Error{SG_ERR_CALLBACK, "proof stream fiat_shamir callback failed"};
   const size_t c = f->num_colinearity_tests;
   sample_indices(seed, 32, st.lengths[1], st.lengths.back(), c, top);
+  mark("fri_sample_indices");
   // Every opening of every round is known once the top indices are: gather all
   // leaf values and authentication-path digests with one launch each, then push
   // Leafs / Path objects in the reference's order (fri.rs:174-208, 231-245).
@@ -984,9 +987,11 @@ void fri_prove_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, con
       for (uint64_t d : p) dg_addr.push_back(bn + 64 * d);
     }
   }
+  mark("fri_query_addresses");
   const fe* vals = nullptr;
   const uint8_t* digs = nullptr;
   gather_openings(ctx, fe_addr, dg_addr, &vals, &digs);
+  mark("fri_query_gather");
   // payloads are written in place: straight into a native stream's body, else into
   // one reused buffer handed to the push callback
   size_t fpos = 0, dpos = 0;
@@ -1014,6 +1019,7 @@ void fri_prove_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, con
       }
     }
   }
+  mark("fri_query_push");
 }
 
 }  // namespace sg

@@ -2,6 +2,9 @@
 // poly.cpp, stark.cpp): error guard, element conversion, NTT/LDE drivers,
 // retained Merkle trees and the FRI driver.
 #pragma once
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cstdint>
 #include <memory>
 #include <new>
@@ -108,6 +111,21 @@ void path_indices(const sg_tree* t, uint64_t index, std::vector<uint64_t>& idx);
 void gather_digests(sg_ctx* ctx, const sg_tree* t, const std::vector<uint64_t>& idx, uint8_t* out);
 
 size_t fri_num_rounds(const sg_fri* f);
+// SG_PROVE_TIMING=1: host-clock phase marks of the prover on stderr (diagnostics only)
+struct PhaseMarks {
+  bool on;
+  std::chrono::steady_clock::time_point t0, last;
+  PhaseMarks() : on(getenv("SG_PROVE_TIMING") != nullptr), t0(std::chrono::steady_clock::now()), last(t0) {}
+  void operator()(const char* name) {
+    if (!on) return;
+    auto now = std::chrono::steady_clock::now();
+    fprintf(stderr, "sg-phase %-22s %8.3f ms (at %8.3f)\n", name,
+            std::chrono::duration<double, std::milli>(now - last).count(),
+            std::chrono::duration<double, std::milli>(now - t0).count());
+    last = now;
+  }
+};
+
 void push_obj(const sg_proof_stream* ps, uint8_t code, const uint8_t* p, size_t len);
 // one object's payload, written in place into a native stream (sg_stream_callbacks) or staged
 // for the push callback of any other stream: p = begin(code, len); fill p[0..len); commit()

@@ -203,7 +203,7 @@ DPoly poly_mul_exact(sg_ctx* ctx, const fe* a, uint64_t la, const fe* b, uint64_
 }
 
 void ref_inner_ntt(sg_ctx* ctx, const fe& root, uint64_t order, const fe* p, uint64_t len, const fe* scale,
-                   DevBuf& out, uint64_t& out_len) {
+                   DevBuf& out, uint64_t& out_len, const fe* host_copy) {
   // the reference's inner(): pad to `order` only when shorter, optional scale, ntt
   out_len = std::max<uint64_t>(next_pow2(std::max<uint64_t>(len, 1)), order);
   out = DevBuf(ctx, out_len * sizeof(fe));
@@ -211,8 +211,12 @@ void ref_inner_ntt(sg_ctx* ctx, const fe& root, uint64_t order, const fe* p, uin
     // a tiny polynomial (a boundary zerofier): its NTT is its values at offset root^k -- Horner
     SmallPoly sp{};
     sp.len = (int)len;
-    SG_HIP(hipMemcpyAsync(sp.c, p, len * sizeof(fe), hipMemcpyDeviceToHost, ctx->stream));
-    SG_HIP(hipStreamSynchronize(ctx->stream));
+    if (host_copy) {
+      memcpy(sp.c, host_copy, len * sizeof(fe));
+    } else {
+      SG_HIP(hipMemcpyAsync(sp.c, p, len * sizeof(fe), hipMemcpyDeviceToHost, ctx->stream));
+      SG_HIP(hipStreamSynchronize(ctx->stream));
+    }
     const fe *A, *B;
     pow_tables2(ctx, root, order, &A, &B);
     SG_HIP(launch_eval_small(out.as<fe>(), sp, order, A, B, to_mont(scale ? *scale : fe_one()), ctx->stream));
@@ -276,7 +280,7 @@ DPoly fast_multiply_dev(sg_ctx* ctx, fe root, uint64_t root_order, const fe* a, 
 }
 
 DPoly fast_coset_divide_dev(sg_ctx* ctx, fe root, uint64_t root_order, const fe& offset, const fe* lhs, uint64_t ll,
-                            const fe* rhs, uint64_t lr, int64_t rhs_degree) {
+                            const fe* rhs, uint64_t lr, int64_t rhs_degree, const fe* rhs_host) {
   check_root(root, root_order);
   int64_t dl, dr;
   if (rhs_degree >= -1) {
@@ -293,7 +297,7 @@ DPoly fast_coset_divide_dev(sg_ctx* ctx, fe root, uint64_t root_order, const fe&
   DevBuf vl, vr;
   uint64_t nl, nr;
   ref_inner_ntt(ctx, pl.root, pl.order, lhs, ll, &offset, vl, nl);
-  ref_inner_ntt(ctx, pl.root, pl.order, rhs, lr, &offset, vr, nr);
+  ref_inner_ntt(ctx, pl.root, pl.order, rhs, lr, &offset, vr, nr, rhs_host);
   return coset_divide_finish(ctx, pl, offset, vl.as<fe>(), vr.as<fe>());
 }
 

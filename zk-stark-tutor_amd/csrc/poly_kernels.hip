@@ -12,6 +12,7 @@
 #include <cstdint>
 
 #include "dev_util.hpp"
+#include <cstdlib>
 #include "fe128.hpp"
 #include "poly_kernels.hpp"
 #include "profiler.hpp"
@@ -391,13 +392,22 @@ hipError_t launch_deriv(fe* out, const fe* c, uint64_t n, const fe& r2, hipStrea
 hipError_t launch_batch_div(fe* out, const fe* a, const fe* b, uint64_t n, const fe& r2, const fe& one_m,
                             unsigned* zero_flag, hipStream_t s) {
   if (!n) return hipSuccess;
-  constexpr int K = 16;
   ProfScope ps("batch_div", (a ? 48 : 32) * n, s);
-  // lanes = ceil(n / K), at least one full block
-  uint64_t lanes = (n + K - 1) / K;
+  // K elements per lane amortize one Fermat inversion (~160 dependent products); below
+  // ~2^17 lanes the chip is latency-bound on that chain, so small n trades the
+  // amortization for lanes: K = 16 from n = 2^21, 8 from 2^20, else 4
+  static const int env_k = [] {
+    const char* v = getenv("SG_BATCH_DIV_K");
+    return v && *v ? atoi(v) : 0;
+  }();
+  const int K = env_k == 4 || env_k == 8 || env_k == 16 ? env_k : n >= ((uint64_t)1 << 21) ? 16 : n >= ((uint64_t)1 << 20) ? 8 : 4;
+  uint64_t lanes = (n + K - 1) / K;  // at least one full block
   uint64_t blocks = (lanes + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL((k_batch_div<K>), dim3((unsigned)blocks), dim3(kBlock), 0, s, out, a, b, n, r2, one_m,
-                     zero_flag);
+  switch (K) {
+    case 4: hipLaunchKernelGGL((k_batch_div<4>), dim3((unsigned)blocks), dim3(kBlock), 0, s, out, a, b, n, r2, one_m, zero_flag); break;
+    case 8: hipLaunchKernelGGL((k_batch_div<8>), dim3((unsigned)blocks), dim3(kBlock), 0, s, out, a, b, n, r2, one_m, zero_flag); break;
+    default: hipLaunchKernelGGL((k_batch_div<16>), dim3((unsigned)blocks), dim3(kBlock), 0, s, out, a, b, n, r2, one_m, zero_flag); break;
+  }
   return hipGetLastError();
 }
 

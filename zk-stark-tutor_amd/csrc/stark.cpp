@@ -537,21 +537,6 @@ std::vector<fe> sample_weights(size_t number, const uint8_t* randomness, size_t 
   return out;
 }
 
-// SG_PROVE_TIMING=1: host-clock phase marks of stark_prove on stderr (diagnostics only)
-struct PhaseMarks {
-  bool on;
-  std::chrono::steady_clock::time_point t0, last;
-  PhaseMarks() : on(getenv("SG_PROVE_TIMING") != nullptr), t0(std::chrono::steady_clock::now()), last(t0) {}
-  void operator()(const char* name) {
-    if (!on) return;
-    auto now = std::chrono::steady_clock::now();
-    fprintf(stderr, "sg-phase %-22s %8.3f ms (at %8.3f)\n", name,
-            std::chrono::duration<double, std::milli>(now - last).count(),
-            std::chrono::duration<double, std::milli>(now - t0).count());
-    last = now;
-  }
-};
-
 // Drains the side stream when the prover's scope ends (normally already joined; on an
 // error it keeps the pool from handing out buffers a side-stream kernel still uses).
 // Declared after the buffers the side stream touches, so it runs before they are released.
@@ -634,7 +619,8 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
     DPoly Z = dpoly_upload(ctx, bz[s].data(), bz[s].size());
     DPoly diff = lincomb(ctx, {{trace_polys[s].p(), 0, trace_polys[s].len, fe_one()},
                                {I.p(), 0, I.len, fe_neg(fe_one())}});
-    bqs.push_back(fast_coset_divide_dev(ctx, st.omicron, D, g, diff.p(), diff.len, Z.p(), Z.len, hp_degree(bz[s])));
+    bqs.push_back(fast_coset_divide_dev(ctx, st.omicron, D, g, diff.p(), diff.len, Z.p(), Z.len, hp_degree(bz[s]),
+                                        bz[s].data()));
   }
   mark("boundary_quotients");
   // boundary-quotient codewords (stark.rs:367-386); their trees hash on the side stream
@@ -668,7 +654,8 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
   const uint64_t T = st.original_trace_length;
   SG_REQUIRE(T >= 2, "transition zerofier needs a trace of at least two rows");
   DPoly tz = zerofier_geometric_dev(ctx, st.omicron, D, T - 1);
-  const int64_t dtz = dev_degree(ctx, tz.p(), tz.len);
+  // prod_{i < T-1} (x - omicron^i) is monic of degree T - 1 (< D: no wrap-around)
+  const int64_t dtz = tz.len == T && T - 1 < D ? (int64_t)(T - 1) : dev_degree(ctx, tz.p(), tz.len);
   std::map<uint64_t, AirCoset> cosets;
   std::map<uint64_t, std::pair<DevBuf, uint64_t>> tz_ntt;  // order -> NTT of scale(tz, g)
   std::vector<DPoly> tqs;
@@ -807,6 +794,7 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
   std::vector<uint64_t> quad = dup;
   for (uint64_t i : dup) quad.push_back((i + Nf / 2) % Nf);
   std::sort(quad.begin(), quad.end());
+  mark("openings_indices");
   std::vector<std::pair<const fe*, const sg_tree*>> cts;
   for (size_t s = 0; s < m; ++s) cts.emplace_back(bq_cw[s].p(), bq_trees[s].get());
   cts.emplace_back(r_cw.p(), r_tree.get());
