@@ -77,6 +77,42 @@ def test_host_transcript_matches_oracle():
     assert sg.IndependentProofStream().digest() == bytes(16)
 
 
+def test_host_transcript_long_streams_match_oracle():
+    """Streams past several sponge blocks and arena growth steps, both stream kinds,
+    repeated so released arenas are reused (proof_stream.rs:15-78, rescue_prime/proof_stream.rs:9-61)."""
+    import random
+    rng = random.Random(7)
+
+    def rand_obj():
+        k = rng.randrange(5)
+        if k == 0:
+            return (o.ROOT, rng.randbytes(64))
+        if k == 1:
+            return (o.PATH, [rng.randbytes(64) for _ in range(rng.randrange(1, 12))])
+        if k == 2:
+            return (o.CODEWORD, [rng.randrange(o.P) for _ in range(rng.randrange(0, 40))])
+        if k == 3:
+            return (o.LEAFS, tuple(rng.randrange(o.P) for _ in range(3)))
+        return (o.VALUE, rng.randrange(o.P))
+
+    for rep in range(3):
+        doc = rng.randbytes(rng.randrange(0, 200))
+        pairs = [(sg.IndependentProofStream(), o.IndependentProofStream()),
+                 (sg.SignatureProofStream(doc), o.SignatureProofStream(doc))]
+        for s, ref in pairs:
+            for i in range(120):
+                ob = rand_obj()
+                s.push(ob)
+                ref.push(ob)
+                if i % 7 == 0:
+                    assert s.fiat_shamir_prover(32) == ref.fiat_shamir_prover(32)
+            assert s.fiat_shamir_prover(64) == ref.fiat_shamir_prover(64)
+            assert s.digest() == ref.digest()
+            for _ in range(50):
+                assert o.serialize([s.pull()]) == o.serialize([ref.pull()])
+            assert s.fiat_shamir_verifier(48) == ref.fiat_shamir_verifier(48)
+
+
 # ---------------------------------------------------------------- host-only native logic
 
 def test_host_rescue_prime_matches_reference_kats():

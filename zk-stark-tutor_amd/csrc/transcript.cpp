@@ -44,9 +44,10 @@ void ByteBuf::swap(ByteBuf& o) {
 namespace {
 
 // released bodies keep their (warm) pages for the next stream: one proof stream per proof
-std::mutex g_body_mu;
+// (never destroyed: streams may be released by a host runtime's own teardown after exit)
+std::mutex& g_body_mu = *new std::mutex;
 constexpr int kBodyCache = 2;
-ByteBuf g_bodies[kBodyCache];
+ByteBuf* const g_bodies = new ByteBuf[kBodyCache];
 int g_nbodies = 0;
 constexpr size_t kBodyMaxCached = (size_t)256 << 20;
 
