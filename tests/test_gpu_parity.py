@@ -260,6 +260,40 @@ def test_large_ntt_roundtrip_and_spot_checks():
         assert sg.to_ints(X[k:k + 1])[0] == o.evaluate(xs, wk)
 
 
+def _sparse(n, nnz, seed):
+    """(n, 2) limb array with nnz random field values at random positions, and those terms."""
+    rng = random.Random(seed)
+    terms = {rng.randrange(n): rng.randrange(o.P) for _ in range(nnz)}
+    x = np.zeros((n, 2), dtype=np.uint64)
+    for j, v in terms.items():
+        x[j, 0], x[j, 1] = v & (2**64 - 1), v >> 64
+    return x, terms
+
+
+def test_prove_size_ntt_and_lde_spot_checks():
+    """The prove's largest transforms (2^25 NTT, degree-2^22 LDE onto 2^25 coset points)
+    on sparse inputs whose outputs are cheap sums on the host: every stage's twiddles and
+    the whole pass plan enter each checked output; plus a dense 2^25 round trip."""
+    logn = 25
+    n = 1 << logn
+    w = o.primitive_nth_root(n)
+    rng = random.Random(25)
+    ks = [0, 1, n - 1, n // 2 + 3] + [rng.randrange(n) for _ in range(4)]
+    x, terms = _sparse(n, 40, 251)
+    X = sg.ntt(w, x)
+    for k in ks:
+        assert sg.to_ints(X[k:k + 1])[0] == sum(c * o.fpow(w, j * k) for j, c in terms.items()) % o.P
+    d = 1 << 22
+    c, cterms = _sparse(d, 40, 252)
+    out = sg.fast_coset_evaluate(w, n, o.GENERATOR, c)
+    for k in ks:
+        pt = o.GENERATOR * o.fpow(w, k) % o.P
+        assert sg.to_ints(out[k:k + 1])[0] == sum(v * o.fpow(pt, j) for j, v in cterms.items()) % o.P
+    dense = np.random.default_rng(253).integers(0, 2**63, size=(n, 2), dtype=np.uint64)
+    dense[:, 1] %= np.uint64(0xCB80000000000000)
+    assert np.array_equal(sg.intt(w, sg.ntt(w, dense)), dense)
+
+
 def test_batched_lde_and_trees_match_single():
     """sg_fast_coset_evaluate_batch_dev / sg_merkle_build_batch_dev == per-item calls == oracle."""
     import torch
