@@ -483,15 +483,8 @@ class RescuePrime:
         num = 2 * m * N
         seed = "Rescue-XLIX({},{},{},{})".format(P, m, capacity, security_level).encode()
         raw = shake256(seed, bytes_per_int * num)
-        out = []
-        f256 = [fpow(256, j) for j in range(bytes_per_int)]
-        for i in range(num):
-            chunk = raw[bytes_per_int * i: bytes_per_int * (i + 1)]
-            acc = 0
-            for j, b in enumerate(chunk):
-                acc = add_mod(acc, mul_mod(f256[j], b))
-            out.append(acc)
-        return out
+        # sum_j (256^j mod p) * b_j mod p == (little-endian integer of the chunk) mod p
+        return [int.from_bytes(raw[bytes_per_int * i: bytes_per_int * (i + 1)], "little") % P for i in range(num)]
 
     def _round(self, state: List[int], r: int) -> List[int]:
         """rescue_prime.rs:52-106 (one round: S-box, MDS, constants, inverse S-box, MDS, constants)."""
@@ -629,6 +622,17 @@ class Stark:
         dom = [self.omicron_pow(i) for i in range(self.original_trace_length - 1)]
         return fast_zerofier(self.omicron, self.omicron_domain_length, dom)
 
+    def transition_zerofier_at(self, xs: Sequence[int]) -> List[int]:
+        """transition_zerofier() (stark.rs:198-206) evaluated at each x: prod_{i < T-1} (x - omicron^i)."""
+        tdom = [self.omicron_pow(i) for i in range(self.original_trace_length - 1)]
+        out = []
+        for x in xs:
+            zx = 1
+            for d in tdom:
+                zx = zx * (x - d) % P
+            out.append(zx)
+        return out
+
     def boundary_zerofiers(self, boundary) -> List[Poly]:
         """stark.rs:208-226."""
         return [fast_zerofier(self.omicron, self.omicron_domain_length,
@@ -762,7 +766,7 @@ class Stark:
         tqdb = self.transition_quotient_degree_bounds(tcs)
         bqdb = self.boundary_quotient_degree_bounds(rtl, boundary)
         # transition_zerofier().evaluate(x) == prod_{i < T-1} (x - omicron^i), evaluated directly
-        tdom = [self.omicron_pow(i) for i in range(self.original_trace_length - 1)]
+        zxs = self.transition_zerofier_at([mul_mod(self.fri.offset, fpow(self.fri.omega, ic)) for ic in indices])
         for ii, ic in enumerate(indices):
             x = mul_mod(self.fri.offset, fpow(self.fri.omega, ic))
             inx = (ic + self.expansion_factor) % N
@@ -774,9 +778,7 @@ class Stark:
             point = [x] + cur + nxt
             tvals = [tc.evaluate(point) for tc in tcs]
             terms = [rnd[ic]]
-            zx = 1
-            for d in tdom:
-                zx = zx * (x - d) % P
+            zx = zxs[ii]
             for s, tv in enumerate(tvals):
                 q = div(tv, zx)
                 terms.append(q)

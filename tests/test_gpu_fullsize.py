@@ -1,0 +1,207 @@
+"""Parity at BASELINE.json's full sizes (VERDICT r01 task 1), checked against the optimized CPU
+restatement (oracle/fast_cpu.cpp, itself pinned to the Python oracle and the reference's KATs by
+tests/test_oracle_fast.py) and against the oracle's own verifiers:
+
+* C2: dense 2^22-point forward + inverse NTT, element for element;
+* C3: FRI::prove at N = 2^24, expansion 8, 64 colinearity tests on the LDE of a seeded
+  degree < 2^21 polynomial: LDE elements, round-0 root and the complete proof-stream bytes equal
+  the checker's, the oracle's FRI.verify (fri.rs:250-416) accepts, a tampered codeword is
+  rejected (fri.rs:514-528);
+* the bench workload: Stark::prove on a Rescue-Prime trace of 2^20 - 1 randomized rows (FRI
+  domain 2^25) verified by the oracle's Stark.verify (stark.rs:565-770) with the AIR evaluated
+  from its structure, and a false claim rejected;
+* C5: the 2^27-point NTT sharded over 2 and 8 ranks (one process per rank on this box's one GPU,
+  gloo host-staged exchange) bit-identical to the single-GPU transform and to the checker.
+"""
+import hashlib
+import os
+import shutil
+import socket
+import tempfile
+import time
+
+import numpy as np
+import pytest
+
+import stark_oracle as o
+import stark_prove_oracle as e
+import starkgpu as sg
+
+pytestmark = pytest.mark.gpu
+P = o.P
+
+
+@pytest.fixture(scope="module")
+def fc():
+    import fast_cpu
+    fast_cpu.lib()
+    return fast_cpu
+
+
+def synthetic(seed: int, tag: bytes, n: int) -> np.ndarray:
+    """SURVEY.md 8(d) value generator: BE 16-byte chunks of SHAKE256(b"sg-bench" || seed || tag) mod p."""
+    raw = hashlib.shake_256(b"sg-bench" + seed.to_bytes(8, "big") + tag).digest(16 * n)
+    be = np.frombuffer(raw, dtype=">u8").reshape(n, 2)
+    hi, lo = be[:, 0].astype(np.uint64), be[:, 1].astype(np.uint64)
+    p_hi, p_lo = np.uint64(P >> 64), np.uint64(P & (2**64 - 1))
+    ge = (hi > p_hi) | ((hi == p_hi) & (lo >= p_lo))
+    borrow = (lo < p_lo) & ge
+    lo = np.where(ge, lo - p_lo, lo)
+    hi = np.where(ge, hi - p_hi - borrow.astype(np.uint64), hi)
+    return np.ascontiguousarray(np.stack([lo, hi], axis=1))
+
+
+def _const(n: int, v: int) -> np.ndarray:
+    x = np.empty((n, 2), dtype=np.uint64)
+    x[:, 0], x[:, 1] = v & (2**64 - 1), v >> 64
+    return x
+
+
+# ------------------------------------------------------------------ C2
+
+def test_c2_dense_2p22_ntt_intt_elementwise(fc):
+    n = 1 << 22
+    root = o.primitive_nth_root(n)
+    x = synthetic(0, b"c2", n)
+    X = sg.ntt(root, x)
+    assert np.array_equal(X, fc.ntt(root, x)), "ntt 2^22 != checker"
+    Y = sg.intt(root, X)
+    assert np.array_equal(Y, fc.intt(root, X)), "intt 2^22 != checker"
+    assert np.array_equal(Y, x)
+    # edge fixtures: all p - 1, an impulse at n - 1, a zero-padded length
+    for v in (_const(n, P - 1), np.zeros((n, 2), dtype=np.uint64)):
+        assert np.array_equal(sg.ntt(root, v), fc.ntt(root, v))
+    imp = np.zeros((n, 2), dtype=np.uint64)
+    imp[n - 1, 0] = 1
+    assert np.array_equal(sg.ntt(root, imp), fc.ntt(root, imp))
+    ragged = x[: n - 5]
+    assert np.array_equal(sg.ntt(root, ragged), fc.ntt(root, ragged))
+
+
+# ------------------------------------------------------------------ C3
+
+def test_c3_fri_prove_2p24_exp8_c64(fc):
+    N, exp, c = 1 << 24, 8, 64
+    d = N // exp
+    w = o.primitive_nth_root(N)
+    coeffs = synthetic(0, b"c3", d)
+    cw = sg.fast_coset_evaluate(w, N, o.GENERATOR, coeffs)
+    assert np.array_equal(cw, fc.fast_coset_evaluate(w, N, o.GENERATOR, coeffs)), "LDE 2^21 -> 2^24 != checker"
+    gps = sg.IndependentProofStream()
+    top = sg.FRI(o.GENERATOR, w, N, exp, c).prove(cw, gps)
+    ref, ref_top = fc.fri_prove(o.GENERATOR, w, cw, exp, c)
+    objs = gps.objects()
+    assert objs[0] == (o.ROOT, fc.merkle_commit(cw)), "round-0 root != checker"
+    assert top == ref_top
+    assert gps.digest() == ref, "FRI::prove proof bytes != checker"
+    ofri = o.FRI(o.GENERATOR, w, N, exp, c)
+    assert len([ob for ob in objs if ob[0] == o.ROOT]) == ofri.num_rounds() == 16
+    ok, err, _ = ofri.verify(o.IndependentProofStream(objs))
+    assert ok, err
+    # fri.rs:514-528: zero a third of the low-degree positions -> verify fails
+    bad = cw.copy()
+    bad[: (d - 1) // 3] = 0
+    bps = sg.IndependentProofStream()
+    sg.FRI(o.GENERATOR, w, N, exp, c).prove(bad, bps)
+    ok, _, _ = ofri.verify(o.IndependentProofStream(bps.objects()))
+    assert not ok
+
+
+# ------------------------------------------------------------------ headline prove
+
+def test_trace_2p20_headline_proof_verified(fc):
+    """bench.py's workload: Rescue-Prime m=2, N = 2^20 - 258 rounds (+256 randomizer rows =
+    2^20 - 1), expansion 8, c = 64, security 128, transition degree 3: omicron domain 2^22, FRI
+    domain 2^25.  Verified by the oracle verifier (AIR from its structure, C++ barycentric
+    round-constant interpolants and zerofier products)."""
+    N = (1 << 20) - 2 - 256
+    rp_g = sg.RescuePrime(2, 1, 128, N)
+    st_g = sg.Stark(8, 64, 128, 2, N + 1, 3)
+    assert st_g.omicron_domain_length == 1 << 22 and st_g.fri_domain_length == 1 << 25
+    air_g = rp_g.transition_constraints(st_g.omicron, st_g.omicron_domain_length)
+    rp_o = e.RescuePrime(2, 1, 128, N)
+    assert rp_g.round_constants == rp_o.round_constants
+    inp = o.sample(b"headline")
+    trace = rp_g.trace_array(inp)
+    out = sg.to_ints(trace[-2:-1])[0]  # last row, register 0: the hash output
+    nrc = st_g.num_randomizer_coefficients(air_g)
+    tr = synthetic(0, b"trace-rand", 2 * st_g.num_randomizers)
+    rc = synthetic(0, b"rand-poly", nrc)
+    bnd = rp_o.boundary_constraints(out)
+    ps = sg.IndependentProofStream()
+    t0 = time.perf_counter()
+    st_g.prove(trace, air_g, bnd, ps, tr, rc)
+    print("trace 2^20 prove (host buffers): %.1f ms, %d bytes" % ((time.perf_counter() - t0) * 1e3, len(ps.digest())))
+    objs = ps.objects()
+    vst = fc.verifier_stark(8, 64, 128, 2, N + 1, 3)
+    sair = fc.rescue_air_at_point(rp_o, vst.omicron)
+    assert st_g.transition_degree_bounds(air_g) == vst.transition_degree_bounds(sair)
+    ok, err = vst.verify(sair, bnd, o.IndependentProofStream(objs))
+    assert ok, err
+    ok, _ = vst.verify(sair, rp_o.boundary_constraints(o.add_mod(out, 1)), o.IndependentProofStream(objs))
+    assert not ok
+
+
+# ------------------------------------------------------------------ C5 sharded
+
+C5_LOG = 27
+
+
+def _c5_worker(rank, world, port, tmp):
+    import torch
+    import torch.distributed as dist
+    from starkgpu import dist as D
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ctx = sg.Context(0)
+        ds = D.DistStark(D.GpuRows(ctx), D.Comm())
+        n = 1 << C5_LOG
+        n1, n2 = D.plan(n, world)
+        rows, R = n1 // world, n2 // world
+        x = np.load(os.path.join(tmp, "x.npy"), mmap_mode="r")
+        X = np.load(os.path.join(tmp, "X.npy"), mmap_mode="r")
+        # column shard: row r = x[(rank rows + r) + N1 j2], j2 < N2
+        cols = np.ascontiguousarray(x.reshape(n2, n1, 2)[:, rank * rows:(rank + 1) * rows].transpose(1, 0, 2))
+        dev = torch.device("cuda", 0)
+        shard = torch.from_numpy(cols.view(np.int64).reshape(-1)).to(dev)
+        root = o.primitive_nth_root(n)
+        out = ds.ntt(root, shard, n2, n)
+        got = out.cpu().numpy().view(np.uint64).reshape(n1, R, 2)
+        want = X.reshape(n1, n2, 2)[:, rank * R:(rank + 1) * R]
+        ok = bool(np.array_equal(got, want))
+        flags = [None] * world
+        dist.all_gather_object(flags, ok)
+        assert all(flags), f"sharded 2^{C5_LOG} NTT differs from the single-GPU transform: {flags}"
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.fixture(scope="module")
+def c5_reference(fc):
+    """x (2^27 seeded elements) and X = single-GPU sg.ntt(x), checked against the CPU checker."""
+    n = 1 << C5_LOG
+    tmp = tempfile.mkdtemp(prefix="sg_c5_")
+    try:
+        rng = np.random.default_rng(2027)
+        x = rng.integers(0, 2**63, size=(n, 2), dtype=np.uint64)
+        x[:, 1] %= np.uint64(0xCB80000000000000)
+        root = o.primitive_nth_root(n)
+        X = sg.ntt(root, x)
+        assert np.array_equal(X, fc.ntt(root, x)), "single-GPU 2^27 NTT != checker"
+        np.save(os.path.join(tmp, "x.npy"), x)
+        np.save(os.path.join(tmp, "X.npy"), X)
+        del x, X
+        yield tmp
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_c5_sharded_2p27_ntt_one_gpu_gloo(c5_reference, world):
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.spawn(_c5_worker, args=(world, port, c5_reference), nprocs=world, join=True)

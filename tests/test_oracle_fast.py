@@ -1,0 +1,141 @@
+"""The optimized CPU checker (oracle/fast_cpu.cpp: Montgomery, OpenMP) agrees with the
+reference's known-answer vectors and with the Python restatement, so it
+can stand in for the oracle at sizes Python cannot reach (2^22..2^27 transforms, 2^24
+FRI proofs, trace-2^20 verification)."""
+import os
+import subprocess
+
+import pytest
+
+import stark_oracle as o
+import stark_prove_oracle as e
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def fc():
+    subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True, capture_output=True)
+    import fast_cpu
+    return fast_cpu
+
+
+def test_fast_checker_kats(fc, kats):
+    for v in kats["ntt"]:
+        root = o.primitive_nth_root(v["n"])
+        assert fc.ints(fc.ntt(root, [int(x) for x in v["input"]])) == [int(x) for x in v["output"]], v["src"]
+    for v in kats["intt"]:
+        root = o.primitive_nth_root(v["n"])
+        assert fc.ints(fc.intt(root, [int(x) for x in v["input"]])) == [int(x) for x in v["output"]], v["src"]
+    for v in kats["merkle_commit"]:
+        assert fc.merkle_commit([int(x) for x in v["leaves"]]).hex() == v["root_hex"], v["src"]
+    for v in kats["blake2b512"]:
+        assert fc.blake2b512(bytes.fromhex(v["in_hex"])).hex() == v["out_hex"], v["src"]
+    for v in kats["fe_mul"]:
+        a, b = fc.arr([int(v["a"])]), fc.arr([int(v["b"])])
+        out = fc.arr([0])
+        fc.lib().fc_mul(fc._p(a), fc._p(b), fc._p(out))
+        assert fc.ints(out)[0] == int(v["out"]), v["src"]
+    for v in kats["fe_inverse"]:
+        a, out = fc.arr([int(v["a"])]), fc.arr([0])
+        fc.lib().fc_inv(fc._p(a), fc._p(out))
+        assert fc.ints(out)[0] == int(v["out"]), v["src"]
+    # SHAKE256 vs hashlib over rate-boundary lengths (the KATs' inputs are Debug strings)
+    import hashlib
+    for n in (0, 1, 135, 136, 137, 300):
+        d = bytes(range(256)) * 2
+        assert fc.shake256(d[:n], 77) == hashlib.shake_256(d[:n]).digest(77)
+    for n in (0, 1, 127, 128, 129, 300):
+        d = bytes((7 * i) & 255 for i in range(n))
+        assert fc.blake2b512(d) == hashlib.blake2b(d, digest_size=64).digest()
+
+
+@pytest.mark.parametrize("logn", [0, 1, 2, 5, 10, 12, 13, 14])
+def test_fast_ntt_matches_oracle(fc, logn):
+    n = 1 << logn
+    x = o.synthetic_elements(logn, b"fast", n)
+    w = o.primitive_nth_root(n)
+    assert fc.ints(fc.ntt(w, x)) == o.ntt(w, x)
+    if n >= 2:
+        assert fc.ints(fc.intt(w, x)) == o.intt(w, x)
+        # zero padding (ntt.rs:14 bit_reverse_copy) and a non-primitive root (same DIT graph)
+        assert fc.ints(fc.ntt(w, x[: n // 2 + 1])) == o.ntt(w, x[: n // 2 + 1])
+        w2 = o.fpow(w, 2)
+        assert fc.ints(fc.ntt(w2, x)) == o.ntt(w2, x)
+    d = max(n // 8, 1)
+    assert fc.ints(fc.fast_coset_evaluate(w, n, o.GENERATOR, x[:d])) == o.fast_coset_evaluate(w, n, o.GENERATOR, x[:d])
+    assert fc.merkle_commit(x) == o.merkle_commit(x)
+
+
+def test_fast_edge_values(fc):
+    n = 1 << 10
+    w = o.primitive_nth_root(n)
+    for x in ([0] * n, [o.P - 1] * n, [1] + [0] * (n - 1), [0] * (n - 1) + [1]):
+        assert fc.ints(fc.ntt(w, x)) == o.ntt(w, x)
+        assert fc.merkle_commit(x) == o.merkle_commit(x)
+    assert fc.ints(fc.intt(w, [5])) == [5]  # ntt.rs:55-57: fewer than two elements unchanged
+
+
+@pytest.mark.parametrize("n,exp,c", [(1 << 11, 8, 16), (1 << 12, 4, 17), (1 << 13, 8, 64)])
+def test_fast_fri_prove_stream(fc, n, exp, c):
+    w = o.primitive_nth_root(n)
+    cw = o.fast_coset_evaluate(w, n, o.GENERATOR, o.synthetic_elements(3, b"fri", n // exp))
+    prefix = [(o.ROOT, bytes(range(64)))]
+    ps = o.IndependentProofStream(prefix)
+    top = o.FRI(o.GENERATOR, w, n, exp, c).prove(cw, ps)
+    data, ftop = fc.fri_prove(o.GENERATOR, w, cw, exp, c, prefix=o.serialize(prefix))
+    assert ftop == top
+    assert data == ps.digest()
+
+
+def test_fast_barycentric_and_zerofier(fc):
+    q = o.primitive_nth_root(1 << 8)
+    n = 100
+    cols = [o.synthetic_elements(1, b"c1", n), o.synthetic_elements(2, b"c2", n)]
+    xs = [o.GENERATOR, 12345, o.fpow(q, 150), o.fpow(q, 7)]  # off-domain points, then a node q^7
+    bary = e.GeometricBarycentric(q, n, {0: cols[0], 1: cols[1]})
+    got = fc.geometric_bary(q, cols, xs)
+    for j, x in enumerate(xs[:3]):
+        assert got[j] == [bary.value(x, 0), bary.value(x, 1)]
+    assert got[3] == [cols[0][7], cols[1][7]]  # at a node the interpolant takes the node's value
+    dom = [o.fpow(q, r) for r in range(n)]
+    for x, z in zip(xs, fc.geometric_prod(q, n, xs)):
+        want = 1
+        for d in dom:
+            want = want * (x - d) % o.P
+        assert z == want
+
+
+def test_fast_barycentric_handle(fc):
+    q = o.primitive_nth_root(1 << 9)
+    n = 300
+    cols = {"a": o.synthetic_elements(4, b"a", n), "b": o.synthetic_elements(5, b"b", n)}
+    ref = e.GeometricBarycentric(q, n, cols)
+    fast = fc.Barycentric(q, n, {k: fc.arr(v) for k, v in cols.items()})
+    for x in (o.GENERATOR, 777, o.fpow(o.GENERATOR, 5)):
+        for k in cols:
+            assert fast.value(x, k) == ref.value(x, k)
+
+
+def test_fast_verifier_pieces_verify_oracle_proof(fc):
+    """The accelerated verifier pieces the trace-2^20 GPU test uses (Rescue AIR at a point with
+    C++ barycentric interpolants, transition zerofier by C++ products) accept a proof made by the
+    oracle prover at the reference test's size (stark.rs:823-840) and reject a false claim."""
+    rp = e.RescuePrime(2, 1, 2, 27)
+    st = e.Stark(4, 2, 2, 2, 28, 2)
+    air = rp.transition_constraints(st.omicron, st.omicron_domain_length)
+    inp = o.sample(b"fastverify")
+    out = rp.hash(inp)
+    trace, bnd = rp.trace(inp), rp.boundary_constraints(out)
+    r = e.randomness_from_seed(b"fv", 2 * st.num_randomizers + st.num_randomizer_coefficients(air))
+    tr = [r[2 * i:2 * i + 2] for i in range(st.num_randomizers)]
+    rc = r[2 * st.num_randomizers:]
+    ps = o.IndependentProofStream()
+    st.prove(trace, air, bnd, ps, tr, rc)
+    vst = fc.verifier_stark(4, 2, 2, 2, 28, 2)
+    sair = fc.rescue_air_at_point(rp, vst.omicron)
+    assert vst.transition_degree_bounds(sair) == st.transition_degree_bounds(air)
+    ok, err = vst.verify(sair, bnd, o.IndependentProofStream(ps.objects))
+    assert ok, err
+    ok, _ = vst.verify(sair, rp.boundary_constraints(o.add_mod(out, 1)), o.IndependentProofStream(ps.objects))
+    assert not ok
