@@ -46,9 +46,9 @@ COLINEARITY = 64
 REGISTERS = 2       # Rescue-Prime m = 2
 HBM_PEAK_GBS = 8000.0
 # PMC HBM bytes of this workload's kernels (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes on
-# `bench.py --steps 3 --warmup 1 --no-side`, tools/_gpu_full_e2e.sh + tools/pmc_traffic.py)
-PMC_TRAFFIC_FILE = "r01_pmc_traffic_e2e.json"
-PMC_VALU_FILE = "r01_pmc_valu_e2e.json"  # SQ_INSTS_VALU pass (tools/_pmc_valu_e2e.sh + tools/pmc_valu.py)
+# `bench.py --steps 3 --warmup 1 --no-side`, tools/pmc_passes.sh + tools/pmc_traffic.py)
+PMC_TRAFFIC_FILE = "r02_pmc_traffic_e2e.json"
+PMC_VALU_FILE = "r02_pmc_valu_e2e.json"  # SQ_INSTS_VALU pass (tools/pmc_passes.sh + tools/pmc_valu.py)
 
 
 def synthetic_fe(seed: int, tag: bytes, n: int) -> np.ndarray:
@@ -335,57 +335,123 @@ def side_sharded(ctx: sg.Context, device, world: int, rank: int, iters: int = 3)
     return out
 
 
-def cpu_baseline_leg(seconds_budget: float = 15.0):
-    """The reference-faithful C restatement (oracle/ref_cpu.c) on one host core, on a bounded sample.
+def host_cpu_info() -> dict:
+    """The GPU box's host CPU as lscpu reports it (model, logical CPUs) and this process's affinity."""
+    info = {"affinity_cpus": len(os.sched_getaffinity(0))}
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            k, _, v = line.partition(":")
+            if k.strip() in ("Model name", "CPU(s)", "Socket(s)", "Thread(s) per core"):
+                info[k.strip()] = v.strip()
+    except (OSError, subprocess.SubprocessError):
+        pass
+    return info
 
-    The LDE + commit + FRI part of the prove (4 LDEs, 3 Merkle commits, FRI commit +
-    query with the reference's O(n)-per-opening Merkle::open) at trace 2^9
-    (N = 2^12), repeated until ~seconds_budget of CPU time.  The reference's
-    trace interpolation and quotient algebra are O(T^2) and are
-    timed separately through the Python restatement (cpu_baseline_e2e).
+
+def faithful_block_step(rc, o, N: int) -> float:
+    """One LDE + commit + FRI block (4 LDEs of N/32 coefficients onto N points, 3 Merkle commits, FRI
+    commit + query with the reference's O(n)-per-opening Merkle::open) through oracle/ref_cpu.c; seconds.
+    d = N/32 is the headline prove's shape: quotients of degree ~2^20 on a FRI domain of 2^25."""
+    d = N // 32
+    omega = o.primitive_nth_root(N)
+    polys = [synthetic_fe(0, t, d) for t in (b"bq0", b"bq1", b"rand", b"comb")]
+    fri = o.FRI(o.GENERATOR, omega, N, EXPANSION, COLINEARITY)
+    t0 = time.perf_counter()
+    stream = bytes(16)
+    for k in range(REGISTERS + 1):
+        cw = rc.fast_coset_evaluate(omega, N, o.GENERATOR, polys[k])
+        stream += bytes([0]) + (64).to_bytes(8, "big") + rc.merkle_commit(cw)
+    o.shake256(stream, o.PROOF_BYTES)  # combination weights
+    cw = rc.fast_coset_evaluate(omega, N, o.GENERATOR, polys[3])
+    stream, roots, cws = rc.fri_commit(o.GENERATOR, omega, cw, EXPANSION, COLINEARITY, prefix=stream,
+                                       want_codewords=True)
+    top = fri.sample_indices(o.shake256(stream, o.PROOF_BYTES), len(cws[1]), len(cws[-1]), COLINEARITY)
+    idx = list(top)
+    for r in range(len(cws) - 1):  # fri.rs:231-245 -> query (fri.rs:174-208)
+        half = len(cws[r]) // 2
+        idx = [i % half for i in idx]
+        for i in idx:
+            rc.merkle_open(i, cws[r])
+            rc.merkle_open(i + half, cws[r])
+            rc.merkle_open(i, cws[r + 1])
+    return time.perf_counter() - t0
+
+
+def cpu_baseline_leg(headline_N: int, log_Ns=(12, 13, 14, 15, 16)) -> dict:
+    """The reference-faithful C restatement (oracle/ref_cpu.c: bit-serial mul_mod, xgcd inverse,
+    per-element pow + division in the fold, recursive Merkle with to_string leaves and O(n) opens)
+    on ONE host core -- the reference is single-threaded.
+
+    The prove's LDE + commit + FRI block is timed at N = 2^12 .. 2^16, one step each, and
+    extrapolated to the headline FRI domain N = 2^25 with the block's cost model
+    t(N) = a N log2 N + b N (NTTs; hashing, folds and the O(N) opens), fitted by least squares
+    (SURVEY.md 8(d)(i)).  The reference's trace interpolation and quotient algebra are O(T^2)
+    and are not in this leg (cpu_baseline_e2e times them through the Python restatement).
     """
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import ref_cpu as rc
     import stark_oracle as o
-    log_trace = 9
-    d = 1 << log_trace
-    N = d * EXPANSION
-    omega = o.primitive_nth_root(N)
-    polys = [synthetic_fe(0, t, d) for t in (b"bq0", b"bq1", b"rand", b"comb")]
-    fri = o.FRI(o.GENERATOR, omega, N, EXPANSION, COLINEARITY)
-    steps = 0
-    t0 = time.perf_counter()
-    while True:
-        stream = bytes(16)
-        for k in range(REGISTERS + 1):
-            cw = rc.fast_coset_evaluate(omega, N, o.GENERATOR, polys[k])
-            stream += bytes([0]) + (64).to_bytes(8, "big") + rc.merkle_commit(cw)
-        o.shake256(stream, o.PROOF_BYTES)  # combination weights
-        cw = rc.fast_coset_evaluate(omega, N, o.GENERATOR, polys[3])
-        stream, roots, cws = rc.fri_commit(o.GENERATOR, omega, cw, EXPANSION, COLINEARITY, prefix=stream,
-                                           want_codewords=True)
-        top = fri.sample_indices(o.shake256(stream, o.PROOF_BYTES), len(cws[1]), len(cws[-1]), COLINEARITY)
-        idx = list(top)
-        for r in range(len(cws) - 1):  # fri.rs:231-245 -> query (fri.rs:174-208)
-            half = len(cws[r]) // 2
-            idx = [i % half for i in idx]
-            for i in idx:
-                rc.merkle_open(i, cws[r])
-                rc.merkle_open(i + half, cws[r])
-                rc.merkle_open(i, cws[r + 1])
-        steps += 1
-        el = time.perf_counter() - t0
-        if el >= seconds_budget or steps >= 20:
-            break
-    per_step = el / steps
+    pts = []
+    for ln in log_Ns:
+        pts.append((1 << ln, faithful_block_step(rc, o, 1 << ln)))
+    from scipy.optimize import nnls
+    A = np.array([[n * np.log2(n), n] for n, _ in pts], dtype=np.float64)
+    y = np.array([t for _, t in pts], dtype=np.float64)
+    (a, b), _ = nnls(A, y)  # non-negative least squares: both cost terms are real work
+    Nh = headline_N
+    t_h = a * Nh * np.log2(Nh) + b * Nh
+    N_last, t_last = pts[-1]
     return {
-        "value": round((REGISTERS + 2) * N / per_step / 1e9, 8),
+        "value": round((REGISTERS + 2) * N_last / t_last / 1e9, 8),
         "unit": "Gelem/s",
         "cores": 1,
         "kind": "port",
-        "sample": f"same block at trace 2^{log_trace} (N=2^{log_trace + 3}, c={COLINEARITY}), {steps} step(s), "
-                  f"{per_step * 1e3:.1f} ms/step; oracle/ref_cpu.c: bit-serial mul_mod, xgcd inverse, "
-                  f"per-element pow+div fold, O(n) Merkle opens, single thread",
+        "sample": f"the prove's LDE+commit+FRI block (4 LDEs, 3 commits, FRI prove, c={COLINEARITY}) at "
+                  f"N=2^{N_last.bit_length() - 1} on one core (value), measured at "
+                  + ", ".join(f"2^{n.bit_length() - 1}: {t:.2f} s" for n, t in pts)
+                  + "; oracle/ref_cpu.c keeps the reference's algorithms",
+        "extrapolated_headline": {"N": Nh, "block_s": round(float(t_h), 1),
+                                  "value": round((REGISTERS + 2) * Nh / float(t_h) / 1e9, 8),
+                                  "model": f"t = {a:.3e} N log2 N + {b:.3e} N (least squares over the "
+                                           f"measured points, non-negative)", "label": "extrapolated"},
+    }
+
+
+def cpu_baseline_allcores(N: int) -> dict:
+    """The optimized C++ restatement (oracle/fast_cpu.cpp: Montgomery arithmetic, twiddle tables,
+    OpenMP over every host core) on the headline block AT the headline size: LDEs of 2^20
+    coefficients (the trace-2^20 quotients) onto the FRI domain N = 2^25, Merkle commits of 2^25
+    leaves, FRI::prove(2^25, expansion 8, c=64).
+
+    Each component is timed once at full size and the block composed exactly as the prove runs it
+    (4 LDEs + 3 commits + FRI prove, the FRI prove committing its own codeword), so the sample is
+    ~one block of CPU time."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import fast_cpu as fc
+    import stark_oracle as o
+    d = N // 32
+    omega = o.primitive_nth_root(N)
+    coeffs = synthetic_fe(0, b"comb", d)
+    t0 = time.perf_counter()
+    cw = fc.fast_coset_evaluate(omega, N, o.GENERATOR, coeffs)
+    t1 = time.perf_counter()
+    fc.merkle_commit(cw)
+    t2 = time.perf_counter()
+    fc.fri_prove(o.GENERATOR, omega, cw, EXPANSION, COLINEARITY)
+    t3 = time.perf_counter()
+    lde, mk, fri = t1 - t0, t2 - t1, t3 - t2
+    block = (REGISTERS + 2) * lde + (REGISTERS + 1) * mk + fri
+    return {
+        "value": round((REGISTERS + 2) * N / block / 1e9, 6),
+        "unit": "Gelem/s",
+        "cores": fc.threads(),
+        "kind": "port",
+        "sample": f"the prove's LDE+commit+FRI block at the headline size (d=2^{d.bit_length() - 1} -> "
+                  f"N=2^{N.bit_length() - 1}): "
+                  f"LDE {lde:.2f} s, Merkle commit {mk:.2f} s, FRI prove {fri:.2f} s, each timed once; "
+                  f"block = 4 LDE + 3 commits + FRI = {block:.1f} s; oracle/fast_cpu.cpp (Montgomery, OpenMP)",
+        "host": host_cpu_info(),
     }
 
 
@@ -511,29 +577,48 @@ def main():
     pmc_file = os.path.join(ROOT, "profiles", PMC_TRAFFIC_FILE)
     if os.path.exists(pmc_file) and args.log_trace == LOG_TRACE:
         pmc = json.load(open(pmc_file))["kernels"].get(name)
-        if pmc:
-            traffic = int(pmc["hbm_bytes_per_launch"])
-            traffic_src = f"profiles/{PMC_TRAFFIC_FILE} (FETCH_SIZE x2 + WRITE_SIZE per launch, same workload)"
-    # VALU issue of the dominant kernel (rocprofv3 SQ_INSTS_VALU pass on this workload): the
-    # kernels are integer-VALU-bound, so this is the roof that actually binds them
+        if pmc and pmc.get("hbm_bytes_per_lane") and st.get("elems"):
+            traffic = int(pmc["hbm_bytes_per_lane"] * st["elems"] / st["launches"])
+            traffic_src = (f"profiles/{PMC_TRAFFIC_FILE} (FETCH_SIZE x2 + WRITE_SIZE per lane of the same workload, "
+                           f"scaled to the live launches' lanes)")
+    # VALU issue of the dominant kernel: instructions per wave from a rocprofv3 SQ_INSTS_VALU pass on
+    # this workload (tools/pmc_valu.py), times the waves the live launches ran (their lane count),
+    # over their live duration -- one launch population.  The kernels are integer-VALU-bound, so this
+    # is the roof that actually binds them.
     valu = None
     valu_file = os.path.join(ROOT, "profiles", PMC_VALU_FILE)
-    if os.path.exists(valu_file) and args.log_trace == LOG_TRACE:
+    if os.path.exists(valu_file) and st.get("elems"):
         vk = json.load(open(valu_file))["kernels"].get(name)
         if vk:
-            inst = vk["valu_wave_instr_per_launch"] * st["launches"] / max(st["launches"], 1)
-            live = inst / (st["ms"] / st["launches"] * 1e-3)
-            valu = {"unit": "wave64 VALU instr/s", "instr_per_launch": int(inst),
+            inst = vk["valu_instr_per_wave"] * st["elems"] / 64.0
+            live = inst / (st["ms"] * 1e-3)
+            valu = {"unit": "wave64 VALU instr/s", "instr_per_launch": int(inst / st["launches"]),
+                    "instr_per_wave": round(vk["valu_instr_per_wave"], 1),
                     "achieved": round(live, -6), "peak": round(vk["peak_wave_instr_per_s"], -6),
-                    "frac": round(live / vk["peak_wave_instr_per_s"], 4), "clock_ghz": round(vk["clock_ghz"], 3),
-                    "source": f"profiles/{PMC_VALU_FILE} (SQ_INSTS_VALU per launch; roof = 1 instr/SIMD/4 clk, "
-                              f"1024 SIMDs, measured clock); achieved uses the live launch time"}
+                    "frac": round(live / vk["peak_wave_instr_per_s"], 4),
+                    "mix_roof": round(vk.get("mix_roof_wave_instr_per_s", 0.0), -6) or None,
+                    "mix_frac": round(live / vk["mix_roof_wave_instr_per_s"], 4)
+                    if vk.get("mix_roof_wave_instr_per_s") else None,
+                    "clock_ghz": round(vk["clock_ghz"], 3),
+                    "source": f"profiles/{PMC_VALU_FILE} (SQ_INSTS_VALU per wave); peak = 1 wave64 instr / SIMD / "
+                              f"2 clk (SIMD-32) x 1024 SIMDs at the PMC pass's clock; mix_roof = the kernel's "
+                              f"full/half-rate instruction mix at the measured per-op rates (tools/valu_mix.py); "
+                              f"achieved = per-wave count x the live launches' waves / their live time"}
     # the same kernel alone on the chip (in the prove, the boundary-quotient and randomizer
     # trees share the CUs with the main stream's algebra, which stretches their launches)
     alone = standalone_launch(ctx, device, name, wl.fri_len)
     phases = {k: {"launches": v["launches"], "ms_per_step": round(v["ms"], 4),
                   "GBps": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1) if v["ms"] > 0 else None}
               for k, v in sorted(breakdown.items(), key=lambda kv: -kv[1]["ms"])}
+    # the workload's own NTT throughput: transform elements of every NTT/INTT/LDE in one prove over
+    # the device time of all their passes (last warmup step, every launch event-timed)
+    ntt_keys = [k for k in breakdown if k.startswith(("ntt_", "bitrev_gather", "scale_const"))]
+    ntt_ms = sum(breakdown[k]["ms"] for k in ntt_keys)
+    ntt_elems = sum(breakdown[k].get("elems", 0) for k in ntt_keys)
+    ntt_stats = {"ntt_gelem_s": round(ntt_elems / (ntt_ms * 1e-3) / 1e9, 3) if ntt_ms > 0 else None,
+                 "ntt_elements_per_prove": int(ntt_elems), "ntt_device_ms_per_prove": round(ntt_ms, 3),
+                 "definition": "sum of transform lengths (NTT, INTT, LDE) in one prove / device time of their "
+                               "passes, each launch timed with HIP events in the last warmup step"}
 
     result = {
         "metric": "NTT Gelem/s + prove ms, Rescue-Prime trace 2^20, at 1/2/4/8 MI355X",
@@ -550,27 +635,37 @@ def main():
         "dtype": "u128 (F_p, p = 1 + 407*2^119)",
         "data": "synthetic: Rescue-Prime execution trace of a seeded input; randomizers from a seeded "
                 "SHAKE256 stream (SURVEY.md 8(d))",
+        "ntt": ntt_stats,
         "config": {"workload": f"Stark::prove, Rescue-Prime m={REGISTERS} trace {wl.rows} rows "
                                f"(+{wl.stark.num_randomizers} randomizers = 2^{args.log_trace} - 1), "
                                f"expansion {EXPANSION}, c={COLINEARITY}, security 128, transition degree 3 "
                                f"(omicron domain 2^{wl.stark.omicron_domain_length.bit_length() - 1}, "
                                f"FRI domain 2^{wl.fri_len.bit_length() - 1})",
                    "codeword_elements_per_step_per_gpu": wl.elements_per_step(),
+                   "value_definition": "Gelem/s = committed codeword elements per second over all ranks: "
+                                       "(m + 2) codewords of the FRI domain per proof (2 boundary quotients, the "
+                                       "randomizer, the combination) x proofs / wall time; prove_ms = ms per "
+                                       "proof; the workload's NTT rate is ntt.ntt_gelem_s",
                    "proof_bytes": len(wl.last_proof.digest()) if wl.last_proof is not None else None,
                    "parallelism": f"replicas x{world} (independent traces, no data-path collective)"},
-        "roofline": {"kernel": name, "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+        "roofline": {"kernel": name, "bound": "hbm", "binding": "valu" if valu else "hbm",
+                     "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                      "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "traffic_source": traffic_src,
                      "avg_launch_ms": round(st["ms"] / st["launches"], 4),
                      "launches": st["launches"],
                      "alg_bytes_per_launch": int(st["bytes"] / st["launches"]),
-                     "note": "integer-VALU-bound (BLAKE2b / 128-bit Montgomery): see roofline.valu and DESIGN.md "
-                             "section 4; launches overlap other kernels (side stream), standalone = alone on the chip",
+                     "note": "achieved/peak/frac are the contract's HBM roofline (algorithmic bytes / live launch "
+                             "time vs 8 TB/s); the roof that binds this integer kernel is VALU issue "
+                             "(binding = valu): roofline.valu gives its fraction of the SIMD-32 peak and of its "
+                             "instruction-mix roof (DESIGN.md section 4); launches overlap other kernels (side "
+                             "stream), standalone = alone on the chip",
                      "valu": valu,
                      "standalone": alone},
         "kernels_one_step": phases,  # every launch timed, last warmup step
         "host_phases_ms": {k: round(v / args.steps * 1e3, 3) for k, v in host_phases.items()},
     }
+    fri_len = wl.fri_len
     if world == 1 and not args.no_side:
         del wl
         ctx.trim()
@@ -595,7 +690,8 @@ def main():
         if watchdog is not None:
             watchdog.cancel()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline_leg()
+        result["cpu_baseline"] = cpu_baseline_leg(fri_len)
+        result["cpu_baseline_allcores"] = cpu_baseline_allcores(fri_len)
         result["cpu_baseline_e2e"] = cpu_baseline_e2e()
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -1,4 +1,5 @@
-# PMC refresh of the E2E step: FETCH_SIZE / WRITE_SIZE / VALU passes, one counter group per run
+# PMC passes of the E2E step: FETCH_SIZE / WRITE_SIZE / VALU, one counter group per run; then
+# reduce locally: tools/pmc_traffic.py (HBM bytes per lane) and tools/pmc_valu.py (VALU per wave)
 set -e
 cd /tmp && export TMPDIR=/tmp
 R=$GRAFT_REPO_ROOT

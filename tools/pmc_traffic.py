@@ -32,7 +32,7 @@ def load(fn):
     for r in csv.DictReader(open(fn)):
         a = alias(r["Kernel_Name"])
         if a:
-            out[a].append(float(r["Counter_Value"]) * 1024.0)
+            out[a].append((float(r["Counter_Value"]) * 1024.0, int(r["Grid_Size"])))
     return out
 
 
@@ -41,10 +41,13 @@ def main():
     res = {}
     for k in sorted(set(fetch) & set(write)):
         n = min(len(fetch[k]), len(write[k]))
-        rd = 2.0 * sum(fetch[k][:n]) / n
-        wr = sum(write[k][:n]) / n
-        res[k] = {"launches": n, "read_bytes_per_launch": rd, "write_bytes_per_launch": wr,
-                  "hbm_bytes_per_launch": rd + wr}
+        rd = 2.0 * sum(v for v, _ in fetch[k][:n])
+        wr = sum(v for v, _ in write[k][:n])
+        lanes = sum(g for _, g in fetch[k][:n])
+        # per launch (this pass's population) and per lane (Grid_Size), so bench.py can scale the
+        # measured bytes to the lanes its own live launches ran
+        res[k] = {"launches": n, "read_bytes_per_launch": rd / n, "write_bytes_per_launch": wr / n,
+                  "hbm_bytes_per_launch": (rd + wr) / n, "hbm_bytes_per_lane": (rd + wr) / lanes}
     json.dump({"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes; read = 2*FETCH_SIZE",
                "kernels": res}, open(sys.argv[3], "w"), indent=1)
     print(json.dumps(res, indent=1))

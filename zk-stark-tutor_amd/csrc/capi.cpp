@@ -128,11 +128,20 @@ const fe* sg_ctx::stage_twiddles(const fe& root, int logn) {
   auto key = std::make_pair(std::make_pair(fe_lo(root), fe_hi(root)), logn);
   auto it = stage_tables.find(key);
   if (it != stage_tables.end()) return reinterpret_cast<const fe*>(it->second);
-  uint64_t n = (uint64_t)1 << logn;
-  const fe* pw = pow_table(root, n / 2);
+  // two-level powers of root: A (4096) and B (root^4096 powers) cover every exponent e < n/2
+  const uint64_t nb = logn > 13 ? (uint64_t)1 << (logn - 13) : 1;
+  const fe* A = pow_table(root, 4096);
+  const fe* B = pow_table(fe_pow(root, 4096), nb);
   void* t = nullptr;
-  SG_HIP(hipMalloc(&t, std::max<uint64_t>(n - 1, 1) * sizeof(fe)));
-  SG_HIP(launch_stage_twiddles(reinterpret_cast<fe*>(t), pw, logn, stream));
+  const uint64_t entries = ntt_tw_entries(logn);
+  SG_HIP(hipMalloc(&t, entries * sizeof(fe)));
+  SG_HIP(launch_stage_twiddles(reinterpret_cast<fe*>(t), A, B, logn, stream));
+  const int cut = ntt_tw_cut(logn);
+  if (cut < logn) {  // stages above the cut multiply A[e & 4095] * B[e >> 12] on the fly
+    fe* tail = reinterpret_cast<fe*>(t) + (((uint64_t)1 << cut) - 1);
+    SG_HIP(hipMemcpyAsync(tail, A, 4096 * sizeof(fe), hipMemcpyDeviceToDevice, stream));
+    SG_HIP(hipMemcpyAsync(tail + 4096, B, nb * sizeof(fe), hipMemcpyDeviceToDevice, stream));
+  }
   SG_HIP(hipStreamSynchronize(stream));
   stage_tables[key] = t;
   return reinterpret_cast<const fe*>(t);
@@ -272,8 +281,9 @@ extern "C" int sg_ctx_profile_report(sg_ctx* ctx, char* buf, size_t cap, size_t*
     bool first = true;
     for (auto& kv : ctx->prof.totals) {
       char tmp[256];
-      snprintf(tmp, sizeof(tmp), "%s\"%s\": {\"launches\": %llu, \"ms\": %.6f, \"bytes\": %.0f}", first ? "" : ", ",
-               kv.first.c_str(), (unsigned long long)kv.second.launches, kv.second.ms, kv.second.bytes);
+      snprintf(tmp, sizeof(tmp), "%s\"%s\": {\"launches\": %llu, \"ms\": %.6f, \"bytes\": %.0f, \"elems\": %.0f}",
+               first ? "" : ", ", kv.first.c_str(), (unsigned long long)kv.second.launches, kv.second.ms,
+               kv.second.bytes, kv.second.elems);
       js += tmp;
       first = false;
     }

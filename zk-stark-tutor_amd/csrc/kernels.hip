@@ -63,15 +63,23 @@ __global__ void k_pow_table(fe* __restrict__ tw, const fe* __restrict__ A, const
   st_fe(tw + e, mont_mul(ld_fe(A + (e & 4095)), ld_fe(B + (e >> 12))));
 }
 
-// Stage-major twiddles: for stage S = 1..logn, entries [2^(S-1) - 1, 2^S - 1)
-// hold Montgomery(root^(k * n / 2^S)), k < 2^(S-1): a pass reads consecutive k
-// with consecutive lanes (coalesced) instead of striding the power table by n/2^S.
-__global__ void k_stage_twiddles(fe* __restrict__ out, const fe* __restrict__ pw, int logn) {
-  uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // < n - 1
-  if (idx + 1 >= ((uint64_t)1 << logn)) return;
+// Twiddle plan of a 2^logn transform (one buffer, built once per (root, logn)):
+//  * stage-major entries for stages S = 1..s_cut: entries [2^(S-1) - 1, 2^S - 1)
+//    hold Montgomery(root^(k * n / 2^S)), k < 2^(S-1), so a pass reads consecutive
+//    k with consecutive lanes (coalesced);
+//  * then A[e] = Montgomery(root^e), e < 4096, and B[e] = Montgomery(root^(4096 e)),
+//    e < max(n / 2^13, 1): a twiddle of a stage above s_cut is A[e & 4095] * B[e >> 12]
+//    with e = k * n / 2^S -- one Montgomery product instead of streaming a table of
+//    n/2 entries (512 MB at 2^25) that no cache holds.
+// A and B are the caller's (A: 4096 entries, B: n/2^13 entries, Montgomery form).
+__global__ void k_stage_twiddles(fe* __restrict__ out, const fe* __restrict__ A, const fe* __restrict__ B, int logn,
+                                 int s_cut) {
+  uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;  // < 2^s_cut - 1
+  if (idx + 1 >= ((uint64_t)1 << s_cut)) return;
   int S = 63 - __builtin_clzll(idx + 1) + 1;  // idx in [2^(S-1) - 1, 2^S - 1)
   uint64_t k = idx + 1 - ((uint64_t)1 << (S - 1));
-  st_fe(out + idx, ld_fe(pw + (k << (logn - S))));
+  uint64_t e = k << (logn - S);
+  st_fe(out + idx, mont_mul(ld_fe(A + (e & 4095)), ld_fe(B + (e >> 12))));
 }
 
 // --------------------------------------------------- bit reversal (+ LDE scale)
@@ -133,16 +141,29 @@ struct PassArgs {
   int b0;              // index bits below the group bits (= first stage of the pass - 1)
   int L;               // stages in this pass (group bits [b0, b0+L))
   int logC;            // columns per tile (consecutive low-bit indices), C <= 2^b0
+  int s_cut;           // stages above s_cut compute their twiddles from the A/B tables
   uint64_t ys;         // != 0: strided rows, transform blockIdx.y at data[0] + y * ys
 };
 
-// COLK: the tile's columns are consecutive low index bits (they enter the twiddle
-// index k); false when the columns are independent transforms' tiles (first pass).
+// twiddle of global stage S (1-based) for index k < 2^(S-1): Montgomery(root^(k n / 2^S)),
+// from the stage-major table (S <= s_cut) or as A[e & 4095] * B[e >> 12], e = k n / 2^S
+__device__ __forceinline__ fe twiddle_tab(const PassArgs& a, int S, uint64_t k) {
+  return ld_fe(a.tw + (((uint64_t)1 << (S - 1)) - 1) + k);
+}
+__device__ __forceinline__ fe twiddle_comp(const PassArgs& a, int S, uint64_t k) {
+  const fe* tA = a.tw + (((uint64_t)1 << a.s_cut) - 1);
+  const uint64_t e = k << (a.logn - S);
+  return mont_mul(ld_fe(tA + (e & 4095)), ld_fe(tA + 4096 + (e >> 12)));
+}
+
 // R radix-2 stages (tile-local stages t+1 .. t+R) on the 2^R elements of one group held
 // in registers: x[m] is tile row g0 + m * 2^t with g_low = g0 mod 2^t; `low` = the index
 // bits below b0 (cb*C + c; 0 when the columns are independent transforms).
-template <int R>
-__device__ __forceinline__ void radix_regs(fe* x, const PassArgs& a, int t, uint32_t g_low, uint64_t low) {
+// COMP: every twiddle of the step computed from A/B (the step reaches above s_cut), else
+// every twiddle from the table -- one uniform choice per step, so the step's twiddle loads
+// stay branch-free and are issued together.
+template <int R, bool COMP>
+__device__ __forceinline__ void radix_regs_impl(fe* x, const PassArgs& a, int t, uint32_t g_low, uint64_t low) {
 #pragma unroll
   for (int u = 0; u < R; ++u) {
     const int S = a.b0 + t + u + 1;  // global stage, 1-based
@@ -151,8 +172,7 @@ __device__ __forceinline__ void radix_regs(fe* x, const PassArgs& a, int t, uint
       if (m & (1 << u)) continue;
       uint64_t gmod = (uint64_t)g_low + ((uint64_t)(m & ((1 << u) - 1)) << t);
       uint64_t k = (gmod << a.b0) + low;
-      // stage-major table: stage S's twiddles root^(k * n/2^S), k < 2^(S-1), start at 2^(S-1) - 1
-      fe w = ld_fe(a.tw + (((uint64_t)1 << (S - 1)) - 1) + k);
+      fe w = COMP ? twiddle_comp(a, S, k) : twiddle_tab(a, S, k);
       fe o = mont_mul(x[m + (1 << u)], w);
       fe ev = x[m];
       x[m] = fe_add_lazy(ev, o);  // tile values stay in [0, 2^128) until the last store
@@ -161,6 +181,15 @@ __device__ __forceinline__ void radix_regs(fe* x, const PassArgs& a, int t, uint
   }
 }
 
+// MAYCOMP = false: the caller's stages never exceed s_cut (the first pass: <= 9 < 12 <= s_cut)
+template <int R, bool MAYCOMP = true>
+__device__ __forceinline__ void radix_regs(fe* x, const PassArgs& a, int t, uint32_t g_low, uint64_t low) {
+  if (!MAYCOMP || a.b0 + t + R <= a.s_cut) radix_regs_impl<R, false>(x, a, t, g_low, low);
+  else radix_regs_impl<R, true>(x, a, t, g_low, low);
+}
+
+// COLK: the tile's columns are consecutive low index bits (they enter the twiddle
+// index k); false when the columns are independent transforms' tiles (first pass).
 template <int R, bool COLK = true>
 __device__ __forceinline__ void radix_step(fe_lds* lds, const PassArgs& a, int t, uint64_t lowbase) {
   const int logC = a.logC;
@@ -175,7 +204,7 @@ __device__ __forceinline__ void radix_step(fe_lds* lds, const PassArgs& a, int t
     fe x[1 << R];
 #pragma unroll
     for (int m = 0; m < (1 << R); ++m) x[m] = lds[((g0 + ((uint32_t)m << t)) << logC) + c];
-    radix_regs<R>(x, a, t, g_low, COLK ? lowbase + c : 0);
+    radix_regs<R, COLK>(x, a, t, g_low, COLK ? lowbase + c : 0);
 #pragma unroll
     for (int m = 0; m < (1 << R); ++m) lds[((g0 + ((uint32_t)m << t)) << logC) + c] = x[m];
   }
@@ -319,6 +348,7 @@ struct FirstArgs {
   int L;
   int logC;
   int skip;
+  int s_cut;
   uint64_t in_ys, out_ys;  // != 0: strided rows (see GatherArgs)
 };
 
@@ -342,6 +372,7 @@ __global__ __launch_bounds__(256, SG_NTT_WPE) void k_ntt_first(FirstArgs a) {
   pa.b0 = 0;
   pa.L = L;
   pa.logC = logC;
+  pa.s_cut = a.s_cut;
   // one radix-8 group per thread in the first and last steps (column c, group qq)
   const bool regs = L >= 6 && ((1u << (L - 3)) << logC) == blockDim.x;
   int t = skip;
@@ -359,7 +390,7 @@ __global__ __launch_bounds__(256, SG_NTT_WPE) void k_ntt_first(FirstArgs a) {
         if (a.sA) x[j] = mont_mul(x[j], mont_mul(ld_fe(a.sA + (idx & 4095)), ld_fe(a.sB + (idx >> 12))));
       }
     }
-    radix_regs<3>(x, pa, 0, 0, 0);
+    radix_regs<3, false>(x, pa, 0, 0, 0);
 #pragma unroll
     for (int j = 0; j < 8; ++j) lds[((8 * qq + j) << logC) + c] = x[j];
     t = 3;
@@ -391,7 +422,7 @@ __global__ __launch_bounds__(256, SG_NTT_WPE) void k_ntt_first(FirstArgs a) {
     fe x[8];
 #pragma unroll
     for (int mm = 0; mm < 8; ++mm) x[mm] = lds[((qq + ((uint32_t)mm << tl)) << logC) + c];
-    radix_regs<3>(x, pa, tl, qq, 0);
+    radix_regs<3, false>(x, pa, tl, qq, 0);
     const uint64_t h = __builtin_bitreverse64(c0 + c) >> (64 - (m - L));
 #pragma unroll
     for (int mm = 0; mm < 8; ++mm) st_fe(out + (h << L) + qq + ((uint32_t)mm << tl), x[mm]);
@@ -487,7 +518,11 @@ __device__ __forceinline__ void merkle_root_publish(const MerkleArgs& a, bool wr
 
 template <bool LEAF, int MAXB, bool FOLD = false>
 __global__ __launch_bounds__(MAXB) void k_merkle_levels(MerkleArgs a) {
-  __shared__ Digest sm[MAXB];
+  // fused levels hand digests over through LDS word-major (sm[word][lane]): a lane
+  // writes word i at an 8-byte lane stride and reads its two children's word i as one
+  // 16-byte pair, both conflict-free (a 64-byte digest per lane put every lane of a
+  // ds_read at a 128-byte stride, i.e. on the same banks)
+  __shared__ uint64_t sm[8][MAXB];
   const uint32_t tid = threadIdx.x;
   const uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + tid;
   uint64_t* __restrict__ tree = merkle_tree_ptr(a);
@@ -528,13 +563,17 @@ __global__ __launch_bounds__(MAXB) void k_merkle_levels(MerkleArgs a) {
   uint32_t count = blockDim.x;  // digests of this block at the current level
   for (int lev = 1; lev < a.fuse; ++lev) {
 #pragma unroll
-    for (int i = 0; i < 8; ++i) sm[tid].h[i] = d[i];
+    for (int i = 0; i < 8; ++i) sm[i][tid] = d[i];
     __syncthreads();
     count >>= 1;
     if (tid < count) {
       uint64_t l[8], r[8];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) { l[i] = sm[2 * tid].h[i]; r[i] = sm[2 * tid + 1].h[i]; }
+      for (int i = 0; i < 8; ++i) {
+        const ulonglong2 lr = *reinterpret_cast<const ulonglong2*>(&sm[i][2 * tid]);
+        l[i] = lr.x;
+        r[i] = lr.y;
+      }
       blake2b_node(l, r, d);
       uint64_t gidx = (uint64_t)blockIdx.x * count + tid;
       st_digest(tree + (a.off[lev + 1] + gidx) * 8, d);
@@ -873,11 +912,31 @@ hipError_t launch_pow_table(fe* tw, const fe* A, const fe* B, uint64_t count, hi
   return hipGetLastError();
 }
 
-hipError_t launch_stage_twiddles(fe* out, const fe* pw, int logn, hipStream_t s) {
-  uint64_t n = (uint64_t)1 << logn;
-  if (n < 2) return hipSuccess;
-  ProfScope ps("stage_twiddles", 32 * n, s);
-  hipLaunchKernelGGL(k_stage_twiddles, dim3(nblocks(n - 1, 256)), dim3(256), 0, s, out, pw, logn);
+int ntt_tw_cut(int logn) {
+  // the top SG_NTT_TWTOP (default 3) stages of a transform of >= 2^15 points compute their
+  // twiddles: A/B on MI355X (tools/ab_ntt_tw.sh) -- at 2^22 and 2^25 the top three stages'
+  // n/2 + n/4 + n/8 table entries cost more HBM time than one Montgomery product per twiddle,
+  // deeper cuts trade too much VALU.  SG_NTT_TWCUT forces an absolute cut (experiments).
+  static const int top = env_int("SG_NTT_TWTOP", 3);
+  static const int forced = env_int("SG_NTT_TWCUT", 0);
+  int c = forced > 0 ? forced : (logn >= 15 ? logn - top : logn);
+  if (c < 12) c = 12;
+  return logn < c ? logn : c;
+}
+
+uint64_t ntt_tw_entries(int logn) {
+  const int c = ntt_tw_cut(logn);
+  if (c == logn) return logn ? ((uint64_t)1 << logn) - 1 : 1;
+  const uint64_t nb = logn > 13 ? (uint64_t)1 << (logn - 13) : 1;
+  return (((uint64_t)1 << c) - 1) + 4096 + nb;
+}
+
+hipError_t launch_stage_twiddles(fe* out, const fe* A, const fe* B, int logn, hipStream_t s) {
+  const int c = ntt_tw_cut(logn);
+  uint64_t cnt = ((uint64_t)1 << c) - 1;
+  if (cnt == 0) return hipSuccess;
+  ProfScope ps("stage_twiddles", 16 * cnt, s);
+  hipLaunchKernelGGL(k_stage_twiddles, dim3(nblocks(cnt, 256)), dim3(256), 0, s, out, A, B, logn, c);
   return hipGetLastError();
 }
 
@@ -898,7 +957,7 @@ hipError_t launch_bitrev_gather(fe* const* out, const fe* const* in, int batch, 
   }
   ga.in_ys = in_ys;
   ga.out_ys = out_ys;
-  ProfScope ps("bitrev_gather", batch * (16 * (n_in < n ? n_in : n) + 16 * n), s);
+  ProfScope ps("bitrev_gather", batch * (16 * (n_in < n ? n_in : n) + 16 * n), s, (uint64_t)batch * n);
   hipLaunchKernelGGL(k_bitrev_gather, dim3(nblocks(n, 256), batch), dim3(256), 0, s, ga, n_in, logn, sA, sB, skip);
   return hipGetLastError();
 }
@@ -949,6 +1008,7 @@ hipError_t launch_ntt_dit(fe* const* data, int batch, const fe* tw, int logn, co
     a.ys = ys;
     a.tw = tw;
     a.logn = logn;
+    a.s_cut = ntt_tw_cut(logn);
     a.b0 = b0;
     int rem = logn - b0;
     int lmax = tile_log - (b0 < 3 ? b0 : 3);
@@ -1013,9 +1073,10 @@ hipError_t launch_ntt_fused(fe* const* out, const fe* const* in, int batch, uint
   a.L = L1;
   a.logC = LOGC1;
   a.skip = skip;
+  a.s_cut = ntt_tw_cut(logn);
   uint64_t n = (uint64_t)1 << logn;
   {
-    ProfScope ps("ntt_first", batch * (16 * (n_in < n ? n_in : n) + 16 * n), s);
+    ProfScope ps("ntt_first", batch * (16 * (n_in < n ? n_in : n) + 16 * n), s, (uint64_t)batch * n);
     hipLaunchKernelGGL(k_ntt_first<TL>, dim3((unsigned)(n >> TL), batch), dim3(256), (size_t)16 << TL, s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -1104,11 +1165,14 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
     uint64_t digests = 0;
     for (int k = 0; k < fuse; ++k) digests += count >> k;
     // a fused fold reads 2 source elements and writes the folded one instead of reading the leaf
-    ProfScope ps(level == 0 ? (fold_here ? "merkle_fold_leaves" : "merkle_leaves")
-                            : (kind == 3 ? "merkle_nodes_quad" : "merkle_nodes"),
-                 batch * ((level == 0 ? (fold_here ? 48 : 16) * count : 0) + 64 * digests), s);
     const uint64_t per_block = kind == 3 ? bs / 4 : bs;
     dim3 grid((unsigned)((count + per_block - 1) / per_block), batch);
+    // elems = lanes launched (the rocprofv3 Grid_Size of this dispatch), so per-wave PMC
+    // instruction counts scale to any launch population
+    ProfScope ps(level == 0 ? (fold_here ? "merkle_fold_leaves" : "merkle_leaves")
+                            : (kind == 3 ? "merkle_nodes_quad" : "merkle_nodes"),
+                 batch * ((level == 0 ? (fold_here ? 48 : 16) * count : 0) + 64 * digests), s,
+                 (uint64_t)grid.x * grid.y * bs);
     switch (kind) {
       case 0:
         if (fold_here) hipLaunchKernelGGL((k_merkle_levels<true, 256, true>), grid, dim3(bs), 0, s, a);

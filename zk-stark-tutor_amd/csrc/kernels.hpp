@@ -6,7 +6,11 @@
 
 namespace sg {
 
-hipError_t launch_stage_twiddles(fe* out, const fe* pw, int logn, hipStream_t s);
+// NTT twiddle plan (see k_stage_twiddles): stage-major entries up to ntt_tw_cut(logn), then
+// the two power tables A (4096) and B (n / 2^13) the higher stages multiply on the fly.
+int ntt_tw_cut(int logn);
+uint64_t ntt_tw_entries(int logn);
+hipError_t launch_stage_twiddles(fe* out, const fe* A, const fe* B, int logn, hipStream_t s);
 hipError_t launch_pow_table(fe* tw, const fe* A, const fe* B, uint64_t count, hipStream_t s);
 // Batched over up to 4 independent transforms / trees (one pointer each, blockIdx.y),
 // or, with a non-zero row stride (`ys`), over up to 65535 strided rows from

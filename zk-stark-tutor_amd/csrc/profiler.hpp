@@ -19,6 +19,7 @@ struct KernelProfiler {
     const char* name;
     hipEvent_t a, b;
     uint64_t bytes;
+    uint64_t elems;  // transform elements (set on the first launch of an NTT), else 0
   };
   std::vector<Rec> recs;
   std::vector<hipEvent_t> spare;
@@ -36,6 +37,7 @@ struct KernelProfiler {
     uint64_t launches = 0;
     double ms = 0;
     double bytes = 0;
+    double elems = 0;
   };
   std::map<std::string, Total> totals;
   // resolve recorded events (caller synchronizes the stream first)
@@ -47,6 +49,7 @@ struct KernelProfiler {
       t.launches += 1;
       t.ms += ms;
       t.bytes += (double)r.bytes;
+      t.elems += (double)r.elems;
       spare.push_back(r.a);
       spare.push_back(r.b);
     }
@@ -65,11 +68,12 @@ struct ProfScope {
   KernelProfiler* p;
   KernelProfiler::Rec r;
   hipStream_t s;
-  ProfScope(const char* name, uint64_t bytes, hipStream_t stream) : p(g_prof), s(stream) {
+  ProfScope(const char* name, uint64_t bytes, hipStream_t stream, uint64_t elems = 0) : p(g_prof), s(stream) {
     if (p && !p->only.empty() && p->only != name) p = nullptr;
     if (p) {
       r.name = name;
       r.bytes = bytes;
+      r.elems = elems;
       r.a = p->get();
       r.b = p->get();
       (void)hipEventRecord(r.a, s);
