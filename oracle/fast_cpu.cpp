@@ -660,6 +660,39 @@ void fc_geometric_prod(const uint64_t* q, uint64_t n, const uint64_t* xs, uint64
   }
 }
 
+// prod_{i<n} (x - d_i) on an ARBITRARY domain, coefficients (length n + 1): the exact product
+// that fast_zerofier (ntt_arithmetics.rs:66-113) returns while its fast_multiply does not wrap
+// (n < root_order).  Schoolbook, one root at a time, each update split over the threads: O(n^2).
+void fc_poly_from_roots(const uint64_t* dom, uint64_t n, uint64_t* out) {
+  std::vector<u128> c(n + 1, 0), nxt(n + 1, 0);
+  c[0] = 1;
+  for (uint64_t i = 0; i < n; ++i) {
+    const u128 dm = to_m(ld(dom + 2 * i));
+    // c * (x - d): nxt[j] = c[j-1] - d c[j], degree i -> i + 1
+#pragma omp parallel for schedule(static) if (i > 4096)
+    for (int64_t j = 0; j <= (int64_t)i + 1; ++j) {
+      const u128 lo = j ? c[j - 1] : 0;
+      const u128 hi = j <= (int64_t)i ? mont(c[j], dm) : 0;
+      nxt[j] = fsub(lo, hi);
+    }
+    std::swap(c, nxt);
+  }
+  for (uint64_t j = 0; j <= n; ++j) st(out + 2 * j, c[j]);
+}
+
+// out[k] = sum_j coeffs[j] xs[k]^j (Polynomial::evaluate, polynomial.rs), Horner, points over threads
+void fc_eval_points(const uint64_t* coeffs, uint64_t len, const uint64_t* xs, uint64_t m, uint64_t* out) {
+  std::vector<u128> c(len);
+  for (uint64_t j = 0; j < len; ++j) c[j] = ld(coeffs + 2 * j);
+#pragma omp parallel for schedule(dynamic, 16)
+  for (int64_t k = 0; k < (int64_t)m; ++k) {
+    const u128 xm = to_m(ld(xs + 2 * k));
+    u128 acc = 0;
+    for (uint64_t j = len; j-- > 0;) acc = fadd(mont(acc, xm), c[j]);
+    st(out + 2 * k, acc);
+  }
+}
+
 // Interpolant through (q^r, cols[c][r]), r < n (q of order >= n), evaluated at x by the
 // barycentric formula P(x) = Z(x) sum_r v_r w_r / (x - q^r), Z(x) = prod_r (x - q^r),
 // 1/w_r = prod_{i != r} (q^r - q^i) = q^(e_r) A_r B_(n-1-r), e_r = r(r-1)/2 + r(n-1-r),

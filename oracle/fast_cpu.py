@@ -39,6 +39,8 @@ def lib():
         l.fc_fri_prove.restype = ctypes.c_long
         l.fc_free.argtypes = [vp]
         l.fc_geometric_prod.argtypes = [vp, u64, vp, u64, vp]
+        l.fc_poly_from_roots.argtypes = [vp, u64, vp]
+        l.fc_eval_points.argtypes = [vp, u64, vp, u64, vp]
         l.fc_geometric_bary.argtypes = [vp, u64, vp, u64, vp, u64, vp]
         l.fc_bary_create.argtypes = [vp, u64, vp, u64]
         l.fc_bary_create.restype = ctypes.c_void_p
@@ -151,6 +153,22 @@ def fri_prove(offset: int, omega: int, codeword, expansion: int, colinearity: in
     finally:
         lib().fc_free(out)
     return data, [int(t) for t in top]
+
+
+def poly_from_roots(domain) -> np.ndarray:
+    """prod (x - d) over an arbitrary domain, length n + 1 (fast_zerofier without wrap-around)."""
+    d = arr(domain)
+    out = np.zeros((len(d) + 1, 2), dtype=np.uint64)
+    lib().fc_poly_from_roots(_p(d), len(d), _p(out))
+    return out
+
+
+def eval_points(coeffs, xs) -> np.ndarray:
+    """Polynomial::evaluate at every x (Horner, points over threads)."""
+    c, x = arr(coeffs), arr(xs)
+    out = np.zeros((len(x), 2), dtype=np.uint64)
+    lib().fc_eval_points(_p(c), len(c), _p(x), len(x), _p(out))
+    return out
 
 
 def geometric_prod(q: int, n: int, xs):

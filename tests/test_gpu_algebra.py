@@ -128,3 +128,87 @@ def test_interpolate_geometric_large(logD, n):
     assert len(p) == n
     cw = sg.fast_coset_evaluate(q, D, 1, p.array())
     assert sg.to_ints(cw[:n]) == vals
+
+
+# ---- arbitrary (non-geometric) domains of any size (ntt_arithmetics.rs:66-113, 172-237) ----
+
+def _fc():
+    import fast_cpu as fc
+    return fc
+
+
+def test_zerofier_interpolate_arbitrary_2p10_vs_oracle():
+    """2^10 random points: the coefficient vectors equal the oracle's recursion exactly."""
+    rng = random.Random(10)
+    n, D = 1 << 10, 1 << 12
+    w = o.primitive_nth_root(D)
+    dom = [rng.randrange(P) for _ in range(n)]
+    vals = [rng.randrange(P) for _ in range(n)]
+    assert sg.fast_zerofier(w, D, dom).coefficients == e.fast_zerofier(w, D, dom)
+    assert sg.fast_interpolate_domain(w, D, dom, vals).coefficients == e.fast_interpolate_domain(w, D, dom, vals)
+
+
+@pytest.mark.parametrize("logn", [11, 12, 13, 14])
+def test_zerofier_arbitrary_large(logn):
+    """Z = prod (x - d_i) of 2^logn random points + a ragged count: equal to the exact product
+    (oracle/fast_cpu.cpp, O(n^2)), which is the reference's result below root_order."""
+    fc = _fc()
+    rng = random.Random(logn)
+    for n in ((1 << logn), (1 << logn) - 3):
+        D = 1 << (logn + 1)
+        w = o.primitive_nth_root(D)
+        dom = [rng.randrange(P) for _ in range(n)]
+        got = sg.fast_zerofier(w, D, dom).coefficients
+        assert len(got) == n + 1
+        assert got == fc.ints(fc.poly_from_roots(dom))
+
+
+@pytest.mark.parametrize("logn", [11, 12, 13, 14])
+def test_interpolate_arbitrary_large(logn):
+    """The interpolant through 2^logn (and a ragged count of) random points: length n, and it takes
+    every value at its point -- the unique polynomial of degree < n, i.e. the reference's result."""
+    fc = _fc()
+    rng = random.Random(100 + logn)
+    for n in ((1 << logn), (1 << logn) - 5):
+        D = 1 << (logn + 1)
+        w = o.primitive_nth_root(D)
+        dom = [rng.randrange(P) for _ in range(n)]
+        vals = [rng.randrange(P) for _ in range(n)]
+        got = sg.fast_interpolate_domain(w, D, dom, vals).coefficients
+        assert len(got) == n
+        assert fc.ints(fc.eval_points(got, dom)) == vals
+
+
+def test_zerofier_arbitrary_wraps_like_the_reference():
+    """Domains at and above root_order: the reference's fast_multiply wraps its cyclic
+    convolution; the recursion above the exact subtrees reproduces that output."""
+    rng = random.Random(21)
+    for D, n in ((16, 16), (16, 40), (64, 64), (64, 200)):
+        w = o.primitive_nth_root(D)
+        dom = [rng.randrange(P) for _ in range(n)]
+        assert sg.fast_zerofier(w, D, dom).coefficients == e.fast_zerofier(w, D, dom), (D, n)
+
+
+def test_interpolate_arbitrary_edge_cases():
+    rng = random.Random(22)
+    D = 1 << 8
+    w = o.primitive_nth_root(D)
+    # 0..9 points (below one leaf lane), and the largest domain whose half-zerofiers stay below
+    # root_order (ceil(n/2) < D: n = 2D - 2)
+    for n in list(range(10)) + [2 * D - 2]:
+        dom = [rng.randrange(P) for _ in range(n)]
+        vals = [rng.randrange(P) for _ in range(n)]
+        assert sg.fast_interpolate_domain(w, D, dom, vals).coefficients == e.fast_interpolate_domain(w, D, dom, vals)
+    # one more point and the reference's half-zerofier wraps: rejected, not silently different
+    dom = [rng.randrange(P) for _ in range(2 * D - 1)]
+    with pytest.raises(sg.StarkGpuError, match="wrap"):
+        sg.fast_interpolate_domain(w, D, dom, dom)
+    # a repeated point: the reference divides by zero (field_element.rs:82-90)
+    dom = [rng.randrange(P) for _ in range(20)]
+    dom[7] = dom[3]
+    with pytest.raises(sg.StarkGpuError, match="divide by zero"):
+        sg.fast_interpolate_domain(w, D, dom, [1] * 20)
+    # zero values and a zero point
+    dom = [0] + [rng.randrange(P) for _ in range(30)]
+    vals = [0] * 31
+    assert sg.fast_interpolate_domain(w, D, dom, vals).coefficients == [0] * 31

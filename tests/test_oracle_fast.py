@@ -139,3 +139,17 @@ def test_fast_verifier_pieces_verify_oracle_proof(fc):
     assert ok, err
     ok, _ = vst.verify(sair, rp.boundary_constraints(o.add_mod(out, 1)), o.IndependentProofStream(ps.objects))
     assert not ok
+
+
+def test_fast_cpu_arbitrary_domain_checkers_vs_oracle(fc):
+    """The O(n^2) exact product and the Horner evaluator the arbitrary-domain GPU tests check
+    against agree with the oracle's fast_zerofier / fast_interpolate_domain recursion."""
+    import random
+    rng = random.Random(5)
+    for n in (1, 2, 7, 33, 100):
+        dom = [rng.randrange(o.P) for _ in range(n)]
+        vals = [rng.randrange(o.P) for _ in range(n)]
+        w = o.primitive_nth_root(256)
+        assert fc.ints(fc.poly_from_roots(dom)) == e.fast_zerofier(w, 256, dom)
+        ip = e.fast_interpolate_domain(w, 256, dom, vals)
+        assert fc.ints(fc.eval_points(ip, dom)) == vals

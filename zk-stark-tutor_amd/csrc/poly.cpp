@@ -402,6 +402,124 @@ void coset_values_dev(sg_ctx* ctx, const fe* coeffs, uint64_t len, uint64_t L, c
   ntt_sized(ctx, root_of_order(L), coeffs, len, ilog2_exact(L), out, &offset);
 }
 
+// ------------------------------------------------------------------ arbitrary domains
+
+// `rows` contiguous transforms of 2^logn (row stride 2^logn in and out); post (host, Montgomery)
+// multiplies every output (the INTT's n^-1)
+void ntt_rows_dev(sg_ctx* ctx, const fe& root, const fe* in, uint64_t rows, int logn, fe* out, const fe* post_host) {
+  const uint64_t n = (uint64_t)1 << logn;
+  SG_REQUIRE(!ranges_overlap(in, n * rows, out, n * rows), "ntt rows: output must not alias the input");
+  const fe* tw = ctx->stage_twiddles(root, logn);
+  DevBuf dpost;
+  const fe* post = nullptr;
+  if (post_host) {
+    dpost = DevBuf(ctx, sizeof(fe));
+    SG_HIP(hipMemcpyAsync(dpost.get(), post_host, sizeof(fe), hipMemcpyHostToDevice, ctx->stream));
+    post = dpost.as<fe>();
+  }
+  constexpr uint64_t kRows = 65535;  // grid.y limit
+  for (uint64_t r0 = 0; r0 < rows; r0 += kRows) {
+    const int cnt = (int)std::min<uint64_t>(kRows, rows - r0);
+    fe* o = out + r0 * n;
+    const fe* i = in + r0 * n;
+    SG_HIP(launch_ntt_fused(&o, &i, cnt, n, logn, tw, nullptr, nullptr, 0, post, ctx->stream, n, n));
+  }
+}
+
+// Bottom-up product tree over d_dom[0..n) (see poly_kernels.hip): Z = prod (x - d_i), length n + 1,
+// and with d_c, N = sum_i c_i prod_{j != i} (x - d_j), length n.  Exact polynomial products (every
+// level's NTT is longer than its products), so the result is the reference's whenever its own
+// fast_multiply does not wrap (degree < root_order).
+void tree_exact(sg_ctx* ctx, const fe* d_dom, uint64_t n, const fe* d_c, DPoly* Zout, DPoly* Nout) {
+  SG_REQUIRE(n >= 1, "product tree: empty domain");
+  constexpr int kLeafLog = 3;  // kTreeLeaf = 8 points per lane, level-3 rows of 16
+  uint64_t N2 = (uint64_t)1 << kLeafLog;
+  while (N2 < n) N2 <<= 1;
+  const int L = ilog2_exact(N2);
+  const fe r2 = fe_r2();
+  uint64_t rows = N2 >> kLeafLog;
+  DevBuf Z(ctx, rows * 16 * sizeof(fe)), Nb;
+  if (d_c) Nb = DevBuf(ctx, rows * 16 * sizeof(fe));
+  SG_HIP(launch_tree_leaves(d_dom, n, rows, Z.as<fe>(), d_c, d_c ? Nb.as<fe>() : nullptr, r2, ctx->stream));
+  for (int l = kLeafLog; l < L; ++l) {
+    const int logM = l + 1;
+    const uint64_t M = (uint64_t)1 << logM, P = rows / 2;
+    const fe w = root_of_order(M);
+    const fe winv = fe_inv(w);
+    const fe minv = to_mont(fe_inv(fe_from_u64(M)));
+    DevBuf Zh(ctx, rows * M * sizeof(fe)), Nh;
+    ntt_rows_dev(ctx, w, Z.as<fe>(), rows, logM, Zh.as<fe>(), nullptr);
+    if (d_c) {
+      Nh = DevBuf(ctx, rows * M * sizeof(fe));
+      ntt_rows_dev(ctx, w, Nb.as<fe>(), rows, logM, Nh.as<fe>(), nullptr);
+    }
+    DevBuf Zp(ctx, P * M * sizeof(fe)), Np;
+    if (d_c) Np = DevBuf(ctx, P * M * sizeof(fe));
+    SG_HIP(launch_tree_combine(Zh.as<fe>(), d_c ? Nh.as<fe>() : nullptr, P, logM, Zp.as<fe>(),
+                               d_c ? Np.as<fe>() : nullptr, r2, ctx->stream));
+    // back to coefficients (mod x^M - 1), into the next level's rows of 2M
+    ntt_rows_dev(ctx, winv, Zp.as<fe>(), P, logM, Zh.as<fe>(), &minv);
+    DevBuf Z2(ctx, P * 2 * M * sizeof(fe));
+    SG_HIP(launch_tree_fix(Zh.as<fe>(), P, logM, Z2.as<fe>(), n >> logM, ctx->stream));
+    Z = std::move(Z2);
+    if (d_c) {
+      ntt_rows_dev(ctx, winv, Np.as<fe>(), P, logM, Nh.as<fe>(), &minv);
+      DevBuf N2b(ctx, P * 2 * M * sizeof(fe));
+      SG_HIP(launch_tree_fix(Nh.as<fe>(), P, logM, N2b.as<fe>(), 0, ctx->stream));
+      Nb = std::move(N2b);
+    }
+    rows = P;
+  }
+  if (Zout) *Zout = dpoly_copy(ctx, Z.as<fe>(), n + 1);
+  if (Nout && d_c) *Nout = dpoly_copy(ctx, Nb.as<fe>(), n);
+}
+
+namespace {
+bool is_pow2(uint64_t v) { return v && (v & (v - 1)) == 0; }
+}  // namespace
+
+// ntt_arithmetics.rs:66-113 on any domain (device array d_dom).  A node of the reference's
+// recursion (half = len / 2) whose product has degree < root_order (a power of two) is an exact
+// product: the product tree.  Larger nodes (degree >= root_order: the reference's fast_multiply
+// wraps its cyclic convolution) and every node under a non-power-of-two order follow the
+// recursion literally through fast_multiply_dev, so the wrapped results are the reference's too.
+DPoly zerofier_any_dev(sg_ctx* ctx, const fe& root, uint64_t root_order, const fe* d_dom, uint64_t n) {
+  if (n == 0) return DPoly{};
+  if (n == 1 || (is_pow2(root_order) && n < root_order)) {
+    DPoly z;
+    tree_exact(ctx, d_dom, n, nullptr, &z, nullptr);
+    return z;
+  }
+  const uint64_t half = n / 2;
+  DPoly l = zerofier_any_dev(ctx, root, root_order, d_dom, half);
+  DPoly r = zerofier_any_dev(ctx, root, root_order, d_dom + half, n - half);
+  return fast_multiply_dev(ctx, root, root_order, l.p(), l.len, r.p(), r.len);
+}
+
+// ntt_arithmetics.rs:172-237 on any domain: the unique interpolant of degree < n, length n (the
+// reference's length: left * Z_right + right * Z_left keeps n coefficients), as
+// sum_i y_i / Z'(d_i) * Z / (x - d_i): Z'(d_i) = prod_{j != i} (d_i - d_j) by one O(n^2) kernel,
+// the quotients in one batched division (a zero -- a repeated point -- is the reference's
+// "divide by zero"), the sum by the product tree.  Exact while every zerofier the reference builds
+// (at most ceil(n / 2) points) stays below root_order; above that its result is a wrapped
+// artefact, which this path rejects.
+DPoly interpolate_any_dev(sg_ctx* ctx, const fe& root, uint64_t root_order, const fe* d_dom, const fe* d_val,
+                          uint64_t n) {
+  (void)root;
+  if (n == 0) return DPoly{};
+  if (n == 1) return dpoly_copy(ctx, d_val, 1);
+  SG_REQUIRE(is_pow2(root_order) && (n + 1) / 2 < root_order,
+             "fast_interpolate_domain: the reference's zerofiers wrap for this domain (ceil(n/2) >= root_order "
+             "or a non-power-of-two root_order); not supported");
+  DevBuf prod(ctx, n * sizeof(fe)), c(ctx, n * sizeof(fe));
+  const fe rn = fe_pow(to_mont(fe_one()), n - 1);  // R^(n-1) mod p
+  SG_HIP(launch_bary_prod(d_dom, n, prod.as<fe>(), rn, ctx->stream));
+  dev_div(ctx, c.as<fe>(), d_val, prod.as<fe>(), n);
+  DPoly out;
+  tree_exact(ctx, d_dom, n, c.as<fe>(), nullptr, &out);
+  return out;
+}
+
 // ------------------------------------------------------------------ host polynomials
 
 int64_t hp_degree(const HPoly& a) {
@@ -511,7 +629,6 @@ void done(sg_ctx* ctx) {
   check_div_zero(ctx);
 }
 uint64_t dlen(const sg_poly* p) { return p ? p->d.len : 0; }
-constexpr uint64_t kHostDomainMax = 1024;
 }  // namespace
 
 extern "C" int sg_poly_create(sg_ctx* ctx, const sg_fe* coeffs, size_t len, sg_poly** out) {
@@ -598,11 +715,10 @@ extern "C" int sg_fast_zerofier(sg_ctx* ctx, sg_fe root, uint64_t root_order, co
       *out = wrap(std::move(z));
       return;
     }
-    SG_REQUIRE(n <= kHostDomainMax, "fast_zerofier: non-geometric domains above 1024 points are not supported");
-    HPoly z = hp_zerofier(std::vector<fe>(dom, dom + n));
-    DPoly d = dpoly_upload(ctx, z.data(), z.size());
-    SG_HIP(hipStreamSynchronize(ctx->stream));
-    *out = wrap(std::move(d));
+    DPoly dd = dpoly_upload(ctx, dom, n);
+    DPoly z = zerofier_any_dev(ctx, r, root_order, dd.p(), n);
+    done(ctx);
+    *out = wrap(std::move(z));
   });
 }
 
@@ -624,12 +740,10 @@ extern "C" int sg_fast_interpolate_domain(sg_ctx* ctx, sg_fe root, uint64_t root
       *out = wrap(std::move(ip));
       return;
     }
-    SG_REQUIRE(n <= kHostDomainMax,
-               "fast_interpolate_domain: non-geometric domains above 1024 points are not supported");
-    HPoly ip = hp_interpolate(std::vector<fe>(dom, dom + n), std::vector<fe>(val, val + n));
-    DPoly d = dpoly_upload(ctx, ip.data(), ip.size());
-    SG_HIP(hipStreamSynchronize(ctx->stream));
-    *out = wrap(std::move(d));
+    DPoly dd = dpoly_upload(ctx, dom, n), dv = dpoly_upload(ctx, val, n);
+    DPoly ip = interpolate_any_dev(ctx, r, root_order, dd.p(), dv.p(), n);
+    done(ctx);
+    *out = wrap(std::move(ip));
   });
 }
 

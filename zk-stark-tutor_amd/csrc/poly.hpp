@@ -94,6 +94,13 @@ void coset_interpolate_dev(sg_ctx* ctx, const fe* values, uint64_t L, const fe& 
 // out (length L, a power of two >= len) = [P(offset w^k)], w of order L
 void coset_values_dev(sg_ctx* ctx, const fe* coeffs, uint64_t len, uint64_t L, const fe& offset, fe* out);
 
+// arbitrary (non-geometric) domains: ntt_arithmetics.rs:66-113 / 172-237 on the device
+void ntt_rows_dev(sg_ctx* ctx, const fe& root, const fe* in, uint64_t rows, int logn, fe* out, const fe* post_host);
+void tree_exact(sg_ctx* ctx, const fe* d_dom, uint64_t n, const fe* d_c, DPoly* Zout, DPoly* Nout);
+DPoly zerofier_any_dev(sg_ctx* ctx, const fe& root, uint64_t root_order, const fe* d_dom, uint64_t n);
+DPoly interpolate_any_dev(sg_ctx* ctx, const fe& root, uint64_t root_order, const fe* d_dom, const fe* d_val,
+                          uint64_t n);
+
 // ---- host polynomials (small: boundary interpolants / zerofiers, constants) ----
 using HPoly = std::vector<fe>;
 int64_t hp_degree(const HPoly& a);

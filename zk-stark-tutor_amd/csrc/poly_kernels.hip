@@ -142,6 +142,122 @@ __global__ __launch_bounds__(kBlock) void k_batch_div(fe* __restrict__ out, cons
   }
 }
 
+// ------------------------------------------- product tree (arbitrary domains)
+//
+// fast_zerofier / fast_interpolate_domain on an arbitrary domain of n points
+// (ntt_arithmetics.rs:66-113, 172-237) as a bottom-up product tree over the points
+// padded to a power of two (padding leaves are the constant 1).  Level l holds one
+// row of 2^(l+1) coefficients per node: Z = prod (x - d_i) over the node's points
+// and, for interpolation, N = sum_i c_i Z / (x - d_i) (the reference's
+// left * Z_right + right * Z_left, unrolled).  The leaf kernel builds level 3
+// (8 points per lane, schoolbook); each level above multiplies pairs in the NTT
+// domain of size M = 2^(l+1) and fixes the one wrapped coefficient of a full node
+// (its monic x^M term lands on x^0).
+
+constexpr int kTreeLeaf = 8;  // points per lane at the bottom level (level 3, rows of 16)
+
+__global__ __launch_bounds__(kBlock) void k_tree_leaves(const fe* __restrict__ dom, uint64_t n, uint64_t nodes,
+                                                        fe* __restrict__ Z, const fe* __restrict__ c,
+                                                        fe* __restrict__ N, fe r2) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= nodes) return;
+  const uint64_t base = t * kTreeLeaf;
+  fe z[kTreeLeaf + 1];
+  z[0] = fe_one_c();
+#pragma unroll
+  for (int j = 1; j <= kTreeLeaf; ++j) z[j] = fe_make(0, 0);
+  // z *= (x - d_i) for the real points (a prefix of the node): z'[j] = z[j-1] - d z[j]
+#pragma unroll
+  for (int i = 0; i < kTreeLeaf; ++i) {
+    if (base + i < n) {
+      const fe dm = mont_mul(ld_fe(dom + base + i), r2);
+#pragma unroll
+      for (int j = i + 1; j >= 1; --j) z[j] = fe_sub(z[j - 1], mont_mul(z[j], dm));
+      z[0] = fe_sub(fe_make(0, 0), mont_mul(z[0], dm));
+    }
+  }
+  fe* zr = Z + t * (2 * kTreeLeaf);
+#pragma unroll
+  for (int j = 0; j < 2 * kTreeLeaf; ++j) st_fe(zr + j, j <= kTreeLeaf ? z[j] : fe_make(0, 0));
+  if (!c) return;
+  // N = sum_i c_i q_i, q_i = Z / (x - d_i) by synthetic division (exact: d_i is a root)
+  fe acc[kTreeLeaf];
+#pragma unroll
+  for (int j = 0; j < kTreeLeaf; ++j) acc[j] = fe_make(0, 0);
+#pragma unroll
+  for (int i = 0; i < kTreeLeaf; ++i) {
+    if (base + i < n) {
+      const fe dm = mont_mul(ld_fe(dom + base + i), r2);
+      const fe cm = mont_mul(ld_fe(c + base + i), r2);
+      fe q = z[kTreeLeaf];  // q[k-1] = z[k] + d q[k], from the top
+#pragma unroll
+      for (int k = kTreeLeaf; k >= 1; --k) {
+        if (k < kTreeLeaf) q = fe_add(z[k], mont_mul(q, dm));
+        acc[k - 1] = fe_add(acc[k - 1], mont_mul(q, cm));
+      }
+    }
+  }
+  fe* nr = N + t * (2 * kTreeLeaf);
+#pragma unroll
+  for (int j = 0; j < 2 * kTreeLeaf; ++j) st_fe(nr + j, j < kTreeLeaf ? acc[j] : fe_make(0, 0));
+}
+
+// parents p < P, j < M (NTT domain): Zp = Zl Zr; Np = Nl Zr + Nr Zl (N optional)
+__global__ __launch_bounds__(kBlock) void k_tree_combine(const fe* __restrict__ Zh, const fe* __restrict__ Nh,
+                                                         uint64_t P, int logM, fe* __restrict__ Zp,
+                                                         fe* __restrict__ Np, fe r2) {
+  const uint64_t total = P << logM;
+  const uint64_t M = (uint64_t)1 << logM;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t p = i >> logM, j = i & (M - 1);
+    const uint64_t l = (2 * p) * M + j, r = l + M;
+    const fe zl = ld_fe(Zh + l), zr = ld_fe(Zh + r);
+    st_fe(Zp + i, mont_mul(mont_mul(zl, zr), r2));
+    if (Nh) st_fe(Np + i, mont_mul(fe_add(mont_mul(ld_fe(Nh + l), zr), mont_mul(ld_fe(Nh + r), zl)), r2));
+  }
+}
+
+// rows of M coefficients (mod x^M - 1) -> rows of 2M; a full node (all M of its leaf
+// positions are real points, p < full) is monic of degree M: move its wrapped 1 from x^0 to x^M
+__global__ __launch_bounds__(kBlock) void k_tree_fix(const fe* __restrict__ in, uint64_t P, int logM,
+                                                     fe* __restrict__ out, uint64_t full) {
+  const uint64_t M = (uint64_t)1 << logM;
+  const uint64_t total = P << (logM + 1);
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t p = i >> (logM + 1), j = i & (2 * M - 1);
+    fe v = fe_make(0, 0);
+    if (j < M) v = ld_fe(in + p * M + j);
+    if (p < full) {
+      if (j == 0) v = fe_sub(v, fe_one_c());
+      else if (j == M) v = fe_one_c();
+    }
+    st_fe(out + i, v);
+  }
+}
+
+// out[i] = prod_{j != i} (d_i - d_j): Z'(d_i) of the domain's zerofier (barycentric weights'
+// reciprocals).  Lanes own i, the block streams tiles of d_j through LDS.  Each Montgomery
+// product contributes a factor R^-1: starting from rn = R^(n-1) mod p the n - 1 products
+// leave exactly prod (d_i - d_j).
+__global__ __launch_bounds__(kBlock) void k_bary_prod(const fe* __restrict__ dom, uint64_t n, fe* __restrict__ out,
+                                                      fe rn) {
+  __shared__ fe tile[kBlock];  // every lane reads the same entry: an LDS broadcast
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const fe di = i < n ? ld_fe(dom + i) : fe_make(0, 0);
+  fe acc = rn;
+  for (uint64_t j0 = 0; j0 < n; j0 += kBlock) {
+    __syncthreads();
+    if (j0 + threadIdx.x < n) tile[threadIdx.x] = ld_fe(dom + j0 + threadIdx.x);
+    __syncthreads();
+    const uint64_t cnt = n - j0 < kBlock ? n - j0 : kBlock;
+    for (uint64_t k = 0; k < cnt; ++k) {
+      if (j0 + k == i) continue;
+      acc = mont_mul(acc, fe_sub(di, tile[k]));
+    }
+  }
+  if (i < n) st_fe(out + i, acc);
+}
+
 // --------------------------------------------------------- prefix products
 
 // Inclusive prefix product over 1024-element tiles (256 lanes x 4): each lane
@@ -473,6 +589,40 @@ hipError_t launch_lincomb(const LinCombArgs& a, hipStream_t s) {
   if (a.nterms > kLinCombMaxTerms) return hipErrorInvalidValue;
   ProfScope ps("lincomb", 16 * a.n * (a.nterms + 1), s);
   hipLaunchKernelGGL(k_lincomb, dim3((unsigned)grid_for(a.n)), dim3(kBlock), 0, s, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_tree_leaves(const fe* dom, uint64_t n, uint64_t nodes, fe* Z, const fe* c, fe* N, const fe& r2,
+                              hipStream_t s) {
+  if (!nodes) return hipSuccess;
+  ProfScope ps("tree_leaves", 16 * n * (c ? 2 : 1) + 2 * 16 * 16 * nodes, s);
+  hipLaunchKernelGGL(k_tree_leaves, dim3((unsigned)((nodes + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, dom, n,
+                     nodes, Z, c, N, r2);
+  return hipGetLastError();
+}
+
+hipError_t launch_tree_combine(const fe* Zh, const fe* Nh, uint64_t P, int logM, fe* Zp, fe* Np, const fe& r2,
+                               hipStream_t s) {
+  const uint64_t total = P << logM;
+  if (!total) return hipSuccess;
+  ProfScope ps("tree_combine", (Nh ? 96 : 48) * total, s);
+  hipLaunchKernelGGL(k_tree_combine, dim3((unsigned)grid_for(total)), dim3(kBlock), 0, s, Zh, Nh, P, logM, Zp, Np,
+                     r2);
+  return hipGetLastError();
+}
+
+hipError_t launch_tree_fix(const fe* in, uint64_t P, int logM, fe* out, uint64_t full, hipStream_t s) {
+  const uint64_t total = P << (logM + 1);
+  if (!total) return hipSuccess;
+  ProfScope ps("tree_fix", 16 * (total / 2) + 16 * total, s);
+  hipLaunchKernelGGL(k_tree_fix, dim3((unsigned)grid_for(total)), dim3(kBlock), 0, s, in, P, logM, out, full);
+  return hipGetLastError();
+}
+
+hipError_t launch_bary_prod(const fe* dom, uint64_t n, fe* out, const fe& rn, hipStream_t s) {
+  if (!n) return hipSuccess;
+  ProfScope ps("bary_prod", 32 * n, s);
+  hipLaunchKernelGGL(k_bary_prod, dim3((unsigned)((n + kBlock - 1) / kBlock)), dim3(kBlock), 0, s, dom, n, out, rn);
   return hipGetLastError();
 }
 

@@ -58,5 +58,14 @@ hipError_t launch_lincomb(const LinCombArgs& a, hipStream_t s);
 hipError_t launch_eval_small(fe* out, const SmallPoly& p, uint64_t n, const fe* wA, const fe* wB, const fe& off_m,
                              hipStream_t s);
 hipError_t launch_gather_stride(fe* out, const fe* in, uint64_t n, uint64_t stride, hipStream_t s);
+// product tree over an arbitrary domain (poly.cpp: tree_exact): level-3 leaves (8 points per lane,
+// rows of 16: Z and optionally N = sum c_i Z / (x - d_i)), pairwise NTT-domain combine, wrap fix
+hipError_t launch_tree_leaves(const fe* dom, uint64_t n, uint64_t nodes, fe* Z, const fe* c, fe* N, const fe& r2,
+                              hipStream_t s);
+hipError_t launch_tree_combine(const fe* Zh, const fe* Nh, uint64_t P, int logM, fe* Zp, fe* Np, const fe& r2,
+                               hipStream_t s);
+hipError_t launch_tree_fix(const fe* in, uint64_t P, int logM, fe* out, uint64_t full, hipStream_t s);
+// out[i] = prod_{j != i} (d_i - d_j); rn = R^(n-1) mod p (canonical) undoes the n - 1 Montgomery factors
+hipError_t launch_bary_prod(const fe* dom, uint64_t n, fe* out, const fe& rn, hipStream_t s);
 
 }  // namespace sg
