@@ -277,21 +277,45 @@ def c5_single_gpu(ctx: sg.Context, device, iters: int = 3) -> dict:
     t = (time.perf_counter() - t0) / iters
     del x, y
     ctx.trim()
-    return {"c5_ntt_2p27_ms": round(t * 1e3, 3), "c5_gelem_s": round(n / t / 1e9, 3), "c5_ranks": 1,
-            "c5_alg_hbm_frac": round(32 * n / t / (HBM_PEAK_GBS * 1e9), 4)}
+    out = {"c5_ntt_2p27_ms": round(t * 1e3, 3), "c5_gelem_s": round(n / t / 1e9, 3), "c5_ranks": 1,
+           "c5_alg_hbm_frac": round(32 * n / t / (HBM_PEAK_GBS * 1e9), 4)}
+    # the sharded path on one rank (sg_dist_ntt over a 1-rank RCCL communicator): the four-step's
+    # own cost -- its passes, the epilogue twiddles, the run-shard transpose -- with no peer
+    from starkgpu import dist as D
+    nd = D.NativeDist(ctx, transport="rccl")
+    n1, n2 = nd.plan(n, 1)
+    cols = torch.from_numpy(synthetic_fe(0, b"c5", n).reshape(n2, n1, 2).transpose(1, 0, 2).copy()
+                            .view(np.int64).reshape(-1)).to(device)
+    runs = nd.ntt(root, cols, n2, n)
+    torch.cuda.synchronize(device)
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        runs = nd.ntt(root, cols, n2, n)
+    torch.cuda.synchronize(device)
+    t = (time.perf_counter() - t0) / iters
+    out["c5_dist_world1_ms"] = round(t * 1e3, 3)
+    out["c5_dist_world1_gelem_s"] = round(n / t / 1e9, 3)
+    nd.close()
+    del cols, runs
+    ctx.trim()
+    return out
 
 
 def side_sharded(ctx: sg.Context, device, world: int, rank: int, iters: int = 3) -> dict:
-    """Strong-scaling side measurements over all ranks (BASELINE config C5).
+    """Strong-scaling side measurements over all ranks (BASELINE config C5), through
+    the C ABI's communicator (csrc/dist.cpp: sg_dist_*, RCCL over xGMI; SG_BENCH_BACKEND=gloo
+    rehearses it with the host-staged transport).
 
-    * C5: one 2^27-point NTT sharded across the ranks: four-step, ONE RCCL
-      all-to-all (starkgpu/dist.py), time = max over ranks.
+    * C5: one 2^27-point NTT sharded across the ranks: four-step, ONE all-to-all, time = max
+      over ranks.
     * the north-star block sharded: LDE 2^21 -> 2^24 on the coset + FRI commit
       (exp 8, c = 64) with run-sharded Merkle trees and folds.
     """
     from starkgpu import dist as D
-    ds = D.DistStark(D.GpuRows(ctx), D.Comm())
-    out = {"sharded_ranks": world}
+    backend = dist.get_backend()
+    ds = D.NativeDist(ctx, transport="rccl" if backend == "nccl" else "host")
+    out = {"sharded_ranks": world, "sharded_path": "C ABI sg_dist_* (" +
+           ("RCCL" if backend == "nccl" else "host-staged transport over " + backend) + ")"}
 
     def timed(fn):
         fn()
@@ -307,7 +331,7 @@ def side_sharded(ctx: sg.Context, device, world: int, rank: int, iters: int = 3)
     try:
         n = 1 << 27
         n1, n2 = D.plan(n, world)
-        shard = to_device(synthetic_fe(rank, b"c5", (n1 // world) * n2), device)
+        shard = to_device(synthetic_fe(rank, b"c5", (n1 // world) * n2), device).reshape(-1)
         root = sg.primitive_nth_root(n)
         t = timed(lambda: ds.ntt(root, shard, n2, n))
         out["c5_ntt_2p27_ms"] = round(t * 1e3, 3)
@@ -325,12 +349,13 @@ def side_sharded(ctx: sg.Context, device, world: int, rank: int, iters: int = 3)
         omega, off = sg.primitive_nth_root(N), sg.generator()
 
         def lde_fri():
-            cw = ds.coset_evaluate(omega, N, off, cs, row)
+            cw = ds.coset_evaluate(omega, N, off, cs.reshape(-1), row)
             ds.fri_commit(off, omega, cw, N, EXPANSION, COLINEARITY, sg.IndependentProofStream())
 
         out["sharded_lde_fri_commit_2p24_ms"] = round(timed(lde_fri) * 1e3, 3)
     except Exception as e:  # noqa: BLE001
         out["sharded_lde_fri_error"] = f"{type(e).__name__}: {e}"
+    ds.close()
     ctx.trim()
     return out
 

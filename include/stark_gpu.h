@@ -215,6 +215,48 @@ int sg_fri_fold_runs_dev(sg_ctx* ctx, sg_fe omega, sg_fe offset, sg_fe alpha, co
                          size_t n_local, size_t run, size_t run_stride, size_t run_off,
                          size_t n_global, sg_fe* d_out);
 
+/* ------------------------------------------------ multi-GPU (one process per GPU)
+ * a Rust (or any) caller shards the LDE / NTT / Merkle / FRI commit
+ * without torch.  A communicator binds a context to RCCL over xGMI (sg_dist_create, from a
+ * unique id the caller distributes: rank 0 calls sg_dist_unique_id) or to a host-staged
+ * transport the caller implements (sg_dist_create_transport: MPI, gloo, sockets, tests).
+ * Shards (device, canonical elements), rank g of G, n = N1 N2 (sg_dist_plan):
+ *   column shard [N1/G][row_len]  row r = x[(g N1/G + r) + N1 j], j < row_len <= N2, zero beyond
+ *   run shard    [N1][N2/G]       element [k1][c] = X[k1 N2 + g N2/G + c]
+ * The data exchange of a transform is ONE all-to-all (the four-step transpose); the Merkle
+ * commit all-gathers N1 64-byte run roots; FRI folds are rank-local.  Outputs equal the
+ * single-GPU / reference results bit for bit (roots of order exactly n). */
+#define SG_DIST_ID_BYTES 128
+typedef struct sg_dist sg_dist;
+typedef struct {
+  void* user;
+  /* host buffers: send = nranks blocks of `bytes` (block h goes to rank h); recv = nranks blocks
+   * (block h came from rank h).  Return 0 on success. */
+  int (*all_to_all)(void* user, const void* send, void* recv, size_t bytes);
+  /* send = one block of `bytes`; recv = every rank's block in rank order */
+  int (*all_gather)(void* user, const void* send, void* recv, size_t bytes);
+} sg_dist_transport;
+int sg_dist_unique_id(uint8_t* id /* SG_DIST_ID_BYTES */);                   /* ncclGetUniqueId */
+int sg_dist_create(sg_ctx* ctx, const uint8_t* id, int nranks, int rank, sg_dist** out); /* RCCL */
+int sg_dist_create_transport(sg_ctx* ctx, int nranks, int rank, const sg_dist_transport* t,
+                             sg_dist** out);
+void sg_dist_destroy(sg_dist* d);
+/* N1 = 2^floor(log2 n / 2), N2 = n / N1; needs N1 >= G and N2 >= 4 G */
+int sg_dist_plan(size_t n, int nranks, size_t* n1, size_t* n2);
+/* fft/ntt.rs:7-49 over the ranks: column shard in, run shard out */
+int sg_dist_ntt(sg_dist* d, sg_fe root, const sg_fe* d_cols, size_t row_len, size_t n,
+                sg_fe* d_runs);
+/* fft/ntt.rs:51-68: run shard in, column shard (rows of N2) out */
+int sg_dist_intt(sg_dist* d, sg_fe root, const sg_fe* d_runs, size_t n, sg_fe* d_cols);
+/* fft/ntt_arithmetics.rs:161-170: coefficients as a column shard, codeword as a run shard */
+int sg_dist_coset_evaluate(sg_dist* d, sg_fe generator, size_t root_order, sg_fe offset,
+                           const sg_fe* d_cols, size_t row_len, sg_fe* d_runs);
+/* merkle_root.rs:21-32 of the natural-order codeword held as run shards (same root on every rank) */
+int sg_dist_merkle_root(sg_dist* d, const sg_fe* d_runs, size_t n, uint8_t* root);
+/* fri.rs:115-172 FRI::commit of a run-sharded codeword: every rank writes the same stream bytes */
+int sg_dist_fri_commit(sg_dist* d, const sg_fri* fri, const sg_fe* d_runs, size_t n,
+                       const sg_proof_stream* ps);
+
 /* ------------------------------------------- polynomial algebra (fft/ntt_arithmetics.rs)
  * A polynomial is a device-resident coefficient vector owned by the library
  * (field/polynomial.rs Polynomial: never trimmed; degree() skips trailing zeros).

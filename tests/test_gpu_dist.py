@@ -238,3 +238,80 @@ def test_dist_world2_one_gpu_gloo():
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     mp.spawn(_world2_worker, args=(2, port, 14), nprocs=2, join=True)
+
+
+# ------------------------------------------------------------------ the C-ABI communicator (sg_dist_*)
+
+def _native_checks(nd, ctx, world, rank, logn, gather):
+    """sg_dist_ntt / intt / coset_evaluate / merkle_root / fri_commit against the single-GPU path
+    (itself pinned to the oracle by the parity suite); gather(local ndarray) -> every rank's."""
+    import starkgpu as sg
+    from starkgpu import dist as D
+    n = 1 << logn
+    root = sg.primitive_nth_root(n)
+    x = _rand(1000 + logn, n)
+    cols, row = D.scatter_columns_np(x, n, world, rank)
+    runs = nd.ntt(root, _t(cols), row, n)
+    full = D.gather_runs_np(gather(_np(runs)), n, world)
+    assert np.array_equal(full, sg.ntt(root, x, ctx=ctx)), "ntt"
+    assert np.array_equal(_np(nd.intt(root, runs, n)), cols), "intt"
+    # a short column shard (zero tails: the row transforms skip stages)
+    d = n // 8
+    cc, crow = D.scatter_columns_np(x[:d], n, world, rank)
+    cw = nd.coset_evaluate(root, n, sg.generator(), _t(cc), crow)
+    cw_full = D.gather_runs_np(gather(_np(cw)), n, world)
+    assert np.array_equal(cw_full, sg.fast_coset_evaluate(root, n, sg.generator(), x[:d], ctx=ctx)), "lde"
+    assert nd.merkle_root(cw, n) == sg.MerkleRoot.commit(cw_full, ctx=ctx), "merkle"
+    # FRI: c = 16 folds down to one run per rank and finishes on the gathered codeword; c = n/16
+    # (two rounds) ends while still sharded and gathers the last codeword
+    for c in (16, n // 16):
+        ref = sg.IndependentProofStream()
+        sg.FRI(sg.generator(), root, n, 8, c, ctx=ctx).commit(cw_full, ref)
+        got = sg.IndependentProofStream()
+        nd.fri_commit(sg.generator(), root, cw, n, 8, c, got)
+        assert got.digest() == ref.digest(), f"fri stream c={c}"
+
+
+def test_native_dist_world1_rccl():
+    """sg_dist_create from an RCCL unique id (1 rank: the collectives run through RCCL)."""
+    import starkgpu as sg
+    from starkgpu import dist as D
+    ctx = sg.Context(0)
+    nd = D.NativeDist(ctx, transport="rccl")
+    try:
+        _native_checks(nd, ctx, 1, 0, 12, lambda a: [a])
+    finally:
+        nd.close()
+
+
+def _native_worker(rank, world, port, logn):
+    import torch.distributed as dist
+    import starkgpu as sg
+    from starkgpu import dist as D
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ctx = sg.Context(0)
+        nd = D.NativeDist(ctx, transport="host")
+
+        def gather(a):
+            out = [None] * world
+            dist.all_gather_object(out, a)
+            return out
+
+        _native_checks(nd, ctx, world, rank, logn, gather)
+        nd.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,logn", [(2, 14), (8, 14), (4, 17)])
+def test_native_dist_one_gpu_host_transport(world, logn):
+    """world ranks sharing this box's GPU, the library's all-to-all / all-gather staged through
+    host buffers over gloo (RCCL refuses two ranks on one device)."""
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.spawn(_native_worker, args=(world, port, logn), nprocs=world, join=True)

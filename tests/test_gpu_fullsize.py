@@ -198,6 +198,52 @@ def c5_reference(fc):
         shutil.rmtree(tmp, ignore_errors=True)
 
 
+def _c5_native_worker(rank, world, port, tmp):
+    """C5 through the C ABI (sg_dist_ntt / sg_dist_intt, host-staged transport over gloo)."""
+    import torch
+    import torch.distributed as dist
+    from starkgpu import dist as D
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ctx = sg.Context(0)
+        nd = D.NativeDist(ctx, transport="host")
+        n = 1 << C5_LOG
+        n1, n2 = nd.plan(n, world)
+        rows, R = n1 // world, n2 // world
+        x = np.load(os.path.join(tmp, "x.npy"), mmap_mode="r")
+        X = np.load(os.path.join(tmp, "X.npy"), mmap_mode="r")
+        cols = np.ascontiguousarray(x.reshape(n2, n1, 2)[:, rank * rows:(rank + 1) * rows].transpose(1, 0, 2))
+        dev = torch.device("cuda", 0)
+        shard = torch.from_numpy(cols.view(np.int64).reshape(-1)).to(dev)
+        root = o.primitive_nth_root(n)
+        runs = nd.ntt(root, shard, n2, n)
+        got = runs.cpu().numpy().view(np.uint64).reshape(n1, R, 2)
+        want = X.reshape(n1, n2, 2)[:, rank * R:(rank + 1) * R]
+        ok = bool(np.array_equal(got, want))
+        back = nd.intt(root, runs, n)
+        ok_inv = bool(torch.equal(back, shard))
+        flags = [None] * world
+        dist.all_gather_object(flags, (ok, ok_inv))
+        assert all(f[0] for f in flags), f"sg_dist_ntt 2^{C5_LOG} differs from the single-GPU transform: {flags}"
+        assert all(f[1] for f in flags), f"sg_dist_intt did not invert sg_dist_ntt at 2^{C5_LOG}: {flags}"
+        nd.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_c5_native_dist_2p27_one_gpu(c5_reference, world):
+    """BASELINE config C5 (2^27-point NTT sharded over the ranks) through the C ABI: bit-identical
+    to the single-GPU NTT (checked against the CPU checker), and sg_dist_intt inverts it."""
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.spawn(_c5_native_worker, args=(world, port, c5_reference), nprocs=world, join=True)
+
+
 @pytest.mark.parametrize("world", [2, 8])
 def test_c5_sharded_2p27_ntt_one_gpu_gloo(c5_reference, world):
     import torch.multiprocessing as mp

@@ -1,0 +1,440 @@
+// Multi-GPU LDE / NTT / Merkle / FRI commit behind the C ABI.
+//
+// One process per GPU; a sg_dist binds a context to a communicator: RCCL over xGMI
+// (sg_dist_create: ncclCommInitRank from a unique id, collectives stream-ordered on the
+// context's stream) or a host-staged transport the caller supplies (sg_dist_create_transport:
+// all-to-all / all-gather callbacks over host buffers -- how the tests run 2 and 8 ranks on one
+// GPU over gloo, since RCCL refuses two ranks on one device).  The reference is single-threaded
+// and has no counterpart; the data path is the four-step decomposition:
+//
+//   n = N1 N2, input index j = j1 + N1 j2, output index k = k2 + N2 k1
+//   X[k2 + N2 k1] = sum_j1 w_N1^(j1 k1) w^(j1 k2) sum_j2 w_N2^(j2 k2) x[j1 + N1 j2]
+//
+// with G ranks, rows = N1 / G, R = N2 / G:
+//   column shard [rows][row_len]  row r = x[(g rows + r) + N1 j2], zero beyond row_len
+//   run shard    [N1][R]          element [k1][c] = X[k1 N2 + g R + c]
+//
+// Per rank, HBM passes of a forward transform:
+//   1. size-N2 NTTs over the column shard; their LAST pass multiplies by w^(j1 k2) and stores
+//      straight into the all-to-all send buffer [h][r][c] (kernels.hip NttEpilogue);
+//   2. ONE all-to-all (ncclAllToAll): recv = [j1][c];
+//   3. size-N1 NTTs over the R interleaved columns of recv, read in place by the first pass
+//      (launch_ntt_fused in_il) -- no transpose before them;
+//   4. one transpose [c][k1] -> [k1][c] into the run shard (the only extra pass).
+// The inverse reads the run shard as the interleaved column shard of (N2, N1) and writes the
+// column shard directly (n^-1 folded into its last pass): no extra pass at all.
+// For a root of order exactly n the DFT is unique, so outputs are bit-identical to the
+// reference's radix-2 DIT (fft/ntt.rs:7-49); roots of smaller order are rejected.
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cstring>
+#include <memory>
+#include <vector>
+
+#include "host_field.hpp"
+#include "internal.hpp"
+
+struct sg_dist {
+  sg_ctx* ctx = nullptr;
+  int G = 1, g = 0;
+  ncclComm_t comm = nullptr;
+  sg_dist_transport tr{};
+  bool staged = false;
+  // pinned staging for the host transport (grown on demand)
+  void* hsend = nullptr;
+  void* hrecv = nullptr;
+  size_t hsend_bytes = 0, hrecv_bytes = 0;
+  ~sg_dist() {
+    if (comm) (void)ncclCommDestroy(comm);
+    if (hsend) (void)hipHostFree(hsend);
+    if (hrecv) (void)hipHostFree(hrecv);
+  }
+};
+
+namespace sg {
+namespace {
+
+#define SG_NCCL(call)                                                                          \
+  do {                                                                                         \
+    ncclResult_t _r = (call);                                                                  \
+    if (_r != ncclSuccess) throw Error{SG_ERR_HIP, std::string(#call) + ": " + ncclGetErrorString(_r)}; \
+  } while (0)
+
+constexpr uint64_t kRows = 65532;  // rows per launch: grid.y limit, a multiple of 4 (interleaved tiles)
+
+void grow_pinned(void*& p, size_t& have, size_t need) {
+  if (have >= need) return;
+  if (p) (void)hipHostFree(p);
+  p = nullptr;
+  have = 0;
+  SG_HIP(hipHostMalloc(&p, need, hipHostMallocDefault));
+  have = need;
+}
+
+// equal-block all-to-all (a2a) or all-gather of `bytes` per rank, device buffers
+void exchange(sg_dist* d, const void* dsend, void* drecv, size_t bytes, bool a2a) {
+  sg_ctx* ctx = d->ctx;
+  const size_t total = bytes * d->G;
+  if (d->comm) {  // RCCL over xGMI, stream-ordered (a 1-rank communicator runs the same calls)
+    if (a2a)
+      SG_NCCL(ncclAllToAll(dsend, drecv, bytes, ncclUint8, d->comm, ctx->stream));
+    else
+      SG_NCCL(ncclAllGather(dsend, drecv, bytes, ncclUint8, d->comm, ctx->stream));
+    return;
+  }
+  if (d->G == 1) {
+    SG_HIP(hipMemcpyAsync(drecv, dsend, bytes, hipMemcpyDeviceToDevice, ctx->stream));
+    return;
+  }
+  const size_t sbytes = a2a ? total : bytes;
+  grow_pinned(d->hsend, d->hsend_bytes, sbytes);
+  grow_pinned(d->hrecv, d->hrecv_bytes, total);
+  SG_HIP(hipMemcpyAsync(d->hsend, dsend, sbytes, hipMemcpyDeviceToHost, ctx->stream));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  const int rc = a2a ? d->tr.all_to_all(d->tr.user, d->hsend, d->hrecv, bytes)
+                     : d->tr.all_gather(d->tr.user, d->hsend, d->hrecv, bytes);
+  if (rc != 0) throw Error{SG_ERR_CALLBACK, a2a ? "all_to_all transport callback failed"
+                                                : "all_gather transport callback failed"};
+  SG_HIP(hipMemcpyAsync(drecv, d->hrecv, total, hipMemcpyHostToDevice, ctx->stream));
+}
+
+void plan(uint64_t n, int G, uint64_t& n1, uint64_t& n2) {
+  SG_REQUIRE(n >= 2 && (n & (n - 1)) == 0, "distributed transform: n must be a power of two >= 2");
+  SG_REQUIRE(G >= 1 && (G & (G - 1)) == 0, "distributed transform: the rank count must be a power of two");
+  const int logn = ilog2_exact(n);
+  n1 = (uint64_t)1 << (logn / 2);
+  n2 = n / n1;
+  SG_REQUIRE(n1 % G == 0 && n2 % (4 * (uint64_t)G) == 0,
+             "distributed transform: n too small for this many ranks (needs N1 >= G and N2 >= 4 G)");
+}
+
+void check_order_n(const fe& root, uint64_t n) {
+  SG_REQUIRE(fe_is_canonical(root), "root must be canonical");
+  SG_REQUIRE(fe_eq(fe_pow(root, n / 2), fe_neg(fe_one())), "distributed ntt needs a root of order exactly n");
+}
+
+void tables3(sg_ctx* ctx, const fe& base, const fe** T) {
+  T[0] = ctx->pow_table(base, 4096);
+  T[1] = ctx->pow_table(fe_pow(base, (uint64_t)1 << 12), 4096);
+  T[2] = ctx->pow_table(fe_pow(base, (uint64_t)1 << 24), 4096);
+}
+
+// X = DFT_root over (n1, n2): input rows (row_len entries per row, zero beyond; or, with in_il,
+// R' interleaved rows of n2 entries: row r's element j at in[j * in_il + r]); output
+// [R][n1] rows (row c = k2 - g R, element k1); post: Montgomery constant on every output
+void four_step(sg_dist* d, const fe& root, const fe* in, uint64_t row_len, uint64_t in_il, uint64_t n1, uint64_t n2,
+               fe* out, const fe* post_host) {
+  sg_ctx* ctx = d->ctx;
+  const int G = d->G;
+  const uint64_t rows = n1 / G, R = n2 / G;
+  SG_REQUIRE(row_len >= 1 && row_len <= n2, "distributed transform: row length must be in [1, N2]");
+  SG_REQUIRE((uint64_t)n1 * n2 <= ((uint64_t)1 << 36), "distributed transform: n above 2^36");
+  const int log1 = ilog2_exact(n1), log2 = ilog2_exact(n2);
+  const fe w2 = fe_pow(root, n1);  // order n2
+  const fe w1 = fe_pow(root, n2);  // order n1
+  const fe* tw2 = ctx->stage_twiddles(w2, log2);
+  const fe* tw1 = ctx->stage_twiddles(w1, log1);
+  const fe* T[3];
+  tables3(ctx, root, T);
+  DevBuf z(ctx, rows * n2 * sizeof(fe)), send(ctx, rows * n2 * sizeof(fe)), recv(ctx, n1 * R * sizeof(fe));
+  // 1. size-N2 NTTs; the last pass applies w^(j1 k2) and packs [h][r][c] for the all-to-all
+  int skip = 0;
+  if (!in_il)
+    while (skip < log2 && (row_len << (skip + 1)) <= n2) ++skip;
+  for (uint64_t r0 = 0; r0 < rows; r0 += kRows) {
+    const uint64_t cnt = std::min<uint64_t>(kRows, rows - r0);
+    NttEpilogue ep{send.as<fe>(), T[0], T[1], T[2], r0, (uint64_t)d->g * rows, rows, ilog2_exact(R)};
+    fe* zo = z.as<fe>() + r0 * n2;
+    const fe* ii = in_il ? in + r0 : in + r0 * row_len;
+    SG_HIP(launch_ntt_fused(&zo, &ii, (int)cnt, row_len, log2, tw2, nullptr, nullptr, skip, nullptr, ctx->stream,
+                            in_il ? 1 : row_len, n2, in_il, &ep));
+  }
+  // 2. the one exchange: rank h receives block h of every rank -> recv = [j1][c]
+  exchange(d, send.get(), recv.get(), rows * R * sizeof(fe), /*a2a=*/true);
+  // 3. size-N1 NTTs over the R interleaved columns of recv
+  DevBuf dpost;
+  const fe* post = nullptr;
+  if (post_host) {
+    dpost = DevBuf(ctx, sizeof(fe));
+    SG_HIP(hipMemcpyAsync(dpost.get(), post_host, sizeof(fe), hipMemcpyHostToDevice, ctx->stream));
+    post = dpost.as<fe>();
+  }
+  for (uint64_t c0 = 0; c0 < R; c0 += kRows) {
+    const uint64_t cnt = std::min<uint64_t>(kRows, R - c0);
+    fe* oo = out + c0 * n1;
+    const fe* rr = recv.as<fe>() + c0;
+    SG_HIP(launch_ntt_fused(&oo, &rr, (int)cnt, n1, log1, tw1, nullptr, nullptr, 0, post, ctx->stream, 1, n1, R,
+                            nullptr));
+  }
+}
+
+void dist_ntt(sg_dist* d, const fe& root, const fe* cols, uint64_t row_len, uint64_t n, fe* runs) {
+  uint64_t n1, n2;
+  plan(n, d->G, n1, n2);
+  check_order_n(root, n);
+  const uint64_t R = n2 / d->G;
+  DevBuf t(d->ctx, R * n1 * sizeof(fe));
+  four_step(d, root, cols, row_len, 0, n1, n2, t.as<fe>(), nullptr);
+  SG_HIP(launch_swap01(t.as<fe>(), runs, R, n1, 1, d->ctx->stream));  // [c][k1] -> [k1][c]
+}
+
+void dist_intt(sg_dist* d, const fe& root, const fe* runs, uint64_t n, fe* cols) {
+  uint64_t n1, n2;
+  plan(n, d->G, n1, n2);
+  check_order_n(root, n);
+  // the run shard [n1][R] is the interleaved column shard of (N1', N2') = (n2, n1): row c of
+  // length n1 at runs[k1 R + c]; the inverse four-step's output rows [n1/G][n2] are the column shard
+  const fe inv = fe_inv(root);
+  const fe ninv = to_mont(fe_inv(fe_from_u64(n)));
+  SG_REQUIRE(n2 % d->G == 0 && (n1 / d->G) % 4 == 0 && n1 / d->G >= 4,
+             "distributed intt: n too small for this many ranks (needs N1 >= 4 G)");
+  four_step(d, inv, runs, n1, n2 / d->G, n2, n1, cols, &ninv);
+}
+
+void dist_coset_evaluate(sg_dist* d, const fe& gen, uint64_t n, const fe& offset, const fe* cols, uint64_t row_len,
+                         fe* runs) {
+  uint64_t n1, n2;
+  plan(n, d->G, n1, n2);
+  const uint64_t rows = n1 / d->G;
+  SG_REQUIRE(row_len >= 1 && row_len <= n2, "distributed LDE: row length must be in [1, N2]");
+  // Polynomial::scale (polynomial.rs:109-121): coefficient j = (g rows + r) + N1 c times offset^j
+  DevBuf sc(d->ctx, rows * row_len * sizeof(fe));
+  SG_HIP(hipMemcpyAsync(sc.get(), cols, rows * row_len * sizeof(fe), hipMemcpyDeviceToDevice, d->ctx->stream));
+  const fe* T[3];
+  tables3(d->ctx, offset, T);
+  SG_HIP(launch_mul_pow(sc.as<fe>(), rows, row_len, n1, 0, (uint64_t)d->g * rows, 1, T[0], T[1], T[2],
+                        d->ctx->stream));
+  dist_ntt(d, gen, sc.as<fe>(), row_len, n, runs);
+}
+
+// root of the natural-order codeword held as runs [k1s][R] on every rank (merkle_root.rs:21-32):
+// a forest of k1s subtrees per rank, the run roots all-gathered (64 B each), the top on every rank
+void dist_merkle_root(sg_dist* d, const fe* runs, uint64_t k1s, uint64_t R, uint8_t root[64]) {
+  sg_ctx* ctx = d->ctx;
+  SG_REQUIRE(R >= 1 && (R & (R - 1)) == 0 && k1s >= 1 && (k1s & (k1s - 1)) == 0, "Leafs len must be power of two");
+  const uint64_t per = merkle_tree_digests(R) * 8;  // u64 per subtree
+  DevBuf forest(ctx, k1s * per * 8), roots(ctx, k1s * 64), all(ctx, d->G * k1s * 64), ordered(ctx, d->G * k1s * 64);
+  for (uint64_t t0 = 0; t0 < k1s; t0 += kRows) {
+    const int cnt = (int)std::min<uint64_t>(kRows, k1s - t0);
+    const fe* lv = runs + t0 * R;
+    uint64_t* tr = forest.as<uint64_t>() + t0 * per;
+    SG_HIP(launch_merkle_tree(&lv, &tr, cnt, R, nullptr, ctx->stream, R, per, 0));
+  }
+  SG_HIP(launch_gather_roots(forest.as<uint64_t>(), per, (2 * R - 2) * 8, roots.as<uint64_t>(), k1s, ctx->stream));
+  exchange(d, roots.get(), all.get(), k1s * 64, /*a2a=*/false);  // [g][k1]
+  // [g][k1] -> [k1][g]: global run order (a digest is 4 field-element slots)
+  SG_HIP(launch_swap01(all.as<fe>(), ordered.as<fe>(), d->G, k1s, 4, ctx->stream));
+  const uint64_t m = d->G * k1s;
+  if (m == 1) {
+    SG_HIP(hipMemcpyAsync(root, ordered.get(), 64, hipMemcpyDeviceToHost, ctx->stream));
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+    return;
+  }
+  DevBuf top(ctx, merkle_tree_digests(m) * 64);
+  SG_HIP(hipMemcpyAsync(top.get(), ordered.get(), m * 64, hipMemcpyDeviceToDevice, ctx->stream));
+  uint64_t* tr = top.as<uint64_t>();
+  uint64_t* root_dev = ctx->pinned_roots_dev;
+  SG_HIP(launch_merkle_tree(nullptr, &tr, 1, m, &root_dev, ctx->stream, 0, 0, 1));
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  memcpy(root, ctx->pinned_roots, 64);
+}
+
+// fri.rs:115-172 on a run-sharded codeword.  The fold partner of i is i + n/2: same k2,
+// k1 + N1/2, i.e. on the same rank, so folds stay local while more than one run per rank is
+// left; every rank pushes the same roots, so the Fiat-Shamir challenges agree without a
+// broadcast.  With one run per rank left, the N2-element codeword is all-gathered and the
+// remaining rounds run through the single-GPU commit.
+void dist_fri_commit(sg_dist* d, const sg_fri* f, const fe* runs, uint64_t n, const sg_proof_stream* ps) {
+  sg_ctx* ctx = d->ctx;
+  SG_REQUIRE(ps && ps->push && ps->fiat_shamir_prover, "proof stream callbacks required");
+  SG_REQUIRE(n == f->domain_length, "Length of the domain doesnt match the length of initial codeword");
+  const size_t rounds = fri_num_rounds(f);
+  SG_REQUIRE(rounds >= 1, "FRI: zero rounds for this domain");
+  uint64_t n1, n2;
+  plan(n, d->G, n1, n2);
+  const uint64_t R = n2 / d->G;
+  fe omega = to_fe(f->omega), offset = to_fe(f->offset);
+  SG_REQUIRE(fe_is_canonical(omega) && fe_is_canonical(offset), "FRI omega/offset must be canonical");
+  const fe inv2 = fe_inv(fe_from_u64(2));
+  const fe* cur = runs;
+  DevBuf owned;
+  uint64_t k1s = n1, length = n;
+  size_t r = 0;
+  while (k1s > 1 && r < rounds) {
+    const fe winv = fe_inv(omega);
+    SG_REQUIRE(fe_eq(fe_pow(omega, length - 1), winv), "error in commit: omega does not have the right order!");
+    uint8_t root[64];
+    dist_merkle_root(d, cur, k1s, R, root);
+    push_obj(ps, SG_OBJ_ROOT, root, 64);
+    if (r == rounds - 1) break;
+    uint8_t chal[32];
+    if (ps->fiat_shamir_prover(ps->user, 32, chal) != 0)
+      throw Error{SG_ERR_CALLBACK, "proof stream fiat_shamir callback failed"};
+    const fe alpha = fe_sample(chal, 32);
+    // fri.rs:151-159 on the local runs: local l is global (l / R) n2 + g R + l % R
+    const uint64_t half = k1s * R / 2;
+    DevBuf nxt(ctx, half * sizeof(fe));
+    const fe* T[3];
+    tables3(ctx, winv, T);
+    const fe K = to_mont(fe_mul(fe_mul(alpha, fe_inv(offset)), inv2));
+    SG_HIP(launch_fri_fold_runs(nxt.as<fe>(), cur, half, R, n2, (uint64_t)d->g * R, T[0], T[1], T[2], K,
+                                ctx->stream));
+    owned = std::move(nxt);
+    cur = owned.as<fe>();
+    k1s /= 2;
+    length /= 2;
+    omega = fe_mul(omega, omega);
+    offset = fe_mul(offset, offset);
+    ++r;
+  }
+  if (r == rounds - 1 && k1s > 1) {
+    // every round done while still sharded: gather the last codeword (fri.rs:166) in natural order
+    DevBuf all(ctx, d->G * k1s * R * sizeof(fe)), nat(ctx, d->G * k1s * R * sizeof(fe));
+    exchange(d, cur, all.get(), k1s * R * sizeof(fe), /*a2a=*/false);          // [g][k1][c]
+    SG_HIP(launch_swap01(all.as<fe>(), nat.as<fe>(), d->G, k1s, R, ctx->stream));  // [k1][g][c]
+    const uint64_t len = d->G * k1s * R;
+    std::vector<fe> last(len);
+    SG_HIP(hipMemcpyAsync(last.data(), nat.get(), len * sizeof(fe), hipMemcpyDeviceToHost, ctx->stream));
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+    std::vector<uint8_t> payload;
+    payload.reserve(len * 16);
+    for (auto& v : last) put_u128_be(payload, v);
+    push_obj(ps, SG_OBJ_CODEWORD, payload.data(), payload.size());
+    return;
+  }
+  // one run per rank left: [g][c] is the natural order of the N2-element codeword
+  DevBuf full(ctx, d->G * R * sizeof(fe));
+  exchange(d, cur, full.get(), R * sizeof(fe), /*a2a=*/false);
+  sg_fri sub = *f;
+  sub.offset = from_fe(offset);
+  sub.omega = from_fe(omega);
+  sub.domain_length = length;
+  SG_REQUIRE(fri_num_rounds(&sub) == rounds - r, "FRI tail round count mismatch");
+  sg_fri_state st;
+  fri_commit_dev(ctx, &sub, full.as<fe>(), length, ps, st, /*borrow_input=*/true);
+}
+
+sg_dist* checked(sg_dist* d) {
+  if (!d || !d->ctx) throw Error{SG_ERR_INVALID, "null communicator"};
+  return d;
+}
+
+}  // namespace
+}  // namespace sg
+
+using namespace sg;
+
+extern "C" int sg_dist_unique_id(uint8_t* id) {
+  return guard(nullptr, [&] {
+    SG_REQUIRE(id, "null argument");
+    ncclUniqueId u;
+    SG_NCCL(ncclGetUniqueId(&u));
+    memcpy(id, u.internal, SG_DIST_ID_BYTES);
+  });
+}
+
+extern "C" int sg_dist_create(sg_ctx* ctx, const uint8_t* id, int nranks, int rank, sg_dist** out) {
+  return guard(ctx, [&] {
+    SG_REQUIRE(out && id, "null argument");
+    SG_REQUIRE(nranks >= 1 && rank >= 0 && rank < nranks, "bad rank / rank count");
+    set_device(ctx);
+    std::unique_ptr<sg_dist> d(new sg_dist());
+    d->ctx = ctx;
+    d->G = nranks;
+    d->g = rank;
+    ncclUniqueId u;
+    memcpy(u.internal, id, SG_DIST_ID_BYTES);
+    SG_NCCL(ncclCommInitRank(&d->comm, nranks, u, rank));
+    *out = d.release();
+  });
+}
+
+extern "C" int sg_dist_create_transport(sg_ctx* ctx, int nranks, int rank, const sg_dist_transport* t,
+                                        sg_dist** out) {
+  return guard(ctx, [&] {
+    SG_REQUIRE(out && t && t->all_to_all && t->all_gather, "transport callbacks required");
+    SG_REQUIRE(nranks >= 1 && rank >= 0 && rank < nranks, "bad rank / rank count");
+    set_device(ctx);
+    std::unique_ptr<sg_dist> d(new sg_dist());
+    d->ctx = ctx;
+    d->G = nranks;
+    d->g = rank;
+    d->tr = *t;
+    d->staged = true;
+    *out = d.release();
+  });
+}
+
+extern "C" void sg_dist_destroy(sg_dist* d) { delete d; }
+
+extern "C" int sg_dist_plan(size_t n, int nranks, size_t* n1, size_t* n2) {
+  return guard(nullptr, [&] {
+    SG_REQUIRE(n1 && n2, "null argument");
+    uint64_t a, b;
+    plan(n, nranks, a, b);
+    *n1 = a;
+    *n2 = b;
+  });
+}
+
+extern "C" int sg_dist_ntt(sg_dist* d, sg_fe root, const sg_fe* d_cols, size_t row_len, size_t n, sg_fe* d_runs) {
+  sg_ctx* ctx = d ? d->ctx : nullptr;
+  return guard(ctx, [&] {
+    checked(d);
+    set_device(ctx);
+    SG_REQUIRE(d_cols && d_runs, "null buffer");
+    dist_ntt(d, to_fe(root), reinterpret_cast<const fe*>(d_cols), row_len, n, reinterpret_cast<fe*>(d_runs));
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+  });
+}
+
+extern "C" int sg_dist_intt(sg_dist* d, sg_fe root, const sg_fe* d_runs, size_t n, sg_fe* d_cols) {
+  sg_ctx* ctx = d ? d->ctx : nullptr;
+  return guard(ctx, [&] {
+    checked(d);
+    set_device(ctx);
+    SG_REQUIRE(d_cols && d_runs, "null buffer");
+    dist_intt(d, to_fe(root), reinterpret_cast<const fe*>(d_runs), n, reinterpret_cast<fe*>(d_cols));
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+  });
+}
+
+extern "C" int sg_dist_coset_evaluate(sg_dist* d, sg_fe generator, size_t root_order, sg_fe offset,
+                                      const sg_fe* d_cols, size_t row_len, sg_fe* d_runs) {
+  sg_ctx* ctx = d ? d->ctx : nullptr;
+  return guard(ctx, [&] {
+    checked(d);
+    set_device(ctx);
+    SG_REQUIRE(d_cols && d_runs, "null buffer");
+    const fe off = to_fe(offset);
+    SG_REQUIRE(fe_is_canonical(off), "offset must be canonical");
+    dist_coset_evaluate(d, to_fe(generator), root_order, off, reinterpret_cast<const fe*>(d_cols), row_len,
+                        reinterpret_cast<fe*>(d_runs));
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+  });
+}
+
+extern "C" int sg_dist_merkle_root(sg_dist* d, const sg_fe* d_runs, size_t n, uint8_t* root) {
+  sg_ctx* ctx = d ? d->ctx : nullptr;
+  return guard(ctx, [&] {
+    checked(d);
+    set_device(ctx);
+    SG_REQUIRE(d_runs && root, "null argument");
+    uint64_t n1, n2;
+    plan(n, d->G, n1, n2);
+    dist_merkle_root(d, reinterpret_cast<const fe*>(d_runs), n1, n2 / d->G, root);
+  });
+}
+
+extern "C" int sg_dist_fri_commit(sg_dist* d, const sg_fri* fri, const sg_fe* d_runs, size_t n,
+                                  const sg_proof_stream* ps) {
+  sg_ctx* ctx = d ? d->ctx : nullptr;
+  return guard(ctx, [&] {
+    checked(d);
+    set_device(ctx);
+    SG_REQUIRE(fri && d_runs, "null argument");
+    dist_fri_commit(d, fri, reinterpret_cast<const fe*>(d_runs), n, ps);
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+  });
+}

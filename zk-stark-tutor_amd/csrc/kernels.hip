@@ -93,6 +93,7 @@ struct GatherArgs {
   fe* out[kMaxBatch];
   const fe* in[kMaxBatch];
   uint64_t in_ys, out_ys;  // != 0: strided rows, row blockIdx.y at in[0] + y * in_ys / out[0] + y * out_ys
+  uint64_t in_es;          // element stride of an input row (1; R for R interleaved rows, in_ys = 1)
 };
 
 __global__ void k_bitrev_gather(GatherArgs ga, uint64_t n_in, int logn, const fe* __restrict__ sA,
@@ -105,7 +106,7 @@ __global__ void k_bitrev_gather(GatherArgs ga, uint64_t n_in, int logn, const fe
   uint64_t i = logn ? (__builtin_bitreverse64(jj) >> (64 - logn)) : 0;
   fe v = fe_zero();
   if (i < n_in) {
-    v = ld_fe(in + i);
+    v = ld_fe(in + i * ga.in_es);
     if (sA) {
       fe f = mont_mul(ld_fe(sA + (i & 4095)), ld_fe(sB + (i >> 12)));  // Montgomery of offset^i
       v = mont_mul(v, f);
@@ -143,7 +144,33 @@ struct PassArgs {
   int logC;            // columns per tile (consecutive low-bit indices), C <= 2^b0
   int s_cut;           // stages above s_cut compute their twiddles from the A/B tables
   uint64_t ys;         // != 0: strided rows, transform blockIdx.y at data[0] + y * ys
+  // four-step epilogue of a transform's last pass (ep_out != nullptr, strided rows): output k of
+  // row r = ep_row0 + blockIdx.y is multiplied by w^((ep_j0 + r) k) and stored to the all-to-all
+  // send buffer [k >> ep_logR][r][k & (2^ep_logR - 1)] instead of back in place
+  fe* ep_out;
+  const fe* ep_T0;
+  const fe* ep_T1;
+  const fe* ep_T2;
+  uint64_t ep_row0, ep_j0, ep_rows;
+  int ep_logR;
 };
+
+// store of a transform's element k (row pointer `row`) at the end of a pass
+__device__ __forceinline__ void pass_store(const PassArgs& a, fe* row, uint64_t k, fe v, bool post, bool last,
+                                           const fe& pc) {
+  if (last && a.ep_out) {
+    const uint64_t r = a.ep_row0 + blockIdx.y;
+    const uint64_t e = (a.ep_j0 + r) * k;  // < 2^36 (host-checked)
+    const fe w = mont_mul(mont_mul(ld_fe(a.ep_T0 + (e & 4095)), ld_fe(a.ep_T1 + ((e >> 12) & 4095))),
+                          ld_fe(a.ep_T2 + (e >> 24)));
+    const uint64_t R = (uint64_t)1 << a.ep_logR;
+    st_fe(a.ep_out + ((k >> a.ep_logR) * a.ep_rows + r) * R + (k & (R - 1)), mont_mul(v, w));
+    return;
+  }
+  if (post) v = mont_mul(v, pc);
+  else if (last) v = fe_canon(v);
+  st_fe(row + k, v);
+}
 
 // twiddle of global stage S (1-based) for index k < 2^(S-1): Montgomery(root^(k n / 2^S)),
 // from the stage-major table (S <= s_cut) or as A[e & 4095] * B[e >> 12], e = k n / 2^S
@@ -264,18 +291,12 @@ __global__ __launch_bounds__(256, SG_NTT_WPE) void k_ntt_pass(PassArgs a) {
     for (int k = 0; k < PER; ++k) {
       uint32_t l = threadIdx.x + 256u * k;
       uint32_t g = l >> logC, c = l & (C - 1);
-      fe v = lds[l];
-      if (post) v = mont_mul(v, pc);
-      else if (last) v = fe_canon(v);
-      st_fe(data + base + ((uint64_t)g << a.b0) + c, v);
+      pass_store(a, data, base + ((uint64_t)g << a.b0) + c, lds[l], post, last, pc);
     }
   } else {
     for (uint32_t l = threadIdx.x; l < tile; l += blockDim.x) {
       uint32_t g = l >> logC, c = l & (C - 1);
-      fe v = lds[l];
-      if (post) v = mont_mul(v, pc);
-      else if (last) v = fe_canon(v);
-      st_fe(data + base + ((uint64_t)g << a.b0) + c, v);
+      pass_store(a, data, base + ((uint64_t)g << a.b0) + c, lds[l], post, last, pc);
     }
   }
 }
@@ -320,12 +341,8 @@ __global__ __launch_bounds__(256, SG_NTT_WPE) void k_ntt_pass_rr(PassArgs a) {
   const bool last = a.b0 + L == a.logn;  // the transform's last pass stores canonical values
   const fe pc = post ? ld_fe(a.post) : fe_zero();
 #pragma unroll
-  for (int m = 0; m < 8; ++m) {
-    fe v = x[m];
-    if (post) v = mont_mul(v, pc);
-    else if (last) v = fe_canon(v);
-    st_fe(data + base + ((uint64_t)(qq + ((uint32_t)m << tl)) << a.b0) + c, v);
-  }
+  for (int m = 0; m < 8; ++m)
+    pass_store(a, data, base + ((uint64_t)(qq + ((uint32_t)m << tl)) << a.b0) + c, x[m], post, last, pc);
 }
 
 // First pass with the bit-reversal fused in (fft/ntt.rs:14 bit_reverse_copy).
@@ -350,6 +367,10 @@ struct FirstArgs {
   int skip;
   int s_cut;
   uint64_t in_ys, out_ys;  // != 0: strided rows (see GatherArgs)
+  // != 0: the rows are interleaved, row y's element i at in[0] + i * in_il + y; the tile's C
+  // columns are then C consecutive rows at one bit-reversed position h (64-byte runs across rows)
+  // instead of C positions of one row -- the butterflies are the same (columns are independent)
+  uint64_t in_il;
 };
 
 template <int TL>
@@ -362,9 +383,21 @@ __global__ __launch_bounds__(256, SG_NTT_WPE) void k_ntt_first(FirstArgs a) {
   // a contiguous range of column groups; neighbouring C-runs then share its L2
   uint32_t bx = blockIdx.x;
   if ((gridDim.x & 7) == 0) bx = (bx & 7) * (gridDim.x >> 3) + (bx >> 3);
-  const uint64_t c0 = (uint64_t)bx << logC;
-  const fe* __restrict__ in = a.in_ys ? a.in[0] + (uint64_t)blockIdx.y * a.in_ys : a.in[blockIdx.y];
-  fe* __restrict__ out = a.out_ys ? a.out[0] + (uint64_t)blockIdx.y * a.out_ys : a.out[blockIdx.y];
+  const bool il = a.in_il != 0;
+  // column k of the tile: position h = hcol(k) of row ycol(k)
+  const uint64_t c0 = il ? (uint64_t)bx : (uint64_t)bx << logC;
+  const uint64_t y0 = il ? (uint64_t)blockIdx.y << logC : (uint64_t)blockIdx.y;
+  auto hcol = [&](uint64_t k) { return il ? c0 : c0 + k; };
+  auto ycol = [&](uint64_t k) { return il ? y0 + k : y0; };
+  // element idx of column k's row
+  auto in_at = [&](uint64_t k, uint64_t idx) -> const fe* {
+    if (il) return a.in[0] + idx * a.in_il + ycol(k);
+    return (a.in_ys ? a.in[0] + y0 * a.in_ys : a.in[y0]) + idx;
+  };
+  auto out_row = [&](uint64_t k) -> fe* {
+    const uint64_t y = ycol(k);
+    return a.out_ys ? a.out[0] + y * a.out_ys : a.out[y];
+  };
   PassArgs pa;
   pa.tw = a.tw;
   pa.post = nullptr;
@@ -373,6 +406,7 @@ __global__ __launch_bounds__(256, SG_NTT_WPE) void k_ntt_first(FirstArgs a) {
   pa.L = L;
   pa.logC = logC;
   pa.s_cut = a.s_cut;
+  pa.ep_out = nullptr;
   // one radix-8 group per thread in the first and last steps (column c, group qq)
   const bool regs = L >= 6 && ((1u << (L - 3)) << logC) == blockDim.x;
   int t = skip;
@@ -383,10 +417,10 @@ __global__ __launch_bounds__(256, SG_NTT_WPE) void k_ntt_first(FirstArgs a) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const uint32_t u = __builtin_bitreverse32(8 * qq + j) >> (32 - L);
-      const uint64_t idx = c0 + c + ((uint64_t)u << (m - L));
+      const uint64_t idx = hcol(c) + ((uint64_t)u << (m - L));
       x[j] = fe_zero();
       if (idx < a.n_in) {
-        x[j] = ld_fe(in + idx);
+        x[j] = ld_fe(in_at(c, idx));
         if (a.sA) x[j] = mont_mul(x[j], mont_mul(ld_fe(a.sA + (idx & 4095)), ld_fe(a.sB + (idx >> 12))));
       }
     }
@@ -399,10 +433,10 @@ __global__ __launch_bounds__(256, SG_NTT_WPE) void k_ntt_first(FirstArgs a) {
     const uint32_t rep = 1u << skip;
     for (uint32_t l = threadIdx.x; l < rows * C; l += blockDim.x) {
       const uint32_t k = l & (C - 1), u = l >> logC;
-      const uint64_t idx = c0 + k + ((uint64_t)u << (m - L));
+      const uint64_t idx = hcol(k) + ((uint64_t)u << (m - L));
       fe v = fe_zero();
       if (idx < a.n_in) {
-        v = ld_fe(in + idx);
+        v = ld_fe(in_at(k, idx));
         if (a.sA) v = mont_mul(v, mont_mul(ld_fe(a.sA + (idx & 4095)), ld_fe(a.sB + (idx >> 12))));
       }
       const uint32_t tr = __builtin_bitreverse32(u) >> (32 - L);
@@ -423,9 +457,10 @@ __global__ __launch_bounds__(256, SG_NTT_WPE) void k_ntt_first(FirstArgs a) {
 #pragma unroll
     for (int mm = 0; mm < 8; ++mm) x[mm] = lds[((qq + ((uint32_t)mm << tl)) << logC) + c];
     radix_regs<3, false>(x, pa, tl, qq, 0);
-    const uint64_t h = __builtin_bitreverse64(c0 + c) >> (64 - (m - L));
+    const uint64_t h = __builtin_bitreverse64(hcol(c)) >> (64 - (m - L));
+    fe* const orow = out_row(c);
 #pragma unroll
-    for (int mm = 0; mm < 8; ++mm) st_fe(out + (h << L) + qq + ((uint32_t)mm << tl), x[mm]);
+    for (int mm = 0; mm < 8; ++mm) st_fe(orow + (h << L) + qq + ((uint32_t)mm << tl), x[mm]);
     return;
   }
   while (t < L) {
@@ -437,9 +472,8 @@ __global__ __launch_bounds__(256, SG_NTT_WPE) void k_ntt_first(FirstArgs a) {
   const uint32_t tile = 1u << (L + logC);
   for (uint32_t l = threadIdx.x; l < tile; l += blockDim.x) {
     const uint32_t tt = l & ((1u << L) - 1), k = l >> L;
-    const uint64_t c = c0 + k;
-    const uint64_t h = __builtin_bitreverse64(c) >> (64 - (m - L));
-    st_fe(out + (h << L) + tt, lds[(tt << logC) + k]);
+    const uint64_t h = __builtin_bitreverse64(hcol(k)) >> (64 - (m - L));
+    st_fe(out_row(k) + (h << L) + tt, lds[(tt << logC) + k]);
   }
 }
 
@@ -946,7 +980,7 @@ static bool batch_ok(int batch, uint64_t ys) {
 
 hipError_t launch_bitrev_gather(fe* const* out, const fe* const* in, int batch, uint64_t n_in, int logn,
                                 const fe* sA, const fe* sB, int skip, hipStream_t s, uint64_t in_ys,
-                                uint64_t out_ys) {
+                                uint64_t out_ys, uint64_t in_es) {
   if (!batch_ok(batch, out_ys) || (in_ys != 0) != (out_ys != 0)) return hipErrorInvalidValue;
   uint64_t n = (uint64_t)1 << logn;
   GatherArgs ga;
@@ -957,6 +991,7 @@ hipError_t launch_bitrev_gather(fe* const* out, const fe* const* in, int batch, 
   }
   ga.in_ys = in_ys;
   ga.out_ys = out_ys;
+  ga.in_es = in_es ? in_es : 1;
   ProfScope ps("bitrev_gather", batch * (16 * (n_in < n ? n_in : n) + 16 * n), s, (uint64_t)batch * n);
   hipLaunchKernelGGL(k_bitrev_gather, dim3(nblocks(n, 256), batch), dim3(256), 0, s, ga, n_in, logn, sA, sB, skip);
   return hipGetLastError();
@@ -972,8 +1007,9 @@ hipError_t launch_scale_const(fe* data, uint64_t n, const fe* cst, hipStream_t s
 // stages on 2^L x C tiles (<= 4096 elements = 64 KiB of LDS), with C
 // consecutive low-bit indices per tile so global accesses are C*16-byte runs.
 hipError_t launch_ntt_dit(fe* const* data, int batch, const fe* tw, int logn, const fe* post, int first_b0,
-                          hipStream_t s, uint64_t ys) {
+                          hipStream_t s, uint64_t ys, const NttEpilogue* ep) {
   if (!batch_ok(batch, ys)) return hipErrorInvalidValue;
+  if (ep && (!ys || post || first_b0 >= logn)) return hipErrorInvalidValue;  // the epilogue needs a last pass
   if (ys && ys != ((uint64_t)1 << logn)) return hipErrorInvalidValue;  // rows are contiguous transforms
   const int np = ys ? 1 : batch;
   static bool lds_attr = false;
@@ -1016,6 +1052,16 @@ hipError_t launch_ntt_dit(fe* const* data, int batch, const fe* tw, int logn, co
     a.L = (rem + passes - 1) / passes;
     a.logC = b0 < tile_log - a.L ? b0 : tile_log - a.L;
     a.post = (b0 + a.L == logn) ? post : nullptr;
+    a.ep_out = (ep && b0 + a.L == logn) ? ep->out : nullptr;
+    if (a.ep_out) {
+      a.ep_T0 = ep->T0;
+      a.ep_T1 = ep->T1;
+      a.ep_T2 = ep->T2;
+      a.ep_row0 = ep->row0;
+      a.ep_j0 = ep->j0;
+      a.ep_rows = ep->rows;
+      a.ep_logR = ep->logR;
+    }
     uint64_t tile = (uint64_t)1 << (a.L + a.logC);
     uint64_t ntiles = ((uint64_t)1 << logn) / tile;
     unsigned threads = tile >= 2048 ? 256 : (unsigned)(tile / 8 > 64 ? tile / 8 : 64);
@@ -1043,8 +1089,9 @@ hipError_t launch_ntt_dit(fe* const* data, int batch, const fe* tw, int logn, co
 // later pass), then launch_ntt_dit from stage L1 + 1.  `out` must not alias `in`.
 hipError_t launch_ntt_fused(fe* const* out, const fe* const* in, int batch, uint64_t n_in, int logn, const fe* tw,
                             const fe* sA, const fe* sB, int skip, const fe* post, hipStream_t s, uint64_t in_ys,
-                            uint64_t out_ys) {
+                            uint64_t out_ys, uint64_t in_il, const NttEpilogue* ep) {
   if (!batch_ok(batch, out_ys) || (in_ys != 0) != (out_ys != 0)) return hipErrorInvalidValue;
+  if (in_il && (!out_ys || (batch & 3))) return hipErrorInvalidValue;  // interleaved rows: strided, 4 per tile
   const int np = out_ys ? 1 : batch;
   static bool lds_attr = false;
   if (!lds_attr) {
@@ -1054,9 +1101,10 @@ hipError_t launch_ntt_fused(fe* const* out, const fe* const* in, int batch, uint
   }
   constexpr int TL = 11, LOGC1 = 2, L1 = TL - LOGC1;
   if (logn <= L1 + LOGC1 || logn - L1 > 63) {
-    hipError_t e = launch_bitrev_gather(out, in, batch, n_in, logn, sA, sB, skip, s, in_ys, out_ys);
+    hipError_t e = launch_bitrev_gather(out, in, batch, n_in, logn, sA, sB, skip, s, in_il ? 1 : in_ys, out_ys,
+                                        in_il);
     if (e != hipSuccess) return e;
-    return launch_ntt_dit(out, batch, tw, logn, post, skip, s, out_ys);
+    return launch_ntt_dit(out, batch, tw, logn, post, skip, s, out_ys, ep);
   }
   FirstArgs a;
   for (int b = 0; b < kMaxBatch; ++b) {
@@ -1074,16 +1122,19 @@ hipError_t launch_ntt_fused(fe* const* out, const fe* const* in, int batch, uint
   a.logC = LOGC1;
   a.skip = skip;
   a.s_cut = ntt_tw_cut(logn);
+  a.in_il = in_il;
   uint64_t n = (uint64_t)1 << logn;
   {
     ProfScope ps("ntt_first", batch * (16 * (n_in < n ? n_in : n) + 16 * n), s, (uint64_t)batch * n);
-    hipLaunchKernelGGL(k_ntt_first<TL>, dim3((unsigned)(n >> TL), batch), dim3(256), (size_t)16 << TL, s, a);
+    // interleaved rows: a tile is 4 rows at one position (grid: positions x row quads)
+    const dim3 grid = in_il ? dim3((unsigned)(n >> L1), (unsigned)(batch >> LOGC1)) : dim3((unsigned)(n >> TL), batch);
+    hipLaunchKernelGGL(k_ntt_first<TL>, grid, dim3(256), (size_t)16 << TL, s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
   // trivial stages beyond L1 are not replicated across tiles: later passes run
   // them as real butterflies on zeros, (a, 0) -> (a, a), which is exact
-  return launch_ntt_dit(out, batch, tw, logn, post, L1, s, out_ys);
+  return launch_ntt_dit(out, batch, tw, logn, post, L1, s, out_ys, ep);
 }
 
 uint64_t merkle_tree_digests(uint64_t n) { return 2 * n - 1; }

@@ -17,14 +17,28 @@ hipError_t launch_pow_table(fe* tw, const fe* A, const fe* B, uint64_t count, hi
 // pointer [0] (row y at ptr[0] + y * stride).
 hipError_t launch_bitrev_gather(fe* const* out, const fe* const* in, int batch, uint64_t n_in, int logn,
                                 const fe* sA, const fe* sB, int skip, hipStream_t s, uint64_t in_ys = 0,
-                                uint64_t out_ys = 0);
+                                uint64_t out_ys = 0, uint64_t in_es = 1);
 hipError_t launch_scale_const(fe* data, uint64_t n, const fe* cst, hipStream_t s);
+// Four-step epilogue of the last pass (multi-GPU NTT, dist.cpp): output k of row r (= row0 + the
+// launch's row) times w^((j0 + r) k), w^e = T0[e & 4095] T1[(e >> 12) & 4095] T2[e >> 24]
+// (Montgomery tables, e < 2^36), stored to out[k >> logR][r][k & (2^logR - 1)] (rows = rows of
+// the whole shard): the twiddle multiply and the all-to-all pack without their own HBM passes.
+struct NttEpilogue {
+  fe* out;
+  const fe* T0;
+  const fe* T1;
+  const fe* T2;
+  uint64_t row0, j0, rows;
+  int logR;
+};
 hipError_t launch_ntt_dit(fe* const* data, int batch, const fe* tw, int logn, const fe* post, int first_b0,
-                          hipStream_t s, uint64_t ys = 0);
-// bit-reversal (+ LDE scale, + `skip` trivial stages) fused into the first pass; out must not alias in
+                          hipStream_t s, uint64_t ys = 0, const NttEpilogue* ep = nullptr);
+// bit-reversal (+ LDE scale, + `skip` trivial stages) fused into the first pass; out must not alias in.
+// in_il != 0: `batch` interleaved input rows (row y's element i at in[0] + i * in_il + y; batch a
+// multiple of 4, strided output rows) -- a transpose folded into the first pass's gather.
 hipError_t launch_ntt_fused(fe* const* out, const fe* const* in, int batch, uint64_t n_in, int logn, const fe* tw,
                             const fe* sA, const fe* sB, int skip, const fe* post, hipStream_t s, uint64_t in_ys = 0,
-                            uint64_t out_ys = 0);
+                            uint64_t out_ys = 0, uint64_t in_il = 0, const NttEpilogue* ep = nullptr);
 uint64_t merkle_tree_digests(uint64_t n);
 // root_host (optional, per tree; pointer mode only): host-coherent 64-byte slots that receive the root.
 // start_level 1: level 0 of `tree` already holds n digests (a tree over given digests).

@@ -46,6 +46,13 @@ class sg_proof_stream(ctypes.Structure):
     _fields_ = [("user", ctypes.c_void_p), ("push", PUSH_CB), ("fiat_shamir_prover", FS_CB)]
 
 
+A2A_CB = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
+
+
+class sg_dist_transport(ctypes.Structure):
+    _fields_ = [("user", ctypes.c_void_p), ("all_to_all", A2A_CB), ("all_gather", A2A_CB)]
+
+
 # name -> (restype, argtypes)
 _P = ctypes.POINTER
 _vp = ctypes.c_void_p
@@ -117,6 +124,17 @@ PROTOTYPES = {
     "sg_forest_free": (None, [_vp, _vp]),
     "sg_merkle_top_dev": (ctypes.c_int, [_vp, _vp, _sz, _P(_vp)]),
     "sg_fri_fold_runs_dev": (ctypes.c_int, [_vp, sg_fe, sg_fe, sg_fe, _vp, _sz, _sz, _sz, _sz, _sz, _vp]),
+    # multi-GPU communicator (RCCL or a host-staged transport)
+    "sg_dist_unique_id": (ctypes.c_int, [_vp]),
+    "sg_dist_create": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int, _P(_vp)]),
+    "sg_dist_create_transport": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _P(sg_dist_transport), _P(_vp)]),
+    "sg_dist_destroy": (None, [_vp]),
+    "sg_dist_plan": (ctypes.c_int, [_sz, ctypes.c_int, _P(_sz), _P(_sz)]),
+    "sg_dist_ntt": (ctypes.c_int, [_vp, sg_fe, _vp, _sz, _sz, _vp]),
+    "sg_dist_intt": (ctypes.c_int, [_vp, sg_fe, _vp, _sz, _vp]),
+    "sg_dist_coset_evaluate": (ctypes.c_int, [_vp, sg_fe, _sz, sg_fe, _vp, _sz, _vp]),
+    "sg_dist_merkle_root": (ctypes.c_int, [_vp, _vp, _sz, _vp]),
+    "sg_dist_fri_commit": (ctypes.c_int, [_vp, _P(sg_fri), _vp, _sz, _P(sg_proof_stream)]),
     # polynomial algebra (fft/ntt_arithmetics.rs)
     "sg_poly_create": (ctypes.c_int, [_vp, _vp, _sz, _P(_vp)]),
     "sg_poly_create_dev": (ctypes.c_int, [_vp, _vp, _sz, _P(_vp)]),

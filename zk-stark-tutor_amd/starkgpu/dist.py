@@ -37,6 +37,7 @@ from __future__ import annotations
 import ctypes
 from typing import List, Optional, Sequence, Tuple
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -396,6 +397,126 @@ class DistStark:
         be.fri_commit(offset, omega, length, expansion, c, full, proof_stream)
 
 
+# ---------------------------------------------------------------- the C-ABI communicator
+
+class NativeDist:
+    """The sharded pipeline inside libstarkgpu (csrc/dist.cpp, include/stark_gpu.h sg_dist_*):
+    what a Rust caller binds.  ``transport="rccl"`` creates an RCCL communicator from a unique id
+    broadcast over the torch.distributed group (RCCL over xGMI, collectives on the library's
+    stream); ``transport="host"`` hands the library all-to-all / all-gather callbacks over host
+    buffers that run on the torch.distributed group (gloo), e.g. several ranks on one GPU.
+
+    Shards are int64 device tensors (2 words per element) in the layouts of ``DistStark``:
+    column shard in, run shard out (ntt / coset_evaluate), the reverse for intt."""
+
+    def __init__(self, ctx: Optional[api.Context] = None, transport: str = "rccl", group=None):
+        from ._lib import A2A_CB, sg_dist_transport
+        self.ctx = api._ctx(ctx)
+        self._lib = lib()
+        self.group = group
+        init = dist.is_available() and dist.is_initialized()
+        self.G = dist.get_world_size(group) if init else 1
+        self.g = dist.get_rank(group) if init else 0
+        self.device = torch.device("cuda", self.ctx.device)
+        h = ctypes.c_void_p()
+        if transport == "rccl":
+            uid = (ctypes.c_uint8 * 128)()
+            if self.g == 0:
+                self.ctx.check(self._lib.sg_dist_unique_id(uid))
+            if self.G > 1:
+                box = [bytes(uid)]
+                dist.broadcast_object_list(box, src=0, group=group)
+                uid = (ctypes.c_uint8 * 128).from_buffer_copy(box[0])
+            self.ctx.check(self._lib.sg_dist_create(self.ctx.handle, uid, self.G, self.g, ctypes.byref(h)))
+        elif transport == "host":
+            def _view(ptr, nbytes):  # host buffer as int64 words (elements are 16 B, digests 64 B)
+                return torch.from_numpy(np.ctypeslib.as_array((ctypes.c_int64 * (nbytes // 8)).from_address(ptr)))
+
+            def a2a(_user, send, recv, nbytes):
+                try:
+                    dist.all_to_all_single(_view(recv, nbytes * self.G), _view(send, nbytes * self.G),
+                                           group=self.group)
+                    return 0
+                except Exception:  # noqa: BLE001 - reported to the library as a callback failure
+                    return 1
+
+            def ag(_user, send, recv, nbytes):
+                try:
+                    parts = list(_view(recv, nbytes * self.G).chunk(self.G))
+                    dist.all_gather(parts, _view(send, nbytes).clone(), group=self.group)
+                    return 0
+                except Exception:  # noqa: BLE001
+                    return 1
+
+            self._cbs = (A2A_CB(a2a), A2A_CB(ag))  # keep the thunks alive
+            self._tr = sg_dist_transport(None, self._cbs[0], self._cbs[1])
+            self.ctx.check(self._lib.sg_dist_create_transport(self.ctx.handle, self.G, self.g, ctypes.byref(self._tr),
+                                                              ctypes.byref(h)))
+        else:
+            raise ValueError(f"unknown transport {transport!r}")
+        self.handle = h
+
+    def close(self) -> None:
+        if self.handle:
+            self._lib.sg_dist_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        self.close()
+
+    @staticmethod
+    def plan(n: int, world: int) -> Tuple[int, int]:
+        a, b = ctypes.c_size_t(), ctypes.c_size_t()
+        rc = lib().sg_dist_plan(n, world, ctypes.byref(a), ctypes.byref(b))
+        if rc != 0:
+            raise StarkGpuError(rc, f"no plan for n = {n} over {world} ranks")
+        return a.value, b.value
+
+    def _alloc(self, count: int) -> torch.Tensor:
+        return torch.empty(2 * count, dtype=torch.int64, device=self.device)
+
+    def ntt(self, root: int, cols: torch.Tensor, row_len: int, n: int) -> torch.Tensor:
+        """fft/ntt.rs:7-49: column shard -> run shard."""
+        n1, n2 = self.plan(n, self.G)
+        out = self._alloc(n1 * (n2 // self.G))
+        self.ctx.check(self._lib.sg_dist_ntt(self.handle, api._fe(root), ctypes.c_void_p(cols.data_ptr()), row_len,
+                                             n, ctypes.c_void_p(out.data_ptr())))
+        return out
+
+    def intt(self, root: int, runs: torch.Tensor, n: int) -> torch.Tensor:
+        """fft/ntt.rs:51-68: run shard -> column shard (rows of N2)."""
+        n1, n2 = self.plan(n, self.G)
+        out = self._alloc((n1 // self.G) * n2)
+        self.ctx.check(self._lib.sg_dist_intt(self.handle, api._fe(root), ctypes.c_void_p(runs.data_ptr()), n,
+                                              ctypes.c_void_p(out.data_ptr())))
+        return out
+
+    def coset_evaluate(self, generator: int, root_order: int, offset: int, cols: torch.Tensor,
+                       row_len: int) -> torch.Tensor:
+        """fft/ntt_arithmetics.rs:161-170: coefficient column shard -> codeword run shard."""
+        n1, n2 = self.plan(root_order, self.G)
+        out = self._alloc(n1 * (n2 // self.G))
+        self.ctx.check(self._lib.sg_dist_coset_evaluate(self.handle, api._fe(generator), root_order, api._fe(offset),
+                                                        ctypes.c_void_p(cols.data_ptr()), row_len,
+                                                        ctypes.c_void_p(out.data_ptr())))
+        return out
+
+    def merkle_root(self, runs: torch.Tensor, n: int) -> bytes:
+        root = (ctypes.c_uint8 * 64)()
+        self.ctx.check(self._lib.sg_dist_merkle_root(self.handle, ctypes.c_void_p(runs.data_ptr()), n, root))
+        return bytes(root)
+
+    def fri_commit(self, offset: int, omega: int, runs: torch.Tensor, n: int, expansion: int, c: int,
+                   proof_stream) -> None:
+        fri = api.FRI(offset, omega, n, expansion, c, ctx=self.ctx)
+        cb, adapter = fri._stream(proof_stream)
+        rc = self._lib.sg_dist_fri_commit(self.handle, ctypes.byref(fri._p), ctypes.c_void_p(runs.data_ptr()), n,
+                                          ctypes.byref(cb))
+        if adapter is not None and adapter.error is not None:
+            raise adapter.error
+        self.ctx.check(rc)
+
+
 def gather_runs_sized(shards: Sequence[Sequence[int]], n1: int, n2: int, world: int) -> List[int]:
     """Natural order of a codeword of n1 * n2 held as run shards [n1][n2 / world]."""
     r = n2 // world
@@ -406,6 +527,6 @@ def gather_runs_sized(shards: Sequence[Sequence[int]], n1: int, n2: int, world: 
     return out
 
 
-__all__ = ["Comm", "DistStark", "GpuRows", "plan", "scatter_columns", "scatter_columns_np", "gather_runs",
+__all__ = ["Comm", "DistStark", "GpuRows", "NativeDist", "plan", "scatter_columns", "scatter_columns_np", "gather_runs",
            "gather_runs_np", "gather_runs_sized",
            "StarkGpuError"]
