@@ -18,5 +18,7 @@ for v in ${AB_VARIANTS:-head new table head new table}; do
     table) run table_only "SG_NTT_TWCUT=40" ;;
     top2) run top2 "SG_NTT_TWTOP=2" ;;
     top4) run top4 "SG_NTT_TWTOP=4" ;;
+    prev) run prev "SG_LIB_PATH=$GRAFT_REPO_ROOT/ab/libstarkgpu_prev.so" ;;
+    cur) run cur "SG_X=1" ;;
   esac
 done

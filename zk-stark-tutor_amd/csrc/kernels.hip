@@ -208,6 +208,27 @@ __device__ __forceinline__ void radix_regs_impl(fe* x, const PassArgs& a, int t,
   }
 }
 
+// The first radix-8 step of a whole transform (stages 1..3: t = 0, b0 = 0, no column bits):
+// k = m mod 2^u is known at compile time, and 7 of its 12 twiddles are root^0 = 1.  A product
+// by Montgomery(1) is the canonical residue, so those butterflies take fe_canon(x) (stage 1:
+// x itself -- the gathered inputs are canonical) instead of a Montgomery product: same values.
+__device__ __forceinline__ void radix8_first(fe* x, const PassArgs& a) {
+#pragma unroll
+  for (int u = 0; u < 3; ++u) {
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      if (m & (1 << u)) continue;
+      const int k = m & ((1 << u) - 1);
+      fe o;
+      if (k == 0) o = u == 0 ? x[m + (1 << u)] : fe_canon(x[m + (1 << u)]);
+      else o = mont_mul(x[m + (1 << u)], twiddle_tab(a, u + 1, (uint64_t)k));
+      fe ev = x[m];
+      x[m] = fe_add_lazy(ev, o);
+      x[m + (1 << u)] = fe_sub_lazy(ev, o);
+    }
+  }
+}
+
 // MAYCOMP = false: the caller's stages never exceed s_cut (the first pass: <= 9 < 12 <= s_cut)
 template <int R, bool MAYCOMP = true>
 __device__ __forceinline__ void radix_regs(fe* x, const PassArgs& a, int t, uint32_t g_low, uint64_t low) {
@@ -424,7 +445,7 @@ __global__ __launch_bounds__(256, SG_NTT_WPE) void k_ntt_first(FirstArgs a) {
         if (a.sA) x[j] = mont_mul(x[j], mont_mul(ld_fe(a.sA + (idx & 4095)), ld_fe(a.sB + (idx >> 12))));
       }
     }
-    radix_regs<3, false>(x, pa, 0, 0, 0);
+    radix8_first(x, pa);
 #pragma unroll
     for (int j = 0; j < 8; ++j) lds[((8 * qq + j) << logC) + c] = x[j];
     t = 3;
