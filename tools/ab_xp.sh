@@ -1,0 +1,8 @@
+# timing-only NTT experiments: xp1 = twiddles without loads, xp2 = no Montgomery products
+set -e
+cd $GRAFT_REPO_ROOT
+for v in "" _xp1 _xp2; do
+  echo "== lib$v"
+  SG_LIB_PATH=$PWD/zk-stark-tutor_amd/starkgpu/libstarkgpu$v.so SG_NO_CHECK=1 timeout -k 10 100 python tools/bench_ntt.py 22
+  SG_LIB_PATH=$PWD/zk-stark-tutor_amd/starkgpu/libstarkgpu$v.so SG_NO_CHECK=1 timeout -k 10 100 python tools/bench_ntt.py 25
+done
