@@ -786,6 +786,83 @@ void ObjWriter::commit() {
   if (!direct) push_obj(ps, code, scratch.data(), scratch.size());
 }
 
+void TailWriter::value(const fe* d_src) {
+  TailItem it{};
+  it.src[0] = (uint64_t)(uintptr_t)d_src;
+  it.dst = bytes;
+  it.code = SG_OBJ_VALUE;
+  it.count = 1;
+  items.push_back(it);
+  offs.push_back(bytes);
+  bytes += 9 + 16;
+  field = true;
+}
+
+void TailWriter::leafs(const fe* a, const fe* b, const fe* c) {
+  TailItem it{};
+  it.src[0] = (uint64_t)(uintptr_t)a;
+  it.src[1] = (uint64_t)(uintptr_t)b;
+  it.src[2] = (uint64_t)(uintptr_t)c;
+  it.dst = bytes;
+  it.code = SG_OBJ_LEAFS;
+  it.count = 3;
+  items.push_back(it);
+  offs.push_back(bytes);
+  bytes += 9 + 48;
+  field = true;
+}
+
+void TailWriter::path(const sg_tree* t, uint64_t index) {
+  SG_REQUIRE(t->logn <= 64, "tree too deep");
+  TailItem it{};
+  it.src[0] = (uint64_t)(uintptr_t)t->buf.get();
+  it.dst = bytes;
+  it.n = t->n;
+  it.index = index;
+  it.code = SG_OBJ_PATH;
+  it.count = (uint32_t)t->logn;
+  items.push_back(it);
+  offs.push_back(bytes);
+  bytes += 9 + 72 * (size_t)t->logn;
+}
+
+void TailWriter::flush(sg_ctx* ctx, const sg_proof_stream* ps) {
+  if (items.empty()) return;
+  const size_t ni = items.size();
+  TailItem* up = static_cast<TailItem*>(ctx->staging(0, ni * sizeof(TailItem)));
+  memcpy(up, items.data(), ni * sizeof(TailItem));
+  DevBuf di(ctx, ni * sizeof(TailItem)), dout(ctx, bytes);
+  SG_HIP(hipMemcpyAsync(di.get(), up, ni * sizeof(TailItem), hipMemcpyHostToDevice, ctx->stream));
+  SG_HIP(launch_serialize_tail(di.as<TailItem>(), (uint32_t)ni, dout.as<uint8_t>(), bytes, ctx->stream));
+  if (ps->push == stream_push_cb) {
+    // a native stream: the block lands in its body by one device copy (or through staging when the
+    // runtime refuses to page-lock the body)
+    Stream& st = reinterpret_cast<sg_stream*>(ps->user)->s;
+    st.body.reserve(st.body.size() + bytes);  // grow first: the registration covers the block
+    const bool pinned = st.body.pin();
+    uint8_t* dst = st.append_block(bytes, offs, field);
+    if (pinned) {
+      SG_HIP(hipMemcpyAsync(dst, dout.get(), bytes, hipMemcpyDeviceToHost, ctx->stream));
+      SG_HIP(hipStreamSynchronize(ctx->stream));
+    } else {
+      uint8_t* stg = static_cast<uint8_t*>(ctx->staging(1, bytes));
+      SG_HIP(hipMemcpyAsync(stg, dout.get(), bytes, hipMemcpyDeviceToHost, ctx->stream));
+      SG_HIP(hipStreamSynchronize(ctx->stream));
+      memcpy(dst, stg, bytes);
+    }
+  } else {
+    uint8_t* stg = static_cast<uint8_t*>(ctx->staging(1, bytes));
+    SG_HIP(hipMemcpyAsync(stg, dout.get(), bytes, hipMemcpyDeviceToHost, ctx->stream));
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+    for (const TailItem& it : items)
+      push_obj(ps, (uint8_t)it.code, stg + it.dst + 9, (it.code == SG_OBJ_PATH ? 72 : 16) * (size_t)it.count);
+  }
+  items.clear();
+  offs.clear();
+  bytes = 0;
+  field = false;
+}
+
 void put_u128_be_at(uint8_t* out, const fe& a) {
   uint64_t hi = fe_hi(a), lo = fe_lo(a);
   for (int i = 0; i < 8; ++i) out[i] = (uint8_t)(hi >> (8 * (7 - i)));
@@ -924,28 +1001,8 @@ void sample_indices(const uint8_t* seed, size_t seed_len, size_t size, size_t re
   }
 }
 
-// fri.rs:174-208 for every round, then returns top-level indices (fri.rs:210-248)
-void gather_openings(sg_ctx* ctx, const std::vector<uint64_t>& fe_addr, const std::vector<uint64_t>& dg_addr,
-                     const fe** vals, const uint8_t** digs) {
-  const size_t nf = fe_addr.size(), nd = dg_addr.size();
-  uint8_t* up = static_cast<uint8_t*>(ctx->staging(0, (nf + nd) * 8 + 8));
-  uint8_t* down = static_cast<uint8_t*>(ctx->staging(1, nf * 16 + nd * 64 + 16));
-  memcpy(up, fe_addr.data(), nf * 8);
-  memcpy(up + nf * 8, dg_addr.data(), nd * 8);
-  DevBuf da(ctx, (nf + nd) * 8 + 8), dv(ctx, nf * 16 + nd * 64 + 16);
-  SG_HIP(hipMemcpyAsync(da.get(), up, (nf + nd) * 8, hipMemcpyHostToDevice, ctx->stream));
-  if (nf) SG_HIP(launch_gather_fe_ptrs(da.as<uint64_t>(), dv.as<fe>(), (uint32_t)nf, ctx->stream));
-  if (nd)
-    SG_HIP(launch_gather_digest_ptrs(da.as<uint64_t>() + nf, reinterpret_cast<uint64_t*>(dv.as<uint8_t>() + nf * 16),
-                                     (uint32_t)nd, ctx->stream));
-  SG_HIP(hipMemcpyAsync(down, dv.get(), nf * 16 + nd * 64, hipMemcpyDeviceToHost, ctx->stream));
-  SG_HIP(hipStreamSynchronize(ctx->stream));
-  *vals = reinterpret_cast<const fe*>(down);
-  *digs = down + nf * 16;
-}
-
 void fri_prove_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, const sg_proof_stream* ps,
-                   size_t* top) {
+                   size_t* top, const std::function<void(const size_t* top, TailWriter& tw)>& extra) {
   PhaseMarks mark;
   sg_fri_state st;
   fri_commit_dev(ctx, f, d_cw, n, ps, st, /*borrow_input=*/true);
@@ -957,78 +1014,29 @@ void fri_prove_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, con
   const size_t c = f->num_colinearity_tests;
   sample_indices(seed, 32, st.lengths[1], st.lengths.back(), c, top);
   mark("fri_sample_indices");
-  // Every opening of every round is known once the top indices are: gather all
-  // leaf values and authentication-path digests with one launch each, then push
-  // Leafs / Path objects in the reference's order (fri.rs:174-208, 231-245).
+  // Every opening of every round is known once the top indices are: the Leafs / Path objects of
+  // all rounds, in the reference's order (fri.rs:174-208, 231-245), are serialized on the device
+  // in one launch together with the caller's `extra` objects.
   const size_t R = st.codewords.size() - 1;  // query rounds
-  std::vector<std::vector<size_t>> idx_per_round(R);
-  {
-    std::vector<size_t> indices(top, top + c);
-    for (size_t r = 0; r < R; ++r) {
-      uint64_t len = st.lengths[r];
-      for (auto& i : indices) i = i % (len / 2);
-      idx_per_round[r] = indices;
-    }
-  }
-  std::vector<uint64_t> fe_addr, dg_addr;
-  fe_addr.reserve(R * c * 3);
+  TailWriter tw;
+  std::vector<size_t> indices(top, top + c);
   for (size_t r = 0; r < R; ++r) {
-    uint64_t len = st.lengths[r];
-    uint64_t cur = (uint64_t)(uintptr_t)st.cw[r];
-    uint64_t nxt = (uint64_t)(uintptr_t)st.cw[r + 1];
-    for (size_t s = 0; s < c; ++s) {
-      size_t i = idx_per_round[r][s];
-      fe_addr.push_back(cur + 16 * (uint64_t)i);
-      fe_addr.push_back(cur + 16 * (uint64_t)(i + len / 2));
-      fe_addr.push_back(nxt + 16 * (uint64_t)i);
-    }
+    const uint64_t len = st.lengths[r];
+    for (auto& i : indices) i = i % (len / 2);
+    const fe* cur = st.cw[r];
+    const fe* nxt = st.cw[r + 1];
+    for (size_t s = 0; s < c; ++s) tw.leafs(cur + indices[s], cur + indices[s] + len / 2, nxt + indices[s]);
     const sg_tree* tc = st.trees[r].get();
     const sg_tree* tn = st.trees[r + 1].get();
-    uint64_t bc = (uint64_t)(uintptr_t)tc->buf.get(), bn = (uint64_t)(uintptr_t)tn->buf.get();
-    std::vector<uint64_t> p;
     for (size_t s = 0; s < c; ++s) {
-      size_t i = idx_per_round[r][s];
-      p.clear();
-      path_indices(tc, i, p);
-      path_indices(tc, i + len / 2, p);
-      for (uint64_t d : p) dg_addr.push_back(bc + 64 * d);
-      p.clear();
-      path_indices(tn, i, p);
-      for (uint64_t d : p) dg_addr.push_back(bn + 64 * d);
+      tw.path(tc, indices[s]);
+      tw.path(tc, indices[s] + len / 2);
+      tw.path(tn, indices[s]);
     }
   }
-  mark("fri_query_addresses");
-  const fe* vals = nullptr;
-  const uint8_t* digs = nullptr;
-  gather_openings(ctx, fe_addr, dg_addr, &vals, &digs);
-  mark("fri_query_gather");
-  // payloads are written in place: straight into a native stream's body, else into
-  // one reused buffer handed to the push callback
-  size_t fpos = 0, dpos = 0;
-  uint8_t leafs[48];
-  ObjWriter w{ps};
-  for (size_t r = 0; r < R; ++r) {
-    for (size_t s = 0; s < c; ++s) {
-      for (int k = 0; k < 3; ++k) put_u128_be_at(leafs + 16 * k, vals[fpos + 3 * s + k]);
-      push_obj(ps, SG_OBJ_LEAFS, leafs, 48);
-    }
-    fpos += 3 * c;
-    const size_t lc = (size_t)st.trees[r]->logn, ln = (size_t)st.trees[r + 1]->logn;
-    for (size_t s = 0; s < c; ++s) {
-      const size_t lens[3] = {lc, lc, ln};
-      for (int which = 0; which < 3; ++which) {
-        // Path payload: per digest [len u64 BE = 64][64 bytes] (proof_stream_enum.rs:95-110)
-        uint8_t* p = w.begin(SG_OBJ_PATH, lens[which] * 72);
-        for (size_t k = 0; k < lens[which]; ++k, p += 72) {
-          static const uint8_t len64[8] = {0, 0, 0, 0, 0, 0, 0, 64};
-          memcpy(p, len64, 8);
-          memcpy(p + 8, digs + (dpos + k) * 64, 64);
-        }
-        dpos += lens[which];
-        w.commit();
-      }
-    }
-  }
+  if (extra) extra(top, tw);
+  mark("fri_query_items");
+  tw.flush(ctx, ps);  // the round states stay alive until the serialization has read them
   mark("fri_query_push");
 }
 

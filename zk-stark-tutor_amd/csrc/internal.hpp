@@ -3,6 +3,7 @@
 // retained Merkle trees and the FRI driver.
 #pragma once
 #include <chrono>
+#include <functional>
 #include <cstdio>
 #include <cstdlib>
 #include <cstdint>
@@ -141,11 +142,23 @@ void put_u128_be_at(uint8_t* out, const fe& a);
 void put_u128_be(std::vector<uint8_t>& out, const fe& a);
 void fri_commit_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, const sg_proof_stream* ps,
                     sg_fri_state& st, bool borrow_input = false);
+// Objects pushed after a proof's last Fiat-Shamir draw (the FRI query phase, fri.rs:174-208, and
+// the Stark openings, stark.rs:524-560): collected as TailItems, serialized by one device launch
+// (k_serialize_tail) and appended with one copy -- straight into a native stream's page-locked
+// body, else pushed object by object to the callback stream from pinned staging.
+struct TailWriter {
+  std::vector<TailItem> items;
+  std::vector<size_t> offs;  // header offset of each object in the block
+  size_t bytes = 0;
+  bool field = false;        // a Value / Leafs object (sets the stream's field header)
+  void value(const fe* d_src);
+  void leafs(const fe* a, const fe* b, const fe* c);
+  void path(const sg_tree* t, uint64_t index);
+  void flush(sg_ctx* ctx, const sg_proof_stream* ps);
+};
+// fri.rs:210-248.  `extra`, when given, appends further tail objects after the query phase's
+// (called with the top-level indices) so they share its single serialization launch and copy.
 void fri_prove_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, const sg_proof_stream* ps,
-                   size_t* top);
-// one launch each: field elements and digests at the given device addresses, into pinned
-// staging memory (valid until the next call on this context)
-void gather_openings(sg_ctx* ctx, const std::vector<uint64_t>& fe_addr, const std::vector<uint64_t>& dg_addr,
-                     const fe** vals, const uint8_t** digs);
+                   size_t* top, const std::function<void(const size_t* top, TailWriter& tw)>& extra = {});
 
 }  // namespace sg

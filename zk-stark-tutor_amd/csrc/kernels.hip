@@ -907,18 +907,43 @@ __global__ void k_gather_fe(const fe* __restrict__ src, const uint64_t* __restri
 }
 
 // gather from a list of absolute device addresses (one launch for every round's openings)
-__global__ void k_gather_digest_ptrs(const uint64_t* __restrict__ addrs, uint64_t* __restrict__ out, uint32_t count) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= count) return;
-  uint64_t d[8];
-  ld_digest(reinterpret_cast<const uint64_t*>(addrs[i]), d);
-  st_digest(out + (uint64_t)i * 8, d);
+// --------------------------------------------- proof-stream tail serialization
+
+__device__ __forceinline__ void put_be64_dev(uint8_t* o, uint64_t v) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o[i] = (uint8_t)(v >> (56 - 8 * i));
 }
 
-__global__ void k_gather_fe_ptrs(const uint64_t* __restrict__ addrs, fe* __restrict__ out, uint32_t count) {
-  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= count) return;
-  st_fe(out + i, ld_fe(reinterpret_cast<const fe*>(addrs[i])));
+// one 64-lane block per object (TailItem in kernels.hpp); lane 0 writes the 9-byte header,
+// lane k the k-th element / path entry (a path has log2(n) <= 64 entries)
+__global__ __launch_bounds__(64) void k_serialize_tail(const TailItem* __restrict__ items, uint8_t* __restrict__ out) {
+  const TailItem it = items[blockIdx.x];
+  const uint32_t l = threadIdx.x;
+  uint8_t* o = out + it.dst;
+  const bool path = it.code == 2;  // SG_OBJ_PATH
+  if (l == 0) {
+    o[0] = (uint8_t)it.code;
+    put_be64_dev(o + 1, (path ? 72ull : 16ull) * it.count);
+  }
+  if (l >= it.count) return;
+  if (path) {
+    uint8_t* e = o + 9 + 72 * (uint64_t)l;
+    put_be64_dev(e, 64);
+    const uint64_t d = 2 * it.n - 2 * (it.n >> l) + ((it.index >> l) ^ 1);  // level l sibling
+    const uint4* q = reinterpret_cast<const uint4*>(it.src[0] + 64 * d);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint4 v = q[k];
+      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int j = 0; j < 16; ++j) e[8 + 16 * k + j] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
+    }
+  } else {
+    const fe v = ld_fe(reinterpret_cast<const fe*>(it.src[l]));
+    uint8_t* e = o + 9 + 16 * (uint64_t)l;
+    put_be64_dev(e, fe_hi(v));
+    put_be64_dev(e + 8, fe_lo(v));
+  }
 }
 
 // ------------------------------------------------------------- launchers
@@ -929,25 +954,18 @@ static int env_int(const char* name, int def) {
   return v && *v ? atoi(v) : def;
 }
 
-hipError_t launch_gather_digest_ptrs(const uint64_t* addrs, uint64_t* out, uint32_t count, hipStream_t s) {
-  if (!count) return hipSuccess;
-  ProfScope ps("gather_digests", 128ull * count, s);
-  hipLaunchKernelGGL(k_gather_digest_ptrs, dim3((count + 255) / 256), dim3(256), 0, s, addrs, out, count);
-  return hipGetLastError();
-}
-
-hipError_t launch_gather_fe_ptrs(const uint64_t* addrs, fe* out, uint32_t count, hipStream_t s) {
-  if (!count) return hipSuccess;
-  ProfScope ps("gather_fe", 40ull * count, s);
-  hipLaunchKernelGGL(k_gather_fe_ptrs, dim3((count + 255) / 256), dim3(256), 0, s, addrs, out, count);
-  return hipGetLastError();
-}
-
 hipError_t launch_gather_digests(const uint64_t* tree, const uint64_t* idx, uint64_t* out, uint32_t count,
                                  hipStream_t s) {
   if (!count) return hipSuccess;
   ProfScope ps("gather_digests", 128ull * count, s);
   hipLaunchKernelGGL(k_gather_digests, dim3((count + 255) / 256), dim3(256), 0, s, tree, idx, out, count);
+  return hipGetLastError();
+}
+
+hipError_t launch_serialize_tail(const TailItem* items, uint32_t count, uint8_t* out, uint64_t bytes, hipStream_t s) {
+  if (!count) return hipSuccess;
+  ProfScope ps("serialize_tail", bytes, s);
+  hipLaunchKernelGGL(k_serialize_tail, dim3(count), dim3(64), 0, s, items, out);
   return hipGetLastError();
 }
 

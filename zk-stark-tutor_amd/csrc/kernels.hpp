@@ -58,9 +58,22 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
                               uint64_t root_seq = 0, const FoldLeaves* fold = nullptr);
 hipError_t launch_gather_digests(const uint64_t* tree, const uint64_t* idx, uint64_t* out, uint32_t count,
                                  hipStream_t s);
-hipError_t launch_gather_digest_ptrs(const uint64_t* addrs, uint64_t* out, uint32_t count, hipStream_t s);
-hipError_t launch_gather_fe_ptrs(const uint64_t* addrs, fe* out, uint32_t count, hipStream_t s);
 hipError_t launch_gather_fe(const fe* src, const uint64_t* idx, fe* out, uint32_t count, hipStream_t s);
+
+// Proof-stream objects serialized on the device (the tail of a proof: FRI query phase and the
+// Stark openings): [code u8][len u64 BE][payload] at byte offset `dst` of the output, with
+// Value / Leafs payloads as `count` big-endian u128 elements read from src[0..count) and a Path
+// payload as `count` = log2(n) entries [64 u64 BE][digest] of leaf `index` in the tree whose
+// digests start at src[0] (merkle_root.rs:34-53 order, proof_stream_enum.rs:95-126).
+struct TailItem {
+  uint64_t src[3];
+  uint64_t dst;
+  uint64_t n;
+  uint64_t index;
+  uint32_t code;
+  uint32_t count;
+};
+hipError_t launch_serialize_tail(const TailItem* items, uint32_t count, uint8_t* out, uint64_t bytes, hipStream_t s);
 
 // row-sharded helpers (four-step NTT, sharded Merkle / FRI)
 hipError_t launch_mul_pow(fe* data, uint64_t rows, uint64_t cols, uint64_t a0, uint64_t a1, uint64_t b0,

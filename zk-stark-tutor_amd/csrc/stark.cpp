@@ -9,7 +9,8 @@
 //     a coset of size L > degree and interpolated back (the unique polynomial
 //     evaluate_symbolic returns), then fast_coset_divide by the transition zerofier
 //   combination polynomial (weighted, shifted terms) -> LDE -> FRI::prove
-//   openings of the boundary-quotient and randomizer codewords (batched gathers).
+//   openings of the boundary-quotient and randomizer codewords, serialized on the device
+//     together with the FRI query phase (TailWriter: one launch, one copy).
 // The thread_rng draws (trace randomizers, randomizer polynomial) are explicit inputs.
 #include <chrono>
 #include <cstdio>
@@ -491,40 +492,6 @@ DPoly transition_values(sg_ctx* ctx, const MPoly& tc, const AirCoset& co, const 
   return vals;
 }
 
-// proof_stream pushes of (Value, Path) for `idx` in each retained codeword/tree, in order
-// (stark.rs:545-560); every opening of every tree is gathered with one launch each
-void push_openings(sg_ctx* ctx, const sg_proof_stream* ps, const std::vector<std::pair<const fe*, const sg_tree*>>& cts,
-                   const std::vector<uint64_t>& idx) {
-  std::vector<uint64_t> fe_addr, dg_addr, p;
-  for (auto& ct : cts)
-    for (uint64_t i : idx) {
-      fe_addr.push_back((uint64_t)(uintptr_t)ct.first + 16 * i);
-      p.clear();
-      path_indices(ct.second, i, p);
-      for (uint64_t d : p) dg_addr.push_back((uint64_t)(uintptr_t)ct.second->buf.get() + 64 * d);
-    }
-  const fe* vals = nullptr;
-  const uint8_t* digs = nullptr;
-  gather_openings(ctx, fe_addr, dg_addr, &vals, &digs);
-  static const uint8_t len64[8] = {0, 0, 0, 0, 0, 0, 0, 64};
-  size_t vk = 0, dk = 0;
-  ObjWriter w{ps};
-  for (auto& ct : cts) {
-    const size_t depth = (size_t)ct.second->logn;
-    for (size_t k = 0; k < idx.size(); ++k, ++vk) {
-      uint8_t v[16];
-      put_u128_be_at(v, vals[vk]);
-      push_obj(ps, SG_OBJ_VALUE, v, 16);
-      uint8_t* q = w.begin(SG_OBJ_PATH, depth * 72);
-      for (size_t d = 0; d < depth; ++d, q += 72, ++dk) {
-        memcpy(q, len64, 8);
-        memcpy(q + 8, digs + dk * 64, 64);
-      }
-      w.commit();
-    }
-  }
-}
-
 std::vector<fe> sample_weights(size_t number, const uint8_t* randomness, size_t len) {
   // stark.rs:268-274: sample(0^i || randomness)
   std::vector<fe> out;
@@ -783,22 +750,28 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
     coset_evaluate_batch(ctx, st.omega, Nf, g, &in, comb.len, &out, 1);
   }
   mark("combination_lde");
-  // FRI (stark.rs:514-522)
+  // FRI (stark.rs:514-522) and the openings (stark.rs:524-560): the openings' indices follow from
+  // FRI's top-level indices, so their Value / Path objects join the FRI query phase's single
+  // device serialization (TailWriter)
   std::vector<size_t> top(st.fri.num_colinearity_tests);
-  fri_prove_dev(ctx, &st.fri, comb_cw.p(), Nf, ps, top.data());
-  mark("fri_prove");
-  // openings (stark.rs:524-560)
-  std::vector<uint64_t> dup;
-  for (size_t i : top) dup.push_back(i);
-  for (size_t i : top) dup.push_back((i + st.expansion) % Nf);
-  std::vector<uint64_t> quad = dup;
-  for (uint64_t i : dup) quad.push_back((i + Nf / 2) % Nf);
-  std::sort(quad.begin(), quad.end());
-  mark("openings_indices");
   std::vector<std::pair<const fe*, const sg_tree*>> cts;
   for (size_t s = 0; s < m; ++s) cts.emplace_back(bq_cw[s].p(), bq_trees[s].get());
   cts.emplace_back(r_cw.p(), r_tree.get());
-  push_openings(ctx, ps, cts, quad);
+  fri_prove_dev(ctx, &st.fri, comb_cw.p(), Nf, ps, top.data(), [&](const size_t* tp, TailWriter& tw) {
+    const size_t c = st.fri.num_colinearity_tests;
+    std::vector<uint64_t> dup;
+    for (size_t k = 0; k < c; ++k) dup.push_back(tp[k]);
+    for (size_t k = 0; k < c; ++k) dup.push_back((tp[k] + st.expansion) % Nf);
+    std::vector<uint64_t> quad = dup;
+    for (uint64_t i : dup) quad.push_back((i + Nf / 2) % Nf);
+    std::sort(quad.begin(), quad.end());
+    for (auto& ct : cts)
+      for (uint64_t i : quad) {
+        tw.value(ct.first + i);
+        tw.path(ct.second, i);
+      }
+  });
+  mark("fri_prove_and_openings");
   SG_HIP(hipStreamSynchronize(ctx->stream));
   check_div_zero(ctx);
   mark("openings");

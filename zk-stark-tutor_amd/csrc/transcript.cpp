@@ -8,6 +8,8 @@
 //   deserialize              stark/stark.rs:30-67
 #include "transcript.hpp"
 
+#include <hip/hip_runtime.h>
+
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -19,17 +21,24 @@ namespace sg {
 
 // ---------------------------------------------------------------- byte buffer
 
-ByteBuf::~ByteBuf() { free(p); }
+ByteBuf::~ByteBuf() {
+  unpin();
+  free(p);
+}
+
+void ByteBuf::reserve(size_t want) {
+  if (want <= cap) return;
+  size_t c = cap ? cap : 4096;
+  while (c < want) c *= 2;
+  unpin();  // the registration belongs to the old block
+  void* q = realloc(p, c);
+  if (!q) throw std::bad_alloc();
+  p = static_cast<uint8_t*>(q);
+  cap = c;
+}
 
 uint8_t* ByteBuf::grow(size_t add) {
-  if (n + add > cap) {
-    size_t c = cap ? cap : 4096;
-    while (c < n + add) c *= 2;
-    void* q = realloc(p, c);
-    if (!q) throw std::bad_alloc();
-    p = static_cast<uint8_t*>(q);
-    cap = c;
-  }
+  reserve(n + add);
   uint8_t* at = p + n;
   n += add;
   return at;
@@ -39,6 +48,25 @@ void ByteBuf::swap(ByteBuf& o) {
   std::swap(p, o.p);
   std::swap(n, o.n);
   std::swap(cap, o.cap);
+  std::swap(pinned_p, o.pinned_p);
+}
+
+bool ByteBuf::pin() {
+  if (!p) return false;
+  if (pinned_p == p) return true;
+  unpin();
+  if (hipHostRegister(p, cap, hipHostRegisterDefault) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  pinned_p = p;
+  return true;
+}
+
+void ByteBuf::unpin() {
+  if (!pinned_p) return;
+  (void)hipHostUnregister(pinned_p);
+  pinned_p = nullptr;
 }
 
 namespace {
@@ -95,6 +123,14 @@ uint8_t* Stream::push_reserve(uint8_t code, size_t len) {
   for (int i = 0; i < 8; ++i) h[1 + i] = (uint8_t)((uint64_t)len >> (8 * (7 - i)));
   field = field || carries_field(code, len);
   return h + 9;
+}
+
+uint8_t* Stream::append_block(size_t bytes, const std::vector<size_t>& obj_offsets, bool carries_field_) {
+  const size_t base = body.n;
+  uint8_t* at = body.grow(bytes);
+  for (size_t o : obj_offsets) offs.push_back(base + o);
+  field = field || carries_field_;
+  return at;
 }
 
 void Stream::push(uint8_t code, const uint8_t* p, size_t len) {

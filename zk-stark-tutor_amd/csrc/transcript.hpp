@@ -17,9 +17,17 @@ struct ByteBuf {
   ByteBuf& operator=(const ByteBuf&) = delete;
   ~ByteBuf();
   uint8_t* grow(size_t add);  // n += add; returns the old end
+  void reserve(size_t c);     // capacity >= c
   const uint8_t* data() const { return p; }
   size_t size() const { return n; }
   void swap(ByteBuf& o);
+  // page-locks the whole capacity for device copies (hipHostRegister; kept until the buffer
+  // moves or dies, so a cached body registers once); false if the runtime refuses
+  bool pin();
+  uint8_t* pinned_p = nullptr;
+
+ private:
+  void unpin();
 };
 
 // A proof stream held in its serialized form (stark/proof_stream_enum.rs:161-190 without
@@ -56,6 +64,9 @@ struct Stream {
   // appends an object and returns its payload bytes (len of them) for the caller to fill
   uint8_t* push_reserve(uint8_t code, size_t len);
   void push(uint8_t code, const uint8_t* p, size_t len);
+  // appends `bytes` of already serialized objects (headers included) whose headers sit at the
+  // given offsets of the block, and returns the block for the caller to fill
+  uint8_t* append_block(size_t bytes, const std::vector<size_t>& obj_offsets, bool carries_field);
 
   size_t digest_size(size_t count) const;
   void digest_into(size_t count, uint8_t* out) const;  // header || first `count` objects
