@@ -512,6 +512,16 @@ struct SideDrain {
   ~SideDrain() { (void)hipStreamSynchronize(ctx->side); }
 };
 
+// launches of library helpers that use ctx->stream go to `s` inside the scope
+struct StreamSwap {
+  sg_ctx* ctx;
+  hipStream_t prev;
+  StreamSwap(sg_ctx* c, hipStream_t s) : ctx(c), prev(c->stream) { c->stream = s; }
+  ~StreamSwap() { ctx->stream = prev; }
+  StreamSwap(const StreamSwap&) = delete;
+  StreamSwap& operator=(const StreamSwap&) = delete;
+};
+
 struct AsyncScope {
   sg_ctx* ctx;
   bool prev;
@@ -550,18 +560,24 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
   for (size_t s = 0; s < m; ++s) bq_trees[s] = new_tree(ctx, Nf);
   std::unique_ptr<sg_tree> r_tree = new_tree(ctx, Nf);
   SideDrain side_drain{ctx};
-  // randomizer codeword (stark.rs:424-445) first: it depends on nothing else, and its tree
-  // then hashes on the side stream while the main stream interpolates the trace
-  {
-    const fe* in = d_rcoef;
-    fe* out = r_cw.p();
-    coset_evaluate_batch(ctx, st.omega, Nf, g, &in, nrc, &out, 1);
-  }
+  // randomizer codeword (stark.rs:424-445) first: it depends on nothing else, so its LDE and
+  // its tree run on the side stream while the main stream interpolates the trace.  The tables
+  // the LDE reads are created (cached) on the main stream before the fork: the side stream
+  // allocates nothing and only launches the transform passes and the tree.
   constexpr int kRandSlot = 4;
   uint64_t r_seq, bq_seq;
   {
+    (void)ctx->stage_twiddles(st.omega, ilog2_exact(next_pow2(Nf)));
+    (void)ctx->pow_table(g, 4096);
+    (void)ctx->pow_table(fe_pow(g, 4096), (std::max<uint64_t>(nrc, 1) + 4095) / 4096);
     SG_HIP(hipEventRecord(ctx->ev_fork, ctx->stream));
     SG_HIP(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
+    const fe* in = d_rcoef;
+    fe* out = r_cw.p();
+    {
+      StreamSwap on_side(ctx, ctx->side);
+      coset_evaluate_batch(ctx, st.omega, Nf, g, &in, nrc, &out, 1);
+    }
     const fe* leaves = r_cw.p();
     sg_tree* t = r_tree.get();
     r_seq = launch_trees(ctx, &leaves, 1, &t, kRandSlot, ctx->side);
