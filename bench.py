@@ -169,6 +169,11 @@ class BlockWorkload:
         return (REGISTERS + 2) * self.N
 
 
+def median_of(fn, reps: int) -> float:
+    vals = sorted(fn() for _ in range(reps))
+    return vals[len(vals) // 2]
+
+
 def side_measurements(ctx: sg.Context, device, iters: int = 5) -> dict:
     """The other two configs BASELINE.json names, timed the same way (inputs in HBM):
     C2 = 2^22-point forward + inverse NTT; north star = 2^24 LDE (2^21 coefficients) + FRI commit."""
@@ -182,12 +187,17 @@ def side_measurements(ctx: sg.Context, device, iters: int = 5) -> dict:
     sg.intt_dev(w, y.data_ptr(), n, z.data_ptr(), ctx=ctx)
     assert torch.equal(x, z), "C2 INTT(NTT(x)) != x"
     torch.cuda.synchronize(device)
-    t0 = time.perf_counter()
-    for _ in range(iters):
-        sg.ntt_dev(w, x.data_ptr(), n, y.data_ptr(), ctx=ctx)
-        sg.intt_dev(w, y.data_ptr(), n, z.data_ptr(), ctx=ctx)
-    torch.cuda.synchronize(device)
-    t = (time.perf_counter() - t0) / iters
+
+    def c2_rep():
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            sg.ntt_dev(w, x.data_ptr(), n, y.data_ptr(), ctx=ctx)
+            sg.intt_dev(w, y.data_ptr(), n, z.data_ptr(), ctx=ctx)
+        torch.cuda.synchronize(device)
+        return (time.perf_counter() - t0) / iters
+
+    # a sub-millisecond figure: the median of 5 repetitions, so one slow moment does not set it
+    t = median_of(c2_rep, 5)
     out["c2_ntt_fwd_inv_2p22_ms"] = round(t * 1e3, 3)
     out["c2_ntt_gelem_s"] = round(2 * n / t / 1e9, 3)
     del x, y, z
