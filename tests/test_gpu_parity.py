@@ -228,6 +228,28 @@ def test_fri_commit_matches_oracle_and_callback_stream():
     assert cps.digest() == ops.digest()
 
 
+@pytest.mark.parametrize("stream_kind", ["callback", "native_unpinned"])
+def test_fri_prove_tail_paths_match_oracle(stream_kind, monkeypatch):
+    """The proof tail (query-phase Leafs/Path objects, serialized on the device) reaches a foreign
+    ProofStream through the push callback, and a native stream whose body cannot be page-locked
+    through pinned staging -- byte-identical to the oracle either way."""
+    n, exp, c = 1 << 11, 8, 12
+    omega, cw = _fri_case(n, exp, c, 23)
+    ofri = o.FRI(o.GENERATOR, omega, n, exp, c)
+    ops = o.IndependentProofStream()
+    otop = ofri.prove(cw, ops)
+    gfri = sg.FRI(o.GENERATOR, omega, n, exp, c)
+    if stream_kind == "callback":
+        gps = o.IndependentProofStream()
+        gtop = gfri.prove(cw, gps)
+    else:
+        monkeypatch.setenv("SG_STREAM_NO_PIN", "1")
+        gps = sg.IndependentProofStream()
+        gtop = gfri.prove(cw, gps)
+    assert gtop == otop
+    assert gps.digest() == ops.digest()
+
+
 def test_fri_tampered_codeword_rejected():
     """fri.rs:514-528: zeroing a third of the low-degree positions makes verify fail."""
     n, exp, c = 256, 4, 17

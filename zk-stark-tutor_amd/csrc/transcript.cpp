@@ -52,7 +52,8 @@ void ByteBuf::swap(ByteBuf& o) {
 }
 
 bool ByteBuf::pin() {
-  if (!p) return false;
+  // SG_STREAM_NO_PIN: callers take their staging fallback (tests exercise it this way)
+  if (!p || getenv("SG_STREAM_NO_PIN")) return false;
   if (pinned_p == p) return true;
   unpin();
   if (hipHostRegister(p, cap, hipHostRegisterDefault) != hipSuccess) {
