@@ -345,6 +345,18 @@ def side_sharded(ctx: sg.Context, device, world: int, rank: int, iters: int = 3)
 
     # every rank runs the same code on the same shapes, so an error is raised on all of them
     try:
+        # C2's size sharded the same way (the NTT part of the curve at 1/2/4/8)
+        n = 1 << 22
+        n1, n2 = D.plan(n, world)
+        shard = to_device(synthetic_fe(rank, b"c2", (n1 // world) * n2), device).reshape(-1)
+        root = sg.primitive_nth_root(n)
+        t = timed(lambda: ds.ntt(root, shard, n2, n))
+        out["c2_sharded_ntt_2p22_ms"] = round(t * 1e3, 3)
+        out["c2_sharded_gelem_s"] = round(n / t / 1e9, 3)
+        del shard
+    except Exception as e:  # noqa: BLE001
+        out["c2_sharded_error"] = f"{type(e).__name__}: {e}"
+    try:
         n = 1 << 27
         n1, n2 = D.plan(n, world)
         shard = to_device(synthetic_fe(rank, b"c5", (n1 // world) * n2), device).reshape(-1)
@@ -524,6 +536,24 @@ def cpu_baseline_e2e(seconds_budget: float = 6.0) -> dict:
                       f"{per * 1e3:.1f} ms/proof; Python restatement of the reference's algorithms"}
 
 
+def hbm_copy_gbs(device, mib: int = 1024, iters: int = 10):
+    """Device-to-device copy rate of a 1 GiB buffer (bytes read + bytes written per second), torch's
+    copy kernel, HIP events on torch's stream."""
+    n = mib * (1 << 20) // 8
+    a = torch.ones(n, dtype=torch.int64, device=device)
+    b = torch.empty_like(a)
+    b.copy_(a)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        b.copy_(a)
+    e1.record()
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / iters
+    del a, b
+    return round(2 * mib * (1 << 20) / (ms * 1e-3) / 1e9, 1)
+
+
 def standalone_launch(ctx, device, name: str, n: int):
     """Event-timed launches of the dominant kernel alone on the chip: a tree over n seeded leaves."""
     if name != "merkle_leaves":
@@ -645,6 +675,9 @@ def main():
                               f"2 clk (SIMD-32) x 1024 SIMDs at the PMC pass's clock; mix_roof = the kernel's "
                               f"full/half-rate instruction mix at the measured per-op rates (tools/valu_mix.py); "
                               f"achieved = per-wave count x the live launches' waves / their live time"}
+    # the HBM rate a plain device copy reaches on this box (1 GiB read + 1 GiB written), beside the
+    # 8 TB/s spec the contract prices against ("measure actual HBM with a copy kernel")
+    copy_gbs = hbm_copy_gbs(device)
     # the same kernel alone on the chip (in the prove, the boundary-quotient and randomizer
     # trees share the CUs with the main stream's algebra, which stretches their launches)
     alone = standalone_launch(ctx, device, name, wl.fri_len)
@@ -702,7 +735,9 @@ def main():
                              "instruction-mix roof (DESIGN.md section 4); launches overlap other kernels (side "
                              "stream), standalone = alone on the chip",
                      "valu": valu,
-                     "standalone": alone},
+                     "standalone": alone,
+                     "hbm_copy_measured_gbs": copy_gbs,
+                     "frac_of_measured_copy": round(achieved / copy_gbs, 4) if copy_gbs else None},
         "kernels_one_step": phases,  # every launch timed, last warmup step
         "host_phases_ms": {k: round(v / args.steps * 1e3, 3) for k, v in host_phases.items()},
     }
