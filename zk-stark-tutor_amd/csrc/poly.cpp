@@ -272,10 +272,10 @@ DPoly fast_multiply_dev(sg_ctx* ctx, fe root, uint64_t root_order, const fe* a, 
   ref_inner_ntt(ctx, root, order, b, lb, nullptr, vb, nb);
   // Hadamard over the first `order` entries, intt over `order` entries
   dev_mul(ctx, va.as<fe>(), va.as<fe>(), vb.as<fe>(), order);
-  DevBuf c(ctx, order * sizeof(fe));
-  intt_sized(ctx, root, va.as<fe>(), ilog2_exact(order), c.as<fe>());
-  uint64_t keep = std::min(result_len, order);
-  DPoly out = dpoly_copy(ctx, c.as<fe>(), keep);
+  // the inverse transform writes the result's own buffer (order >= keep slots): no copy
+  DPoly out = dpoly_alloc(ctx, order);
+  intt_sized(ctx, root, va.as<fe>(), ilog2_exact(order), out.p());
+  out.len = std::min(result_len, order);
   return out;
 }
 
@@ -385,8 +385,10 @@ DPoly interpolate_geometric_dev(sg_ctx* ctx, const fe& q, uint64_t D, const fe* 
   const fe *iA, *iB;
   pow_tables2(ctx, fe_inv(q), D, &iA, &iB);
   SG_HIP(launch_interp_assemble(va.as<fe>(), y, Zv.as<fe>(), S.as<fe>(), n, D, iA, iB, fe_r2(), ctx->stream));
-  intt_sized(ctx, q, va.as<fe>(), logD, S.as<fe>());
-  DPoly out = dpoly_copy(ctx, S.as<fe>(), n);
+  // the coefficients land in the result's own buffer (D >= n slots): no copy of the n kept
+  DPoly out = dpoly_alloc(ctx, D);
+  intt_sized(ctx, q, va.as<fe>(), logD, out.p());
+  out.len = n;
   return out;
 }
 
