@@ -16,9 +16,10 @@ sg = bench.sg
 
 def main():
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+    log_trace = int(sys.argv[2]) if len(sys.argv) > 2 else bench.LOG_TRACE
     dev = torch.device("cuda", 0)
     ctx = sg.Context(0)
-    wl = bench.ProveWorkload(0, dev, ctx)
+    wl = bench.ProveWorkload(0, dev, ctx, log_trace)
     wl.step()
     wl.step()
     torch.cuda.synchronize(dev)

@@ -280,12 +280,12 @@ DPoly fast_multiply_dev(sg_ctx* ctx, fe root, uint64_t root_order, const fe* a, 
 }
 
 DPoly fast_coset_divide_dev(sg_ctx* ctx, fe root, uint64_t root_order, const fe& offset, const fe* lhs, uint64_t ll,
-                            const fe* rhs, uint64_t lr, int64_t rhs_degree, const fe* rhs_host) {
+                            const fe* rhs, uint64_t lr, int64_t rhs_degree, const fe* rhs_host, int64_t lhs_degree) {
   check_root(root, root_order);
   int64_t dl, dr;
   if (rhs_degree >= -1) {
     dr = rhs_degree;
-    dl = dev_degree(ctx, lhs, ll);
+    dl = lhs_degree >= -1 ? lhs_degree : dev_degree(ctx, lhs, ll);
   } else {
     std::vector<int64_t> d = dev_degrees(ctx, {{lhs, ll}, {rhs, lr}});
     dl = d[0];

@@ -74,9 +74,11 @@ void ref_inner_ntt(sg_ctx* ctx, const fe& root, uint64_t order, const fe* p, uin
                    DevBuf& out, uint64_t& out_len, const fe* host_copy = nullptr);
 DPoly coset_divide_finish(sg_ctx* ctx, const DivPlan& pl, const fe& offset, fe* lhs_v, const fe* rhs_v);
 // ntt_arithmetics.rs:239-310
-// rhs_degree: the divisor's degree when the caller knows it (-1 = zero polynomial), -2 = query the device
+// rhs_degree / lhs_degree: the divisor's / dividend's degree when the caller knows it (-1 = zero
+// polynomial), -2 = query the device
 DPoly fast_coset_divide_dev(sg_ctx* ctx, fe root, uint64_t root_order, const fe& offset, const fe* lhs, uint64_t ll,
-                            const fe* rhs, uint64_t lr, int64_t rhs_degree = -2, const fe* rhs_host = nullptr);
+                            const fe* rhs, uint64_t lr, int64_t rhs_degree = -2, const fe* rhs_host = nullptr,
+                            int64_t lhs_degree = -2);
 // prod_{i<n} (x - q^i) for q of order D (ntt_arithmetics.rs:66-113 on the domain q^0..q^(n-1)), length n + 1;
 // n == D reproduces the reference's wrapped result (D zeros)
 DPoly zerofier_geometric_dev(sg_ctx* ctx, const fe& q, uint64_t D, uint64_t n);

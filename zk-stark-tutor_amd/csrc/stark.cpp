@@ -408,8 +408,11 @@ AirCoset air_coset(sg_ctx* ctx, const std::vector<DPoly>& trace_polys, uint64_t 
   return c;
 }
 
-// values on the coset of the polynomial evaluate_symbolic returns (m_polynomial.rs:124-139)
-DPoly transition_values(sg_ctx* ctx, const MPoly& tc, const AirCoset& co, const fe& offset) {
+// values on the coset of the polynomial evaluate_symbolic returns (m_polynomial.rs:124-139).
+// The x-polynomial values and the kernel's pointer tables move into `keep` (the caller's scope):
+// they outlive the launch without a host wait.
+DPoly transition_values(sg_ctx* ctx, const MPoly& tc, const AirCoset& co, const fe& offset,
+                        std::vector<DevBuf>& keep) {
   const uint64_t L = co.L;
   const int nv = (int)co.var.size();
   SG_REQUIRE(tc.nvars <= 1 + (uint32_t)nv, "transition constraint has more variables than the point");
@@ -488,7 +491,8 @@ DPoly transition_values(sg_ctx* ctx, const MPoly& tc, const AirCoset& co, const 
   a.one_m = to_mont(fe_one());
   for (int j = 0; j < nv; ++j) a.vshift[j] = co.shift[j];
   SG_HIP(launch_air_eval(a, ctx->stream));
-  SG_HIP(hipStreamSynchronize(ctx->stream));  // pointer tables return to the pool
+  keep.push_back(std::move(dt));
+  for (auto& q : Q) keep.push_back(std::move(q.buf));
   return vals;
 }
 
@@ -597,13 +601,21 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
   // boundary quotients (stark.rs:326-362)
   std::vector<HPoly> bi = boundary_interpolants(st, bnd), bz = boundary_zerofiers(st, bnd);
   std::vector<DPoly> bqs;
-  for (size_t s = 0; s < m; ++s) {
-    DPoly I = dpoly_upload(ctx, bi[s].data(), bi[s].size());
-    DPoly Z = dpoly_upload(ctx, bz[s].data(), bz[s].size());
-    DPoly diff = lincomb(ctx, {{trace_polys[s].p(), 0, trace_polys[s].len, fe_one()},
-                               {I.p(), 0, I.len, fe_neg(fe_one())}});
-    bqs.push_back(fast_coset_divide_dev(ctx, st.omicron, D, g, diff.p(), diff.len, Z.p(), Z.len, hp_degree(bz[s]),
-                                        bz[s].data()));
+  {
+    // every register's numerator first, then their degrees in one host round trip
+    std::vector<DPoly> Zs, diffs;
+    std::vector<std::pair<const fe*, uint64_t>> nums;
+    for (size_t s = 0; s < m; ++s) {
+      DPoly I = dpoly_upload(ctx, bi[s].data(), bi[s].size());
+      Zs.push_back(dpoly_upload(ctx, bz[s].data(), bz[s].size()));
+      diffs.push_back(lincomb(ctx, {{trace_polys[s].p(), 0, trace_polys[s].len, fe_one()},
+                                    {I.p(), 0, I.len, fe_neg(fe_one())}}));
+      nums.emplace_back(diffs.back().p(), diffs.back().len);
+    }
+    const std::vector<int64_t> dnum = dev_degrees(ctx, nums);
+    for (size_t s = 0; s < m; ++s)
+      bqs.push_back(fast_coset_divide_dev(ctx, st.omicron, D, g, diffs[s].p(), diffs[s].len, Zs[s].p(), Zs[s].len,
+                                          hp_degree(bz[s]), bz[s].data(), dnum[s]));
   }
   mark("boundary_quotients");
   // boundary-quotient codewords (stark.rs:367-386); their trees hash on the side stream
@@ -639,52 +651,25 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
   DPoly tz = zerofier_geometric_dev(ctx, st.omicron, D, T - 1);
   // prod_{i < T-1} (x - omicron^i) is monic of degree T - 1 (< D: no wrap-around)
   const int64_t dtz = tz.len == T && T - 1 < D ? (int64_t)(T - 1) : dev_degree(ctx, tz.p(), tz.len);
+  std::vector<DevBuf> air_keep;  // AIR tables and x-polynomial values, alive until the quotients are done
   std::map<uint64_t, AirCoset> cosets;
   std::map<uint64_t, std::pair<DevBuf, uint64_t>> tz_ntt;  // order -> NTT of scale(tz, g)
   std::vector<DPoly> tqs;
-  for (const MPoly* tc : tcs) {
-    const uint64_t len = symbolic_degree_bound(*tc, Tp - 1) + 1;
-    const uint64_t L = next_pow2(len);
-    auto cit = cosets.find(L);
-    if (cit == cosets.end()) cit = cosets.emplace(L, air_coset(ctx, trace_polys, L, st.omicron, g, st.D)).first;
-    DPoly vals = transition_values(ctx, *tc, cit->second, g);
-    auto tz_values = [&](const DivPlan& pl) -> const fe* {
-      auto zit = tz_ntt.find(pl.order);
-      if (zit == tz_ntt.end()) {
-        std::pair<DevBuf, uint64_t> z;
-        ref_inner_ntt(ctx, pl.root, pl.order, tz.p(), tz.len, &g, z.first, z.second);
-        zit = tz_ntt.emplace(pl.order, std::move(z)).first;
-      }
-      return zit->second.first.as<fe>();
-    };
-    // Fast path: if the division by Z is exact, q = INTT(vals / Z) has degree dl - dr <= len - 1 - dr
-    // and then dl = deg(q) + dr exactly (q Z agrees with the transition polynomial on L > its
-    // degree points); with dl >= L/2 the reference's order is L, its lhs NTT is `vals` and its
-    // truncated quotient is q -- no coefficient transform of the lhs is needed.
-    if (L <= D && (uint64_t)dtz < len) {
-      DivPlan pl;
-      pl.root = root_of_order(L);
-      pl.order = L;
-      DevBuf qv(ctx, L * sizeof(fe)), qc(ctx, L * sizeof(fe));
-      dev_div(ctx, qv.as<fe>(), vals.p(), tz_values(pl), L);
-      intt_sized(ctx, pl.root, qv.as<fe>(), ilog2_exact(L), qc.as<fe>());
-      const int64_t dq = dev_degree(ctx, qc.as<fe>(), L);
-      const uint64_t dl = (uint64_t)dq + (uint64_t)dtz;
-      if (dq >= 0 && dl <= len - 1 && std::max<uint64_t>(dl, (uint64_t)dtz) >= L / 2) {
-        DPoly out = dpoly_alloc(ctx, (uint64_t)dq + 1);
-        dev_scale_pow(ctx, out.p(), qc.as<fe>(), out.len, fe_inv(g));
-        tqs.push_back(std::move(out));
-        continue;
-      }
+  auto tz_values = [&](const DivPlan& pl) -> const fe* {
+    auto zit = tz_ntt.find(pl.order);
+    if (zit == tz_ntt.end()) {
+      std::pair<DevBuf, uint64_t> z;
+      ref_inner_ntt(ctx, pl.root, pl.order, tz.p(), tz.len, &g, z.first, z.second);
+      zit = tz_ntt.emplace(pl.order, std::move(z)).first;
     }
-    // general path (inexact division or a degree below L/2): the reference's steps
+    return zit->second.first.as<fe>();
+  };
+  // the reference's steps (inexact division or a degree below L/2)
+  auto general_quotient = [&](const DPoly& vals, uint64_t len, uint64_t L) -> DPoly {
     DPoly coeffs = dpoly_alloc(ctx, L);
     coset_interpolate_dev(ctx, vals.p(), L, g, coeffs.p());  // coefficients len..L-1 are zero
     const DivPlan pl = coset_divide_plan(st.omicron, D, dev_degree(ctx, coeffs.p(), len), dtz);
-    if (pl.zero_lhs) {
-      tqs.push_back(DPoly{});
-      continue;
-    }
+    if (pl.zero_lhs) return DPoly{};
     DevBuf lhs_own;
     fe* lhs_v = vals.p();
     if (!(pl.order == L && len <= pl.order)) {
@@ -692,17 +677,69 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
       ref_inner_ntt(ctx, pl.root, pl.order, coeffs.p(), len, &g, lhs_own, nl);
       lhs_v = lhs_own.as<fe>();
     }
-    tqs.push_back(coset_divide_finish(ctx, pl, g, lhs_v, tz_values(pl)));
+    return coset_divide_finish(ctx, pl, g, lhs_v, tz_values(pl));
+  };
+  // Fast path: if the division by Z is exact, q = INTT(vals / Z) has degree dl - dr <= len - 1 - dr
+  // and then dl = deg(q) + dr exactly (q Z agrees with the transition polynomial on L > its
+  // degree points); with dl >= L/2 the reference's order is L, its lhs NTT is `vals` and its
+  // truncated quotient is q -- no coefficient transform of the lhs is needed.  Whether it holds
+  // depends on deg(q), which is read with every other quotient's degree in one round trip below;
+  // a constraint that fails the check (an inexact division: a false witness) is then redone the
+  // reference's way.
+  struct Pending {
+    size_t idx;
+    DPoly vals;
+    uint64_t len, L;
+  };
+  std::vector<Pending> pending;
+  for (const MPoly* tc : tcs) {
+    const uint64_t len = symbolic_degree_bound(*tc, Tp - 1) + 1;
+    const uint64_t L = next_pow2(len);
+    auto cit = cosets.find(L);
+    if (cit == cosets.end()) cit = cosets.emplace(L, air_coset(ctx, trace_polys, L, st.omicron, g, st.D)).first;
+    DPoly vals = transition_values(ctx, *tc, cit->second, g, air_keep);
+    if (L <= D && (uint64_t)dtz < len) {
+      DivPlan pl;
+      pl.root = root_of_order(L);
+      pl.order = L;
+      DevBuf qv(ctx, L * sizeof(fe)), qc(ctx, L * sizeof(fe));
+      dev_div(ctx, qv.as<fe>(), vals.p(), tz_values(pl), L);
+      intt_sized(ctx, pl.root, qv.as<fe>(), ilog2_exact(L), qc.as<fe>());
+      DPoly out = dpoly_alloc(ctx, L);  // all L coefficients unscaled: zeros stay zero
+      dev_scale_pow(ctx, out.p(), qc.as<fe>(), L, fe_inv(g));
+      pending.push_back(Pending{tqs.size(), std::move(vals), len, L});
+      tqs.push_back(std::move(out));
+      continue;
+    }
+    tqs.push_back(general_quotient(vals, len, L));
   }
   mark("transition_quotients");
   // every quotient's degree with one host round trip (checked after the weights, as the
   // reference does, and used again by the terms below); it drains the main stream past
   // every division, so a zero divisor is reported before any root is pushed
-  std::vector<std::pair<const fe*, uint64_t>> qpolys;
-  for (const DPoly& q : tqs) qpolys.emplace_back(q.p(), q.len);
-  for (const DPoly& q : bqs) qpolys.emplace_back(q.p(), q.len);
-  const std::vector<int64_t> qdeg = dev_degrees(ctx, qpolys);
+  auto quotient_degrees = [&]() {
+    std::vector<std::pair<const fe*, uint64_t>> qpolys;
+    for (const DPoly& q : tqs) qpolys.emplace_back(q.p(), q.len);
+    for (const DPoly& q : bqs) qpolys.emplace_back(q.p(), q.len);
+    return dev_degrees(ctx, qpolys);
+  };
+  std::vector<int64_t> qdeg = quotient_degrees();
   check_div_zero(ctx);
+  bool redone = false;
+  for (Pending& pd : pending) {
+    const int64_t dq = qdeg[pd.idx];
+    const uint64_t dl = (uint64_t)dq + (uint64_t)dtz;
+    if (dq >= 0 && dl <= pd.len - 1 && std::max<uint64_t>(dl, (uint64_t)dtz) >= pd.L / 2) {
+      tqs[pd.idx].len = (uint64_t)dq + 1;  // the reference's truncated quotient
+    } else {
+      tqs[pd.idx] = general_quotient(pd.vals, pd.len, pd.L);
+      redone = true;
+    }
+  }
+  if (redone) {
+    qdeg = quotient_degrees();
+    check_div_zero(ctx);
+  }
   // roots in the reference's order: boundary quotients (stark.rs:373-386), randomizer (:443)
   {
     sg_tree* t[4];
