@@ -124,6 +124,19 @@ void* sg_ctx::staging(int slot, size_t bytes) {
   return staging_ptr[slot];
 }
 
+bool sg_ctx::domain_cache_on() const {
+  static const bool off = [] {
+    const char* v = getenv("SG_NO_DOMAIN_CACHE");
+    return v && *v && *v != '0';
+  }();
+  return !off;
+}
+
+void* sg_ctx::domain_table(const std::vector<uint64_t>& key) const {
+  auto it = domain_tables.find(key);
+  return it == domain_tables.end() ? nullptr : it->second;
+}
+
 const fe* sg_ctx::stage_twiddles(const fe& root, int logn) {
   auto key = std::make_pair(std::make_pair(fe_lo(root), fe_hi(root)), logn);
   auto it = stage_tables.find(key);
@@ -240,6 +253,7 @@ extern "C" void sg_ctx_destroy(sg_ctx* ctx) {
   for (auto& kv : ctx->pow_tables) (void)hipFree(kv.second.ptr);
   for (auto& kv : ctx->stage_tables) (void)hipFree(kv.second);
   for (auto& kv : ctx->interp_tables) (void)hipFree(kv.second);
+  for (auto& kv : ctx->domain_tables) (void)hipFree(kv.second);
   for (void* p : ctx->staging_ptr)
     if (p) (void)hipHostFree(p);
   if (ctx->pinned_roots) (void)hipHostFree(ctx->pinned_roots);
@@ -309,6 +323,8 @@ extern "C" int sg_ctx_trim(sg_ctx* ctx) {
     ctx->stage_tables.clear();
     for (auto& kv : ctx->interp_tables) (void)hipFree(kv.second);
     ctx->interp_tables.clear();
+    for (auto& kv : ctx->domain_tables) (void)hipFree(kv.second);
+    ctx->domain_tables.clear();
   });
 }
 

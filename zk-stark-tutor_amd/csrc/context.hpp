@@ -96,6 +96,14 @@ struct sg_ctx {
   std::map<std::pair<std::pair<uint64_t, uint64_t>, int>, void*> stage_tables;
   // geometric interpolation kernels NTT_D(1 / (1 - q^-j)) keyed by (q limbs, D) (poly.cpp)
   std::map<std::pair<std::pair<uint64_t, uint64_t>, uint64_t>, void*> interp_tables;
+  // other values that depend only on a proof's public domain (the trace domain's zerofier and its
+  // transforms, the transition zerofier's coset values and their inverses), cached like the
+  // twiddle plans: key = a tag and the parameters, value = a device buffer owned by the context.
+  // SG_NO_DOMAIN_CACHE=1 recomputes them in every call instead.
+  std::map<std::vector<uint64_t>, void*> domain_tables;
+  bool domain_cache_on() const;
+  void* domain_table(const std::vector<uint64_t>& key) const;
+  void domain_table_put(const std::vector<uint64_t>& key, void* p) { domain_tables[key] = p; }
   // pinned host staging buffers (grown on demand): slot 0 uploads gather addresses,
   // slot 1 receives gathered openings -- pageable copies of MBs cost ~10x more
   void* staging_ptr[2] = {nullptr, nullptr};

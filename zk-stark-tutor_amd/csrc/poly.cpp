@@ -358,33 +358,46 @@ DPoly interpolate_geometric_dev(sg_ctx* ctx, const fe& q, uint64_t D, const fe* 
     intt_sized(ctx, q, y, logD, out.p());
       return out;
   }
-  // Z, Z(q^m) and Z'(q^i) (cached per domain)
+  // Z, Z(q^m) and Z'(q^i): they depend on the domain only, so the context keeps them like a
+  // twiddle plan (else `cache` shares them between the calls of one prove)
+  const std::vector<uint64_t> key = {kDomainGeoInterp, fe_lo(q), fe_hi(q), D, n};
+  const fe* Zv = ctx->domain_cache_on() ? static_cast<const fe*>(ctx->domain_table(key)) : nullptr;
+  const fe* Zdv = Zv ? Zv + D : nullptr;
   GeoInterpCache local;
   GeoInterpCache& zc = cache ? *cache : local;
-  if (!(zc.n == n && zc.D == D && fe_eq(zc.q, q))) {
-    DPoly Z = zerofier_geometric_dev(ctx, q, D, n);
-    DevBuf Zd(ctx, n * sizeof(fe));
-    zc.Zv = DevBuf(ctx, D * sizeof(fe));
-    zc.Zdv = DevBuf(ctx, D * sizeof(fe));
-    ntt_sized(ctx, q, Z.p(), n + 1, logD, zc.Zv.as<fe>());
-    SG_HIP(launch_deriv(Zd.as<fe>(), Z.p(), n, fe_r2(), ctx->stream));
-    ntt_sized(ctx, q, Zd.as<fe>(), n, logD, zc.Zdv.as<fe>());
-    zc.q = q;
-    zc.D = D;
-    zc.n = n;
+  if (!Zv) {
+    if (!(zc.n == n && zc.D == D && fe_eq(zc.q, q))) {
+      DPoly Z = zerofier_geometric_dev(ctx, q, D, n);
+      DevBuf Zd(ctx, n * sizeof(fe));
+      zc.Zv = DevBuf(ctx, D * sizeof(fe));
+      zc.Zdv = DevBuf(ctx, D * sizeof(fe));
+      ntt_sized(ctx, q, Z.p(), n + 1, logD, zc.Zv.as<fe>());
+      SG_HIP(launch_deriv(Zd.as<fe>(), Z.p(), n, fe_r2(), ctx->stream));
+      ntt_sized(ctx, q, Zd.as<fe>(), n, logD, zc.Zdv.as<fe>());
+      zc.q = q;
+      zc.D = D;
+      zc.n = n;
+    }
+    Zv = zc.Zv.as<fe>();
+    Zdv = zc.Zdv.as<fe>();
+    if (ctx->domain_cache_on()) {
+      void* t = nullptr;
+      SG_HIP(hipMalloc(&t, 2 * D * sizeof(fe)));
+      SG_HIP(hipMemcpyAsync(t, Zv, D * sizeof(fe), hipMemcpyDeviceToDevice, ctx->stream));
+      SG_HIP(hipMemcpyAsync(static_cast<fe*>(t) + D, Zdv, D * sizeof(fe), hipMemcpyDeviceToDevice, ctx->stream));
+      ctx->domain_table_put(key, t);
+    }
   }
-  const DevBuf& Zv = zc.Zv;
-  const DevBuf& Zdv = zc.Zdv;
   // a_i = y_i / Z'(q^i); S = a (*) b cyclically, b[j] = 1 / (1 - q^-j)
   DevBuf a(ctx, n * sizeof(fe)), va(ctx, D * sizeof(fe)), S(ctx, D * sizeof(fe));
-  dev_div(ctx, a.as<fe>(), y, Zdv.as<fe>(), n);
+  dev_div(ctx, a.as<fe>(), y, Zdv, n);
   ntt_sized(ctx, q, a.as<fe>(), n, logD, va.as<fe>());
   dev_mul(ctx, va.as<fe>(), va.as<fe>(), interp_kernel(ctx, q, D), D);
   intt_sized(ctx, q, va.as<fe>(), logD, S.as<fe>());
   // values on the whole group, then the coefficients
   const fe *iA, *iB;
   pow_tables2(ctx, fe_inv(q), D, &iA, &iB);
-  SG_HIP(launch_interp_assemble(va.as<fe>(), y, Zv.as<fe>(), S.as<fe>(), n, D, iA, iB, fe_r2(), ctx->stream));
+  SG_HIP(launch_interp_assemble(va.as<fe>(), y, Zv, S.as<fe>(), n, D, iA, iB, fe_r2(), ctx->stream));
   // the coefficients land in the result's own buffer (D >= n slots): no copy of the n kept
   DPoly out = dpoly_alloc(ctx, D);
   intt_sized(ctx, q, va.as<fe>(), logD, out.p());

@@ -82,6 +82,8 @@ DPoly fast_coset_divide_dev(sg_ctx* ctx, fe root, uint64_t root_order, const fe&
 // prod_{i<n} (x - q^i) for q of order D (ntt_arithmetics.rs:66-113 on the domain q^0..q^(n-1)), length n + 1;
 // n == D reproduces the reference's wrapped result (D zeros)
 DPoly zerofier_geometric_dev(sg_ctx* ctx, const fe& q, uint64_t D, uint64_t n);
+// tags of the context's domain tables (sg_ctx::domain_tables keys start with one)
+enum : uint64_t { kDomainGeoInterp = 1, kDomainTzCoeffs = 2, kDomainTzValues = 3, kDomainTzInverse = 4 };
 // Z(q^m) and Z'(q^i) of the domain q^0..q^(n-1), reusable across interpolations on one domain
 struct GeoInterpCache {
   fe q;

@@ -648,21 +648,73 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
   // they are reused; the zerofier's NTT is shared by all constraints.
   const uint64_t T = st.original_trace_length;
   SG_REQUIRE(T >= 2, "transition zerofier needs a trace of at least two rows");
-  DPoly tz = zerofier_geometric_dev(ctx, st.omicron, D, T - 1);
+  // The transition zerofier prod_{i < T-1} (x - omicron^i), its coset values and their inverses
+  // depend on the public domain only (omicron, D, T, the coset offset): the context keeps them
+  // like twiddle plans (sg_ctx::domain_tables; SG_NO_DOMAIN_CACHE=1 recomputes them per prove).
+  const bool dcache = ctx->domain_cache_on() && T - 1 < D;
+  const std::vector<uint64_t> tz_key = {kDomainTzCoeffs, fe_lo(st.omicron), fe_hi(st.omicron), D, T};
+  DPoly tz_own;
+  const fe* tz_p = dcache ? static_cast<const fe*>(ctx->domain_table(tz_key)) : nullptr;
+  uint64_t tz_len = T;  // T - 1 < D: length T (no wrap-around)
+  if (!tz_p) {
+    tz_own = zerofier_geometric_dev(ctx, st.omicron, D, T - 1);
+    tz_p = tz_own.p();
+    tz_len = tz_own.len;
+    if (dcache) {
+      void* t = nullptr;
+      SG_HIP(hipMalloc(&t, tz_len * sizeof(fe)));
+      SG_HIP(hipMemcpyAsync(t, tz_p, tz_len * sizeof(fe), hipMemcpyDeviceToDevice, ctx->stream));
+      ctx->domain_table_put(tz_key, t);
+    }
+  }
   // prod_{i < T-1} (x - omicron^i) is monic of degree T - 1 (< D: no wrap-around)
-  const int64_t dtz = tz.len == T && T - 1 < D ? (int64_t)(T - 1) : dev_degree(ctx, tz.p(), tz.len);
+  const int64_t dtz = tz_len == T && T - 1 < D ? (int64_t)(T - 1) : dev_degree(ctx, tz_p, tz_len);
   std::vector<DevBuf> air_keep;  // AIR tables and x-polynomial values, alive until the quotients are done
   std::map<uint64_t, AirCoset> cosets;
   std::map<uint64_t, std::pair<DevBuf, uint64_t>> tz_ntt;  // order -> NTT of scale(tz, g)
   std::vector<DPoly> tqs;
+  auto tz_key_at = [&](uint64_t tag, const DivPlan& pl) {
+    return std::vector<uint64_t>{tag, fe_lo(st.omicron), fe_hi(st.omicron), D, T, pl.order, fe_lo(pl.root),
+                                 fe_hi(pl.root), fe_lo(g), fe_hi(g)};
+  };
   auto tz_values = [&](const DivPlan& pl) -> const fe* {
+    const std::vector<uint64_t> key = tz_key_at(kDomainTzValues, pl);
+    if (dcache)
+      if (void* t = ctx->domain_table(key)) return static_cast<const fe*>(t);
     auto zit = tz_ntt.find(pl.order);
     if (zit == tz_ntt.end()) {
       std::pair<DevBuf, uint64_t> z;
-      ref_inner_ntt(ctx, pl.root, pl.order, tz.p(), tz.len, &g, z.first, z.second);
+      ref_inner_ntt(ctx, pl.root, pl.order, tz_p, tz_len, &g, z.first, z.second);
       zit = tz_ntt.emplace(pl.order, std::move(z)).first;
     }
+    if (dcache) {
+      void* t = nullptr;
+      SG_HIP(hipMalloc(&t, zit->second.second * sizeof(fe)));
+      SG_HIP(hipMemcpyAsync(t, zit->second.first.get(), zit->second.second * sizeof(fe), hipMemcpyDeviceToDevice,
+                            ctx->stream));
+      ctx->domain_table_put(key, t);
+      return static_cast<const fe*>(t);
+    }
     return zit->second.first.as<fe>();
+  };
+  // 1 / tz on the coset, for the fast path's division (a product by the cached inverse: the field's
+  // a / b is a * b^-1, field_element.rs:82-90, so the quotient is the same).  Built once per
+  // domain; the build checks for a zero divisor before the table is kept.
+  auto tz_inverse = [&](const DivPlan& pl) -> const fe* {
+    const std::vector<uint64_t> key = tz_key_at(kDomainTzInverse, pl);
+    if (void* t = ctx->domain_table(key)) return static_cast<const fe*>(t);
+    void* t = nullptr;
+    SG_HIP(hipMalloc(&t, pl.order * sizeof(fe)));
+    dev_div(ctx, static_cast<fe*>(t), nullptr, tz_values(pl), pl.order);
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+    try {
+      check_div_zero(ctx);
+    } catch (...) {
+      (void)hipFree(t);
+      throw;
+    }
+    ctx->domain_table_put(key, t);
+    return static_cast<const fe*>(t);
   };
   // the reference's steps (inexact division or a degree below L/2)
   auto general_quotient = [&](const DPoly& vals, uint64_t len, uint64_t L) -> DPoly {
@@ -703,7 +755,8 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
       pl.root = root_of_order(L);
       pl.order = L;
       DevBuf qv(ctx, L * sizeof(fe)), qc(ctx, L * sizeof(fe));
-      dev_div(ctx, qv.as<fe>(), vals.p(), tz_values(pl), L);
+      if (dcache) dev_mul(ctx, qv.as<fe>(), vals.p(), tz_inverse(pl), L);
+      else dev_div(ctx, qv.as<fe>(), vals.p(), tz_values(pl), L);
       intt_sized(ctx, pl.root, qv.as<fe>(), ilog2_exact(L), qc.as<fe>());
       DPoly out = dpoly_alloc(ctx, L);  // all L coefficients unscaled: zeros stay zero
       dev_scale_pow(ctx, out.p(), qc.as<fe>(), L, fe_inv(g));
