@@ -153,6 +153,7 @@ MPoly mp_pow(sg_ctx* ctx, const MPoly& a, unsigned __int128 e) {
 MPolyDevice::~MPolyDevice() {
   for (void* p : ptr)
     if (p) (void)hipFree(p);
+  for (auto& kv : coset) (void)hipFree(kv.second);
 }
 
 const MPolyDevice& mp_device(sg_ctx* ctx, const MPoly& a) {

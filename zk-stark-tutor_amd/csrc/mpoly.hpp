@@ -32,6 +32,9 @@ struct MPolyDevice {
   std::vector<HPoly> small;     // host copy of those with len <= kSmallPolyMax (else empty)
   std::vector<int32_t> qidx;    // per group (map order): index into ptr, -1 for an all-zero group
   std::vector<fe> scale;        // per group: x-polynomial = scale * ptr[qidx]
+  // values of x-polynomial q on a coset {q, L, offset limbs} -> L elements: public (the AIR and the
+  // domain), kept like the context's domain tables (stark.cpp transition_values)
+  mutable std::map<std::vector<uint64_t>, void*> coset;
   ~MPolyDevice();
 };
 

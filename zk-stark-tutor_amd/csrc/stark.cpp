@@ -419,8 +419,18 @@ DPoly transition_values(sg_ctx* ctx, const MPoly& tc, const AirCoset& co, const 
   SG_REQUIRE(nv <= kAirMaxVars, "at most 4 registers are supported by the AIR kernel");
   // distinct group x-polynomials (device-resident, uploaded once per constraint) on the coset
   const MPolyDevice& xd = mp_device(ctx, tc);
-  std::vector<DPoly> Q;
+  std::vector<DPoly> Q;        // values computed by this call (when not kept)
+  std::vector<const fe*> qp;   // per distinct x-polynomial: its values on the coset
+  const bool kept = ctx->domain_cache_on();
   for (size_t q = 0; q < xd.ptr.size(); ++q) {
+    const std::vector<uint64_t> key = {q, L, fe_lo(offset), fe_hi(offset)};
+    if (kept) {
+      auto it = xd.coset.find(key);
+      if (it != xd.coset.end()) {
+        qp.push_back(static_cast<const fe*>(it->second));
+        continue;
+      }
+    }
     Q.push_back(dpoly_alloc(ctx, L));
     fe* out = Q.back().p();
     if (!xd.small[q].empty()) {  // a tiny polynomial (e.g. the constant 1): Horner at offset w_L^k
@@ -430,10 +440,19 @@ DPoly transition_values(sg_ctx* ctx, const MPoly& tc, const AirCoset& co, const 
       const fe *A, *B;
       pow_tables2(ctx, root_of_order(L), L, &A, &B);
       SG_HIP(launch_eval_small(out, sp, L, A, B, to_mont(offset), ctx->stream));
-      continue;
+    } else {
+      const fe* in = reinterpret_cast<const fe*>(xd.ptr[q]);
+      coset_evaluate_batch(ctx, root_of_order(L), L, offset, &in, xd.len[q], &out, 1);
     }
-    const fe* in = reinterpret_cast<const fe*>(xd.ptr[q]);
-    coset_evaluate_batch(ctx, root_of_order(L), L, offset, &in, xd.len[q], &out, 1);
+    if (kept) {
+      void* t = nullptr;
+      SG_HIP(hipMalloc(&t, L * sizeof(fe)));
+      SG_HIP(hipMemcpyAsync(t, out, L * sizeof(fe), hipMemcpyDeviceToDevice, ctx->stream));
+      xd.coset[key] = t;
+      qp.push_back(static_cast<const fe*>(t));
+    } else {
+      qp.push_back(out);
+    }
   }
   // non-zero groups bucketed by their distinct x-polynomial (an all-zero group adds nothing:
   // its products are zero polynomials)
@@ -465,8 +484,7 @@ DPoly transition_values(sg_ctx* ctx, const MPoly& tc, const AirCoset& co, const 
     memcpy(tab.data() + o, p, bytes);
     return o;
   };
-  std::vector<const fe*> qp, vp;
-  for (auto& q : Q) qp.push_back(q.p());
+  std::vector<const fe*> vp;
   for (int j = 0; j < nv; ++j) vp.push_back(co.V[co.var[j]].p());
   const size_t oq = put(qp.data(), qp.size() * sizeof(void*));
   const size_t ov = put(vp.data(), vp.size() * sizeof(void*));
