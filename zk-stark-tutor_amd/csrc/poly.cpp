@@ -243,9 +243,11 @@ DivPlan coset_divide_plan(fe root, uint64_t root_order, int64_t dl, int64_t dr) 
   return pl;
 }
 
-DPoly coset_divide_finish(sg_ctx* ctx, const DivPlan& pl, const fe& offset, fe* lhs_v, const fe* rhs_v) {
+DPoly coset_divide_finish(sg_ctx* ctx, const DivPlan& pl, const fe& offset, fe* lhs_v, const fe* rhs_v,
+                          bool rhs_is_inverse) {
   if (pl.zero_lhs) return DPoly{};
-  dev_div(ctx, lhs_v, lhs_v, rhs_v, pl.order);
+  if (rhs_is_inverse) dev_mul(ctx, lhs_v, lhs_v, rhs_v, pl.order);  // a / b = a * b^-1 (field_element.rs:82-90)
+  else dev_div(ctx, lhs_v, lhs_v, rhs_v, pl.order);
   DevBuf c(ctx, pl.order * sizeof(fe));
   intt_sized(ctx, pl.root, lhs_v, ilog2_exact(pl.order), c.as<fe>());
   uint64_t keep = std::min(pl.result_len, pl.order);
@@ -297,6 +299,33 @@ DPoly fast_coset_divide_dev(sg_ctx* ctx, fe root, uint64_t root_order, const fe&
   DevBuf vl, vr;
   uint64_t nl, nr;
   ref_inner_ntt(ctx, pl.root, pl.order, lhs, ll, &offset, vl, nl);
+  if (rhs_host && lr <= 64 && ctx->domain_cache_on()) {
+    // a small divisor known on the host (a boundary zerofier: public): 1 / its coset values is
+    // kept in the context, keyed by its coefficients and the coset, so the division is a product
+    std::vector<uint64_t> key = {kDomainDivisorInverse, pl.order, fe_lo(pl.root), fe_hi(pl.root), fe_lo(offset),
+                                 fe_hi(offset), lr};
+    for (uint64_t i = 0; i < lr; ++i) {
+      key.push_back(fe_lo(rhs_host[i]));
+      key.push_back(fe_hi(rhs_host[i]));
+    }
+    const fe* inv = static_cast<const fe*>(ctx->domain_table(key));
+    if (!inv) {
+      ref_inner_ntt(ctx, pl.root, pl.order, rhs, lr, &offset, vr, nr, rhs_host);
+      void* t = nullptr;
+      SG_HIP(hipMalloc(&t, pl.order * sizeof(fe)));
+      dev_div(ctx, static_cast<fe*>(t), nullptr, vr.as<fe>(), pl.order);
+      SG_HIP(hipStreamSynchronize(ctx->stream));
+      try {
+        check_div_zero(ctx);  // a zero divisor is reported now and the table is not kept
+      } catch (...) {
+        (void)hipFree(t);
+        throw;
+      }
+      ctx->domain_table_put(key, t);
+      inv = static_cast<const fe*>(t);
+    }
+    return coset_divide_finish(ctx, pl, offset, vl.as<fe>(), inv, true);
+  }
   ref_inner_ntt(ctx, pl.root, pl.order, rhs, lr, &offset, vr, nr, rhs_host);
   return coset_divide_finish(ctx, pl, offset, vl.as<fe>(), vr.as<fe>());
 }

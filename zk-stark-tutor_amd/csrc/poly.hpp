@@ -72,7 +72,9 @@ DivPlan coset_divide_plan(fe root, uint64_t root_order, int64_t deg_lhs, int64_t
 // host_copy: the polynomial's coefficients on the host, if the caller has them (saves a read-back)
 void ref_inner_ntt(sg_ctx* ctx, const fe& root, uint64_t order, const fe* p, uint64_t len, const fe* scale,
                    DevBuf& out, uint64_t& out_len, const fe* host_copy = nullptr);
-DPoly coset_divide_finish(sg_ctx* ctx, const DivPlan& pl, const fe& offset, fe* lhs_v, const fe* rhs_v);
+// rhs_is_inverse: rhs_v holds 1 / (the divisor's coset values), so the division is a product
+DPoly coset_divide_finish(sg_ctx* ctx, const DivPlan& pl, const fe& offset, fe* lhs_v, const fe* rhs_v,
+                          bool rhs_is_inverse = false);
 // ntt_arithmetics.rs:239-310
 // rhs_degree / lhs_degree: the divisor's / dividend's degree when the caller knows it (-1 = zero
 // polynomial), -2 = query the device
@@ -83,7 +85,8 @@ DPoly fast_coset_divide_dev(sg_ctx* ctx, fe root, uint64_t root_order, const fe&
 // n == D reproduces the reference's wrapped result (D zeros)
 DPoly zerofier_geometric_dev(sg_ctx* ctx, const fe& q, uint64_t D, uint64_t n);
 // tags of the context's domain tables (sg_ctx::domain_tables keys start with one)
-enum : uint64_t { kDomainGeoInterp = 1, kDomainTzCoeffs = 2, kDomainTzValues = 3, kDomainTzInverse = 4 };
+enum : uint64_t { kDomainGeoInterp = 1, kDomainTzCoeffs = 2, kDomainTzValues = 3, kDomainTzInverse = 4,
+                  kDomainDivisorInverse = 5 };
 // Z(q^m) and Z'(q^i) of the domain q^0..q^(n-1), reusable across interpolations on one domain
 struct GeoInterpCache {
   fe q;
