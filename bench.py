@@ -721,6 +721,10 @@ def main():
                                        "randomizer, the combination) x proofs / wall time; prove_ms = ms per "
                                        "proof; the workload's NTT rate is ntt.ntt_gelem_s",
                    "proof_bytes": len(wl.last_proof.digest()) if wl.last_proof is not None else None,
+                   "plans": "twiddle plans and public domain/AIR tables (zerofier transforms, their coset values "
+                            "and inverses, AIR x-polynomial coset values) are built by the first (warmup) proof and "
+                            "kept in the context, like FFT plans; witness- and transcript-dependent work is all "
+                            "redone every step (DESIGN.md section 5; SG_NO_DOMAIN_CACHE=1 disables the tables)",
                    "parallelism": f"replicas x{world} (independent traces, no data-path collective)"},
         "roofline": {"kernel": name, "bound": "hbm", "binding": "valu" if valu else "hbm",
                      "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,

@@ -133,6 +133,22 @@ def test_stark_prove_bytes_vs_oracle(N, exp, c, sec, tcd):
     assert ok == (st_o.max_degree(air_o) < st_o.omicron_domain_length), err
 
 
+def test_stark_prove_domain_tables_cached_and_recomputed(monkeypatch):
+    """The public domain tables the context keeps (trace-domain zerofier transforms, the transition
+    zerofier's coset values and inverse, the AIR x-polynomials' coset values, boundary-divisor
+    inverses) give the same proof bytes as recomputing them: first proof (tables built), second
+    proof (tables reused), and a proof with SG_NO_DOMAIN_CACHE=1 -- all equal to the oracle's."""
+    rp, st_o, st_g, air_o, air_g, trace, bnd, tr, rc, out = _case(40, 4, 3, 4, 2, b"domain-cache")
+    want = st_o.prove(trace, air_o, bnd, o.IndependentProofStream(), tr, rc)
+    ctx = sg.Context(0)  # a fresh context: nothing cached yet
+    st = sg.Stark(4, 3, 4, 2, 41, 2, ctx=ctx)
+    air = sg.RescuePrime(2, 1, 4, 40, ctx=ctx).transition_constraints(st.omicron, st.omicron_domain_length)
+    assert st.prove(trace, air, bnd, sg.IndependentProofStream(), tr, rc) == want
+    assert st.prove(trace, air, bnd, sg.IndependentProofStream(), tr, rc) == want
+    monkeypatch.setenv("SG_NO_DOMAIN_CACHE", "1")
+    assert st.prove(trace, air, bnd, sg.IndependentProofStream(), tr, rc) == want
+
+
 def test_stark_false_witness_and_claim():
     """stark.rs:845-880: a false witness gives the reference's (rejected) proof bytes; a false
     claim is rejected by the verifier."""

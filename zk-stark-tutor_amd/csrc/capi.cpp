@@ -125,11 +125,8 @@ void* sg_ctx::staging(int slot, size_t bytes) {
 }
 
 bool sg_ctx::domain_cache_on() const {
-  static const bool off = [] {
-    const char* v = getenv("SG_NO_DOMAIN_CACHE");
-    return v && *v && *v != '0';
-  }();
-  return !off;
+  const char* v = getenv("SG_NO_DOMAIN_CACHE");  // read per call: tests toggle it between proofs
+  return !(v && *v && *v != '0');
 }
 
 void* sg_ctx::domain_table(const std::vector<uint64_t>& key) const {
