@@ -212,3 +212,23 @@ def test_interpolate_arbitrary_edge_cases():
     dom = [0] + [rng.randrange(P) for _ in range(30)]
     vals = [0] * 31
     assert sg.fast_interpolate_domain(w, D, dom, vals).coefficients == [0] * 31
+
+
+def test_degree_top_down_scan():
+    """Polynomial::degree (polynomial.rs:41-58) on the device: the top-down chunked scan with
+    early exit (k_last_nonzero) at every position class -- leading coefficient in the top
+    chunk, at chunk edges, deep below the top, in the bottom chunk, and the zero polynomial
+    (None) -- on buffers of 1 .. 2^20 + 7 elements."""
+    chunk = 256 * 16
+    for n in (1, 2, 17, chunk - 1, chunk, chunk + 1, 3 * chunk + 5, (1 << 20) + 7):
+        cases = {None, 0, n - 1, n // 2, min(n - 1, chunk), max(0, n - chunk - 1), max(0, n - chunk)}
+        for lead in sorted(cases, key=lambda x: -1 if x is None else x):
+            a = np.zeros((n, 2), dtype=np.uint64)
+            if lead is not None:
+                a[lead, 0] = 1 + lead
+                if lead > 0:
+                    a[lead - 1, 1] = 9   # a nonzero below the leading one
+                if lead >= 3:
+                    a[lead // 3, 0] = 5
+            p = sg.Polynomial.new(a)
+            assert p.degree() == lead, (n, lead)

@@ -345,12 +345,34 @@ __global__ __launch_bounds__(kBlock) void k_interp_assemble(fe* __restrict__ V, 
 // --------------------------------------------------------------- degree
 
 // *last = max{i + 1 : a[i] != 0} (0 when all zero): degree() = *last - 1 (polynomial.rs:41-58)
+// Top-down: block b scans the b-th chunk from the end (kDegPer elements per lane, all loads
+// in flight together) and first reads *last: if a nonzero at or above its chunk's end is
+// already recorded, nothing in the chunk can raise the maximum, so it exits without loading.
+// Blocks are dispatched in index order, so a polynomial whose leading coefficient sits near
+// the end of its buffer (the usual case) is decided by its top chunks.  A stale read only
+// costs the early exit, never the result.
+constexpr unsigned kDegPer = 16;
 __global__ __launch_bounds__(kBlock) void k_last_nonzero(const fe* __restrict__ a, uint64_t n,
                                                          unsigned long long* __restrict__ last) {
   __shared__ unsigned long long wmax[kBlock / 64];
+  __shared__ int skip;
+  constexpr uint64_t chunk = (uint64_t)kBlock * kDegPer;
+  const uint64_t hi = n - (uint64_t)blockIdx.x * chunk;  // this block covers [lo, hi)
+  const uint64_t lo = hi > chunk ? hi - chunk : 0;
+  // one read for the block, so the whole block exits or none of it does
+  if (threadIdx.x == 0) skip = __hip_atomic_load(last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= hi;
+  __syncthreads();
+  if (skip) return;
   unsigned long long best = 0;
-  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x)
-    if (!fe_is_zero(ld_fe(a + i))) best = i + 1;
+  fe v[kDegPer];
+#pragma unroll
+  for (unsigned k = 0; k < kDegPer; ++k) {
+    const uint64_t i = lo + (uint64_t)k * kBlock + threadIdx.x;
+    v[k] = i < hi ? ld_fe(a + i) : fe_zero();
+  }
+#pragma unroll
+  for (unsigned k = 0; k < kDegPer; ++k)
+    if (!fe_is_zero(v[k])) best = lo + (uint64_t)k * kBlock + threadIdx.x + 1;
   // wave max, block max, one atomic per block (a per-wave atomic on one address serializes)
   for (int off = 32; off > 0; off >>= 1) {
     unsigned long long o = __shfl_xor(best, off);
@@ -560,8 +582,7 @@ hipError_t launch_interp_assemble(fe* V, const fe* y, const fe* Zv, const fe* S,
 hipError_t launch_last_nonzero(const fe* a, uint64_t n, unsigned long long* last, hipStream_t s) {
   if (!n) return hipSuccess;
   ProfScope ps("last_nonzero", 16 * n, s);
-  uint64_t blocks = (n + kBlock * 8 - 1) / (kBlock * 8);  // >= 8 elements per lane, <= 1024 atomics
-  if (blocks > 1024) blocks = 1024;
+  const uint64_t blocks = (n + (uint64_t)kBlock * kDegPer - 1) / ((uint64_t)kBlock * kDegPer);
   hipLaunchKernelGGL(k_last_nonzero, dim3((unsigned)blocks), dim3(kBlock), 0, s, a, n, last);
   return hipGetLastError();
 }
