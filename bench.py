@@ -753,22 +753,21 @@ def main():
         result["side"].update(block_and_c4(ctx, device))
         result["side"].update(c5_single_gpu(ctx, device))
     if world > 1 and not args.no_side:
-        # a hang in a collective must not cost the main line: rank 0 prints it and exits
-        watchdog = None
-        if rank == 0:
-            def on_timeout():
+        # a hang in a collective must not cost the main line: rank 0 prints it, and every rank
+        # exits on its own timer (a rank left blocked in a collective would hold the launcher)
+        def on_timeout():
+            if rank == 0:
                 result["side"] = {"error": "sharded side measurements timed out"}
                 print(json.dumps(result), flush=True)
-                os._exit(0)
-            watchdog = threading.Timer(300.0, on_timeout)
-            watchdog.daemon = True
-            watchdog.start()
+            os._exit(0)
+        watchdog = threading.Timer(300.0 + (0 if rank == 0 else 15.0), on_timeout)
+        watchdog.daemon = True
+        watchdog.start()
         try:
             result["side"] = side_sharded(ctx, device, world, rank)
         except Exception as e:  # noqa: BLE001 - reported in the JSON line, main metric stands
             result["side"] = {"error": f"{type(e).__name__}: {e}"}
-        if watchdog is not None:
-            watchdog.cancel()
+        watchdog.cancel()
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline_leg(fri_len)
         result["cpu_baseline_allcores"] = cpu_baseline_allcores(fri_len)
