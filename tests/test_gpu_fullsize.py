@@ -78,6 +78,25 @@ def test_c2_dense_2p22_ntt_intt_elementwise(fc):
     assert np.array_equal(sg.ntt(root, ragged), fc.ntt(root, ragged))
 
 
+@pytest.mark.parametrize("logn", [16, 17, 18, 19, 20, 21, 23])
+def test_ntt_tile_plans_elementwise(fc, logn):
+    """Every first-pass tile plan (kernels.hip ntt_first_tile: 2048-element tiles and three passes
+    at 2^16-2^17 and 2^23, 2^12 tiles + one pass for the rest at 2^18-2^20, 2^13 tiles at 2^21)
+    element for element against the checker: forward, inverse, a ragged (zero-padded) input and an
+    LDE whose first stages are skipped (fft/ntt.rs:7-68, fft/ntt_arithmetics.rs:161-170)."""
+    n = 1 << logn
+    root = o.primitive_nth_root(n)
+    x = synthetic(logn, b"tiles", n)
+    X = sg.ntt(root, x)
+    assert np.array_equal(X, fc.ntt(root, x)), f"ntt 2^{logn}"
+    assert np.array_equal(sg.intt(root, X), fc.intt(root, X)), f"intt 2^{logn}"
+    ragged = x[: n - 3]
+    assert np.array_equal(sg.ntt(root, ragged), fc.ntt(root, ragged)), f"ragged ntt 2^{logn}"
+    coeffs = x[: n >> 3]
+    got = sg.fast_coset_evaluate(root, n, o.GENERATOR, coeffs)
+    assert np.array_equal(np.asarray(got), fc.fast_coset_evaluate(root, n, o.GENERATOR, coeffs)), f"LDE 2^{logn}"
+
+
 # ------------------------------------------------------------------ C3
 
 def test_c3_fri_prove_2p24_exp8_c64(fc):

@@ -328,8 +328,8 @@ __global__ __launch_bounds__(256, SG_NTT_WPE) void k_ntt_pass(PassArgs a) {
 // qq + m 2^(L-3)).  Only the middle stages go through LDS: one LDS write + one read per
 // element plus a round trip per middle step, and L/3 barriers fewer than k_ntt_pass.
 template <int TL>
-__global__ __launch_bounds__(256, SG_NTT_WPE) void k_ntt_pass_rr(PassArgs a) {
-  static_assert(TL == 11, "2048-element tiles, 256 threads");
+__global__ __launch_bounds__(1 << (TL - 3), TL == 11 ? SG_NTT_WPE : 1) void k_ntt_pass_rr(PassArgs a) {
+  static_assert(TL >= 11 && TL <= 13, "2^TL-element tiles, 2^(TL-3) threads");
   extern __shared__ fe_lds lds[];
   const int logC = a.logC, L = a.L;
   const uint32_t C = 1u << logC;
@@ -395,7 +395,7 @@ struct FirstArgs {
 };
 
 template <int TL>
-__global__ __launch_bounds__(256, SG_NTT_WPE) void k_ntt_first(FirstArgs a) {
+__global__ __launch_bounds__(1 << (TL - 3), TL == 11 ? SG_NTT_WPE : 1) void k_ntt_first(FirstArgs a) {
   extern __shared__ fe_lds lds[];
   const int L = a.L, logC = a.logC, m = a.logn;
   const uint32_t C = 1u << logC;
@@ -1046,7 +1046,7 @@ hipError_t launch_scale_const(fe* data, uint64_t n, const fe* cst, hipStream_t s
 // stages on 2^L x C tiles (<= 4096 elements = 64 KiB of LDS), with C
 // consecutive low-bit indices per tile so global accesses are C*16-byte runs.
 hipError_t launch_ntt_dit(fe* const* data, int batch, const fe* tw, int logn, const fe* post, int first_b0,
-                          hipStream_t s, uint64_t ys, const NttEpilogue* ep) {
+                          hipStream_t s, uint64_t ys, const NttEpilogue* ep, int big_tl) {
   if (!batch_ok(batch, ys)) return hipErrorInvalidValue;
   if (ep && (!ys || post || first_b0 >= logn)) return hipErrorInvalidValue;  // the epilogue needs a last pass
   if (ys && ys != ((uint64_t)1 << logn)) return hipErrorInvalidValue;  // rows are contiguous transforms
@@ -1061,6 +1061,14 @@ hipError_t launch_ntt_dit(fe* const* data, int batch, const fe* tw, int logn, co
     lds_attr = true;
   }
   static const bool use_rr = env_int("SG_NTT_RR", 1) != 0;  // register-direct first/last steps
+  const int big = big_tl;
+  static bool big_attr = false;
+  if ((big == 12 || big == 13) && !big_attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)k_ntt_pass_rr<12>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_ntt_pass_rr<13>, hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
+    if (e != hipSuccess) return e;
+    big_attr = true;
+  }
   static const int tile_log = [] {
     int t = env_int("SG_NTT_TILE_LOG", 11);
     return (t == 11 || t == 12) ? t : 11;
@@ -1090,6 +1098,14 @@ hipError_t launch_ntt_dit(fe* const* data, int batch, const fe* tw, int logn, co
     int passes = (rem + lmax - 1) / lmax;
     a.L = (rem + passes - 1) / passes;
     a.logC = b0 < tile_log - a.L ? b0 : tile_log - a.L;
+    // one pass on a 2^big-element tile for all the remaining stages (columns: >= 64-byte runs on
+    // 2^13 tiles, >= 32 on 2^12), 2^(big - 3) threads
+    const bool big_pass = (big == 12 || big == 13) && use_rr && rem >= 6 && rem <= big - (big == 13 ? 2 : 1) &&
+                          b0 >= big - rem && !ep;
+    if (big_pass) {
+      a.L = rem;
+      a.logC = big - rem;
+    }
     a.post = (b0 + a.L == logn) ? post : nullptr;
     a.ep_out = (ep && b0 + a.L == logn) ? ep->out : nullptr;
     if (a.ep_out) {
@@ -1109,7 +1125,11 @@ hipError_t launch_ntt_dit(fe* const* data, int batch, const fe* tw, int logn, co
     ProfScope ps(names[pi < 4 ? pi : 4], batch * 32 * ((uint64_t)1 << logn), s);
     ++pi;
     dim3 grid((unsigned)ntiles, batch);
-    if (tile == 4096 && threads == 256)
+    if (big_pass && big == 13)
+      hipLaunchKernelGGL(k_ntt_pass_rr<13>, grid, dim3(1024), lds, s, a);
+    else if (big_pass)
+      hipLaunchKernelGGL(k_ntt_pass_rr<12>, grid, dim3(512), lds, s, a);
+    else if (tile == 4096 && threads == 256)
       hipLaunchKernelGGL(k_ntt_pass<12>, grid, dim3(256), lds, s, a);
     else if (tile == 2048 && threads == 256 && a.L >= 6 && use_rr)
       hipLaunchKernelGGL(k_ntt_pass_rr<11>, grid, dim3(256), lds, s, a);
@@ -1138,7 +1158,17 @@ hipError_t launch_ntt_fused(fe* const* out, const fe* const* in, int batch, uint
     if (e != hipSuccess) return e;
     lds_attr = true;
   }
-  constexpr int TL = 11, LOGC1 = 2, L1 = TL - LOGC1;
+  static bool big_attr = false;
+  if (!big_attr) {
+    hipError_t e = hipFuncSetAttribute((const void*)k_ntt_first<12>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
+    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_ntt_first<13>, hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
+    if (e != hipSuccess) return e;
+    big_attr = true;
+  }
+  // mid-size transforms: two passes on 2^12 / 2^13-element tiles (11 stages + the rest) instead of
+  // three on 2048-element tiles (the multi-GPU interleaved gather and epilogue keep the latter)
+  const int TL = (!in_il && !ep) ? ntt_first_tile(logn) : 11;
+  const int LOGC1 = TL == 12 ? 1 : 2, L1 = TL - LOGC1;
   if (logn <= L1 + LOGC1 || logn - L1 > 63) {
     hipError_t e = launch_bitrev_gather(out, in, batch, n_in, logn, sA, sB, skip, s, in_il ? 1 : in_ys, out_ys,
                                         in_il);
@@ -1167,13 +1197,30 @@ hipError_t launch_ntt_fused(fe* const* out, const fe* const* in, int batch, uint
     ProfScope ps("ntt_first", batch * (16 * (n_in < n ? n_in : n) + 16 * n), s, (uint64_t)batch * n);
     // interleaved rows: a tile is 4 rows at one position (grid: positions x row quads)
     const dim3 grid = in_il ? dim3((unsigned)(n >> L1), (unsigned)(batch >> LOGC1)) : dim3((unsigned)(n >> TL), batch);
-    hipLaunchKernelGGL(k_ntt_first<TL>, grid, dim3(256), (size_t)16 << TL, s, a);
+    if (TL == 13)
+      hipLaunchKernelGGL(k_ntt_first<13>, grid, dim3(1024), (size_t)16 << 13, s, a);
+    else if (TL == 12)
+      hipLaunchKernelGGL(k_ntt_first<12>, grid, dim3(512), (size_t)16 << 12, s, a);
+    else
+      hipLaunchKernelGGL(k_ntt_first<11>, grid, dim3(256), (size_t)16 << 11, s, a);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
   }
   // trivial stages beyond L1 are not replicated across tiles: later passes run
   // them as real butterflies on zeros, (a, 0) -> (a, a), which is exact
-  return launch_ntt_dit(out, batch, tw, logn, post, L1, s, out_ys, ep);
+  return launch_ntt_dit(out, batch, tw, logn, post, L1, s, out_ys, ep, TL > 11 ? TL : 0);
+}
+
+int ntt_first_tile(int logn) {
+  // fwd+inv on MI355X (tools/ab_big.sh, tools/ab_big2.sh; profiles/r02_ab_ntt_tiles.log):
+  // 2^18-2^20 fastest with 2^12 tiles (11 + 7..9 stages: 2^20 0.148 -> 0.115 ms), 2^21 with 2^13
+  // tiles (11 + 10: 0.202 -> 0.184 ms); at 2^22 and above the three-pass plan on 2048-element
+  // tiles (4 blocks per CU) wins, and below 2^18 the launch count no longer matters
+  static const bool on = env_int("SG_NTT_TILES", 1) != 0;
+  if (!on) return 11;
+  if (logn >= 18 && logn <= 20) return 12;
+  if (logn == 21) return 13;
+  return 11;
 }
 
 uint64_t merkle_tree_digests(uint64_t n) { return 2 * n - 1; }

@@ -31,8 +31,13 @@ struct NttEpilogue {
   uint64_t row0, j0, rows;
   int logR;
 };
+// big_tl (12 / 13): the stages after first_b0 run as ONE pass on 2^big_tl-element tiles when they fit
+// (the plan launch_ntt_fused picks for mid-size transforms); 0: passes on 2048-element tiles
 hipError_t launch_ntt_dit(fe* const* data, int batch, const fe* tw, int logn, const fe* post, int first_b0,
-                          hipStream_t s, uint64_t ys = 0, const NttEpilogue* ep = nullptr);
+                          hipStream_t s, uint64_t ys = 0, const NttEpilogue* ep = nullptr, int big_tl = 0);
+// first-pass tile of a 2^logn transform (log2 elements): 11, or 12 / 13 where a two-pass plan on
+// bigger tiles measured faster (SG_NTT_TILES=0 keeps 11 everywhere)
+int ntt_first_tile(int logn);
 // bit-reversal (+ LDE scale, + `skip` trivial stages) fused into the first pass; out must not alias in.
 // in_il != 0: `batch` interleaved input rows (row y's element i at in[0] + i * in_il + y; batch a
 // multiple of 4, strided output rows) -- a transpose folded into the first pass's gather.
