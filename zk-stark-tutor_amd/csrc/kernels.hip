@@ -134,6 +134,10 @@ struct alignas(16) fe_lds {
   }
 };
 
+// transforms of >= 2^24 elements (>= 256 MiB, the MALL's size) stream their data with the
+// non-temporal hint (2^25 fwd+inv 2.42 -> 2.35 ms; at 2^22 the plain access is faster)
+constexpr int kStreamLogN = 24;
+
 struct PassArgs {
   fe* data[kMaxBatch];  // one transform per blockIdx.y
   const fe* tw;        // stage-major twiddles (see ntt_stage_twiddles), Montgomery form
@@ -169,7 +173,7 @@ __device__ __forceinline__ void pass_store(const PassArgs& a, fe* row, uint64_t 
   }
   if (post) v = mont_mul(v, pc);
   else if (last) v = fe_canon(v);
-  st_fe(row + k, v);
+  st_fe_stream(row + k, v, a.logn >= kStreamLogN);
 }
 
 // twiddle of global stage S (1-based) for index k < 2^(S-1): Montgomery(root^(k n / 2^S)),
@@ -342,7 +346,7 @@ __global__ __launch_bounds__(1 << (TL - 3), TL == 11 ? SG_NTT_WPE : 1) void k_nt
   const uint64_t low = cb * C + c;
   fe x[8];
 #pragma unroll
-  for (int m = 0; m < 8; ++m) x[m] = ld_fe(data + base + ((uint64_t)(8 * qq + m) << a.b0) + c);
+  for (int m = 0; m < 8; ++m) x[m] = ld_fe_stream(data + base + ((uint64_t)(8 * qq + m) << a.b0) + c, a.logn >= kStreamLogN);
   radix_regs<3>(x, a, 0, 0, low);
 #pragma unroll
   for (int m = 0; m < 8; ++m) lds[((8 * qq + m) << logC) + c] = x[m];
@@ -441,7 +445,7 @@ __global__ __launch_bounds__(1 << (TL - 3), TL == 11 ? SG_NTT_WPE : 1) void k_nt
       const uint64_t idx = hcol(c) + ((uint64_t)u << (m - L));
       x[j] = fe_zero();
       if (idx < a.n_in) {
-        x[j] = ld_fe(in_at(c, idx));
+        x[j] = ld_fe_stream(in_at(c, idx), m >= kStreamLogN);
         if (a.sA) x[j] = mont_mul(x[j], mont_mul(ld_fe(a.sA + (idx & 4095)), ld_fe(a.sB + (idx >> 12))));
       }
     }
@@ -481,7 +485,7 @@ __global__ __launch_bounds__(1 << (TL - 3), TL == 11 ? SG_NTT_WPE : 1) void k_nt
     const uint64_t h = __builtin_bitreverse64(hcol(c)) >> (64 - (m - L));
     fe* const orow = out_row(c);
 #pragma unroll
-    for (int mm = 0; mm < 8; ++mm) st_fe(orow + (h << L) + qq + ((uint32_t)mm << tl), x[mm]);
+    for (int mm = 0; mm < 8; ++mm) st_fe_stream(orow + (h << L) + qq + ((uint32_t)mm << tl), x[mm], m >= kStreamLogN);
     return;
   }
   while (t < L) {
