@@ -94,6 +94,16 @@ def test_intt_vs_oracle(n_in):
     assert sg.to_ints(sg.intt(root, x)) == o.intt(root, x)
 
 
+def test_ntt_intt_empty_input():
+    """fft/ntt.rs:11 indexes inputs[0] (the reference panics on an empty ntt input: an error here);
+    intt returns an input shorter than 2 unchanged (fft/ntt.rs:51-68), the empty one included."""
+    root = o.primitive_nth_root(4)
+    with pytest.raises(ValueError):  # the Python mirror checks first; the C ABI returns SG_ERR_INVALID
+        sg.ntt(root, [])
+    assert len(sg.intt(root, [])) == 0
+    assert sg.to_ints(sg.intt(root, [12345])) == [12345]
+
+
 def test_ntt_rejects_noncanonical():
     with pytest.raises(sg.StarkGpuError) as e:
         sg.ntt(o.primitive_nth_root(4), [P, 0, 0, 0])
