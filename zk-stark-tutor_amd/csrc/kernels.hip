@@ -1049,30 +1049,36 @@ hipError_t launch_scale_const(fe* data, uint64_t n, const fe* cst, hipStream_t s
 // Stage plan from `first_b0` (stages first_b0+1 .. logn): each pass runs L
 // stages on 2^L x C tiles (<= 4096 elements = 64 KiB of LDS), with C
 // consecutive low-bit indices per tile so global accesses are C*16-byte runs.
+// dynamic-LDS limits of the NTT kernels (> 64 KiB for the 8192-element tiles), set once per
+// process; a function-local static, so concurrent first calls from several host threads are safe
+static hipError_t ntt_lds_attributes() {
+  static const hipError_t err = [] {
+    const auto set = [](const void* f, int bytes) {
+      return hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+    };
+    hipError_t e = set((const void*)k_ntt_pass<0>, 65536);
+    if (e == hipSuccess) e = set((const void*)k_ntt_pass<12>, 65536);
+    if (e == hipSuccess) e = set((const void*)k_ntt_pass<11>, 65536);
+    if (e == hipSuccess) e = set((const void*)k_ntt_pass_rr<11>, 65536);
+    if (e == hipSuccess) e = set((const void*)k_ntt_pass_rr<12>, 65536);
+    if (e == hipSuccess) e = set((const void*)k_ntt_pass_rr<13>, 131072);
+    if (e == hipSuccess) e = set((const void*)k_ntt_first<11>, 65536);
+    if (e == hipSuccess) e = set((const void*)k_ntt_first<12>, 65536);
+    if (e == hipSuccess) e = set((const void*)k_ntt_first<13>, 131072);
+    return e;
+  }();
+  return err;
+}
+
 hipError_t launch_ntt_dit(fe* const* data, int batch, const fe* tw, int logn, const fe* post, int first_b0,
                           hipStream_t s, uint64_t ys, const NttEpilogue* ep, int big_tl) {
   if (!batch_ok(batch, ys)) return hipErrorInvalidValue;
   if (ep && (!ys || post || first_b0 >= logn)) return hipErrorInvalidValue;  // the epilogue needs a last pass
   if (ys && ys != ((uint64_t)1 << logn)) return hipErrorInvalidValue;  // rows are contiguous transforms
   const int np = ys ? 1 : batch;
-  static bool lds_attr = false;
-  if (!lds_attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)k_ntt_pass<0>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
-    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_ntt_pass<12>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
-    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_ntt_pass<11>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
-    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_ntt_pass_rr<11>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
-    if (e != hipSuccess) return e;
-    lds_attr = true;
-  }
+  if (const hipError_t e = ntt_lds_attributes(); e != hipSuccess) return e;
   static const bool use_rr = env_int("SG_NTT_RR", 1) != 0;  // register-direct first/last steps
   const int big = big_tl;
-  static bool big_attr = false;
-  if ((big == 12 || big == 13) && !big_attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)k_ntt_pass_rr<12>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
-    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_ntt_pass_rr<13>, hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
-    if (e != hipSuccess) return e;
-    big_attr = true;
-  }
   static const int tile_log = [] {
     int t = env_int("SG_NTT_TILE_LOG", 11);
     return (t == 11 || t == 12) ? t : 11;
@@ -1156,19 +1162,7 @@ hipError_t launch_ntt_fused(fe* const* out, const fe* const* in, int batch, uint
   if (!batch_ok(batch, out_ys) || (in_ys != 0) != (out_ys != 0)) return hipErrorInvalidValue;
   if (in_il && (!out_ys || (batch & 3))) return hipErrorInvalidValue;  // interleaved rows: strided, 4 per tile
   const int np = out_ys ? 1 : batch;
-  static bool lds_attr = false;
-  if (!lds_attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)k_ntt_first<11>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
-    if (e != hipSuccess) return e;
-    lds_attr = true;
-  }
-  static bool big_attr = false;
-  if (!big_attr) {
-    hipError_t e = hipFuncSetAttribute((const void*)k_ntt_first<12>, hipFuncAttributeMaxDynamicSharedMemorySize, 65536);
-    if (e == hipSuccess) e = hipFuncSetAttribute((const void*)k_ntt_first<13>, hipFuncAttributeMaxDynamicSharedMemorySize, 131072);
-    if (e != hipSuccess) return e;
-    big_attr = true;
-  }
+  if (const hipError_t e = ntt_lds_attributes(); e != hipSuccess) return e;
   // mid-size transforms: two passes on 2^12 / 2^13-element tiles (11 stages + the rest) instead of
   // three on 2048-element tiles (the multi-GPU interleaved gather and epilogue keep the latter)
   const int TL = (!in_il && !ep) ? ntt_first_tile(logn) : 11;
