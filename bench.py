@@ -760,7 +760,7 @@ def main():
                 result["side"] = {"error": "sharded side measurements timed out"}
                 print(json.dumps(result), flush=True)
             os._exit(0)
-        watchdog = threading.Timer(300.0 + (0 if rank == 0 else 15.0), on_timeout)
+        watchdog = threading.Timer(150.0 + (0 if rank == 0 else 15.0), on_timeout)
         watchdog.daemon = True
         watchdog.start()
         try:
