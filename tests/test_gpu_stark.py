@@ -149,6 +149,45 @@ def test_stark_prove_domain_tables_cached_and_recomputed(monkeypatch):
     assert st.prove(trace, air, bnd, sg.IndependentProofStream(), tr, rc) == want
 
 
+def test_stark_prove_rescue_factored_air_equals_expanded(monkeypatch):
+    """The native Rescue-Prime AIR is evaluated in its factored form (rescue_prime.rs:246-283:
+    sum MDS prev^alpha + first(x) - (sum MDSinv (next - second(x)))^alpha); SG_AIR_GENERIC=1
+    evaluates its expanded monomial groups instead.  Same proof bytes either way, equal to the
+    oracle's, for an honest and a false witness (the transition values differ from zero there)."""
+    rp, st_o, st_g, air_o, air_g, trace, bnd, tr, rc, out = _case(40, 4, 3, 4, 2, b"factored-air")
+    want = st_o.prove(trace, air_o, bnd, o.IndependentProofStream(), tr, rc)
+    bad = [list(r) for r in trace]
+    bad[17][0] = o.add_mod(bad[17][0], 5)
+    want_bad = st_o.prove(bad, air_o, bnd, o.IndependentProofStream(), tr, rc)
+    got = st_g.prove(trace, air_g, bnd, sg.IndependentProofStream(), tr, rc)
+    got_bad = st_g.prove(bad, air_g, bnd, sg.IndependentProofStream(), tr, rc)
+    monkeypatch.setenv("SG_AIR_GENERIC", "1")
+    assert st_g.prove(trace, air_g, bnd, sg.IndependentProofStream(), tr, rc) == want
+    assert st_g.prove(bad, air_g, bnd, sg.IndependentProofStream(), tr, rc) == want_bad
+    assert got == want and got_bad == want_bad
+
+
+def test_stark_prove_c4_factored_air_equals_expanded(monkeypatch):
+    """C4 size (trace 2^16, FRI domain 2^21): factored and expanded AIR evaluation give the same
+    proof bytes (the oracle cannot rebuild the expanded AIR at this size; the factored proof is
+    verified in test_stark_prove_c4_rescue_trace_2p16)."""
+    N = 65278
+    rp_g = sg.RescuePrime(2, 1, 128, N)
+    st_g = sg.Stark(8, 64, 128, 2, N + 1, 3)
+    air_g = rp_g.transition_constraints(st_g.omicron, st_g.omicron_domain_length)
+    rp_o = e.RescuePrime(2, 1, 128, N)
+    inp = o.sample(b"c4-factored")
+    trace = rp_g.trace_array(inp)
+    nrc = st_g.num_randomizer_coefficients(air_g)
+    r = e.randomness_from_seed(b"c4-factored", 2 * st_g.num_randomizers + nrc)
+    tr = sg.fe_array(r[:2 * st_g.num_randomizers])
+    rc = sg.fe_array(r[2 * st_g.num_randomizers:])
+    bnd = rp_o.boundary_constraints(rp_o.hash(inp))
+    factored = st_g.prove(trace, air_g, bnd, sg.IndependentProofStream(), tr, rc)
+    monkeypatch.setenv("SG_AIR_GENERIC", "1")
+    assert st_g.prove(trace, air_g, bnd, sg.IndependentProofStream(), tr, rc) == factored
+
+
 def test_stark_false_witness_and_claim():
     """stark.rs:845-880: a false witness gives the reference's (rejected) proof bytes; a false
     claim is rejected by the verifier."""

@@ -150,6 +150,10 @@ MPoly mp_pow(sg_ctx* ctx, const MPoly& a, unsigned __int128 e) {
   return acc;
 }
 
+RescueXPolys::~RescueXPolys() {
+  for (auto& kv : coset) (void)hipFree(kv.second);
+}
+
 MPolyDevice::~MPolyDevice() {
   for (void* p : ptr)
     if (p) (void)hipFree(p);

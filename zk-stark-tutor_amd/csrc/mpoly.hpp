@@ -38,10 +38,34 @@ struct MPolyDevice {
   ~MPolyDevice();
 };
 
+// The x-polynomials of a Rescue-Prime AIR (its round-constant interpolants first_0..m-1,
+// second_0..m-1) and their values on the cosets the prover evaluates it on (public, kept like the
+// context's domain tables; the key carries the device).
+struct RescueXPolys {
+  std::vector<HPoly> polys;  // first_0 .. first_{m-1}, second_0 .. second_{m-1}
+  mutable std::map<std::vector<uint64_t>, void*> coset;  // {device, poly, L, offset lo, hi} -> L values
+  ~RescueXPolys();
+};
+
+// A transition constraint built by the native Rescue-Prime AIR (rescue_prime.rs:246-283) also
+// carries its factored form
+//   sum_k MDS[i][k] prev_k^alpha + first_i(x) - (sum_k MDSinv[i][k] (next_k - second_k(x)))^alpha,
+// the same polynomial as its expanded groups: the prover evaluates it pointwise in ~4 products per
+// register instead of one product chain per expanded monomial (SG_AIR_GENERIC=1: the groups).
+constexpr int kRescueMaxM = 4;
+struct RescueAirForm {
+  int m = 0, row = 0;
+  uint32_t alpha = 0;
+  fe mds[kRescueMaxM];     // MDS[row][k], canonical
+  fe mds_inv[kRescueMaxM]; // MDSinv[row][k], canonical
+  std::shared_ptr<const RescueXPolys> xp;
+};
+
 struct MPoly {
   uint32_t nvars = 0;                          // key length (0: empty dictionary)
   std::map<std::vector<uint32_t>, HPoly> g;    // exponents of variables 1..nvars-1 -> x coefficients
   mutable std::shared_ptr<MPolyDevice> dev;    // lazily built (polynomials are immutable once built)
+  std::shared_ptr<const RescueAirForm> rescue; // set by the native Rescue-Prime AIR builder only
 };
 
 const MPolyDevice& mp_device(sg_ctx* ctx, const MPoly& a);

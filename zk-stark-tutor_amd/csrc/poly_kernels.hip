@@ -446,6 +446,39 @@ __global__ __launch_bounds__(kBlock) void k_air_eval(AirEvalArgs a) {
   }
 }
 
+// Montgomery x^e (x Montgomery, e >= 1): left-to-right square-and-multiply, a uniform loop
+__device__ __forceinline__ fe mont_pow_m(const fe& xm, uint32_t e) {
+  fe r = xm;
+  for (int b = 30 - __builtin_clz(e); b >= 0; --b) {
+    r = mont_mul(r, r);
+    if ((e >> b) & 1u) r = mont_mul(r, xm);
+  }
+  return r;
+}
+
+// One Rescue-Prime transition row at every coset point (rescue_prime.rs:246-283 factored):
+// ~4 products per register and 4 more for the row, against one product chain per expanded
+// monomial in k_air_eval.  Exact field arithmetic: the same values as the expanded polynomial.
+__global__ __launch_bounds__(kBlock) void k_air_rescue(AirRescueArgs a) {
+  const uint64_t mask = a.n - 1;
+  const fe one = {{1u, 0u, 0u, 0u}};
+  for (uint64_t y = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; y < a.n; y += (uint64_t)gridDim.x * blockDim.x) {
+    fe acc = ld_fe(a.first + y);
+    fe lin = fe_zero();
+#pragma unroll
+    for (int k = 0; k < kAirMaxVars / 2; ++k) {
+      if (k >= a.m) break;  // uniform
+      const fe v = ld_fe(a.V[k] + ((y + a.vshift[k]) & mask));
+      const fe pm = mont_pow_m(mont_mul(v, a.r2), a.alpha);          // Montgomery prev_k^alpha
+      acc = fe_add(acc, mont_mul(pm, a.mds[k]));                     // canonical MDS * prev_k^alpha
+      const fe w = ld_fe(a.V[a.m + k] + ((y + a.vshift[a.m + k]) & mask));
+      lin = fe_add(lin, mont_mul(fe_sub(w, ld_fe(a.second[k] + y)), a.mds_inv_m[k]));
+    }
+    const fe rhs = mont_mul(mont_pow_m(mont_mul(lin, a.r2), a.alpha), one);  // canonical lin^alpha
+    st_fe(a.out + y, fe_sub(acc, rhs));
+  }
+}
+
 // ------------------------------------------------------- linear combination
 
 // out[k] = sum_t w_t * term_t[k - off_t] over off_t <= k < off_t + len_t (w_t Montgomery)
@@ -602,6 +635,14 @@ hipError_t launch_air_eval(const AirEvalArgs& a, hipStream_t s) {
     case 7: hipLaunchKernelGGL(k_air_eval<7>, grid, dim3(kBlock), 0, s, a); break;
     default: hipLaunchKernelGGL(k_air_eval<8>, grid, dim3(kBlock), 0, s, a); break;
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_air_rescue(const AirRescueArgs& a, hipStream_t s) {
+  if (!a.n) return hipSuccess;
+  if (a.m < 1 || a.m > kAirMaxVars / 2 || a.alpha < 1 || (a.n & (a.n - 1))) return hipErrorInvalidValue;
+  ProfScope ps("air_eval", 16 * a.n * (2 * a.m + a.m + 2), s);
+  hipLaunchKernelGGL(k_air_rescue, dim3((unsigned)grid_for(a.n)), dim3(kBlock), 0, s, a);
   return hipGetLastError();
 }
 

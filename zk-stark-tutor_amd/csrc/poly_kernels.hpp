@@ -54,6 +54,22 @@ hipError_t launch_interp_assemble(fe* V, const fe* y, const fe* Zv, const fe* S,
                                   const fe* iA, const fe* iB, const fe& r2, hipStream_t s);
 hipError_t launch_last_nonzero(const fe* a, uint64_t n, unsigned long long* last, hipStream_t s);
 hipError_t launch_air_eval(const AirEvalArgs& a, hipStream_t s);
+// the Rescue-Prime AIR row in its factored form (mpoly.hpp RescueAirForm), pointwise on a coset:
+// out = first(y) + sum_k mds[k] V_k^alpha - (sum_k mds_inv[k] (V_{m+k} - second_k(y)))^alpha
+struct AirRescueArgs {
+  fe* out;
+  const fe* V[kAirMaxVars];       // prev_0..m-1, next_0..m-1 (variable j reads V[j][(y + vshift[j]) mod n])
+  uint64_t vshift[kAirMaxVars];
+  const fe* first;                // first_row on the coset
+  const fe* second[kAirMaxVars / 2];
+  fe mds[kAirMaxVars / 2];        // canonical
+  fe mds_inv_m[kAirMaxVars / 2];  // Montgomery
+  fe r2;
+  uint32_t alpha;                 // >= 1
+  int m;                          // 1 .. kAirMaxVars / 2
+  uint64_t n;                     // a power of two
+};
+hipError_t launch_air_rescue(const AirRescueArgs& a, hipStream_t s);
 hipError_t launch_lincomb(const LinCombArgs& a, hipStream_t s);
 hipError_t launch_eval_small(fe* out, const SmallPoly& p, uint64_t n, const fe* wA, const fe* wB, const fe& off_m,
                              hipStream_t s);

@@ -227,11 +227,13 @@ std::vector<MPoly> rescue_transition_constraints(sg_ctx* ctx, const sg_rescue& r
     for (size_t r = 0; r < N; ++r) vals[r] = rp.rc[2 * r * m + which];
     DPoly y = dpoly_upload(ctx, vals.data(), N);
     DPoly p = N > 1 ? interpolate_geometric_dev(ctx, omicron, D, y.p(), N) : std::move(y);
-    return mp_lift(dpoly_download(ctx, p.p(), p.len), 0);
+    return dpoly_download(ctx, p.p(), p.len);
   };
+  auto xp = std::make_shared<RescueXPolys>();
+  for (size_t i = 0; i < 2 * m; ++i) xp->polys.push_back(interp(i));  // first_0..m-1, second_0..m-1
   std::vector<MPoly> first(m), second(m);
-  for (size_t i = 0; i < m; ++i) first[i] = interp(i);
-  for (size_t i = 0; i < m; ++i) second[i] = interp(m + i);
+  for (size_t i = 0; i < m; ++i) first[i] = mp_lift(xp->polys[i], 0);
+  for (size_t i = 0; i < m; ++i) second[i] = mp_lift(xp->polys[m + i], 0);
   std::vector<MPoly> vars = mp_variables((uint32_t)(1 + 2 * m));
   std::vector<MPoly> out;
   for (size_t i = 0; i < m; ++i) {
@@ -248,6 +250,18 @@ std::vector<MPoly> rescue_transition_constraints(sg_ctx* ctx, const sg_rescue& r
     }
     rhs = mp_pow(ctx, rhs, rp.alpha);
     out.push_back(mp_sub(lhs, rhs));
+    if (m <= (size_t)kRescueMaxM && rp.alpha >= 1 && rp.alpha <= 0xFFFFFFFFu) {
+      auto form = std::make_shared<RescueAirForm>();
+      form->m = (int)m;
+      form->row = (int)i;
+      form->alpha = (uint32_t)rp.alpha;
+      for (size_t k = 0; k < m; ++k) {
+        form->mds[k] = rp.mds[i][k];
+        form->mds_inv[k] = rp.mds_inv[i][k];
+      }
+      form->xp = xp;
+      out.back().rescue = form;
+    }
   }
   return out;
 }
@@ -408,11 +422,81 @@ AirCoset air_coset(sg_ctx* ctx, const std::vector<DPoly>& trace_polys, uint64_t 
   return c;
 }
 
+// SG_AIR_GENERIC=1: evaluate a Rescue-Prime AIR through its expanded groups too (read per call)
+bool air_generic() {
+  const char* v = getenv("SG_AIR_GENERIC");
+  return v && *v && *v != '0';
+}
+
+// A Rescue-Prime row in its factored form (mpoly.hpp RescueAirForm) on the coset: the same values
+// as the expanded polynomial.  Its round-constant interpolants' coset values are public and kept
+// with the AIR (like the x-polynomial values of the generic path).
+DPoly transition_values_rescue(sg_ctx* ctx, const RescueAirForm& f, const AirCoset& co, const fe& offset,
+                               std::vector<DevBuf>& keep) {
+  const uint64_t L = co.L;
+  const int m = f.m;
+  const bool kept = ctx->domain_cache_on();
+  auto xvals = [&](int idx) -> const fe* {
+    const std::vector<uint64_t> key = {(uint64_t)ctx->device, (uint64_t)idx, L, fe_lo(offset), fe_hi(offset)};
+    if (kept) {
+      auto it = f.xp->coset.find(key);
+      if (it != f.xp->coset.end()) return static_cast<const fe*>(it->second);
+    }
+    const HPoly& hp = f.xp->polys[(size_t)idx];
+    const int64_t deg = hp_degree(hp);
+    void* t = nullptr;
+    fe* out = nullptr;
+    if (kept) {
+      SG_HIP(hipMalloc(&t, L * sizeof(fe)));
+      out = static_cast<fe*>(t);
+    } else {
+      keep.emplace_back(ctx, L * sizeof(fe));
+      out = keep.back().as<fe>();
+    }
+    try {
+      if (deg < 0) {
+        SG_HIP(hipMemsetAsync(out, 0, L * sizeof(fe), ctx->stream));
+      } else {
+        DPoly in = dpoly_upload(ctx, hp.data(), (uint64_t)deg + 1);
+        const fe* ip = in.p();
+        coset_evaluate_batch(ctx, root_of_order(L), L, offset, &ip, (size_t)deg + 1, &out, 1);
+        keep.push_back(std::move(in.buf));
+      }
+    } catch (...) {
+      if (t) (void)hipFree(t);
+      throw;
+    }
+    if (kept) f.xp->coset[key] = t;
+    return out;
+  };
+  AirRescueArgs a{};
+  DPoly vals = dpoly_alloc(ctx, L);
+  a.out = vals.p();
+  for (int j = 0; j < 2 * m; ++j) {
+    a.V[j] = co.V[(size_t)co.var[(size_t)j]].p();
+    a.vshift[j] = co.shift[(size_t)j];
+  }
+  a.first = xvals(f.row);
+  for (int k = 0; k < m; ++k) {
+    a.second[k] = xvals(m + k);
+    a.mds[k] = f.mds[k];
+    a.mds_inv_m[k] = to_mont(f.mds_inv[k]);
+  }
+  a.r2 = fe_r2();
+  a.alpha = f.alpha;
+  a.m = m;
+  a.n = L;
+  SG_HIP(launch_air_rescue(a, ctx->stream));
+  return vals;
+}
+
 // values on the coset of the polynomial evaluate_symbolic returns (m_polynomial.rs:124-139).
 // The x-polynomial values and the kernel's pointer tables move into `keep` (the caller's scope):
 // they outlive the launch without a host wait.
 DPoly transition_values(sg_ctx* ctx, const MPoly& tc, const AirCoset& co, const fe& offset,
                         std::vector<DevBuf>& keep) {
+  if (tc.rescue && (int)co.var.size() == 2 * tc.rescue->m && !air_generic())
+    return transition_values_rescue(ctx, *tc.rescue, co, offset, keep);
   const uint64_t L = co.L;
   const int nv = (int)co.var.size();
   SG_REQUIRE(tc.nvars <= 1 + (uint32_t)nv, "transition constraint has more variables than the point");
