@@ -387,11 +387,11 @@ DPoly interpolate_geometric_dev(sg_ctx* ctx, const fe& q, uint64_t D, const fe* 
     intt_sized(ctx, q, y, logD, out.p());
       return out;
   }
-  // Z, Z(q^m) and Z'(q^i): they depend on the domain only, so the context keeps them like a
+  // Z, Z(q^m) and 1 / Z'(q^i): they depend on the domain only, so the context keeps them like a
   // twiddle plan (else `cache` shares them between the calls of one prove)
   const std::vector<uint64_t> key = {kDomainGeoInterp, fe_lo(q), fe_hi(q), D, n};
   const fe* Zv = ctx->domain_cache_on() ? static_cast<const fe*>(ctx->domain_table(key)) : nullptr;
-  const fe* Zdv = Zv ? Zv + D : nullptr;
+  const fe* Zdi = Zv ? Zv + D : nullptr;
   GeoInterpCache local;
   GeoInterpCache& zc = cache ? *cache : local;
   if (!Zv) {
@@ -399,27 +399,34 @@ DPoly interpolate_geometric_dev(sg_ctx* ctx, const fe& q, uint64_t D, const fe* 
       DPoly Z = zerofier_geometric_dev(ctx, q, D, n);
       DevBuf Zd(ctx, n * sizeof(fe));
       zc.Zv = DevBuf(ctx, D * sizeof(fe));
-      zc.Zdv = DevBuf(ctx, D * sizeof(fe));
+      zc.Zdi = DevBuf(ctx, n * sizeof(fe));
       ntt_sized(ctx, q, Z.p(), n + 1, logD, zc.Zv.as<fe>());
       SG_HIP(launch_deriv(Zd.as<fe>(), Z.p(), n, fe_r2(), ctx->stream));
-      ntt_sized(ctx, q, Zd.as<fe>(), n, logD, zc.Zdv.as<fe>());
+      // Z'(q^i) for i < n (the first n values of its size-D transform), inverted once
+      DevBuf Zdfull(ctx, D * sizeof(fe));
+      ntt_sized(ctx, q, Zd.as<fe>(), n, logD, Zdfull.as<fe>());
+      dev_div(ctx, zc.Zdi.as<fe>(), nullptr, Zdfull.as<fe>(), n);
       zc.q = q;
       zc.D = D;
       zc.n = n;
     }
     Zv = zc.Zv.as<fe>();
-    Zdv = zc.Zdv.as<fe>();
+    Zdi = zc.Zdi.as<fe>();
     if (ctx->domain_cache_on()) {
+      // kept only once the inversion is known to have met no zero (the points are distinct, so
+      // Z'(q^i) != 0; a table is never cached unchecked)
+      SG_HIP(hipStreamSynchronize(ctx->stream));
+      check_div_zero(ctx);
       void* t = nullptr;
-      SG_HIP(hipMalloc(&t, 2 * D * sizeof(fe)));
+      SG_HIP(hipMalloc(&t, (D + n) * sizeof(fe)));
       SG_HIP(hipMemcpyAsync(t, Zv, D * sizeof(fe), hipMemcpyDeviceToDevice, ctx->stream));
-      SG_HIP(hipMemcpyAsync(static_cast<fe*>(t) + D, Zdv, D * sizeof(fe), hipMemcpyDeviceToDevice, ctx->stream));
+      SG_HIP(hipMemcpyAsync(static_cast<fe*>(t) + D, Zdi, n * sizeof(fe), hipMemcpyDeviceToDevice, ctx->stream));
       ctx->domain_table_put(key, t);
     }
   }
-  // a_i = y_i / Z'(q^i); S = a (*) b cyclically, b[j] = 1 / (1 - q^-j)
+  // a_i = y_i / Z'(q^i) as a product by the kept inverse; S = a (*) b cyclically, b[j] = 1 / (1 - q^-j)
   DevBuf a(ctx, n * sizeof(fe)), va(ctx, D * sizeof(fe)), S(ctx, D * sizeof(fe));
-  dev_div(ctx, a.as<fe>(), y, Zdv, n);
+  dev_mul(ctx, a.as<fe>(), y, Zdi, n);
   ntt_sized(ctx, q, a.as<fe>(), n, logD, va.as<fe>());
   dev_mul(ctx, va.as<fe>(), va.as<fe>(), interp_kernel(ctx, q, D), D);
   intt_sized(ctx, q, va.as<fe>(), logD, S.as<fe>());

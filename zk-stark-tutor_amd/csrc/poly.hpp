@@ -87,11 +87,12 @@ DPoly zerofier_geometric_dev(sg_ctx* ctx, const fe& q, uint64_t D, uint64_t n);
 // tags of the context's domain tables (sg_ctx::domain_tables keys start with one)
 enum : uint64_t { kDomainGeoInterp = 1, kDomainTzCoeffs = 2, kDomainTzValues = 3, kDomainTzInverse = 4,
                   kDomainDivisorInverse = 5 };
-// Z(q^m) and Z'(q^i) of the domain q^0..q^(n-1), reusable across interpolations on one domain
+// Z(q^m) (m < D) and 1 / Z'(q^i) (i < n) of the domain q^0..q^(n-1), reusable across
+// interpolations on one domain
 struct GeoInterpCache {
   fe q;
   uint64_t D = 0, n = 0;
-  DevBuf Zv, Zdv;
+  DevBuf Zv, Zdi;
 };
 // the interpolant of degree < n through (q^i, y_i), i < n <= D (ntt_arithmetics.rs:172-237), length n
 DPoly interpolate_geometric_dev(sg_ctx* ctx, const fe& q, uint64_t D, const fe* y, uint64_t n,
