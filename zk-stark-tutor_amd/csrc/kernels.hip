@@ -731,11 +731,14 @@ __device__ __forceinline__ void blake2b_quad(const uint64_t* msg, uint64_t t, in
   out_hi = iv4q ^ b ^ d;
 }
 
-// Node levels with a quad per node: 256 threads = 64 nodes at the first level,
-// `fuse` levels computed (64 -> 1 at most 7).  Children of the first level are
+// Node levels with a quad per node: 4 * NODES threads = NODES nodes at the first level,
+// `fuse` levels computed (NODES -> 1 at most).  Children of the first level are
 // read from HBM (level first_level-1), every produced digest is written to the tree.
-__global__ __launch_bounds__(256) void k_merkle_quad(MerkleArgs a) {
-  __shared__ uint64_t msg[64][16];
+// NODES = 64 for wide levels; NODES = 256 takes a tree's last <= 256 nodes to the root
+// in one block (one launch fewer per tree than two 64-node steps).
+template <int NODES>
+__global__ __launch_bounds__(4 * NODES) void k_merkle_quad(MerkleArgs a) {
+  __shared__ uint64_t msg[NODES][16];
   const int tid = threadIdx.x;
   const int q = tid & 3;
   const int node = tid >> 2;
@@ -1265,7 +1268,7 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
     a.first_count = count;
     int fuse;
     unsigned bs;
-    int kind;  // 0: leaf 256, 1: leaf tail 1024, 2: node 256, 3: quad, 4: leaf 512
+    int kind;  // 0: leaf 256, 1: leaf tail 1024, 2: node 256, 3: quad 64, 4: leaf 512, 5: quad 256
     if (level == 0) {
       if (count <= 64) {
         kind = 1; bs = (unsigned)count; fuse = logn + 1;
@@ -1282,8 +1285,12 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
       static const int env_nfuse = env_int("SG_MERKLE_NODE_FUSE", 4);
       kind = 2; bs = 256u; fuse = env_nfuse;
     } else {
-      kind = 3;
-      uint64_t nodes = count < 64 ? count : 64;
+      // the last <= 256 nodes of a tree go to the root in one 1024-lane block
+      // (SG_MERKLE_QUAD_TOP=0: 64-node blocks only)
+      static const int env_top = env_int("SG_MERKLE_QUAD_TOP", 1);
+      const uint64_t cap = (env_top && count <= 256) ? 256 : 64;
+      kind = cap == 256 ? 5 : 3;
+      uint64_t nodes = count < cap ? count : cap;
       bs = (unsigned)(4 * nodes);
       int lg = 0;
       while (((uint64_t)1 << lg) < nodes) ++lg;
@@ -1300,12 +1307,12 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
     uint64_t digests = 0;
     for (int k = 0; k < fuse; ++k) digests += count >> k;
     // a fused fold reads 2 source elements and writes the folded one instead of reading the leaf
-    const uint64_t per_block = kind == 3 ? bs / 4 : bs;
+    const uint64_t per_block = kind >= 3 && kind != 4 ? bs / 4 : bs;
     dim3 grid((unsigned)((count + per_block - 1) / per_block), batch);
     // elems = lanes launched (the rocprofv3 Grid_Size of this dispatch), so per-wave PMC
     // instruction counts scale to any launch population
     ProfScope ps(level == 0 ? (fold_here ? "merkle_fold_leaves" : "merkle_leaves")
-                            : (kind == 3 ? "merkle_nodes_quad" : "merkle_nodes"),
+                            : (kind == 3 || kind == 5 ? "merkle_nodes_quad" : "merkle_nodes"),
                  batch * ((level == 0 ? (fold_here ? 48 : 16) * count : 0) + 64 * digests), s,
                  (uint64_t)grid.x * grid.y * bs);
     switch (kind) {
@@ -1322,7 +1329,8 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
         if (fold_here) hipLaunchKernelGGL((k_merkle_levels<true, 512, true>), grid, dim3(bs), 0, s, a);
         else hipLaunchKernelGGL((k_merkle_levels<true, 512>), grid, dim3(bs), 0, s, a);
         break;
-      default: hipLaunchKernelGGL(k_merkle_quad, grid, dim3(bs), 0, s, a); break;
+      case 5: hipLaunchKernelGGL(k_merkle_quad<256>, grid, dim3(bs), 0, s, a); break;
+      default: hipLaunchKernelGGL(k_merkle_quad<64>, grid, dim3(bs), 0, s, a); break;
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
