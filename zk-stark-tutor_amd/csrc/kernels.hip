@@ -1240,7 +1240,8 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
   //    a tree of <= 1024 leaves with nothing above runs in one 1024-thread block.
   //  * node levels with >= kQuadBelow digests: one lane per node, 4 levels fused;
   //  * smaller levels (latency-bound): a quad of lanes per node, up to 7 levels fused.
-  constexpr uint64_t kQuadBelow = (uint64_t)1 << 16;
+  // SG_MERKLE_QUAD_BELOW = log2 of the threshold (A/B only)
+  static const uint64_t kQuadBelow = (uint64_t)1 << env_int("SG_MERKLE_QUAD_BELOW", 16);
   int logn = 0;
   while (((uint64_t)1 << logn) < n) ++logn;
   int level = start_level;
