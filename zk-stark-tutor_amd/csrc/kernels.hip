@@ -1279,7 +1279,9 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
         unsigned lbs = env_bs == 512 ? 512u : 256u;
         kind = lbs == 512 ? 4 : 0;
         bs = count < lbs ? (unsigned)count : lbs;
-        fuse = count >= ((uint64_t)1 << 18) ? env_fuse : 1;
+        // leaf levels of >= 2^SG_MERKLE_LEAF_FUSE_MIN leaves fuse node levels (A/B knob)
+        static const int env_fmin = env_int("SG_MERKLE_LEAF_FUSE_MIN", 18);
+        fuse = count >= ((uint64_t)1 << env_fmin) ? env_fuse : 1;
         if (bs < lbs) kind = 0;
       }
     } else if (count >= kQuadBelow) {
