@@ -35,6 +35,7 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <string>
 #include <vector>
 
 typedef unsigned __int128 u128;
@@ -456,6 +457,683 @@ uint64_t sample_index(const uint8_t* d, size_t dlen, uint64_t size) {  // fri.rs
   return acc % size;
 }
 
+// path payload of leaf i (merkle_root.rs:34-53, proof_stream_enum.rs:95-126): per level
+// [64 as u64 BE][sibling digest], leaf level first
+std::vector<uint8_t> path_payload(const Tree& t, uint64_t i) {
+  const int lg = log2_exact(t.n);
+  std::vector<uint8_t> pl(72 * (size_t)lg);
+  for (int k = 0; k < lg; ++k) {
+    uint8_t* q = &pl[72 * (size_t)k];
+    memset(q, 0, 8);
+    q[7] = 64;
+    memcpy(q + 8, t.level(k) + 8 * ((i >> k) ^ 1), 64);
+  }
+  return pl;
+}
+
+thread_local std::string g_err;  // message of the last failed checker call
+
+struct CheckError {
+  int code;
+  std::string msg;
+};
+#define FC_REQUIRE(cond, code, msg) \
+  do {                              \
+    if (!(cond)) throw CheckError{code, msg}; \
+  } while (0)
+
+// FRI::prove (fri.rs:210-248): commit (fri.rs:115-172), sample_indices (fri.rs:88-113) over
+// len(codewords[1]) reduced by len(codewords[-1]), query per round (fri.rs:174-208).  Returns the
+// number of rounds; the c top-level indices land in `top`.
+uint64_t fri_prove(Stream& ps, u128 offset, u128 omega, std::vector<u128>&& cw0, uint64_t expansion,
+                   uint64_t colinearity, std::vector<uint64_t>& top) {
+  const uint64_t n = cw0.size();
+  FC_REQUIRE(n && !(n & (n - 1)), -1, "FRI codeword length must be a power of two");
+  uint64_t rounds = 0;
+  for (uint64_t len = n; len > expansion && len > 4 * colinearity; len /= 2) ++rounds;  // fri.rs:40-50
+  FC_REQUIRE(rounds >= 2, -1, "FRI prove needs at least two rounds (reference indexes codewords[1])");
+  u128 w = omega, o = offset;
+  std::vector<std::vector<u128>> cws(rounds);
+  std::vector<Tree> trees(rounds);
+  cws[0] = std::move(cw0);
+  const u128 inv2m = to_m(finv(2));
+  for (uint64_t r = 0; r < rounds; ++r) {
+    const uint64_t len = cws[r].size();
+    FC_REQUIRE(fpow(w, len - 1) == finv(w), -2, "error in commit: omega does not have the right order!");
+    build_tree(cws[r].data(), len, trees[r]);
+    ps.push(0, reinterpret_cast<const uint8_t*>(trees[r].root()), 64, false);
+    if (r == rounds - 1) break;
+    uint8_t ch[32];
+    ps.fiat_shamir(ch);
+    const u128 alpha = sample_field(ch, 32);
+    // c'[i] = 2^-1 ((1 + a/(o w^i)) c[i] + (1 - a/(o w^i)) c[i + h]);  a/(o w^i) = a o^-1 (w^-1)^i
+    const uint64_t half = len / 2;
+    cws[r + 1].resize(half);
+    const u128 am = to_m(fmul(alpha, finv(o))), wim = to_m(finv(w)), Rm = K().R;
+    const u128* c = cws[r].data();
+    u128* nx = cws[r + 1].data();
+#pragma omp parallel
+    {
+      const int T = omp_get_num_threads(), id = omp_get_thread_num();
+      const uint64_t per = (half + T - 1) / T, i0 = std::min(half, per * id), i1 = std::min(half, i0 + per);
+      if (i0 < i1) {
+        u128 abo = mont(am, pow_m(wim, i0));  // Montgomery(a o^-1 w^-i0)
+        for (uint64_t i = i0; i < i1; ++i) {
+          const u128 f = mont(c[i], fadd(Rm, abo)), s = mont(c[half + i], fsub(Rm, abo));
+          nx[i] = mont(fadd(f, s), inv2m);
+          abo = mont(abo, wim);
+        }
+      }
+    }
+    w = fmul(w, w);
+    o = fmul(o, o);
+  }
+  {  // last codeword (fri.rs:166)
+    const std::vector<u128>& last = cws[rounds - 1];
+    std::vector<uint8_t> pl(16 * last.size());
+    for (size_t i = 0; i < last.size(); ++i) put_be128(&pl[16 * i], last[i]);
+    ps.push(1, pl.data(), pl.size(), !last.empty());
+  }
+  uint8_t seed[32];
+  ps.fiat_shamir(seed);
+  const uint64_t size = cws[1].size(), reduced = cws[rounds - 1].size();
+  FC_REQUIRE(colinearity <= 2 * reduced, -3, "Not enough entropy in indices with reference to last codeword");
+  FC_REQUIRE(colinearity <= reduced, -3, "Cannot sample more indices than available in the last codeword");
+  std::vector<uint64_t> idx, red;
+  std::vector<uint8_t> msg(seed, seed + 32);
+  for (uint64_t counter = 0; idx.size() < colinearity; ++counter) {
+    msg.resize(32 + counter, 0);
+    uint8_t d[64];
+    blake2b512(msg.data(), msg.size(), d);
+    const uint64_t index = sample_index(d, 64, size), rr = index % reduced;
+    if (std::find(red.begin(), red.end(), rr) == red.end()) {
+      idx.push_back(index);
+      red.push_back(rr);
+    }
+  }
+  top = idx;
+  std::vector<uint64_t> cur = idx;
+  for (uint64_t r = 0; r + 1 < rounds; ++r) {
+    const uint64_t half = cws[r].size() / 2;
+    for (auto& i : cur) i %= half;
+    for (uint64_t s = 0; s < colinearity; ++s) {
+      uint8_t pl[48];
+      put_be128(pl, cws[r][cur[s]]);
+      put_be128(pl + 16, cws[r][cur[s] + half]);
+      put_be128(pl + 32, cws[r + 1][cur[s]]);
+      ps.push(3, pl, 48, true);
+    }
+    for (uint64_t s = 0; s < colinearity; ++s) {
+      std::vector<uint8_t> a = path_payload(trees[r], cur[s]), b = path_payload(trees[r], cur[s] + half),
+                           c = path_payload(trees[r + 1], cur[s]);
+      ps.push(2, a.data(), a.size(), false);
+      ps.push(2, b.data(), b.size(), false);
+      ps.push(2, c.data(), c.size(), false);
+    }
+  }
+  return rounds;
+}
+
+// ------------------------------------------------------------------ Stark::prove (checker)
+//
+// stark/stark.rs:276-562 for a Rescue-Prime AIR, restated with fast CPU algorithms that give the
+// reference's exact outputs (every polynomial below is the unique one the reference computes, and
+// every step whose result depends on the algorithm -- fast_coset_divide, fast_multiply, the
+// NTT butterfly graph for roots of smaller order -- is the reference's own step):
+//   * trace / round-constant interpolation over q^i, i < n (fast_interpolate_domain,
+//     ntt_arithmetics.rs:172-237; the unique interpolant of degree < n, length n): values on the
+//     whole group <q> by the barycentric formula with closed-form weights, the sum over the domain
+//     as one cyclic convolution, then one INTT;
+//   * the transition zerofier prod_{i<n} (x - q^i) (fast_zerofier, ntt_arithmetics.rs:66-113; no
+//     wrap-around below the domain order) by doubling: Z_2k(x) = Z_k(x) q^(k^2) Z_k(q^-k x);
+//   * evaluate_symbolic of the Rescue-Prime AIR (m_polynomial.rs:124-139 over rescue_prime.rs:
+//     246-283): its values on a coset of size L > its length from the factored form, then one
+//     INTT (the coefficient vector is exact: degree < length <= L);
+//   * fast_coset_divide / fast_multiply / fast_coset_evaluate literally (ntt_arithmetics.rs:5-64,
+//     161-170, 239-310), incl. a NTT of a vector longer than the root's order (the reference's
+//     ntt pads to the next power of two and runs its butterfly graph with the smaller-order root).
+using Vec = std::vector<u128>;
+
+u128 generator_fe() {  // field.rs:41-44: 85408008396924667383611388730472331217
+  static const u128 g = [] {
+    const char* s = "85408008396924667383611388730472331217";
+    u128 v = 0;
+    for (const char* c = s; *c; ++c) v = v * 10 + (u128)(*c - '0');
+    return v;
+  }();
+  return g;
+}
+
+// field.rs:58-71: square the generator (order 2^119) down to order n
+u128 root_of_order(uint64_t n) {
+  FC_REQUIRE(n && !(n & (n - 1)) && log2_exact(n) <= 119, -1, "root order must be a power of two <= 2^119");
+  u128 r = generator_fe();
+  for (int k = 119; k > log2_exact(n); --k) r = fmul(r, r);
+  return r;
+}
+
+int64_t pdegree(const Vec& a) {  // polynomial.rs:41-58
+  for (size_t i = a.size(); i-- > 0;)
+    if (a[i]) return (int64_t)i;
+  return -1;
+}
+
+Vec pneg(const Vec& a) {
+  Vec o(a.size());
+  for (size_t i = 0; i < a.size(); ++i) o[i] = a[i] ? P - a[i] : 0;
+  return o;
+}
+
+// polynomial.rs:251-276: a zero operand returns the other one unchanged (its length kept)
+Vec padd(const Vec& a, const Vec& b) {
+  if (pdegree(a) < 0) return b;
+  if (pdegree(b) < 0) return a;
+  Vec o(std::max(a.size(), b.size()), 0);
+  for (size_t i = 0; i < a.size(); ++i) o[i] = a[i];
+  for (size_t i = 0; i < b.size(); ++i) o[i] = fadd(o[i], b[i]);
+  return o;
+}
+
+Vec psub(const Vec& a, const Vec& b) { return padd(a, pneg(b)); }
+
+// polynomial.rs:109-121: c_i f^i
+Vec pscale(const Vec& a, u128 f) {
+  Vec pw(a.size()), o(a.size());
+  powers_m(f, a.size(), pw.data());
+#pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i < (int64_t)a.size(); ++i) o[i] = mont(a[i], pw[i]);
+  return o;
+}
+
+// in place: a[i] *= c (canonical)
+void pmul_const(Vec& a, u128 c) {
+  const u128 cm = to_m(c);
+#pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i < (int64_t)a.size(); ++i) a[i] = mont(a[i], cm);
+}
+
+// ntt.rs:7-49 (literal): zero-pad to next_pow2(len), bit-reverse, radix-2 DIT with powtable
+// root^k, k < n/2 -- the same butterflies for any root, including roots of smaller order
+Vec ref_ntt(u128 root, const Vec& in) {
+  FC_REQUIRE(!in.empty(), -1, "ntt of an empty input");
+  const int logn = log2_exact(in.size());
+  const uint64_t n = (uint64_t)1 << logn;
+  Vec a(n), pw(std::max<uint64_t>(n / 2, 1));
+  powers_m(root, std::max<uint64_t>(n / 2, 1), pw.data());
+#pragma omp parallel for schedule(static)
+  for (int64_t j = 0; j < (int64_t)n; ++j) {
+    const uint64_t i = logn ? (bitrev64((uint64_t)j) >> (64 - logn)) : 0;
+    a[j] = i < in.size() ? in[i] : 0;
+  }
+  dit(a.data(), logn, pw.data());
+  return a;
+}
+
+// ntt.rs:51-68: fewer than 2 elements are returned unchanged
+Vec ref_intt(u128 root, const Vec& in) {
+  if (in.size() < 2) return in;
+  Vec a = ref_ntt(finv(root), in);
+  pmul_const(a, finv((u128)a.size()));
+  return a;
+}
+
+// ntt_arithmetics.rs:161-170: scale by offset^i, pad to root_order (longer: the reference
+// panics on the usize underflow), ntt(generator)
+Vec coset_eval(u128 gen, uint64_t root_order, u128 offset, const Vec& c) {
+  FC_REQUIRE(c.size() <= root_order, -1, "fast_coset_evaluate: polynomial longer than root_order");
+  Vec s = pscale(c, offset);
+  s.resize(root_order, 0);
+  return ref_ntt(gen, s);
+}
+
+// pointwise a[i] / b[i] with Montgomery's batch inversion (chunks over the threads); a zero
+// divisor is the reference's "divide by zero" panic (field_element.rs:82-90)
+Vec batch_div(const Vec& a, const Vec& b) {
+  const uint64_t n = std::min(a.size(), b.size());
+  Vec out(n);
+  bool zero = false;
+#pragma omp parallel reduction(|| : zero)
+  {
+    const int T = omp_get_num_threads(), id = omp_get_thread_num();
+    const uint64_t per = (n + T - 1) / T, i0 = std::min(n, per * id), i1 = std::min(n, i0 + per);
+    if (i0 < i1) {
+      Vec pre(i1 - i0);
+      u128 acc = K().R;
+      for (uint64_t i = i0; i < i1; ++i) {
+        if (!b[i]) zero = true;
+        pre[i - i0] = acc;
+        acc = mont(acc, to_m(b[i] ? b[i] : 1));
+      }
+      u128 iv = to_m(finv(from_m(acc)));  // Montgomery(1 / prod)
+      for (uint64_t i = i1; i-- > i0;) {
+        const u128 bi = to_m(b[i] ? b[i] : 1);
+        const u128 inv_b = mont(iv, pre[i - i0]);  // Montgomery(1 / b_i)
+        iv = mont(iv, bi);
+        out[i] = mont(a[i], inv_b);
+      }
+    }
+  }
+  FC_REQUIRE(!zero, -5, "divide by zero");
+  return out;
+}
+
+Vec hadamard(const Vec& a, const Vec& b) {
+  const uint64_t n = std::min(a.size(), b.size());
+  Vec o(n);
+#pragma omp parallel for schedule(static)
+  for (int64_t i = 0; i < (int64_t)n; ++i) o[i] = fmul(a[i], b[i]);
+  return o;
+}
+
+void check_root(u128 root, uint64_t order) {  // ntt_arithmetics.rs:11-24
+  FC_REQUIRE(fpow(root, order) == 1, -1, "supplied root does not have supplied root_order");
+  FC_REQUIRE(fpow(root, order / 2) != 1, -1, "supplied root is not a primitive of root_order");
+}
+
+// ntt_arithmetics.rs:5-64
+Vec fast_multiply(u128 root, uint64_t root_order, const Vec& lhs, const Vec& rhs) {
+  check_root(root, root_order);
+  const int64_t dl = pdegree(lhs), dr = pdegree(rhs);
+  if (dl < 0 || dr < 0) return {};
+  const uint64_t deg = (uint64_t)(dl + dr), result_len = deg + 1;
+  uint64_t order = root_order;
+  while (deg < order / 2) {
+    root = fmul(root, root);
+    order /= 2;
+  }
+  auto inner = [&](const Vec& p) {
+    Vec q = p;
+    if (q.size() < order) q.resize(order, 0);
+    return ref_ntt(root, q);
+  };
+  Vec c = ref_intt(root, hadamard(inner(lhs), inner(rhs)));
+  if (result_len < c.size()) c.resize(result_len);
+  return c;
+}
+
+// ntt_arithmetics.rs:239-310
+Vec fast_coset_divide(u128 root, uint64_t root_order, u128 offset, const Vec& lhs, const Vec& rhs) {
+  check_root(root, root_order);
+  FC_REQUIRE(pdegree(rhs) >= 0, -1, "cannot divide by zero polynomial");
+  if (pdegree(lhs) < 0) return {};
+  const int64_t dl = pdegree(lhs), dr = pdegree(rhs);
+  FC_REQUIRE(dl >= dr, -1, "cannot divide by polynomial of larger degree");
+  const uint64_t deg = (uint64_t)std::max(dl, dr), result_len = (uint64_t)(dl - dr + 1);
+  uint64_t order = root_order;
+  while (deg < order / 2) {
+    root = fmul(root, root);
+    order /= 2;
+  }
+  auto inner = [&](const Vec& p) {
+    Vec q = pscale(p, offset);
+    if (q.size() < order) q.resize(order, 0);
+    return ref_ntt(root, q);
+  };
+  Vec c = ref_intt(root, batch_div(inner(lhs), inner(rhs)));
+  if (result_len < c.size()) c.resize(result_len);
+  return pscale(c, finv(offset));
+}
+
+// exact product by NTT (both degrees known; no wrap-around: transform length > deg)
+Vec poly_mul_exact(const Vec& a, const Vec& b) {
+  if (a.empty() || b.empty()) return {};
+  const uint64_t len = a.size() + b.size() - 1, n = (uint64_t)1 << log2_exact(len);
+  const u128 w = root_of_order(std::max<uint64_t>(n, 2));
+  Vec x = a, y = b;
+  x.resize(std::max<uint64_t>(n, 2), 0);
+  y.resize(std::max<uint64_t>(n, 2), 0);
+  Vec c = ref_intt(w, hadamard(ref_ntt(w, x), ref_ntt(w, y)));
+  c.resize(len);
+  return c;
+}
+
+// inclusive prefix products in the Montgomery domain (chunks over the threads)
+Vec prefix_prod_m(const Vec& xm) {
+  const uint64_t n = xm.size();
+  Vec out(n);
+  const int T = omp_get_max_threads();
+  Vec tot(T, K().R);
+#pragma omp parallel num_threads(T)
+  {
+    const int nt = omp_get_num_threads(), id = omp_get_thread_num();
+    const uint64_t per = (n + nt - 1) / nt, i0 = std::min(n, per * id), i1 = std::min(n, i0 + per);
+    u128 acc = K().R;
+    for (uint64_t i = i0; i < i1; ++i) {
+      acc = mont(acc, xm[i]);
+      out[i] = acc;
+    }
+    tot[id] = acc;
+#pragma omp barrier
+    u128 base = K().R;
+    for (int t = 0; t < id; ++t) base = mont(base, tot[t]);
+    for (uint64_t i = i0; i < i1; ++i) out[i] = mont(out[i], base);
+  }
+  return out;
+}
+
+// The unique interpolant of degree < n through (q^i, y_i), i < n, q of order D (a power of two),
+// length n: what fast_interpolate_domain (ntt_arithmetics.rs:172-237) returns on this domain.
+//   P(q^m) = y_m (m < n);  P(q^m) = q^(m(n-1)) C_m / C_(m-n) S(m)  (n <= m < D)
+//   S(m) = sum_i a_i K_(m-i),  a_i = y_i / Z'(q^i),  K_j = 1 / (1 - q^-j),  C_k = prod_{j<=k} (1 - q^-j)
+//   Z'(q^i) = (-1)^(n-1-i) q^(E_i) C_i C_(n-1-i),  E_i = i(n-1) + (n-1-i)(n-i)/2
+// then INTT over <q>; S is one cyclic convolution of length D.
+Vec geo_interpolate(u128 q, uint64_t D, const Vec& y) {
+  const uint64_t n = y.size();
+  FC_REQUIRE(n <= D, -1, "more points than the domain order");
+  if (n == 0) return {};
+  if (n == 1) return {y[0]};
+  if (n == D) return ref_intt(q, y);
+  const u128 qinv = finv(q);
+  // u_j = 1 - q^-j (j >= 1; u_0 := 1), K_j = 1 / u_j (K_0 := 0 for the convolution)
+  Vec qp(D), um(D);
+  powers_m(qinv, D, qp.data());
+  const u128 one_m = K().R;
+#pragma omp parallel for schedule(static)
+  for (int64_t j = 0; j < (int64_t)D; ++j) um[j] = j ? fsub(one_m, qp[j]) : one_m;  // Montgomery(u_j)
+  Vec u(D);
+#pragma omp parallel for schedule(static)
+  for (int64_t j = 0; j < (int64_t)D; ++j) u[j] = from_m(um[j]);
+  Vec ones(D, 1);
+  Vec Kc = batch_div(ones, u);  // canonical 1 / u_j
+  Vec Km(D);
+#pragma omp parallel for schedule(static)
+  for (int64_t j = 0; j < (int64_t)D; ++j) Km[j] = to_m(Kc[j]);
+  const Vec Cm = prefix_prod_m(um), Cim = prefix_prod_m(Km);  // Montgomery C_k, 1 / C_k (index 0 = 1)
+  // a_i = y_i (-1)^(n-1-i) q^(-E_i) / (C_i C_(n-1-i)); E_(i+1) = E_i + i, E_0 = n(n-1)/2
+  Vec a(D, 0);
+  const u128 qim = to_m(qinv);
+#pragma omp parallel
+  {
+    const int T = omp_get_num_threads(), id = omp_get_thread_num();
+    const uint64_t per = (n + T - 1) / T, i0 = std::min(n, per * id), i1 = std::min(n, i0 + per);
+    if (i0 < i1) {
+      const u128 E0 = ((u128)i0 * (n - 1) + (u128)(n - 1 - i0) * (n - i0) / 2) % D;
+      u128 qe = pow_m(qim, E0), qi = pow_m(qim, i0);  // q^-E_i, q^-i
+      for (uint64_t i = i0; i < i1; ++i) {
+        u128 v = mont(mont(mont(to_m(y[i]), qe), Cim[i]), Cim[n - 1 - i]);
+        v = from_m(v);
+        a[i] = ((n - 1 - i) & 1) && v ? P - v : v;
+        qe = mont(qe, qi);
+        qi = mont(qi, qim);
+      }
+    }
+  }
+  Kc[0] = 0;
+  const Vec S = ref_intt(q, hadamard(ref_ntt(q, a), ref_ntt(q, Kc)));
+  Vec vals(D);
+  const u128 qm = to_m(q);
+#pragma omp parallel
+  {
+    const int T = omp_get_num_threads(), id = omp_get_thread_num();
+    const uint64_t per = (D + T - 1) / T, m0 = std::min(D, per * id), m1 = std::min(D, m0 + per);
+    if (m0 < m1) {
+      u128 qe = pow_m(qm, ((u128)m0 * (n - 1)) % D);
+      const u128 step = pow_m(qm, n - 1);
+      for (uint64_t m = m0; m < m1; ++m) {
+        if (m < n) {
+          vals[m] = y[m];
+        } else {
+          vals[m] = from_m(mont(mont(mont(to_m(S[m]), qe), Cm[m]), Cim[m - n]));
+        }
+        qe = mont(qe, step);
+      }
+    }
+  }
+  Vec c = ref_intt(q, vals);
+  c.resize(n);
+  return c;
+}
+
+// prod_{i < nz} (x - q^i), length nz + 1 (fast_zerofier, ntt_arithmetics.rs:66-113, below the
+// domain order): doubling Z_2k(x) = Z_k(x) q^(k^2) Z_k(q^-k x), Z_(k+1) = Z_k(x) (x - q^k)
+Vec geo_zerofier(u128 q, uint64_t nz) {
+  if (nz == 0) return {};
+  Vec Z = {1};
+  uint64_t k = 0;
+  for (int bit = 63 - __builtin_clzll(nz); bit >= 0; --bit) {
+    if (k) {
+      Vec R = pscale(Z, fpow(finv(q), k));
+      pmul_const(R, fpow(q, (u128)k * k));
+      Z = poly_mul_exact(Z, R);
+      k *= 2;
+    }
+    if ((nz >> bit) & 1) {  // Z * (x - q^k)
+      const u128 qk = fpow(q, k), qkm = to_m(qk);
+      Vec N(Z.size() + 1, 0);
+      for (size_t j = 0; j <= Z.size(); ++j) {
+        const u128 lo = j ? Z[j - 1] : 0, hi = j < Z.size() ? mont(Z[j], qkm) : 0;
+        N[j] = fsub(lo, hi);
+      }
+      Z.swap(N);
+      ++k;
+    }
+  }
+  return Z;
+}
+
+// small domains (boundary constraints): fast_zerofier / fast_interpolate_domain restated directly
+Vec small_zerofier(const Vec& dom) {
+  if (dom.empty()) return {};
+  Vec Z = {1};
+  for (u128 d : dom) {
+    Vec N(Z.size() + 1, 0);
+    for (size_t j = 0; j <= Z.size(); ++j) N[j] = fsub(j ? Z[j - 1] : 0, j < Z.size() ? fmul(Z[j], d) : 0);
+    Z.swap(N);
+  }
+  return Z;
+}
+
+Vec small_interpolate(const Vec& dom, const Vec& val) {  // Lagrange; length n (n >= 1)
+  const size_t n = dom.size();
+  if (n == 0) return {};
+  if (n == 1) return {val[0]};
+  Vec out(n, 0);
+  for (size_t i = 0; i < n; ++i) {
+    Vec others;
+    u128 den = 1;
+    for (size_t j = 0; j < n; ++j)
+      if (j != i) {
+        others.push_back(dom[j]);
+        FC_REQUIRE(dom[i] != dom[j], -5, "divide by zero");
+        den = fmul(den, fsub(dom[i], dom[j]));
+      }
+    Vec L = small_zerofier(others);
+    const u128 s = fmul(val[i], finv(den));
+    for (size_t j = 0; j < L.size(); ++j) out[j] = fadd(out[j], fmul(L[j], s));
+  }
+  return out;
+}
+
+// Rescue-Prime transition polynomials (rescue_prime.rs:246-283) as evaluate_symbolic returns them
+// for the point [x, P_s(x), P_s(omicron x)] (stark.rs:388-400): values on the coset g <w_L> of
+//   sum_k MDS[i][k] P_k^alpha + first_i - (sum_k MDSinv[i][k] (P_k(omicron x) - second_k))^alpha
+// and one INTT.  The vector length is 1 + alpha (T - 1): the longest monomials are prev_k^alpha
+// and next_k^alpha over trace polynomials of length T (the round-constant terms have x-degree
+// <= alpha (N - 1) < alpha (T - 1)).
+std::vector<Vec> rescue_tpolys(const std::vector<Vec>& tp, const std::vector<Vec>& first, const std::vector<Vec>& second,
+                               const Vec& mds, const Vec& mds_inv, uint64_t alpha, u128 omicron, u128 g,
+                               uint64_t sym_len) {
+  const size_t m = tp.size();
+  const uint64_t L = (uint64_t)1 << log2_exact(sym_len);
+  const u128 wL = root_of_order(std::max<uint64_t>(L, 2));
+  std::vector<Vec> P(m), Nx(m), F(m), S(m);
+  for (size_t k = 0; k < m; ++k) {
+    P[k] = coset_eval(wL, L, g, tp[k]);
+    Nx[k] = coset_eval(wL, L, fmul(g, omicron), tp[k]);
+    F[k] = coset_eval(wL, L, g, first[k]);
+    S[k] = coset_eval(wL, L, g, second[k]);
+  }
+  std::vector<Vec> out(m);
+  const u128 ginv = finv(g);
+  for (size_t i = 0; i < m; ++i) {
+    Vec vals(L);
+#pragma omp parallel for schedule(static)
+    for (int64_t j = 0; j < (int64_t)L; ++j) {
+      u128 lhs = F[i][j], acc = 0;
+      for (size_t k = 0; k < m; ++k) {
+        lhs = fadd(lhs, fmul(mds[i * m + k], fpow(P[k][j], alpha)));
+        acc = fadd(acc, fmul(mds_inv[i * m + k], fsub(Nx[k][j], S[k][j])));
+      }
+      vals[j] = fsub(lhs, fpow(acc, alpha));
+    }
+    Vec c = pscale(ref_intt(wL, vals), ginv);
+    for (uint64_t j = sym_len; j < c.size(); ++j)
+      FC_REQUIRE(c[j] == 0, -6, "transition polynomial longer than its symbolic length");
+    c.resize(sym_len);
+    out[i] = std::move(c);
+  }
+  return out;
+}
+
+struct StarkArgs {
+  uint64_t m, T_orig, num_randomizers, D, Nf, expansion, colinearity;
+  u128 omicron, omega, g;
+  uint64_t alpha;
+  const Vec* mds;
+  const Vec* mds_inv;
+  const Vec* rc;   // 2 m N round constants
+  uint64_t N;      // Rescue rounds
+  const std::vector<uint64_t>* tqdb;  // transition quotient degree bounds (stark.rs:162-176)
+  uint64_t tcd;                       // max_degree (stark.rs:178-196)
+};
+
+std::vector<uint8_t> stark_prove(const StarkArgs& A, const Vec& trace, uint64_t rows, const Vec& trace_rand,
+                                 const Vec& rcoef, const std::vector<uint64_t>& bcyc, const std::vector<uint64_t>& breg,
+                                 const Vec& bval, double* phase_s) {
+  auto clk = [] { return omp_get_wtime(); };
+  double t0 = clk();
+  int ph = 0;
+  auto mark = [&] {
+    if (phase_s) phase_s[ph++] = clk() - t0;
+  };
+  const uint64_t m = A.m, D = A.D, Nf = A.Nf;
+  const uint64_t T = rows + A.num_randomizers;  // stark.rs:285-301
+  FC_REQUIRE(T <= D, -1, "randomized trace longer than the omicron domain");
+  FC_REQUIRE(rcoef.size() == A.tcd + 1, -1, "randomizer polynomial must have max_degree + 1 coefficients");
+  Stream ps;
+  // trace polynomials (stark.rs:303-324)
+  std::vector<Vec> tp(m);
+  for (uint64_t s = 0; s < m; ++s) {
+    Vec col(T);
+    for (uint64_t r = 0; r < rows; ++r) col[r] = trace[r * m + s];
+    for (uint64_t r = 0; r < A.num_randomizers; ++r) col[rows + r] = trace_rand[r * m + s];
+    tp[s] = geo_interpolate(A.omicron, D, col);
+  }
+  mark();
+  // boundary quotients (stark.rs:326-362)
+  std::vector<Vec> bqs(m), bzs(m);
+  for (uint64_t s = 0; s < m; ++s) {
+    Vec dom, val;
+    for (size_t b = 0; b < bcyc.size(); ++b)
+      if (breg[b] == s) {
+        dom.push_back(fpow(A.omicron, bcyc[b]));
+        val.push_back(bval[b]);
+      }
+    bzs[s] = small_zerofier(dom);
+    bqs[s] = fast_coset_divide(A.omicron, D, A.g, psub(tp[s], small_interpolate(dom, val)), bzs[s]);
+  }
+  mark();
+  // boundary-quotient codewords + commitments (stark.rs:364-386)
+  std::vector<Vec> bq_cw(m);
+  std::vector<Tree> bq_tree(m);
+  for (uint64_t s = 0; s < m; ++s) {
+    bq_cw[s] = coset_eval(A.omega, Nf, A.g, bqs[s]);
+    build_tree(bq_cw[s].data(), Nf, bq_tree[s]);
+    ps.push(0, reinterpret_cast<const uint8_t*>(bq_tree[s].root()), 64, false);
+  }
+  mark();
+  // transition quotients (stark.rs:388-422)
+  std::vector<Vec> first(m), second(m);
+  for (uint64_t i = 0; i < m; ++i) {
+    Vec c1(A.N), c2(A.N);
+    for (uint64_t r = 0; r < A.N; ++r) {
+      c1[r] = (*A.rc)[2 * r * m + i];
+      c2[r] = (*A.rc)[2 * r * m + m + i];
+    }
+    first[i] = geo_interpolate(A.omicron, D, c1);
+    second[i] = geo_interpolate(A.omicron, D, c2);
+  }
+  for (uint64_t s = 0; s < m; ++s) FC_REQUIRE(tp[s].size() == T, -1, "trace polynomial length");
+  const uint64_t sym_len = 1 + A.alpha * (T - 1);
+  std::vector<Vec> tpolys = rescue_tpolys(tp, first, second, *A.mds, *A.mds_inv, A.alpha, A.omicron, A.g, sym_len);
+  FC_REQUIRE(A.T_orig >= 1, -1, "original trace length");
+  const Vec tz = geo_zerofier(A.omicron, A.T_orig - 1);  // stark.rs:198-206
+  std::vector<Vec> tqs(m);
+  for (uint64_t i = 0; i < m; ++i) tqs[i] = fast_coset_divide(A.omicron, D, A.g, tpolys[i], tz);
+  mark();
+  // randomizer polynomial + commitment (stark.rs:424-445)
+  const Vec r_cw = coset_eval(A.omega, Nf, A.g, rcoef);
+  Tree r_tree;
+  build_tree(r_cw.data(), Nf, r_tree);
+  ps.push(0, reinterpret_cast<const uint8_t*>(r_tree.root()), 64, false);
+  mark();
+  // weights (stark.rs:447-450), degree check (:451-465)
+  uint8_t fs[32];
+  ps.fiat_shamir(fs);
+  const size_t nw = 1 + 2 * tqs.size() + 2 * bqs.size();
+  Vec weights(nw);
+  for (size_t i = 0; i < nw; ++i) {
+    std::vector<uint8_t> buf(i, 0);
+    buf.insert(buf.end(), fs, fs + 32);
+    weights[i] = sample_field(buf.data(), buf.size());
+  }
+  for (uint64_t i = 0; i < m; ++i)
+    FC_REQUIRE(pdegree(tqs[i]) >= 0 && (uint64_t)pdegree(tqs[i]) == (*A.tqdb)[i], -7,
+               "transition quotient degrees do not match with expectation");
+  // terms + combination (stark.rs:467-512)
+  std::vector<Vec> terms;
+  terms.push_back(rcoef);
+  auto xpow = [](uint64_t e) {  // polynomial.rs:328-356: [0,1]^e, length e + 1
+    Vec v(e + 1, 0);
+    v[e] = 1;
+    return v;
+  };
+  for (uint64_t i = 0; i < m; ++i) {
+    terms.push_back(tqs[i]);
+    terms.push_back(fast_multiply(A.omicron, D, xpow(A.tcd - (*A.tqdb)[i]), tqs[i]));
+  }
+  for (uint64_t s = 0; s < m; ++s) {
+    const int64_t dz = pdegree(bzs[s]);
+    FC_REQUIRE(dz >= 0, -1, "Couldnt get degree of boundary zerofier");
+    const uint64_t bqdb = T - 1 - (uint64_t)dz;
+    terms.push_back(bqs[s]);
+    terms.push_back(fast_multiply(A.omicron, D, xpow(A.tcd - bqdb), bqs[s]));
+  }
+  Vec comb;
+  bool have = false;
+  for (size_t t = 0; t < terms.size(); ++t) {
+    Vec wt = terms[t];
+    if (!wt.empty()) pmul_const(wt, weights[t]);  // p_mul([w], t): length len(t)
+    comb = have ? padd(comb, wt) : wt;
+    have = true;
+  }
+  const Vec comb_cw = coset_eval(A.omega, Nf, A.g, comb);
+  mark();
+  // FRI (stark.rs:514-522)
+  std::vector<uint64_t> top;
+  fri_prove(ps, A.g, A.omega, Vec(comb_cw), A.expansion, A.colinearity, top);
+  mark();
+  // openings (stark.rs:524-560)
+  std::vector<uint64_t> dup = top;
+  for (uint64_t i : top) dup.push_back((i + A.expansion) % Nf);
+  std::vector<uint64_t> quad = dup;
+  for (uint64_t i : dup) quad.push_back((i + Nf / 2) % Nf);
+  std::sort(quad.begin(), quad.end());
+  auto open = [&](const Vec& cw, const Tree& t) {
+    for (uint64_t i : quad) {
+      uint8_t v[16];
+      put_be128(v, cw[i]);
+      ps.push(4, v, 16, true);
+      std::vector<uint8_t> pl = path_payload(t, i);
+      ps.push(2, pl.data(), pl.size(), false);
+    }
+  };
+  for (uint64_t s = 0; s < m; ++s) open(bq_cw[s], bq_tree[s]);
+  open(r_cw, r_tree);
+  mark();
+  return ps.digest();
+}
+
 }  // namespace
 
 // ======================================================================== C ABI
@@ -463,6 +1141,7 @@ uint64_t sample_index(const uint8_t* d, size_t dlen, uint64_t size) {  // fri.rs
 extern "C" {
 
 int fc_threads(void) { return omp_get_max_threads(); }
+void fc_set_threads(int n) { omp_set_num_threads(n > 0 ? n : 1); }
 
 void fc_mul(const uint64_t* a, const uint64_t* b, uint64_t* out) { st(out, fmul(ld(a), ld(b))); }
 void fc_inv(const uint64_t* a, uint64_t* out) { st(out, finv(ld(a))); }
@@ -533,110 +1212,95 @@ long fc_fri_prove(const uint64_t* offset, const uint64_t* omega, const uint64_t*
                   uint64_t expansion, uint64_t colinearity, const uint8_t* prefix, size_t prefix_len, uint8_t** out,
                   size_t* out_len, uint64_t* top) {
   if (prefix_len < 16 || n == 0 || (n & (n - 1))) return -1;
-  uint64_t rounds = 0;
-  for (uint64_t len = n; len > expansion && len > 4 * colinearity; len /= 2) ++rounds;  // fri.rs:40-50
-  if (rounds < 2) return -1;
   Stream ps;
   ps.body.assign(prefix + 16, prefix + prefix_len);
   for (int b = 0; b < 16; ++b) ps.field = ps.field || prefix[b] != 0;
-  u128 w = ld(omega), o = ld(offset);
-  std::vector<std::vector<u128>> cws(rounds);
-  std::vector<Tree> trees(rounds);
-  cws[0].resize(n);
-  for (uint64_t i = 0; i < n; ++i) cws[0][i] = ld(codeword + 2 * i);
-  const u128 inv2m = to_m(finv(2));
-  // commit (fri.rs:115-172)
-  for (uint64_t r = 0; r < rounds; ++r) {
-    const uint64_t len = cws[r].size();
-    if (fpow(w, len - 1) != finv(w)) return -2;  // fri.rs:133 omega of order len
-    build_tree(cws[r].data(), len, trees[r]);
-    ps.push(0, reinterpret_cast<const uint8_t*>(trees[r].root()), 64, false);
-    if (r == rounds - 1) break;
-    uint8_t ch[32];
-    ps.fiat_shamir(ch);
-    const u128 alpha = sample_field(ch, 32);
-    // c'[i] = 2^-1 ((1 + a/(o w^i)) c[i] + (1 - a/(o w^i)) c[i + h]);  a/(o w^i) = a o^-1 (w^-1)^i
-    const uint64_t half = len / 2;
-    cws[r + 1].resize(half);
-    const u128 am = to_m(fmul(alpha, finv(o))), wim = to_m(finv(w)), Rm = K().R;
-    const u128* c = cws[r].data();
-    u128* nx = cws[r + 1].data();
-#pragma omp parallel
-    {
-      const int T = omp_get_num_threads(), id = omp_get_thread_num();
-      const uint64_t per = (half + T - 1) / T, i0 = std::min(half, per * id), i1 = std::min(half, i0 + per);
-      if (i0 < i1) {
-        u128 abo = mont(am, pow_m(wim, i0));  // Montgomery(a o^-1 w^-i0)
-        for (uint64_t i = i0; i < i1; ++i) {
-          const u128 f = mont(c[i], fadd(Rm, abo)), s = mont(c[half + i], fsub(Rm, abo));
-          nx[i] = mont(fadd(f, s), inv2m);
-          abo = mont(abo, wim);
-        }
-      }
-    }
-    w = fmul(w, w);
-    o = fmul(o, o);
+  std::vector<u128> cw(n);
+  for (uint64_t i = 0; i < n; ++i) cw[i] = ld(codeword + 2 * i);
+  std::vector<uint64_t> tp;
+  uint64_t rounds;
+  try {
+    rounds = fri_prove(ps, ld(offset), ld(omega), std::move(cw), expansion, colinearity, tp);
+  } catch (const CheckError& e) {
+    g_err = e.msg;
+    return e.code;
   }
-  {  // last codeword (fri.rs:166)
-    const std::vector<u128>& last = cws[rounds - 1];
-    std::vector<uint8_t> pl(16 * last.size());
-    for (size_t i = 0; i < last.size(); ++i) put_be128(&pl[16 * i], last[i]);
-    ps.push(1, pl.data(), pl.size(), !last.empty());
-  }
-  // sample_indices (fri.rs:88-113) over len(codewords[1]) reduced by len(codewords[-1])
-  uint8_t seed[32];
-  ps.fiat_shamir(seed);
-  const uint64_t size = cws[1].size(), reduced = cws[rounds - 1].size();
-  if (colinearity > 2 * reduced || colinearity > reduced) return -3;
-  std::vector<uint64_t> idx, red;
-  std::vector<uint8_t> msg(seed, seed + 32);
-  for (uint64_t counter = 0; idx.size() < colinearity; ++counter) {
-    msg.resize(32 + counter, 0);
-    uint8_t d[64];
-    blake2b512(msg.data(), msg.size(), d);
-    const uint64_t index = sample_index(d, 64, size), rr = index % reduced;
-    if (std::find(red.begin(), red.end(), rr) == red.end()) {
-      idx.push_back(index);
-      red.push_back(rr);
-    }
-  }
-  for (uint64_t s = 0; s < colinearity; ++s) top[s] = idx[s];
-  // query (fri.rs:174-208) per round
-  std::vector<uint64_t> cur = idx;
-  auto path = [&](const Tree& t, uint64_t i) {
-    const int lg = log2_exact(t.n);
-    std::vector<uint8_t> pl(72 * lg);
-    for (int k = 0; k < lg; ++k) {
-      uint8_t* q = &pl[72 * k];
-      memset(q, 0, 8);
-      q[7] = 64;
-      memcpy(q + 8, t.level(k) + 8 * ((i >> k) ^ 1), 64);
-    }
-    return pl;
-  };
-  for (uint64_t r = 0; r + 1 < rounds; ++r) {
-    const uint64_t half = cws[r].size() / 2;
-    for (auto& i : cur) i %= half;
-    for (uint64_t s = 0; s < colinearity; ++s) {
-      uint8_t pl[48];
-      put_be128(pl, cws[r][cur[s]]);
-      put_be128(pl + 16, cws[r][cur[s] + half]);
-      put_be128(pl + 32, cws[r + 1][cur[s]]);
-      ps.push(3, pl, 48, true);
-    }
-    for (uint64_t s = 0; s < colinearity; ++s) {
-      std::vector<uint8_t> a = path(trees[r], cur[s]), b = path(trees[r], cur[s] + half), c = path(trees[r + 1], cur[s]);
-      ps.push(2, a.data(), a.size(), false);
-      ps.push(2, b.data(), b.size(), false);
-      ps.push(2, c.data(), c.size(), false);
-    }
-  }
+  for (uint64_t s = 0; s < colinearity; ++s) top[s] = tp[s];
   const std::vector<uint8_t> d = ps.digest();
   *out = static_cast<uint8_t*>(malloc(d.size()));
   if (!*out) return -4;
   memcpy(*out, d.data(), d.size());
   *out_len = d.size();
   return (long)rounds;
+}
+
+const char* fc_last_error(void) { return g_err.c_str(); }
+
+// Stark::prove (stark.rs:276-562) with a Rescue-Prime AIR (rescue_prime.rs:246-283) and explicit
+// randomness (the two thread_rng draws), every argument as the reference's Stark / RescuePrime
+// hold it.  Elements are (lo, hi) u64 pairs; the serialized proof (stark.rs:562) goes to a malloc'd
+// buffer (*out, *out_len; free with fc_free).  phase_s (optional, 8 doubles): cumulative wall
+// seconds at the end of each phase.  Returns 0, or < 0 with fc_last_error().
+long fc_stark_prove_rescue(uint64_t m, uint64_t original_trace_length, uint64_t num_randomizers, uint64_t D,
+                           uint64_t Nf, uint64_t expansion, uint64_t colinearity, const uint64_t* omicron,
+                           const uint64_t* omega, const uint64_t* generator, uint64_t alpha, const uint64_t* mds,
+                           const uint64_t* mds_inv, const uint64_t* round_constants, uint64_t rounds,
+                           const uint64_t* tqdb, uint64_t tcd, const uint64_t* trace, uint64_t trace_rows,
+                           const uint64_t* trace_rand, const uint64_t* rcoef, uint64_t nrc, const uint64_t* bcyc,
+                           const uint64_t* breg, const uint64_t* bval, uint64_t nb, uint8_t** out, size_t* out_len,
+                           double* phase_s) {
+  try {
+    auto vec = [](const uint64_t* p, uint64_t n) {
+      Vec v(n);
+      for (uint64_t i = 0; i < n; ++i) {
+        v[i] = ld(p + 2 * i);
+        FC_REQUIRE(v[i] < P, -1, "non-canonical element");
+      }
+      return v;
+    };
+    const Vec vmds = vec(mds, m * m), vmdsi = vec(mds_inv, m * m), vrc = vec(round_constants, 2 * m * rounds);
+    const std::vector<uint64_t> vtq(tqdb, tqdb + m);
+    StarkArgs A{m, original_trace_length, num_randomizers, D, Nf, expansion, colinearity, ld(omicron), ld(omega),
+                ld(generator), alpha, &vmds, &vmdsi, &vrc, rounds, &vtq, tcd};
+    std::vector<uint64_t> bc(bcyc, bcyc + nb), br(breg, breg + nb);
+    const std::vector<uint8_t> d = stark_prove(A, vec(trace, trace_rows * m), trace_rows,
+                                               vec(trace_rand, num_randomizers * m), vec(rcoef, nrc), bc, br,
+                                               vec(bval, nb), phase_s);
+    *out = static_cast<uint8_t*>(malloc(d.size()));
+    if (!*out) return -4;
+    memcpy(*out, d.data(), d.size());
+    *out_len = d.size();
+    return 0;
+  } catch (const CheckError& e) {
+    g_err = e.msg;
+    return e.code;
+  }
+}
+
+// the unique interpolant through (q^i, y_i), i < n, q of order D (checker building block)
+long fc_geo_interpolate(const uint64_t* q, uint64_t D, const uint64_t* y, uint64_t n, uint64_t* out) {
+  try {
+    Vec v(n);
+    for (uint64_t i = 0; i < n; ++i) v[i] = ld(y + 2 * i);
+    const Vec c = geo_interpolate(ld(q), D, v);
+    for (uint64_t i = 0; i < c.size(); ++i) st(out + 2 * i, c[i]);
+    return (long)c.size();
+  } catch (const CheckError& e) {
+    g_err = e.msg;
+    return e.code;
+  }
+}
+
+// prod_{i < n} (x - q^i), n + 1 coefficients (checker building block)
+long fc_geo_zerofier(const uint64_t* q, uint64_t n, uint64_t* out) {
+  try {
+    const Vec c = geo_zerofier(ld(q), n);
+    for (uint64_t i = 0; i < c.size(); ++i) st(out + 2 * i, c[i]);
+    return (long)c.size();
+  } catch (const CheckError& e) {
+    g_err = e.msg;
+    return e.code;
+  }
 }
 
 void fc_free(void* p) { free(p); }

@@ -23,6 +23,7 @@ def lib():
         l = ctypes.CDLL(LIB_PATH)
         vp, sz, u64 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64
         l.fc_threads.restype = ctypes.c_int
+        l.fc_set_threads.argtypes = [ctypes.c_int]
         for f in (l.fc_ntt, l.fc_intt):
             f.argtypes = [vp, vp, u64, vp]
             f.restype = ctypes.c_int
@@ -46,12 +47,26 @@ def lib():
         l.fc_bary_create.restype = ctypes.c_void_p
         l.fc_bary_eval.argtypes = [vp, vp, vp]
         l.fc_bary_free.argtypes = [vp]
+        l.fc_last_error.restype = ctypes.c_char_p
+        l.fc_stark_prove_rescue.argtypes = [u64] * 7 + [vp, vp, vp, u64, vp, vp, vp, u64, vp, u64, vp, u64, vp, vp,
+                                                        u64, vp, vp, vp, u64, ctypes.POINTER(ctypes.c_void_p),
+                                                        ctypes.POINTER(ctypes.c_size_t), vp]
+        l.fc_stark_prove_rescue.restype = ctypes.c_long
+        l.fc_geo_interpolate.argtypes = [vp, u64, vp, u64, vp]
+        l.fc_geo_interpolate.restype = ctypes.c_long
+        l.fc_geo_zerofier.argtypes = [vp, u64, vp]
+        l.fc_geo_zerofier.restype = ctypes.c_long
         _lib = l
     return _lib
 
 
 def threads() -> int:
     return lib().fc_threads()
+
+
+def set_threads(n: int) -> None:
+    """OpenMP threads of every later call (omp_set_num_threads)."""
+    lib().fc_set_threads(n)
 
 
 def _fe(v: int) -> np.ndarray:
@@ -230,6 +245,83 @@ def _obj_to_arr(v) -> np.ndarray:
     lo = np.array([int(x) & ((1 << 64) - 1) for x in v], dtype=np.uint64)
     hi = np.array([int(x) >> 64 for x in v], dtype=np.uint64)
     return np.ascontiguousarray(np.stack([lo, hi], axis=1))
+
+
+def geo_interpolate(q: int, D: int, values):
+    """Unique interpolant (degree < n, length n) through (q^i, v_i), i < n, q of order D."""
+    y = arr(values)
+    out = np.zeros((max(len(y), 1), 2), dtype=np.uint64)
+    r = lib().fc_geo_interpolate(_p(_fe(q)), D, _p(y), len(y), _p(out))
+    if r < 0:
+        raise ValueError(lib().fc_last_error().decode())
+    return out[:r]
+
+
+def geo_zerofier(q: int, n: int):
+    """prod_{i<n} (x - q^i), n + 1 coefficients."""
+    out = np.zeros((n + 1, 2), dtype=np.uint64)
+    r = lib().fc_geo_zerofier(_p(_fe(q)), n, _p(out))
+    if r < 0:
+        raise ValueError(lib().fc_last_error().decode())
+    return out[:r]
+
+
+def rescue_degree_bounds(rp, st):
+    """(transition quotient degree bounds, max_degree) of RescuePrime.transition_constraints for the
+    Stark `st` (stark.rs:117-196 over the AIR's key set; RescueAirAtPoint carries keys whose maximum
+    equals the expanded AIR's)."""
+    import stark_prove_oracle as e
+    sair = [e.RescueAirAtPoint(rp, i, None) for i in range(rp.m)]
+    return st.transition_quotient_degree_bounds(sair), st.max_degree(sair)
+
+
+PHASES = ("trace_interpolation", "boundary_quotients", "bq_codewords_commit", "transition_quotients",
+          "randomizer_commit", "combination_lde", "fri_prove", "openings")
+
+
+def stark_prove_rescue(rp, st, trace, boundary, trace_randomizers, randomizer_coefficients, bounds=None,
+                       phases=None) -> bytes:
+    """Stark::prove (stark.rs:276-562) of a Rescue-Prime trace on the CPU (Montgomery + OpenMP):
+    the serialized proof stream (IndependentProofStream, stark.rs:562).  `rp` / `st` are the
+    oracle's RescuePrime / Stark (or any objects with the same attributes); `trace` rows x m
+    (list of lists or an (rows * m, 2) array); the two thread_rng draws are explicit like the
+    oracle's prove.  Raises ValueError with the reference's message where it returns Err/panics."""
+    m = rp.m
+    t = arr(trace if isinstance(trace, np.ndarray) else [v for row in trace for v in row])
+    rows = len(t) // m
+    tr = arr(trace_randomizers if isinstance(trace_randomizers, np.ndarray)
+             else [v for row in trace_randomizers for v in row])
+    rc = arr(randomizer_coefficients)
+    tqdb, tcd = bounds if bounds is not None else rescue_degree_bounds(rp, st)
+    mds = arr([v for row in rp.MDS for v in row])
+    mdsi = arr([v for row in rp.MDS_inv for v in row])
+    rcs = _obj_to_arr(np.array(rp.round_constants, dtype=object)) if len(rp.round_constants) \
+        else np.zeros((1, 2), dtype=np.uint64)
+    tq = np.array(tqdb, dtype=np.uint64)
+    bc = np.array([c for (c, _, _) in boundary] or [0], dtype=np.uint64)
+    br = np.array([r for (_, r, _) in boundary] or [0], dtype=np.uint64)
+    bv = arr([v for (_, _, v) in boundary] or [0])
+    out = ctypes.c_void_p()
+    out_len = ctypes.c_size_t()
+    ph = np.zeros(8, dtype=np.float64)
+    r = lib().fc_stark_prove_rescue(m, st.original_trace_length, st.num_randomizers, st.omicron_domain_length,
+                                    st.fri.domain_length, st.expansion_factor, st.fri.num_colinearity_tests,
+                                    _p(_fe(st.omicron)), _p(_fe(st.omega)), _p(_fe(st.generator)), rp.alpha,
+                                    _p(mds), _p(mdsi), _p(rcs), rp.N, _p(tq), tcd, _p(t), rows, _p(tr), _p(rc),
+                                    len(rc), _p(bc), _p(br), _p(bv), len(boundary), ctypes.byref(out),
+                                    ctypes.byref(out_len), _p(ph))
+    if r < 0:
+        raise ValueError(lib().fc_last_error().decode())
+    try:
+        data = ctypes.string_at(out.value, out_len.value)
+    finally:
+        lib().fc_free(out)
+    if phases is not None:
+        prev = 0.0
+        for name, v in zip(PHASES, ph):
+            phases[name] = float(v) - prev
+            prev = float(v)
+    return data
 
 
 def verifier_stark(*args, **kwargs):

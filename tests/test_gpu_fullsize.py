@@ -7,9 +7,11 @@ tests/test_oracle_fast.py) and against the oracle's own verifiers:
   degree < 2^21 polynomial: LDE elements, round-0 root and the complete proof-stream bytes equal
   the checker's, the oracle's FRI.verify (fri.rs:250-416) accepts, a tampered codeword is
   rejected (fri.rs:514-528);
-* the bench workload: Stark::prove on a Rescue-Prime trace of 2^20 - 1 randomized rows (FRI
-  domain 2^25) verified by the oracle's Stark.verify (stark.rs:565-770) with the AIR evaluated
-  from its structure, and a false claim rejected;
+* C4 and the bench workload: Stark::prove on Rescue-Prime traces of 2^16 - 1 and 2^20 - 1 randomized
+  rows (FRI domains 2^21 and 2^25): the GPU's proof bytes equal the CPU checker's Stark::prove
+  (fast_cpu.stark_prove_rescue, itself byte-equal to the oracle's prove at the small parameter sets,
+  tests/test_oracle_fast.py), the oracle's Stark.verify (stark.rs:565-770, AIR evaluated from its
+  structure) accepts the proof and rejects a false claim;
 * C5: the 2^27-point NTT sharded over 2 and 8 ranks (one process per rank on this box's one GPU,
   gloo host-staged exchange) bit-identical to the single-GPU transform and to the checker.
 """
@@ -126,35 +128,64 @@ def test_c3_fri_prove_2p24_exp8_c64(fc):
     assert not ok
 
 
-# ------------------------------------------------------------------ headline prove
+# ------------------------------------------------------------------ C4 + headline prove
 
-def test_trace_2p20_headline_proof_verified(fc):
-    """bench.py's workload: Rescue-Prime m=2, N = 2^20 - 258 rounds (+256 randomizer rows =
-    2^20 - 1), expansion 8, c = 64, security 128, transition degree 3: omicron domain 2^22, FRI
-    domain 2^25.  Verified by the oracle verifier (AIR from its structure, C++ barycentric
-    round-constant interpolants and zerofier products)."""
-    N = (1 << 20) - 2 - 256
+def _prove_gpu_and_checker(fc, log_rows, tag):
+    """Stark::prove (stark.rs:276-562) of a Rescue-Prime trace with 2^log_rows - 1 randomized rows,
+    expansion 8, c = 64, security 128, transition degree 3, on the GPU and on the CPU checker with
+    the same inputs.  Returns (GPU proof stream, checker bytes, oracle RescuePrime, output, gpu Stark)."""
+    N = (1 << log_rows) - 2 - 256
     rp_g = sg.RescuePrime(2, 1, 128, N)
     st_g = sg.Stark(8, 64, 128, 2, N + 1, 3)
-    assert st_g.omicron_domain_length == 1 << 22 and st_g.fri_domain_length == 1 << 25
+    assert st_g.fri_domain_length == 1 << (log_rows + 5)
     air_g = rp_g.transition_constraints(st_g.omicron, st_g.omicron_domain_length)
     rp_o = e.RescuePrime(2, 1, 128, N)
     assert rp_g.round_constants == rp_o.round_constants
-    inp = o.sample(b"headline")
+    st_o = e.Stark(8, 64, 128, 2, N + 1, 3)
+    bounds = fc.rescue_degree_bounds(rp_o, st_o)
+    assert st_g.transition_degree_bounds(air_g) == \
+        [b + (N + 1 - 1) for b in bounds[0]] and st_g.max_degree(air_g) == bounds[1]
+    inp = o.sample(tag)
     trace = rp_g.trace_array(inp)
     out = sg.to_ints(trace[-2:-1])[0]  # last row, register 0: the hash output
-    nrc = st_g.num_randomizer_coefficients(air_g)
-    tr = synthetic(0, b"trace-rand", 2 * st_g.num_randomizers)
-    rc = synthetic(0, b"rand-poly", nrc)
+    nrc = bounds[1] + 1
+    tr = synthetic(0, tag + b"trace-rand", 2 * st_g.num_randomizers)
+    rc = synthetic(0, tag + b"rand-poly", nrc)
     bnd = rp_o.boundary_constraints(out)
     ps = sg.IndependentProofStream()
     t0 = time.perf_counter()
     st_g.prove(trace, air_g, bnd, ps, tr, rc)
-    print("trace 2^20 prove (host buffers): %.1f ms, %d bytes" % ((time.perf_counter() - t0) * 1e3, len(ps.digest())))
+    t1 = time.perf_counter()
+    phases = {}
+    want = fc.stark_prove_rescue(rp_o, st_o, trace, bnd, tr, rc, bounds=bounds, phases=phases)
+    t2 = time.perf_counter()
+    print("trace 2^%d: GPU prove (host buffers) %.1f ms, CPU checker %.1f s (%d threads; %s), %d bytes"
+          % (log_rows, (t1 - t0) * 1e3, t2 - t1, fc.threads(),
+             ", ".join("%s %.2f" % kv for kv in phases.items()), len(want)))
+    return ps, want, rp_o, out, N
+
+
+@pytest.mark.timeout(900)
+def test_c4_proof_bytes_equal_checker(fc):
+    """BASELINE config C4 (trace 2^16, FRI domain 2^21): the GPU's proof bytes == the checker's."""
+    ps, want, rp_o, out, N = _prove_gpu_and_checker(fc, 16, b"c4-bytes")
+    assert ps.digest() == want, "C4 proof bytes differ from the CPU checker's Stark::prove"
+
+
+@pytest.mark.timeout(1800)
+def test_trace_2p20_headline_proof_bytes_and_verified(fc):
+    """bench.py's workload: Rescue-Prime m=2, N = 2^20 - 258 rounds (+256 randomizer rows =
+    2^20 - 1), expansion 8, c = 64, security 128, transition degree 3: omicron domain 2^22, FRI
+    domain 2^25.  Proof bytes == the CPU checker's; the oracle verifier (AIR from its structure,
+    C++ barycentric round-constant interpolants and zerofier products) accepts it and rejects a
+    false claim."""
+    ps, want, rp_o, out, N = _prove_gpu_and_checker(fc, 20, b"headline")
+    assert ps.digest() == want, "headline proof bytes differ from the CPU checker's Stark::prove"
+    del want
     objs = ps.objects()
     vst = fc.verifier_stark(8, 64, 128, 2, N + 1, 3)
     sair = fc.rescue_air_at_point(rp_o, vst.omicron)
-    assert st_g.transition_degree_bounds(air_g) == vst.transition_degree_bounds(sair)
+    bnd = rp_o.boundary_constraints(out)
     ok, err = vst.verify(sair, bnd, o.IndependentProofStream(objs))
     assert ok, err
     ok, _ = vst.verify(sair, rp_o.boundary_constraints(o.add_mod(out, 1)), o.IndependentProofStream(objs))

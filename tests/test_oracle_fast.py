@@ -153,3 +153,56 @@ def test_fast_cpu_arbitrary_domain_checkers_vs_oracle(fc):
         assert fc.ints(fc.poly_from_roots(dom)) == e.fast_zerofier(w, 256, dom)
         ip = e.fast_interpolate_domain(w, 256, dom, vals)
         assert fc.ints(fc.eval_points(ip, dom)) == vals
+
+
+# --------------------------------------------------------- Stark::prove (the end-to-end checker)
+
+def _rescue_case(N, exp, c, sec, tcd, seed, m=2):
+    rp = e.RescuePrime(m, 1, sec, N)
+    st = e.Stark(exp, c, sec, m, N + 1, tcd)
+    air = rp.transition_constraints(st.omicron, st.omicron_domain_length)
+    inp = o.sample(seed)
+    nrc = st.num_randomizer_coefficients(air)
+    r = e.randomness_from_seed(seed, m * st.num_randomizers + nrc)
+    tr = [r[m * i:m * i + m] for i in range(st.num_randomizers)]
+    return rp, st, air, rp.trace(inp), rp.boundary_constraints(rp.hash(inp)), tr, r[m * st.num_randomizers:]
+
+
+def test_fast_geometric_interpolation_and_zerofier_vs_oracle(fc):
+    """The checker's building blocks against fast_interpolate_domain / fast_zerofier
+    (ntt_arithmetics.rs:66-113, 172-237) on prefixes of <q>: the same coefficient vectors."""
+    D = 128
+    q = o.primitive_nth_root(D)
+    for n in (1, 2, 3, 17, 64, 100, 127, 128):
+        vals = o.synthetic_elements(n, b"geo", n)
+        dom = [o.fpow(q, i) for i in range(n)]
+        assert fc.ints(fc.geo_interpolate(q, D, vals)) == e.fast_interpolate_domain(q, D, dom, vals), n
+        if n < D:
+            assert fc.ints(fc.geo_zerofier(q, n)) == e.fast_zerofier(q, D, dom), n
+
+
+@pytest.mark.parametrize("N,exp,c,sec,tcd", [(27, 4, 2, 2, 2), (27, 8, 4, 8, 3), (40, 4, 3, 4, 2), (9, 16, 2, 4, 4)])
+def test_fast_stark_prove_equals_oracle(fc, N, exp, c, sec, tcd):
+    """stark.rs:276-562: the CPU checker's proof bytes equal the oracle's (the GPU tests' parameter
+    sets; (40, 4, 3, 4, 2) has max_degree >= the omicron order, where the reference's products wrap),
+    and its degree bounds (from the AIR's key structure) equal the expanded AIR's."""
+    rp, st, air, trace, bnd, tr, rc = _rescue_case(N, exp, c, sec, tcd, b"case-%d" % N)
+    want = st.prove(trace, air, bnd, o.IndependentProofStream(), tr, rc)
+    bounds = fc.rescue_degree_bounds(rp, st)
+    assert bounds == (st.transition_quotient_degree_bounds(air), st.max_degree(air))
+    assert fc.stark_prove_rescue(rp, st, trace, bnd, tr, rc) == want
+
+
+def test_fast_stark_prove_false_witness_and_errors(fc):
+    """stark.rs:845-880 false witnesses (inexact transition division: the reference's truncated
+    quotient) give the oracle's bytes; the reference's Err / panics map to ValueError."""
+    for (N, exp, c, sec, tcd, seed, row, reg, delta) in (
+            (27, 4, 2, 2, 2, b"bad", 22, 1, 17274817952119230544216945715808633996),
+            (40, 4, 3, 4, 2, b"factored-air", 17, 0, 5)):
+        rp, st, air, trace, bnd, tr, rc = _rescue_case(N, exp, c, sec, tcd, seed)
+        bad = [list(r) for r in trace]
+        bad[row][reg] = o.add_mod(bad[row][reg], delta)
+        assert fc.stark_prove_rescue(rp, st, bad, bnd, tr, rc) == \
+            st.prove(bad, air, bnd, o.IndependentProofStream(), tr, rc)
+    with pytest.raises(ValueError, match="max_degree"):
+        fc.stark_prove_rescue(rp, st, trace, bnd, tr, rc[:-1])
