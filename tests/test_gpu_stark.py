@@ -188,6 +188,20 @@ def test_stark_prove_c4_factored_air_equals_expanded(monkeypatch):
     assert st_g.prove(trace, air_g, bnd, sg.IndependentProofStream(), tr, rc) == factored
 
 
+def test_stark_prove_negated_constraints():
+    """A negated native Rescue-Prime constraint (-tc, and the empty MPolynomial minus tc: the
+    reference's Add returns the other operand) is evaluated as -tc, not through the factored form of
+    +tc; -(-tc) gives tc's proof (m_polynomial.rs:183-229)."""
+    rp, st_o, st_g, air_o, air_g, trace, bnd, tr, rc, out = _case(27, 4, 2, 2, 2, b"neg")
+    neg_o = [-a for a in air_o]
+    want_neg = st_o.prove(trace, neg_o, bnd, o.IndependentProofStream(), tr, rc)
+    want = st_o.prove(trace, air_o, bnd, o.IndependentProofStream(), tr, rc)
+    zero = sg.MPolynomial.new({})
+    assert st_g.prove(trace, [-a for a in air_g], bnd, sg.IndependentProofStream(), tr, rc) == want_neg
+    assert st_g.prove(trace, [zero - a for a in air_g], bnd, sg.IndependentProofStream(), tr, rc) == want_neg
+    assert st_g.prove(trace, [-(-a) for a in air_g], bnd, sg.IndependentProofStream(), tr, rc) == want
+
+
 def test_stark_false_witness_and_claim():
     """stark.rs:845-880: a false witness gives the reference's (rejected) proof bytes; a false
     claim is rejected by the verifier."""

@@ -97,6 +97,7 @@ MPoly mp_lift(const HPoly& poly, uint32_t vi) {
 MPoly mp_neg(const MPoly& a) {
   MPoly r = a;
   r.dev.reset();
+  r.rescue.reset();  // the factored form describes +a: the negation is evaluated from its groups
   for (auto& kv : r.g)
     for (auto& c : kv.second) c = fe_neg(c);
   return r;

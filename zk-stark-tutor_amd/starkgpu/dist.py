@@ -475,10 +475,18 @@ class NativeDist:
     def _alloc(self, count: int) -> torch.Tensor:
         return torch.empty(2 * count, dtype=torch.int64, device=self.device)
 
+    def _torch_ready(self) -> None:
+        """The library works on its own stream: drain torch's current stream first, so an input
+        still being written by queued torch work is complete and an output block torch.empty
+        handed out is no longer used by pending torch work (the library call itself returns
+        after its stream is drained)."""
+        torch.cuda.current_stream(self.device).synchronize()
+
     def ntt(self, root: int, cols: torch.Tensor, row_len: int, n: int) -> torch.Tensor:
         """fft/ntt.rs:7-49: column shard -> run shard."""
         n1, n2 = self.plan(n, self.G)
         out = self._alloc(n1 * (n2 // self.G))
+        self._torch_ready()
         self.ctx.check(self._lib.sg_dist_ntt(self.handle, api._fe(root), ctypes.c_void_p(cols.data_ptr()), row_len,
                                              n, ctypes.c_void_p(out.data_ptr())))
         return out
@@ -487,6 +495,7 @@ class NativeDist:
         """fft/ntt.rs:51-68: run shard -> column shard (rows of N2)."""
         n1, n2 = self.plan(n, self.G)
         out = self._alloc((n1 // self.G) * n2)
+        self._torch_ready()
         self.ctx.check(self._lib.sg_dist_intt(self.handle, api._fe(root), ctypes.c_void_p(runs.data_ptr()), n,
                                               ctypes.c_void_p(out.data_ptr())))
         return out
@@ -496,6 +505,7 @@ class NativeDist:
         """fft/ntt_arithmetics.rs:161-170: coefficient column shard -> codeword run shard."""
         n1, n2 = self.plan(root_order, self.G)
         out = self._alloc(n1 * (n2 // self.G))
+        self._torch_ready()
         self.ctx.check(self._lib.sg_dist_coset_evaluate(self.handle, api._fe(generator), root_order, api._fe(offset),
                                                         ctypes.c_void_p(cols.data_ptr()), row_len,
                                                         ctypes.c_void_p(out.data_ptr())))
@@ -503,6 +513,7 @@ class NativeDist:
 
     def merkle_root(self, runs: torch.Tensor, n: int) -> bytes:
         root = (ctypes.c_uint8 * 64)()
+        self._torch_ready()
         self.ctx.check(self._lib.sg_dist_merkle_root(self.handle, ctypes.c_void_p(runs.data_ptr()), n, root))
         return bytes(root)
 
@@ -510,11 +521,28 @@ class NativeDist:
                    proof_stream) -> None:
         fri = api.FRI(offset, omega, n, expansion, c, ctx=self.ctx)
         cb, adapter = fri._stream(proof_stream)
+        self._torch_ready()
         rc = self._lib.sg_dist_fri_commit(self.handle, ctypes.byref(fri._p), ctypes.c_void_p(runs.data_ptr()), n,
                                           ctypes.byref(cb))
         if adapter is not None and adapter.error is not None:
             raise adapter.error
         self.ctx.check(rc)
+
+
+    def fri_prove(self, offset: int, omega: int, runs: torch.Tensor, n: int, expansion: int, c: int,
+                  proof_stream) -> List[int]:
+        """fri.rs:210-248 on a run-sharded codeword: the same proof-stream bytes and top-level indices
+        as the single-GPU FRI::prove on every rank."""
+        fri = api.FRI(offset, omega, n, expansion, c, ctx=self.ctx)
+        cb, adapter = fri._stream(proof_stream)
+        top = (ctypes.c_size_t * max(c, 1))()
+        self._torch_ready()
+        rc = self._lib.sg_dist_fri_prove(self.handle, ctypes.byref(fri._p), ctypes.c_void_p(runs.data_ptr()), n,
+                                         ctypes.byref(cb), top)
+        if adapter is not None and adapter.error is not None:
+            raise adapter.error
+        self.ctx.check(rc)
+        return [int(t) for t in top[:c]]
 
 
 def gather_runs_sized(shards: Sequence[Sequence[int]], n1: int, n2: int, world: int) -> List[int]:
