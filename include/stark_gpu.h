@@ -50,6 +50,10 @@ const char* sg_last_error(const sg_ctx* ctx);
 void* sg_ctx_stream(sg_ctx* ctx);
 /* release cached device buffers and twiddle tables */
 int sg_ctx_trim(sg_ctx* ctx);
+/* HBM probe (measurement, no reference counterpart): read + write GB/s of a dwordx4 streaming
+ * device copy of `bytes` (multiple of 16), best of `iters`; blocks = 0: one 16-byte element per
+ * lane, else a grid-stride copy over blocks x 256 lanes */
+int sg_hbm_copy_probe(sg_ctx* ctx, size_t bytes, int iters, unsigned blocks, double* gbs);
 /* per-kernel HIP-event timing on the context stream (instrumentation, no reference counterpart):
  * enable resets the totals; the report is JSON {kernel: {launches, ms, bytes}} where bytes are
  * the algorithmic bytes of the launches; len receives the size incl. the NUL. */
@@ -256,6 +260,13 @@ int sg_dist_merkle_root(sg_dist* d, const sg_fe* d_runs, size_t n, uint8_t* root
 /* fri.rs:115-172 FRI::commit of a run-sharded codeword: every rank writes the same stream bytes */
 int sg_dist_fri_commit(sg_dist* d, const sg_fri* fri, const sg_fe* d_runs, size_t n,
                        const sg_proof_stream* ps);
+/* fri.rs:210-248 FRI::prove of a run-sharded codeword (replaces FRI::prove when the codeword is
+ * sharded): the sharded commit keeps every round's runs, forests and top trees; each query opening
+ * comes from the rank that owns the leaf's run (value + subtree path, one all-gather per round)
+ * plus the top path every rank holds.  Every rank writes the same proof-stream bytes as the
+ * single-GPU sg_fri_prove and receives the same c top-level indices in top. */
+int sg_dist_fri_prove(sg_dist* d, const sg_fri* fri, const sg_fe* d_runs, size_t n, const sg_proof_stream* ps,
+                      size_t* top);
 
 /* ------------------------------------------- polynomial algebra (fft/ntt_arithmetics.rs)
  * A polynomial is a device-resident coefficient vector owned by the library
@@ -277,7 +288,8 @@ int sg_fast_multiply(sg_ctx* ctx, sg_fe root, uint64_t root_order, const sg_poly
 int sg_fast_coset_divide(sg_ctx* ctx, sg_fe root, uint64_t root_order, sg_fe offset, const sg_poly* lhs,
                          const sg_poly* rhs, sg_poly** out);
 /* ntt_arithmetics.rs:66-113 fast_zerofier(root, root_order, domain): geometric domains
- * (domain[i] = root^i) in closed form on the GPU, other domains up to 1024 points */
+ * (domain[i] = root^i) in closed form on the GPU; any other domain of any size by a GPU product
+ * tree (exact below root_order; above it the reference's wrapped recursion is reproduced) */
 int sg_fast_zerofier(sg_ctx* ctx, sg_fe root, uint64_t root_order, const sg_fe* domain, size_t n, sg_poly** out);
 /* ntt_arithmetics.rs:172-237 fast_interpolate_domain(root, root_order, domain, values) */
 int sg_fast_interpolate_domain(sg_ctx* ctx, sg_fe root, uint64_t root_order, const sg_fe* domain,

@@ -270,6 +270,13 @@ def _native_checks(nd, ctx, world, rank, logn, gather):
         got = sg.IndependentProofStream()
         nd.fri_commit(sg.generator(), root, cw, n, 8, c, got)
         assert got.digest() == ref.digest(), f"fri stream c={c}"
+        # FRI::prove (fri.rs:210-248): openings gathered from the ranks that own the leaves
+        ref = sg.IndependentProofStream()
+        top = sg.FRI(sg.generator(), root, n, 8, c, ctx=ctx).prove(cw_full, ref)
+        got = sg.IndependentProofStream()
+        gtop = nd.fri_prove(sg.generator(), root, cw, n, 8, c, got)
+        assert gtop == top, f"fri prove top indices c={c}"
+        assert got.digest() == ref.digest(), f"fri prove stream c={c}"
 
 
 def test_native_dist_world1_rccl():
@@ -315,3 +322,74 @@ def test_native_dist_one_gpu_host_transport(world, logn):
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     mp.spawn(_native_worker, args=(world, port, logn), nprocs=world, join=True)
+
+
+# ------------------------------------------------------------------ north-star block, sharded FRI::prove
+
+NS_LOG, NS_EXP, NS_C = 24, 8, 64
+
+
+@pytest.fixture(scope="module")
+def north_star_reference():
+    """The north-star block on one GPU: LDE of a seeded degree < 2^21 polynomial onto 2^24 points
+    (fast_coset_evaluate) + FRI::prove(expansion 8, c = 64): proof bytes and top indices."""
+    import shutil
+    import tempfile
+    import starkgpu as sg
+    n = 1 << NS_LOG
+    d = n // NS_EXP
+    coeffs = _rand(2024, d)
+    root = sg.primitive_nth_root(n)
+    cw = sg.fast_coset_evaluate(root, n, sg.generator(), coeffs)
+    ps = sg.IndependentProofStream()
+    top = sg.FRI(sg.generator(), root, n, NS_EXP, NS_C).prove(cw, ps)
+    tmp = tempfile.mkdtemp(prefix="sg_ns_")
+    try:
+        np.save(os.path.join(tmp, "coeffs.npy"), coeffs)
+        with open(os.path.join(tmp, "proof.bin"), "wb") as f:
+            f.write(ps.digest())
+        np.save(os.path.join(tmp, "top.npy"), np.array(top, dtype=np.uint64))
+        yield tmp
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
+def _north_star_worker(rank, world, port, tmp):
+    import torch.distributed as dist
+    import starkgpu as sg
+    from starkgpu import dist as D
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ctx = sg.Context(0)
+        nd = D.NativeDist(ctx, transport="host")
+        n = 1 << NS_LOG
+        root = sg.primitive_nth_root(n)
+        coeffs = np.load(os.path.join(tmp, "coeffs.npy"))
+        cols, row = D.scatter_columns_np(coeffs, n, world, rank)
+        runs = nd.coset_evaluate(root, n, sg.generator(), _t(cols), row)
+        ps = sg.IndependentProofStream()
+        top = nd.fri_prove(sg.generator(), root, runs, n, NS_EXP, NS_C, ps)
+        want = open(os.path.join(tmp, "proof.bin"), "rb").read()
+        ok = (ps.digest() == want, top == [int(t) for t in np.load(os.path.join(tmp, "top.npy"))])
+        flags = [None] * world
+        dist.all_gather_object(flags, ok)
+        assert all(f[0] for f in flags), f"sharded FRI::prove bytes differ from the single-GPU proof: {flags}"
+        assert all(f[1] for f in flags), f"sharded FRI::prove top indices differ: {flags}"
+        nd.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("world", [2, 8])
+def test_north_star_sharded_lde_fri_prove(north_star_reference, world):
+    """The north-star block sharded over `world` ranks on this box's GPU (host transport over gloo):
+    sg_dist_coset_evaluate (2^21 -> 2^24) + sg_dist_fri_prove (expansion 8, c = 64) write the
+    single-GPU FRI::prove bytes (fri.rs:210-248) on every rank."""
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.spawn(_north_star_worker, args=(world, port, north_star_reference), nprocs=world, join=True)

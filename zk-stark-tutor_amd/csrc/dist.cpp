@@ -208,9 +208,21 @@ void dist_coset_evaluate(sg_dist* d, const fe& gen, uint64_t n, const fe& offset
   dist_ntt(d, gen, sc.as<fe>(), row_len, n, runs);
 }
 
+// A sharded FRI round kept for the query phase: the rank's runs, its forest (one subtree of R
+// leaves per run) and the top tree over the G k1s run roots in global run order (every rank).
+struct ShardedRound {
+  uint64_t k1s = 0, m = 0, per = 0;  // runs per rank, run roots overall, u64 per subtree
+  const fe* cw = nullptr;            // [k1s][R]
+  DevBuf cw_own;
+  DevBuf forest;
+  DevBuf top;                        // m leaves' tree (absent for m == 1)
+};
+
 // root of the natural-order codeword held as runs [k1s][R] on every rank (merkle_root.rs:21-32):
-// a forest of k1s subtrees per rank, the run roots all-gathered (64 B each), the top on every rank
-void dist_merkle_root(sg_dist* d, const fe* runs, uint64_t k1s, uint64_t R, uint8_t root[64]) {
+// a forest of k1s subtrees per rank, the run roots all-gathered (64 B each), the top on every rank.
+// With `keep`, the forest and the top tree move into it (openings).
+void dist_merkle_root(sg_dist* d, const fe* runs, uint64_t k1s, uint64_t R, uint8_t root[64],
+                      ShardedRound* keep = nullptr) {
   sg_ctx* ctx = d->ctx;
   SG_REQUIRE(R >= 1 && (R & (R - 1)) == 0 && k1s >= 1 && (k1s & (k1s - 1)) == 0, "Leafs len must be power of two");
   const uint64_t per = merkle_tree_digests(R) * 8;  // u64 per subtree
@@ -226,9 +238,15 @@ void dist_merkle_root(sg_dist* d, const fe* runs, uint64_t k1s, uint64_t R, uint
   // [g][k1] -> [k1][g]: global run order (a digest is 4 field-element slots)
   SG_HIP(launch_swap01(all.as<fe>(), ordered.as<fe>(), d->G, k1s, 4, ctx->stream));
   const uint64_t m = d->G * k1s;
+  if (keep) {
+    keep->k1s = k1s;
+    keep->m = m;
+    keep->per = per;
+  }
   if (m == 1) {
     SG_HIP(hipMemcpyAsync(root, ordered.get(), 64, hipMemcpyDeviceToHost, ctx->stream));
     SG_HIP(hipStreamSynchronize(ctx->stream));
+    if (keep) keep->forest = std::move(forest);
     return;
   }
   DevBuf top(ctx, merkle_tree_digests(m) * 64);
@@ -238,14 +256,30 @@ void dist_merkle_root(sg_dist* d, const fe* runs, uint64_t k1s, uint64_t R, uint
   SG_HIP(launch_merkle_tree(nullptr, &tr, 1, m, &root_dev, ctx->stream, 0, 0, 1));
   SG_HIP(hipStreamSynchronize(ctx->stream));
   memcpy(root, ctx->pinned_roots, 64);
+  if (keep) {
+    keep->forest = std::move(forest);
+    keep->top = std::move(top);
+  }
 }
+
+// What FRI::prove's query phase (fri.rs:174-248) reads after a sharded commit: the sharded rounds
+// (runs, forests, top trees) and, when the commit finished on the gathered codeword, the
+// single-GPU state of the remaining rounds (identical on every rank).
+struct DistFriState {
+  uint64_t n2 = 0, R = 0;
+  std::vector<ShardedRound> sharded;
+  sg_fri_state tail;
+  std::vector<uint64_t> lengths;  // every round's codeword length
+};
 
 // fri.rs:115-172 on a run-sharded codeword.  The fold partner of i is i + n/2: same k2,
 // k1 + N1/2, i.e. on the same rank, so folds stay local while more than one run per rank is
 // left; every rank pushes the same roots, so the Fiat-Shamir challenges agree without a
 // broadcast.  With one run per rank left, the N2-element codeword is all-gathered and the
-// remaining rounds run through the single-GPU commit.
-void dist_fri_commit(sg_dist* d, const sg_fri* f, const fe* runs, uint64_t n, const sg_proof_stream* ps) {
+// remaining rounds run through the single-GPU commit.  With `keep`, every round's codeword
+// and trees stay for the query phase.
+void dist_fri_commit(sg_dist* d, const sg_fri* f, const fe* runs, uint64_t n, const sg_proof_stream* ps,
+                     DistFriState* keep = nullptr) {
   sg_ctx* ctx = d->ctx;
   SG_REQUIRE(ps && ps->push && ps->fiat_shamir_prover, "proof stream callbacks required");
   SG_REQUIRE(n == f->domain_length, "Length of the domain doesnt match the length of initial codeword");
@@ -254,6 +288,10 @@ void dist_fri_commit(sg_dist* d, const sg_fri* f, const fe* runs, uint64_t n, co
   uint64_t n1, n2;
   plan(n, d->G, n1, n2);
   const uint64_t R = n2 / d->G;
+  if (keep) {
+    keep->n2 = n2;
+    keep->R = R;
+  }
   fe omega = to_fe(f->omega), offset = to_fe(f->offset);
   SG_REQUIRE(fe_is_canonical(omega) && fe_is_canonical(offset), "FRI omega/offset must be canonical");
   const fe inv2 = fe_inv(fe_from_u64(2));
@@ -265,7 +303,15 @@ void dist_fri_commit(sg_dist* d, const sg_fri* f, const fe* runs, uint64_t n, co
     const fe winv = fe_inv(omega);
     SG_REQUIRE(fe_eq(fe_pow(omega, length - 1), winv), "error in commit: omega does not have the right order!");
     uint8_t root[64];
-    dist_merkle_root(d, cur, k1s, R, root);
+    ShardedRound* sr = nullptr;
+    if (keep) {
+      keep->sharded.emplace_back();
+      sr = &keep->sharded.back();
+      sr->cw = cur;
+      if (owned.get()) sr->cw_own = std::move(owned);  // the previous fold's output, kept
+      keep->lengths.push_back(length);
+    }
+    dist_merkle_root(d, cur, k1s, R, root, sr);
     push_obj(ps, SG_OBJ_ROOT, root, 64);
     if (r == rounds - 1) break;
     uint8_t chal[32];
@@ -311,8 +357,154 @@ void dist_fri_commit(sg_dist* d, const sg_fri* f, const fe* runs, uint64_t n, co
   sub.omega = from_fe(omega);
   sub.domain_length = length;
   SG_REQUIRE(fri_num_rounds(&sub) == rounds - r, "FRI tail round count mismatch");
+  if (keep) {
+    fri_commit_dev(ctx, &sub, full.as<fe>(), length, ps, keep->tail, /*borrow_input=*/false);
+    for (uint64_t l : keep->tail.lengths) keep->lengths.push_back(l);
+    return;
+  }
   sg_fri_state st;
   fri_commit_dev(ctx, &sub, full.as<fe>(), length, ps, st, /*borrow_input=*/true);
+}
+
+// Openings of round r at global indices I: values and authentication paths (leaf level first),
+// identical on every rank.  A sharded round's value and subtree part come from the rank that owns
+// the run (i = k1 n2 + g R + c: rank g, run k1, leaf c), exchanged in one all-gather of fixed-size
+// slots; its top part (run index i / R in the top tree) is on every rank.
+void dist_open(sg_dist* d, const DistFriState& s, size_t r, const std::vector<uint64_t>& I, std::vector<fe>& vals,
+               std::vector<uint8_t>& paths, int& depth) {
+  sg_ctx* ctx = d->ctx;
+  const size_t q = I.size();
+  vals.assign(q, fe_zero());
+  if (r >= s.sharded.size()) {  // a round of the single-GPU tail
+    const size_t t = r - s.sharded.size();
+    const sg_tree* tree = s.tail.trees[t].get();
+    depth = tree->logn;
+    std::vector<uint64_t> di;
+    for (uint64_t i : I) di.push_back(i);
+    DevBuf dI(ctx, q * 8), dV(ctx, q * sizeof(fe));
+    SG_HIP(hipMemcpyAsync(dI.get(), di.data(), q * 8, hipMemcpyHostToDevice, ctx->stream));
+    SG_HIP(launch_gather_fe(s.tail.cw[t], dI.as<uint64_t>(), dV.as<fe>(), (uint32_t)q, ctx->stream));
+    SG_HIP(hipMemcpyAsync(vals.data(), dV.get(), q * sizeof(fe), hipMemcpyDeviceToHost, ctx->stream));
+    std::vector<uint64_t> pidx;
+    for (uint64_t i : I) path_indices(tree, i, pidx);
+    paths.assign(pidx.size() * 64, 0);
+    gather_digests(ctx, tree, pidx, paths.data());  // synchronizes the stream
+    return;
+  }
+  const ShardedRound& sr = s.sharded[r];
+  const uint64_t R = s.R, n2 = s.n2;
+  const int lr = ilog2_exact(R), lm = ilog2_exact(sr.m);
+  depth = lr + lm;
+  const size_t slot = 16 + 64 * (size_t)lr;
+  // owned requests: element offsets [k1][c] and subtree digest indices
+  std::vector<uint64_t> own, eidx, didx;
+  for (size_t j = 0; j < q; ++j) {
+    const uint64_t i = I[j];
+    if ((i % n2) / R != (uint64_t)d->g) continue;
+    const uint64_t k1 = i / n2, c = i % R;
+    own.push_back(j);
+    eidx.push_back(k1 * R + c);
+    for (int lv = 0; lv < lr; ++lv) didx.push_back(k1 * (sr.per / 8) + level_offset(R, lv) + ((c >> lv) ^ 1));
+  }
+  std::vector<uint8_t> mine(q * slot, 0);
+  if (!own.empty()) {
+    DevBuf dE(ctx, eidx.size() * 8), dV(ctx, eidx.size() * sizeof(fe));
+    std::vector<fe> v(eidx.size());
+    std::vector<uint8_t> dg(didx.size() * 64);
+    SG_HIP(hipMemcpyAsync(dE.get(), eidx.data(), eidx.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+    SG_HIP(launch_gather_fe(sr.cw, dE.as<uint64_t>(), dV.as<fe>(), (uint32_t)eidx.size(), ctx->stream));
+    SG_HIP(hipMemcpyAsync(v.data(), dV.get(), v.size() * sizeof(fe), hipMemcpyDeviceToHost, ctx->stream));
+    if (!didx.empty()) {
+      DevBuf dD(ctx, didx.size() * 8), dO(ctx, didx.size() * 64);
+      SG_HIP(hipMemcpyAsync(dD.get(), didx.data(), didx.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+      SG_HIP(launch_gather_digests(sr.forest.as<uint64_t>(), dD.as<uint64_t>(), dO.as<uint64_t>(),
+                                   (uint32_t)didx.size(), ctx->stream));
+      SG_HIP(hipMemcpyAsync(dg.data(), dO.get(), dg.size(), hipMemcpyDeviceToHost, ctx->stream));
+    }
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+    for (size_t o = 0; o < own.size(); ++o) {
+      uint8_t* p = mine.data() + own[o] * slot;
+      memcpy(p, &v[o], 16);
+      memcpy(p + 16, dg.data() + o * lr * 64, 64 * (size_t)lr);
+    }
+  }
+  // one all-gather of every rank's slots, then each request takes its owner's
+  DevBuf dsend(ctx, q * slot), drecv(ctx, d->G * q * slot);
+  SG_HIP(hipMemcpyAsync(dsend.get(), mine.data(), q * slot, hipMemcpyHostToDevice, ctx->stream));
+  exchange(d, dsend.get(), drecv.get(), q * slot, /*a2a=*/false);
+  std::vector<uint8_t> all((size_t)d->G * q * slot);
+  SG_HIP(hipMemcpyAsync(all.data(), drecv.get(), all.size(), hipMemcpyDeviceToHost, ctx->stream));
+  // the top part from the top tree every rank holds
+  std::vector<uint64_t> tidx;
+  for (uint64_t i : I)
+    for (int lv = 0; lv < lm; ++lv) tidx.push_back(level_offset(sr.m, lv) + (((i / R) >> lv) ^ 1));
+  std::vector<uint8_t> topd(tidx.size() * 64);
+  if (!tidx.empty()) {
+    DevBuf dT(ctx, tidx.size() * 8), dO(ctx, tidx.size() * 64);
+    SG_HIP(hipMemcpyAsync(dT.get(), tidx.data(), tidx.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+    SG_HIP(launch_gather_digests(sr.top.as<uint64_t>(), dT.as<uint64_t>(), dO.as<uint64_t>(), (uint32_t)tidx.size(),
+                                 ctx->stream));
+    SG_HIP(hipMemcpyAsync(topd.data(), dO.get(), topd.size(), hipMemcpyDeviceToHost, ctx->stream));
+  }
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  paths.assign(q * (size_t)depth * 64, 0);
+  for (size_t j = 0; j < q; ++j) {
+    const uint64_t owner = (I[j] % n2) / R;
+    const uint8_t* p = all.data() + (owner * q + j) * slot;
+    memcpy(&vals[j], p, 16);
+    uint8_t* out = paths.data() + j * (size_t)depth * 64;
+    memcpy(out, p + 16, 64 * (size_t)lr);
+    memcpy(out + 64 * (size_t)lr, topd.data() + j * (size_t)lm * 64, 64 * (size_t)lm);
+  }
+}
+
+// FRI::prove (fri.rs:210-248) on a run-sharded codeword: the sharded commit with every round kept,
+// sample_indices over len(codewords[1]) reduced by len(codewords[-1]) (fri.rs:88-113), then per
+// round the c Leafs objects and 3c Path objects (fri.rs:174-208) -- every rank writes the same bytes.
+void dist_fri_prove(sg_dist* d, const sg_fri* f, const fe* runs, uint64_t n, const sg_proof_stream* ps,
+                    size_t* top) {
+  DistFriState s;
+  dist_fri_commit(d, f, runs, n, ps, &s);
+  SG_REQUIRE(s.lengths.size() >= 2, "FRI prove needs at least two rounds (reference indexes codewords[1])");
+  uint8_t seed[32];
+  if (ps->fiat_shamir_prover(ps->user, 32, seed) != 0)
+    throw Error{SG_ERR_CALLBACK, "proof stream fiat_shamir callback failed"};
+  const size_t c = f->num_colinearity_tests;
+  sample_indices(seed, 32, s.lengths[1], s.lengths.back(), c, top);
+  std::vector<uint64_t> idx(top, top + c);
+  auto put_path = [&](const uint8_t* p, int depth) {
+    std::vector<uint8_t> pl(72 * (size_t)depth);
+    for (int k = 0; k < depth; ++k) {
+      uint8_t* o = pl.data() + 72 * (size_t)k;
+      memset(o, 0, 8);
+      o[7] = 64;
+      memcpy(o + 8, p + 64 * (size_t)k, 64);
+    }
+    push_obj(ps, SG_OBJ_PATH, pl.data(), pl.size());
+  };
+  for (size_t r = 0; r + 1 < s.lengths.size(); ++r) {
+    const uint64_t half = s.lengths[r] / 2;
+    for (auto& i : idx) i %= half;
+    std::vector<uint64_t> ab(idx);
+    for (uint64_t i : idx) ab.push_back(i + half);
+    std::vector<fe> vab, vc;
+    std::vector<uint8_t> pab, pc;
+    int dab = 0, dc = 0;
+    dist_open(d, s, r, ab, vab, pab, dab);
+    dist_open(d, s, r + 1, idx, vc, pc, dc);
+    for (size_t k = 0; k < c; ++k) {
+      uint8_t pl[48];
+      put_u128_be_at(pl, vab[k]);
+      put_u128_be_at(pl + 16, vab[c + k]);
+      put_u128_be_at(pl + 32, vc[k]);
+      push_obj(ps, SG_OBJ_LEAFS, pl, 48);
+    }
+    for (size_t k = 0; k < c; ++k) {
+      put_path(pab.data() + k * (size_t)dab * 64, dab);
+      put_path(pab.data() + (c + k) * (size_t)dab * 64, dab);
+      put_path(pc.data() + k * (size_t)dc * 64, dc);
+    }
+  }
 }
 
 sg_dist* checked(sg_dist* d) {
@@ -424,6 +616,18 @@ extern "C" int sg_dist_merkle_root(sg_dist* d, const sg_fe* d_runs, size_t n, ui
     uint64_t n1, n2;
     plan(n, d->G, n1, n2);
     dist_merkle_root(d, reinterpret_cast<const fe*>(d_runs), n1, n2 / d->G, root);
+  });
+}
+
+extern "C" int sg_dist_fri_prove(sg_dist* d, const sg_fri* fri, const sg_fe* d_runs, size_t n,
+                                 const sg_proof_stream* ps, size_t* top) {
+  sg_ctx* ctx = d ? d->ctx : nullptr;
+  return guard(ctx, [&] {
+    checked(d);
+    set_device(ctx);
+    SG_REQUIRE(fri && d_runs && top, "null argument");
+    dist_fri_prove(d, fri, reinterpret_cast<const fe*>(d_runs), n, ps, top);
+    SG_HIP(hipStreamSynchronize(ctx->stream));
   });
 }
 

@@ -112,6 +112,9 @@ void path_indices(const sg_tree* t, uint64_t index, std::vector<uint64_t>& idx);
 void gather_digests(sg_ctx* ctx, const sg_tree* t, const std::vector<uint64_t>& idx, uint8_t* out);
 
 size_t fri_num_rounds(const sg_fri* f);
+// fri.rs:88-113 (the reduced-index rejection included)
+void sample_indices(const uint8_t* seed, size_t seed_len, size_t size, size_t reduced_size, size_t number,
+                    size_t* out);
 // SG_PROVE_TIMING=1: host-clock phase marks of the prover on stderr (diagnostics only)
 struct PhaseMarks {
   bool on;

@@ -65,6 +65,7 @@ PROTOTYPES = {
     "sg_last_error": (ctypes.c_char_p, [_vp]),
     "sg_ctx_stream": (_vp, [_vp]),
     "sg_ctx_trim": (ctypes.c_int, [_vp]),
+    "sg_hbm_copy_probe": (ctypes.c_int, [_vp, _sz, ctypes.c_int, ctypes.c_uint, _P(ctypes.c_double)]),
     "sg_ctx_set_async": (ctypes.c_int, [_vp, ctypes.c_int]),
     "sg_ctx_synchronize": (ctypes.c_int, [_vp]),
     "sg_ctx_profile": (ctypes.c_int, [_vp, ctypes.c_int]),
@@ -135,6 +136,7 @@ PROTOTYPES = {
     "sg_dist_coset_evaluate": (ctypes.c_int, [_vp, sg_fe, _sz, sg_fe, _vp, _sz, _vp]),
     "sg_dist_merkle_root": (ctypes.c_int, [_vp, _vp, _sz, _vp]),
     "sg_dist_fri_commit": (ctypes.c_int, [_vp, _P(sg_fri), _vp, _sz, _P(sg_proof_stream)]),
+    "sg_dist_fri_prove": (ctypes.c_int, [_vp, _P(sg_fri), _vp, _sz, _P(sg_proof_stream), _P(_sz)]),
     # polynomial algebra (fft/ntt_arithmetics.rs)
     "sg_poly_create": (ctypes.c_int, [_vp, _vp, _sz, _P(_vp)]),
     "sg_poly_create_dev": (ctypes.c_int, [_vp, _vp, _sz, _P(_vp)]),
