@@ -47,8 +47,8 @@ REGISTERS = 2       # Rescue-Prime m = 2
 HBM_PEAK_GBS = 8000.0
 # PMC HBM bytes of this workload's kernels (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes on
 # `bench.py --steps 3 --warmup 1 --no-side`, tools/pmc_passes.sh + tools/pmc_traffic.py)
-PMC_TRAFFIC_FILE = "r02_pmc_traffic_e2e.json"
-PMC_VALU_FILE = "r02_pmc_valu_e2e.json"  # SQ_INSTS_VALU pass (tools/pmc_passes.sh + tools/pmc_valu.py)
+PMC_TRAFFIC_FILE = "r03_pmc_traffic_e2e.json"
+PMC_VALU_FILE = "r03_pmc_valu_e2e.json"  # SQ_INSTS_VALU pass (tools/pmc_passes.sh + tools/pmc_valu.py)
 
 
 def synthetic_fe(seed: int, tag: bytes, n: int) -> np.ndarray:
@@ -325,7 +325,8 @@ def side_sharded(ctx: sg.Context, device, world: int, rank: int, iters: int = 3)
     * C5: one 2^27-point NTT sharded across the ranks: four-step, ONE all-to-all, time = max
       over ranks.
     * the north-star block sharded: LDE 2^21 -> 2^24 on the coset + FRI commit
-      (exp 8, c = 64) with run-sharded Merkle trees and folds.
+      (exp 8, c = 64) with run-sharded Merkle trees and folds, and the same with FRI::prove
+      (sg_dist_fri_prove: openings gathered from the ranks that own the leaves).
     """
     from starkgpu import dist as D
     backend = dist.get_backend()
@@ -381,6 +382,12 @@ def side_sharded(ctx: sg.Context, device, world: int, rank: int, iters: int = 3)
             ds.fri_commit(off, omega, cw, N, EXPANSION, COLINEARITY, sg.IndependentProofStream())
 
         out["sharded_lde_fri_commit_2p24_ms"] = round(timed(lde_fri) * 1e3, 3)
+
+        def lde_fri_prove():  # FRI::prove incl. the query phase's openings from the owning ranks
+            cw = ds.coset_evaluate(omega, N, off, cs.reshape(-1), row)
+            ds.fri_prove(off, omega, cw, N, EXPANSION, COLINEARITY, sg.IndependentProofStream())
+
+        out["sharded_lde_fri_prove_2p24_ms"] = round(timed(lde_fri_prove) * 1e3, 3)
     except Exception as e:  # noqa: BLE001
         out["sharded_lde_fri_error"] = f"{type(e).__name__}: {e}"
     ds.close()
@@ -446,8 +453,15 @@ def cpu_baseline_leg(headline_N: int, log_Ns=(12, 13, 14, 15, 16)) -> dict:
     import ref_cpu as rc
     import stark_oracle as o
     pts = []
-    for ln in log_Ns:
-        pts.append((1 << ln, faithful_block_step(rc, o, 1 << ln)))
+    # the reference is single-threaded: the leg runs pinned to one core (SURVEY.md 8(d)(i) "taskset")
+    prev = os.sched_getaffinity(0)
+    core = min(prev)
+    os.sched_setaffinity(0, {core})
+    try:
+        for ln in log_Ns:
+            pts.append((1 << ln, faithful_block_step(rc, o, 1 << ln)))
+    finally:
+        os.sched_setaffinity(0, prev)
     from scipy.optimize import nnls
     A = np.array([[n * np.log2(n), n] for n, _ in pts], dtype=np.float64)
     y = np.array([t for _, t in pts], dtype=np.float64)
@@ -459,6 +473,7 @@ def cpu_baseline_leg(headline_N: int, log_Ns=(12, 13, 14, 15, 16)) -> dict:
         "value": round((REGISTERS + 2) * N_last / t_last / 1e9, 8),
         "unit": "Gelem/s",
         "cores": 1,
+        "pinned_cpu": core,
         "kind": "port",
         "sample": f"the prove's LDE+commit+FRI block (4 LDEs, 3 commits, FRI prove, c={COLINEARITY}) at "
                   f"N=2^{N_last.bit_length() - 1} on one core (value), measured at "
@@ -471,39 +486,55 @@ def cpu_baseline_leg(headline_N: int, log_Ns=(12, 13, 14, 15, 16)) -> dict:
     }
 
 
-def cpu_baseline_allcores(N: int) -> dict:
-    """The optimized C++ restatement (oracle/fast_cpu.cpp: Montgomery arithmetic, twiddle tables,
-    OpenMP over every host core) on the headline block AT the headline size: LDEs of 2^20
-    coefficients (the trace-2^20 quotients) onto the FRI domain N = 2^25, Merkle commits of 2^25
-    leaves, FRI::prove(2^25, expansion 8, c=64).
+def cpu_threads() -> tuple:
+    """(threads to use, why): the process's CPU affinity, capped by OMP_NUM_THREADS when the
+    environment sets it (the GPU pool gives a one-GPU job a 16-CPU share of a 256-CPU host and
+    exports OMP_NUM_THREADS=16; nproc there reports the whole machine)."""
+    aff = len(os.sched_getaffinity(0))
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and 0 < int(env) < aff:
+        return int(env), (f"OMP_NUM_THREADS={env}: this job's CPU share on a host whose affinity shows "
+                          f"{aff} CPUs (the pool sizes worker pools to the share)")
+    return aff, "every CPU in this process's affinity"
 
-    Each component is timed once at full size and the block composed exactly as the prove runs it
-    (4 LDEs + 3 commits + FRI prove, the FRI prove committing its own codeword), so the sample is
-    ~one block of CPU time."""
+
+def cpu_baseline_allcores(log_rows: int = LOG_TRACE) -> dict:
+    """The whole Stark::prove (stark.rs:276-562) on the host CPU at the headline size: the checker
+    restatement oracle/fast_cpu.cpp (Montgomery arithmetic, OpenMP; the reference's algorithms where
+    they define the bytes, fast ones where the result is unique -- its proof bytes equal the GPU's,
+    tests/test_gpu_fullsize.py) on the same Rescue-Prime workload as the headline line, timed once."""
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import fast_cpu as fc
-    import stark_oracle as o
-    d = N // 32
-    omega = o.primitive_nth_root(N)
-    coeffs = synthetic_fe(0, b"comb", d)
+    import stark_prove_oracle as e
+    threads, why = cpu_threads()
+    fc.set_threads(threads)
+    N = (1 << log_rows) - 2 - 4 * COLINEARITY
+    rp_o = e.RescuePrime(REGISTERS, 1, 128, N)
+    st_o = e.Stark(EXPANSION, COLINEARITY, 128, REGISTERS, N + 1, 3)
+    bounds = fc.rescue_degree_bounds(rp_o, st_o)
+    rp = sg.RescuePrime(REGISTERS, 1, 128, N)  # the trace is an input (host code, not timed)
+    inp = int.from_bytes(hashlib_shake(b"sg-bench-input" + (0).to_bytes(8, "big"), 16), "big") % P
+    trace = rp.trace_array(inp)
+    out = sg.to_ints(trace[-2:-1])[0]
+    tr = synthetic_fe(0, b"trace-rand", REGISTERS * st_o.num_randomizers)
+    rc = synthetic_fe(0, b"rand-poly", bounds[1] + 1)
+    phases = {}
     t0 = time.perf_counter()
-    cw = fc.fast_coset_evaluate(omega, N, o.GENERATOR, coeffs)
-    t1 = time.perf_counter()
-    fc.merkle_commit(cw)
-    t2 = time.perf_counter()
-    fc.fri_prove(o.GENERATOR, omega, cw, EXPANSION, COLINEARITY)
-    t3 = time.perf_counter()
-    lde, mk, fri = t1 - t0, t2 - t1, t3 - t2
-    block = (REGISTERS + 2) * lde + (REGISTERS + 1) * mk + fri
+    proof = fc.stark_prove_rescue(rp_o, st_o, trace, rp_o.boundary_constraints(out), tr, rc, bounds=bounds,
+                                  phases=phases)
+    t = time.perf_counter() - t0
+    nf = st_o.fri.domain_length
     return {
-        "value": round((REGISTERS + 2) * N / block / 1e9, 6),
+        "value": round((REGISTERS + 2) * nf / t / 1e9, 6),
         "unit": "Gelem/s",
-        "cores": fc.threads(),
+        "cores": threads,
+        "cores_note": why,
         "kind": "port",
-        "sample": f"the prove's LDE+commit+FRI block at the headline size (d=2^{d.bit_length() - 1} -> "
-                  f"N=2^{N.bit_length() - 1}): "
-                  f"LDE {lde:.2f} s, Merkle commit {mk:.2f} s, FRI prove {fri:.2f} s, each timed once; "
-                  f"block = 4 LDE + 3 commits + FRI = {block:.1f} s; oracle/fast_cpu.cpp (Montgomery, OpenMP)",
+        "prove_ms": round(t * 1e3, 1),
+        "proof_bytes": len(proof),
+        "phases_s": {k: round(v, 3) for k, v in phases.items()},
+        "sample": f"one complete Stark::prove of the headline workload (trace 2^{log_rows} - 1 rows, FRI domain "
+                  f"2^{nf.bit_length() - 1}) through oracle/fast_cpu.cpp on {threads} threads: {t:.1f} s",
         "host": host_cpu_info(),
     }
 
@@ -536,22 +567,18 @@ def cpu_baseline_e2e(seconds_budget: float = 6.0) -> dict:
                       f"{per * 1e3:.1f} ms/proof; Python restatement of the reference's algorithms"}
 
 
-def hbm_copy_gbs(device, mib: int = 1024, iters: int = 10):
-    """Device-to-device copy rate of a 1 GiB buffer (bytes read + bytes written per second), torch's
-    copy kernel, HIP events on torch's stream."""
-    n = mib * (1 << 20) // 8
-    a = torch.ones(n, dtype=torch.int64, device=device)
-    b = torch.empty_like(a)
-    b.copy_(a)
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(iters):
-        b.copy_(a)
-    e1.record()
-    e1.synchronize()
-    ms = e0.elapsed_time(e1) / iters
-    del a, b
-    return round(2 * mib * (1 << 20) / (ms * 1e-3) / 1e9, 1)
+def hbm_copy_gbs(ctx: sg.Context, mib: int = 2048, iters: int = 10) -> dict:
+    """HBM rate of the library's dwordx4 streaming copy kernel (sg_hbm_copy_probe: non-temporal
+    16-byte loads/stores) over a 2 GiB buffer (bytes read + bytes written per second, best of
+    `iters`, HIP events on the library's stream): one element per lane, and a grid-stride form."""
+    out = {}
+    for blocks in (0, 4096):
+        out[blocks] = ctx.hbm_copy_gbs(mib << 20, iters, blocks)
+    best = max(out.values())
+    return {"gbs": round(best, 1),
+            "per_form": {("one element per lane" if k == 0 else f"grid-stride {k} blocks"): round(v, 1)
+                         for k, v in out.items()},
+            "kernel": "sg_hbm_copy_probe (k_copy16)", "bytes": mib << 20}
 
 
 def standalone_launch(ctx, device, name: str, n: int):
@@ -677,7 +704,8 @@ def main():
                               f"achieved = per-wave count x the live launches' waves / their live time"}
     # the HBM rate a plain device copy reaches on this box (1 GiB read + 1 GiB written), beside the
     # 8 TB/s spec the contract prices against ("measure actual HBM with a copy kernel")
-    copy_gbs = hbm_copy_gbs(device)
+    copy = hbm_copy_gbs(ctx)
+    copy_gbs = copy["gbs"]
     # the same kernel alone on the chip (in the prove, the boundary-quotient and randomizer
     # trees share the CUs with the main stream's algebra, which stretches their launches)
     alone = standalone_launch(ctx, device, name, wl.fri_len)
@@ -741,6 +769,7 @@ def main():
                      "valu": valu,
                      "standalone": alone,
                      "hbm_copy_measured_gbs": copy_gbs,
+                     "hbm_copy_probe": copy,
                      "frac_of_measured_copy": round(achieved / copy_gbs, 4) if copy_gbs else None},
         "kernels_one_step": phases,  # every launch timed, last warmup step
         "host_phases_ms": {k: round(v / args.steps * 1e3, 3) for k, v in host_phases.items()},
@@ -755,22 +784,37 @@ def main():
     if world > 1 and not args.no_side:
         # a hang in a collective must not cost the main line: rank 0 prints it, and every rank
         # exits on its own timer (a rank left blocked in a collective would hold the launcher)
+        # A hang exits NON-ZERO (a stuck collective on a process that has touched the GPU is a failure
+        # the launcher must see); the lock makes the timer and the main thread mutually exclusive,
+        # so at most one of them emits the JSON line.
+        emit_lock = threading.Lock()
+        state = {"done": False}
+
         def on_timeout():
-            if rank == 0:
-                result["side"] = {"error": "sharded side measurements timed out"}
-                print(json.dumps(result), flush=True)
-            os._exit(0)
+            with emit_lock:
+                if state["done"]:
+                    return
+                state["done"] = True
+                if rank == 0:
+                    result["side"] = {"error": "sharded side measurements timed out"}
+                    print(json.dumps(result), flush=True)
+            os._exit(3)
         watchdog = threading.Timer(150.0 + (0 if rank == 0 else 15.0), on_timeout)
         watchdog.daemon = True
         watchdog.start()
         try:
-            result["side"] = side_sharded(ctx, device, world, rank)
+            side = side_sharded(ctx, device, world, rank)
         except Exception as e:  # noqa: BLE001 - reported in the JSON line, main metric stands
-            result["side"] = {"error": f"{type(e).__name__}: {e}"}
-        watchdog.cancel()
+            side = {"error": f"{type(e).__name__}: {e}"}
+        with emit_lock:
+            if state["done"]:  # the timer already reported and is exiting the process
+                return
+            state["done"] = True
+            watchdog.cancel()
+            result["side"] = side
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline_leg(fri_len)
-        result["cpu_baseline_allcores"] = cpu_baseline_allcores(fri_len)
+        result["cpu_baseline_allcores"] = cpu_baseline_allcores(args.log_trace)
         result["cpu_baseline_e2e"] = cpu_baseline_e2e()
     if rank == 0:
         print(json.dumps(result), flush=True)

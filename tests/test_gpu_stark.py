@@ -149,6 +149,22 @@ def test_stark_prove_domain_tables_cached_and_recomputed(monkeypatch):
     assert st.prove(trace, air, bnd, sg.IndependentProofStream(), tr, rc) == want
 
 
+def test_stark_prove_constraints_shared_by_two_contexts():
+    """Constraint objects built on one context and proved on two (the AIR's coset values live in
+    each context's domain tables, not in the shared constraint), with sg_ctx_trim between proofs
+    (it frees them): every proof equals the oracle's."""
+    rp, st_o, st_g, air_o, air_g, trace, bnd, tr, rc, out = _case(40, 4, 3, 4, 2, b"two-contexts")
+    want = st_o.prove(trace, air_o, bnd, o.IndependentProofStream(), tr, rc)
+    c1, c2 = sg.Context(0), sg.Context(0)
+    s1 = sg.Stark(4, 3, 4, 2, 41, 2, ctx=c1)
+    s2 = sg.Stark(4, 3, 4, 2, 41, 2, ctx=c2)
+    air = sg.RescuePrime(2, 1, 4, 40, ctx=c1).transition_constraints(s1.omicron, s1.omicron_domain_length)
+    for ctx_stark in (s1, s2, s1, s2):
+        assert ctx_stark.prove(trace, air, bnd, sg.IndependentProofStream(), tr, rc) == want
+        ctx_stark.ctx.trim()
+    assert s1.prove(trace, air, bnd, sg.IndependentProofStream(), tr, rc) == want
+
+
 def test_stark_prove_rescue_factored_air_equals_expanded(monkeypatch):
     """The native Rescue-Prime AIR is evaluated in its factored form (rescue_prime.rs:246-283:
     sum MDS prev^alpha + first(x) - (sum MDSinv (next - second(x)))^alpha); SG_AIR_GENERIC=1

@@ -20,10 +20,11 @@ MEASURE=${1:?measure}
 ROUNDS=${2:?rounds}
 shift 2
 IFS=: read -r KIND A1 A2 <<< "$MEASURE"
+PICK=""
 case "$KIND" in
   prove)  CMD=(python tools/step_timing.py "${A1:-8}" "${A2:-20}"); LIMIT=200 ;;
   c2)     CMD=(python tools/c2_time.py "${A1:-22}"); LIMIT=120 ;;
-  merkle) CMD=(python tools/bench_merkle.py "${A1:-25}"); LIMIT=120 ;;
+  merkle) CMD=(python tools/bench_merkle.py "${A1:-25}"); LIMIT=120; PICK="ms/build" ;;
   ntt)    CMD=(python tools/bench_ntt.py "${A1:-22}"); LIMIT=120 ;;
   bench)  CMD=(python bench.py --no-cpu-baseline --steps 3 --warmup 1); LIMIT=300 ;;
   *) echo "unknown measure $KIND" >&2; exit 2 ;;
@@ -38,7 +39,11 @@ for ((round = 1; round <= ROUNDS; round++)); do
         if [[ "$kv" == lib=* ]]; then ENVS+=("SG_LIB_PATH=$R/${kv#lib=}"); else ENVS+=("$kv"); fi
       done
     fi
-    OUT=$(env "${ENVS[@]}" timeout -k 10 $LIMIT "${CMD[@]}" 2>&1 | tail -n 1)
+    if [ -n "$PICK" ]; then
+      OUT=$(env "${ENVS[@]}" timeout -k 10 $LIMIT "${CMD[@]}" 2>&1 | grep -m1 "$PICK")
+    else
+      OUT=$(env "${ENVS[@]}" timeout -k 10 $LIMIT "${CMD[@]}" 2>&1 | tail -n 1)
+    fi
     echo "$LABEL: $OUT"
   done
 done

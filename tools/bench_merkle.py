@@ -38,7 +38,7 @@ def main():
     comp = batch * (2 * n - 1)
     dev_ms = sum(v["ms"] for v in rep.values()) / it
     print(f"2^{logn} x{batch} [{os.environ.get('SG_MERKLE_LEAF_BS', '256')}/{os.environ.get('SG_MERKLE_LEAF_FUSE', '4')}]: "
-          f"{t*1e3:.3f} ms/build  device {dev_ms:.3f} ms  {comp/dev_ms/1e6:.2f} G compressions/s")
+          f"{t*1e3:.3f} ms/build  device {dev_ms:.3f} ms  {comp/dev_ms/1e6:.2f} G compressions/s  root {roots[0][:8].hex()}")
     for k, v in sorted(rep.items(), key=lambda kv: -kv[1]["ms"]):
         print(f"  {k:18s} launches/iter {v['launches']/it:.0f}  ms/iter {v['ms']/it:.4f}")
 

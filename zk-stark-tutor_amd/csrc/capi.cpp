@@ -129,6 +129,20 @@ bool sg_ctx::domain_cache_on() const {
   return !(v && *v && *v != '0');
 }
 
+void sg_ctx::domain_table_put_bounded(const std::vector<uint64_t>& key, void* p) {
+  domain_table_put(key, p);
+  bounded_keys.push_back(key);
+  if (bounded_keys.size() <= kBoundedTables) return;
+  SG_HIP(hipStreamSynchronize(stream));  // queued work may still read the oldest table
+  SG_HIP(hipStreamSynchronize(side));
+  auto it = domain_tables.find(bounded_keys.front());
+  if (it != domain_tables.end()) {
+    (void)hipFree(it->second);
+    domain_tables.erase(it);
+  }
+  bounded_keys.erase(bounded_keys.begin());
+}
+
 void* sg_ctx::domain_table(const std::vector<uint64_t>& key) const {
   auto it = domain_tables.find(key);
   return it == domain_tables.end() ? nullptr : it->second;
@@ -313,6 +327,9 @@ extern "C" const char* sg_last_error(const sg_ctx* ctx) {
 extern "C" void* sg_ctx_stream(sg_ctx* ctx) { return ctx ? (void*)ctx->stream : nullptr; }
 extern "C" int sg_ctx_trim(sg_ctx* ctx) {
   return guard(ctx, [&] {
+    SG_REQUIRE(ctx, "null context");
+    SG_HIP(hipStreamSynchronize(ctx->stream));  // nothing queued may still read a table freed here
+    SG_HIP(hipStreamSynchronize(ctx->side));
     ctx->trim();
     for (auto& kv : ctx->pow_tables) (void)hipFree(kv.second.ptr);
     ctx->pow_tables.clear();
@@ -322,6 +339,51 @@ extern "C" int sg_ctx_trim(sg_ctx* ctx) {
     ctx->interp_tables.clear();
     for (auto& kv : ctx->domain_tables) (void)hipFree(kv.second);
     ctx->domain_tables.clear();
+    ctx->bounded_keys.clear();
+  });
+}
+
+// HBM copy probe: the read + write rate of a dwordx4 streaming copy of `bytes` (SURVEY.md 8(d):
+// "measure actual HBM with a copy kernel on the box"), best of `iters` launches, HIP events on the
+// context's stream.  blocks = 0: one 16-byte element per lane (the fastest form); else a
+// grid-stride copy over `blocks` x 256 lanes.
+extern "C" int sg_hbm_copy_probe(sg_ctx* ctx, size_t bytes, int iters, unsigned blocks, double* gbs) {
+  return guard(ctx, [&] {
+    set_device(ctx);
+    SG_REQUIRE(gbs && iters >= 1 && bytes >= 16 && bytes % 16 == 0, "bytes must be a positive multiple of 16");
+    void *src = nullptr, *dst = nullptr;
+    SG_HIP(hipMalloc(&src, bytes));
+    hipError_t e = hipMalloc(&dst, bytes);
+    if (e != hipSuccess) {
+      (void)hipFree(src);
+      SG_HIP(e);
+    }
+    struct Free {
+      void* a;
+      void* b;
+      ~Free() {
+        (void)hipFree(a);
+        (void)hipFree(b);
+      }
+    } fr{src, dst};
+    SG_HIP(hipMemsetAsync(src, 1, bytes, ctx->stream));
+    SG_HIP(launch_copy16(src, dst, bytes, blocks, ctx->stream));  // warm (page mapping, clocks)
+    hipEvent_t e0, e1;
+    SG_HIP(hipEventCreate(&e0));
+    SG_HIP(hipEventCreate(&e1));
+    double best = 0;
+    for (int it = 0; it < iters; ++it) {
+      SG_HIP(hipEventRecord(e0, ctx->stream));
+      SG_HIP(launch_copy16(src, dst, bytes, blocks, ctx->stream));
+      SG_HIP(hipEventRecord(e1, ctx->stream));
+      SG_HIP(hipEventSynchronize(e1));
+      float ms = 0;
+      SG_HIP(hipEventElapsedTime(&ms, e0, e1));
+      best = std::max(best, 2.0 * (double)bytes / ((double)ms * 1e-3) / 1e9);
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    *gbs = best;
   });
 }
 
@@ -949,6 +1011,65 @@ void fri_commit_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, co
   // Round r >= 1 hashes the fold of round r-1 in the same launch that computes it
   // (the fold is written out too: later rounds and the query phase read it).
   FoldLeaves fold{};
+  // SG_FRI_DEVICE_FS=1 (opt-in, read per call): a native stream's Fiat-Shamir continues on the
+  // device (k_fri_fs after each round's tree), every round is enqueued at once with no host round
+  // trip between a root and the next fold, and the roots are pushed afterwards (the host sponge
+  // absorbs them on its next draw).  Byte-identical, but slower on MI355X: a one-wave Keccak
+  // (two permutations per round) costs more than the host round trip it replaces
+  // (profiles/r03_ab_devfs.log: prove 27.4-27.8 vs 26.5-26.9 ms), so the host loop below stays the
+  // default.  Callback streams (any ProofStream implementation) always take the host loop.
+  const char* dev_fs_env = getenv("SG_FRI_DEVICE_FS");
+  if (dev_fs_env && *dev_fs_env == '1' && ps->push == stream_push_cb && rounds >= 2) {
+    Stream& S = reinterpret_cast<sg_stream*>(ps->user)->s;
+    DevTranscript h{};
+    uint8_t pend[136];
+    size_t plen = 0;
+    S.fs_snapshot(h.st, pend, &plen);
+    for (size_t i = 0; i < plen; ++i) h.st[i / 8] ^= (uint64_t)pend[i] << (8 * (i % 8));  // the partial block
+    h.plen = (uint32_t)plen;
+    DevBuf dfs(ctx, sizeof(DevTranscript)), dK(ctx, rounds * sizeof(fe)), droots(ctx, rounds * 64);
+    SG_HIP(hipMemcpyAsync(dfs.get(), &h, sizeof(h), hipMemcpyHostToDevice, ctx->stream));
+    const fe r2 = fe_r2();
+    for (size_t r = 0; r < rounds; ++r) {
+      const uint64_t len = plan[r].len;
+      SG_REQUIRE(fe_eq(fe_pow(plan[r].omega, len - 1), plan[r].winv),
+                 "error in commit: omega does not have the right order!");  // fri.rs:133
+      const fe* lv = st.cw[r];
+      uint64_t* buf = trees[r]->buf.as<uint64_t>();
+      SG_HIP(launch_merkle_tree(&lv, &buf, 1, len, nullptr, ctx->stream, 0, 0, 0, nullptr, 0, r ? &fold : nullptr));
+      const uint64_t* rootp = buf + level_offset(len, trees[r]->logn) * 8;
+      uint64_t* rout = droots.as<uint64_t>() + 8 * r;
+      if (r == rounds - 1) {
+        SG_HIP(hipMemcpyAsync(rout, rootp, 64, hipMemcpyDeviceToDevice, ctx->stream));
+        break;
+      }
+      const fe C = to_mont(fe_mul(plan[r].oinv, inv2));
+      SG_HIP(launch_fri_fs(dfs.as<DevTranscript>(), rootp, rout, dK.as<fe>() + r, C, r2, ctx->stream));
+      fold.src = st.cw[r];
+      fold.dst = const_cast<fe*>(st.cw[r + 1]);
+      fold.Tlo = Tlo;
+      fold.Thi = Thi;
+      fold.shift = (int)r;
+      fold.K = fe_zero();
+      fold.Kp = dK.as<fe>() + r;
+    }
+    std::vector<uint8_t> roots(rounds * 64);
+    const uint64_t last_len = st.lengths.back();
+    std::vector<fe> last(last_len);
+    SG_HIP(hipMemcpyAsync(roots.data(), droots.get(), roots.size(), hipMemcpyDeviceToHost, ctx->stream));
+    SG_HIP(hipMemcpyAsync(last.data(), st.cw.back(), last_len * sizeof(fe), hipMemcpyDeviceToHost, ctx->stream));
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+    for (size_t r = 0; r < rounds; ++r) {
+      memcpy(trees[r]->root, roots.data() + 64 * r, 64);
+      st.trees.push_back(std::move(trees[r]));
+      push_obj(ps, SG_OBJ_ROOT, st.trees.back()->root, 64);
+    }
+    std::vector<uint8_t> payload;
+    payload.reserve(last_len * 16);
+    for (auto& v : last) put_u128_be(payload, v);
+    push_obj(ps, SG_OBJ_CODEWORD, payload.data(), payload.size());  // fri.rs:166
+    return;
+  }
   for (size_t r = 0; r < rounds; ++r) {
     const uint64_t len = plan[r].len;
     // assert omega^(n-1) == omega^-1 (fri.rs:133)

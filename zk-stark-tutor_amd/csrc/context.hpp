@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <deque>
 #include <map>
 #include <string>
 #include <utility>
@@ -104,6 +105,12 @@ struct sg_ctx {
   bool domain_cache_on() const;
   void* domain_table(const std::vector<uint64_t>& key) const;
   void domain_table_put(const std::vector<uint64_t>& key, void* p) { domain_tables[key] = p; }
+  // content-keyed tables (1 / a small divisor's coset values, poly.cpp) are bounded: beyond
+  // kBoundedTables the oldest is freed (after both streams drain), so a long-running prover that
+  // meets many boundary sets does not grow device memory without limit
+  static constexpr size_t kBoundedTables = 64;
+  std::vector<std::vector<uint64_t>> bounded_keys;  // insertion order
+  void domain_table_put_bounded(const std::vector<uint64_t>& key, void* p);
   // pinned host staging buffers (grown on demand): slot 0 uploads gather addresses,
   // slot 1 receives gathered openings -- pageable copies of MBs cost ~10x more
   void* staging_ptr[2] = {nullptr, nullptr};

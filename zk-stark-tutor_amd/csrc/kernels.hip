@@ -557,6 +557,7 @@ struct MerkleArgs {
     const fe* Thi;
     int shift;       // previous round r: exponent = i << r
     fe K;            // Montgomery(alpha * offset_r^-1 * 2^-1)
+    const fe* Kp;    // != nullptr: K is read from here (written by k_fri_fs on the device)
   } fold;
 };
 
@@ -595,7 +596,8 @@ __global__ __launch_bounds__(MAXB) void k_merkle_levels(MerkleArgs a) {
         const fe x = ld_fe(a.fold.src + idx);
         const fe y = ld_fe(a.fold.src + idx + a.first_count);
         const uint64_t e = idx << a.fold.shift;
-        fe t = mont_mul(a.fold.K, ld_fe(a.fold.Tlo + (e & 4095)));
+        const fe K = a.fold.Kp ? ld_fe(a.fold.Kp) : a.fold.K;
+        fe t = mont_mul(K, ld_fe(a.fold.Tlo + (e & 4095)));
         t = mont_mul(t, ld_fe(a.fold.Thi + (e >> 12)));
         v = fe_add(fe_halve(fe_add(x, y)), mont_mul(fe_sub(x, y), t));
         st_fe(a.fold.dst + idx, v);
@@ -913,6 +915,155 @@ __global__ void k_gather_fe(const fe* __restrict__ src, const uint64_t* __restri
   st_fe(out + i, ld_fe(src + idx[i]));
 }
 
+// ---------------------------------------------- FRI Fiat-Shamir on the device
+//
+// FRI::commit's per-round draw (fri.rs:136-146): push(Root) then alpha = Field::sample(
+// fiat_shamir_prover(32)), i.e. SHAKE256 over the serialized stream (proof_stream.rs:36-41,
+// proof_stream_enum.rs:161-190) -- continued on the device from the host sponge's state, so the
+// rounds of a native stream's commit are enqueued back to back with no host round trip.  One
+// lane: the sponge absorbs the 73-byte Root object [0][64 as u64 BE][digest], squeezes 32 bytes
+// from a padded copy, and the fold constant K = Montgomery(alpha offset_r^-1 2^-1) goes to memory
+// for the next round's fold (FoldLeaves::Kp).
+
+__device__ __forceinline__ uint64_t rotl64(uint64_t x, int n) { return n == 0 ? x : rotr64(x, 64 - n); }
+
+// Keccak-f[1600] on 25 lanes held in registers (constant indices only; rounds unrolled so the
+// round constants are immediates: no scratch, no constant-memory loads)
+__device__ __forceinline__ void keccak_round_dev(uint64_t (&a)[25], uint64_t rc) {
+  const uint64_t c0 = a[0] ^ a[5] ^ a[10] ^ a[15] ^ a[20], c1 = a[1] ^ a[6] ^ a[11] ^ a[16] ^ a[21];
+  const uint64_t c2 = a[2] ^ a[7] ^ a[12] ^ a[17] ^ a[22], c3 = a[3] ^ a[8] ^ a[13] ^ a[18] ^ a[23];
+  const uint64_t c4 = a[4] ^ a[9] ^ a[14] ^ a[19] ^ a[24];
+  const uint64_t d0 = c4 ^ rotl64(c1, 1), d1 = c0 ^ rotl64(c2, 1), d2 = c1 ^ rotl64(c3, 1);
+  const uint64_t d3 = c2 ^ rotl64(c4, 1), d4 = c3 ^ rotl64(c0, 1);
+  // theta + rho + pi: b[y, 2x + 3y] = rotl(a[x, y] ^ d[x], r[x, y])
+  const uint64_t b00 = a[0] ^ d0, b10 = rotl64(a[6] ^ d1, 44), b20 = rotl64(a[12] ^ d2, 43);
+  const uint64_t b30 = rotl64(a[18] ^ d3, 21), b40 = rotl64(a[24] ^ d4, 14);
+  const uint64_t b01 = rotl64(a[3] ^ d3, 28), b11 = rotl64(a[9] ^ d4, 20), b21 = rotl64(a[10] ^ d0, 3);
+  const uint64_t b31 = rotl64(a[16] ^ d1, 45), b41 = rotl64(a[22] ^ d2, 61);
+  const uint64_t b02 = rotl64(a[1] ^ d1, 1), b12 = rotl64(a[7] ^ d2, 6), b22 = rotl64(a[13] ^ d3, 25);
+  const uint64_t b32 = rotl64(a[19] ^ d4, 8), b42 = rotl64(a[20] ^ d0, 18);
+  const uint64_t b03 = rotl64(a[4] ^ d4, 27), b13 = rotl64(a[5] ^ d0, 36), b23 = rotl64(a[11] ^ d1, 10);
+  const uint64_t b33 = rotl64(a[17] ^ d2, 15), b43 = rotl64(a[23] ^ d3, 56);
+  const uint64_t b04 = rotl64(a[2] ^ d2, 62), b14 = rotl64(a[8] ^ d3, 55), b24 = rotl64(a[14] ^ d4, 39);
+  const uint64_t b34 = rotl64(a[15] ^ d0, 41), b44 = rotl64(a[21] ^ d1, 2);
+  // chi (+ iota on lane 0); row y holds b[0..4][y]
+  a[0] = b00 ^ (~b10 & b20) ^ rc;
+  a[1] = b10 ^ (~b20 & b30);
+  a[2] = b20 ^ (~b30 & b40);
+  a[3] = b30 ^ (~b40 & b00);
+  a[4] = b40 ^ (~b00 & b10);
+  a[5] = b01 ^ (~b11 & b21);
+  a[6] = b11 ^ (~b21 & b31);
+  a[7] = b21 ^ (~b31 & b41);
+  a[8] = b31 ^ (~b41 & b01);
+  a[9] = b41 ^ (~b01 & b11);
+  a[10] = b02 ^ (~b12 & b22);
+  a[11] = b12 ^ (~b22 & b32);
+  a[12] = b22 ^ (~b32 & b42);
+  a[13] = b32 ^ (~b42 & b02);
+  a[14] = b42 ^ (~b02 & b12);
+  a[15] = b03 ^ (~b13 & b23);
+  a[16] = b13 ^ (~b23 & b33);
+  a[17] = b23 ^ (~b33 & b43);
+  a[18] = b33 ^ (~b43 & b03);
+  a[19] = b43 ^ (~b03 & b13);
+  a[20] = b04 ^ (~b14 & b24);
+  a[21] = b14 ^ (~b24 & b34);
+  a[22] = b24 ^ (~b34 & b44);
+  a[23] = b34 ^ (~b44 & b04);
+  a[24] = b44 ^ (~b04 & b14);
+}
+
+__device__ __forceinline__ void keccak_f1600_dev(uint64_t (&a)[25]) {
+  keccak_round_dev(a, 0x0000000000000001ull); keccak_round_dev(a, 0x0000000000008082ull);
+  keccak_round_dev(a, 0x800000000000808aull); keccak_round_dev(a, 0x8000000080008000ull);
+  keccak_round_dev(a, 0x000000000000808bull); keccak_round_dev(a, 0x0000000080000001ull);
+  keccak_round_dev(a, 0x8000000080008081ull); keccak_round_dev(a, 0x8000000000008009ull);
+  keccak_round_dev(a, 0x000000000000008aull); keccak_round_dev(a, 0x0000000000000088ull);
+  keccak_round_dev(a, 0x0000000080008009ull); keccak_round_dev(a, 0x000000008000000aull);
+  keccak_round_dev(a, 0x000000008000808bull); keccak_round_dev(a, 0x800000000000008bull);
+  keccak_round_dev(a, 0x8000000000008089ull); keccak_round_dev(a, 0x8000000000008003ull);
+  keccak_round_dev(a, 0x8000000000008002ull); keccak_round_dev(a, 0x8000000000000080ull);
+  keccak_round_dev(a, 0x000000000000800aull); keccak_round_dev(a, 0x800000008000000aull);
+  keccak_round_dev(a, 0x8000000080008081ull); keccak_round_dev(a, 0x8000000000008080ull);
+  keccak_round_dev(a, 0x0000000080000001ull); keccak_round_dev(a, 0x8000000080008008ull);
+}
+
+// Two waves.  The sponge lanes live in LDS while the 73 object bytes are XORed in at their
+// (run-time) byte positions -- thread k handles byte k -- so no register array is indexed at run
+// time; thread 0 runs the permutations on the lanes loaded into registers by constant index.
+__global__ __launch_bounds__(128) void k_fri_fs(DevTranscript* __restrict__ fs, const uint64_t* __restrict__ root,
+                                               uint64_t* __restrict__ root_out, fe* __restrict__ k_out, fe C, fe r2) {
+  __shared__ uint64_t S[25];
+  __shared__ uint64_t S2[17];  // bytes past the current block (absorbed after its permutation)
+  const uint32_t k = threadIdx.x;
+  if (k < 25) S[k] = fs->st[k];
+  if (k < 17) S2[k] = 0;
+  if (k < 8) root_out[k] = root[k];
+  const uint32_t pos = fs->plen;  // bytes already in the current block (< 136)
+  __syncthreads();
+  // the Root object (proof_stream_enum.rs:67-127): code 0, payload length 64 (u64 BE), digest
+  constexpr uint32_t kObj = 73;  // <= blockDim.x
+  uint32_t byte = 0;
+  if (k == 8) byte = 64;
+  if (k >= 9 && k < kObj) byte = (uint32_t)(root[(k - 9) >> 3] >> (8 * ((k - 9) & 7))) & 0xFF;
+  uint8_t* Sb = reinterpret_cast<uint8_t*>(S);
+  uint8_t* S2b = reinterpret_cast<uint8_t*>(S2);
+  const uint32_t p = pos + k;
+  if (k < kObj && byte) {
+    if (p < 136) Sb[p] ^= (uint8_t)byte;  // distinct bytes per lane: no two lanes touch one byte
+    else S2b[p - 136] = (uint8_t)byte;
+  }
+  __syncthreads();
+  uint32_t npos = pos + kObj;
+  if (npos >= 136) {  // the block is complete: permute, then the spill bytes start the next one
+    if (k == 0) {
+      uint64_t a[25];
+#pragma unroll
+      for (int i = 0; i < 25; ++i) a[i] = S[i];
+      keccak_f1600_dev(a);
+#pragma unroll
+      for (int i = 0; i < 25; ++i) S[i] = a[i] ^ (i < 17 ? S2[i] : 0);
+    }
+    npos -= 136;
+    __syncthreads();
+  }
+  if (k < 25) fs->st[k] = S[k];
+  if (k == 0) fs->plen = npos;
+  __syncthreads();
+  // fiat_shamir_prover(32): pad (SHAKE256 suffix 0x1F at npos, final bit 0x80 at byte 135), squeeze
+  if (k == 0) {
+    Sb[npos] ^= 0x1F;
+    Sb[135] ^= 0x80;
+    uint64_t a[25];
+#pragma unroll
+    for (int i = 0; i < 25; ++i) a[i] = S[i];
+    keccak_f1600_dev(a);
+    // Field::sample (field.rs:87-99): the last 16 of the 32 bytes, big-endian, mod p (< 2p)
+    const uint64_t hi = __builtin_bswap64(a[2]), lo = __builtin_bswap64(a[3]);
+    fe alpha = fe_make(lo, hi);
+    if (!fe_is_canonical(alpha)) alpha = fe_sub_lazy(alpha, fe_make(1, 0xCB8ull << 52));
+    st_fe(k_out, mont_mul(mont_mul(alpha, r2), C));
+  }
+}
+
+// HBM copy probe (measurement only): one 16-byte element per lane, non-temporal loads and stores
+// (streamed data: no cache keeps it).  tools/microbench_copy.hip measured this flat form fastest
+// (6.6 TB/s read + write over 2 GiB; grid-stride and chunked forms 4.7-5.6 TB/s).
+__global__ void __launch_bounds__(256) k_copy16(const sg_u32x4* __restrict__ src, sg_u32x4* __restrict__ dst,
+                                                uint64_t n) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+}
+
+// grid-stride form (the probe's comparison point: a fixed grid of `blocks`)
+__global__ void __launch_bounds__(256) k_copy16_stride(const sg_u32x4* __restrict__ src, sg_u32x4* __restrict__ dst,
+                                                       uint64_t n) {
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+}
+
 // gather from a list of absolute device addresses (one launch for every round's openings)
 // --------------------------------------------- proof-stream tail serialization
 
@@ -984,6 +1135,28 @@ hipError_t launch_gather_fe(const fe* src, const uint64_t* idx, fe* out, uint32_
 }
 
 static inline unsigned nblocks(uint64_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
+
+hipError_t launch_fri_fs(DevTranscript* fs, const uint64_t* root, uint64_t* root_out, fe* k_out, const fe& C,
+                         const fe& r2, hipStream_t s) {
+  ProfScope ps("fri_fs", 0, s);
+  hipLaunchKernelGGL(k_fri_fs, dim3(1), dim3(128), 0, s, fs, root, root_out, k_out, C, r2);
+  return hipGetLastError();
+}
+
+hipError_t launch_copy16(const void* src, void* dst, uint64_t bytes, unsigned blocks, hipStream_t s) {
+  if (bytes < 16) return hipSuccess;
+  const uint64_t n = bytes / 16;
+  ProfScope ps("copy16", 2 * bytes, s);
+  if (blocks == 0) {
+    if ((n + 255) / 256 > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_copy16, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s,
+                       static_cast<const sg_u32x4*>(src), static_cast<sg_u32x4*>(dst), n);
+  } else {
+    hipLaunchKernelGGL(k_copy16_stride, dim3(blocks), dim3(256), 0, s, static_cast<const sg_u32x4*>(src),
+                       static_cast<sg_u32x4*>(dst), n);
+  }
+  return hipGetLastError();
+}
 
 hipError_t launch_pow_table(fe* tw, const fe* A, const fe* B, uint64_t count, hipStream_t s) {
   if (count == 0) return hipSuccess;
@@ -1238,7 +1411,7 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
   //    fused through LDS (512 -> 64 lanes: every active wave full) when the tree is
   //    large enough to be throughput-bound, else the leaf level only;
   //    a tree of <= 1024 leaves with nothing above runs in one 1024-thread block.
-  //  * node levels with >= kQuadBelow digests: one lane per node, 4 levels fused;
+  //  * node levels with >= kQuadBelow digests: one lane per node, 3 levels fused;
   //  * smaller levels (latency-bound): a quad of lanes per node, up to 7 levels fused.
   // SG_MERKLE_QUAD_BELOW = log2 of the threshold (A/B only)
   static const uint64_t kQuadBelow = (uint64_t)1 << env_int("SG_MERKLE_QUAD_BELOW", 16);
@@ -1262,6 +1435,7 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
     a.fold.Thi = fold_here ? fold->Thi : nullptr;
     a.fold.shift = fold_here ? fold->shift : 0;
     a.fold.K = fold_here ? fold->K : fe_zero();
+    a.fold.Kp = fold_here ? fold->Kp : nullptr;
     a.leaves_ys = leaves_ys;
     a.tree_ys = tree_ys;
     a.root_level = (uint64_t)logn;
@@ -1269,7 +1443,7 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
     a.first_count = count;
     int fuse;
     unsigned bs;
-    int kind;  // 0: leaf 256, 1: leaf tail 1024, 2: node 256, 3: quad 64, 4: leaf 512, 5: quad 256
+    int kind;  // 0: leaf 256, 1: leaf tail 1024, 2: node 256, 3: quad 64, 4: leaf 512, 5: quad 256, 6: node 512
     if (level == 0) {
       if (count <= 64) {
         kind = 1; bs = (unsigned)count; fuse = logn + 1;
@@ -1285,8 +1459,12 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
         if (bs < lbs) kind = 0;
       }
     } else if (count >= kQuadBelow) {
-      static const int env_nfuse = env_int("SG_MERKLE_NODE_FUSE", 4);
-      kind = 2; bs = 256u; fuse = env_nfuse;
+      // 3 levels per launch: same-box A/Bs (profiles/r03_ab_merkle_nodes.log, r03_ab_nodes.log) put 3
+      // ahead of 4 on the 2^25 tree (4.03-4.09 vs 4.12-4.16 ms) and in the prove; coalesced child
+      // loads staged through LDS were slower (4.22-4.27 ms) and were dropped
+      static const int env_nfuse = env_int("SG_MERKLE_NODE_FUSE", 3);
+      static const int env_nbs = env_int("SG_MERKLE_NODE_BS", 256);  // A/B knob: 256 or 512
+      kind = env_nbs == 512 ? 6 : 2; bs = env_nbs == 512 ? 512u : 256u; fuse = env_nfuse;
     } else {
       // the last <= 256 nodes of a tree go to the root in one 1024-lane block
       // (SG_MERKLE_QUAD_TOP=0: 64-node blocks only)
@@ -1310,7 +1488,7 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
     uint64_t digests = 0;
     for (int k = 0; k < fuse; ++k) digests += count >> k;
     // a fused fold reads 2 source elements and writes the folded one instead of reading the leaf
-    const uint64_t per_block = kind >= 3 && kind != 4 ? bs / 4 : bs;
+    const uint64_t per_block = kind == 3 || kind == 5 ? bs / 4 : bs;  // quad kernels: 4 lanes per node
     dim3 grid((unsigned)((count + per_block - 1) / per_block), batch);
     // elems = lanes launched (the rocprofv3 Grid_Size of this dispatch), so per-wave PMC
     // instruction counts scale to any launch population
@@ -1328,6 +1506,7 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
         else hipLaunchKernelGGL((k_merkle_levels<true, 1024>), grid, dim3(bs), 0, s, a);
         break;
       case 2: hipLaunchKernelGGL((k_merkle_levels<false, 256>), grid, dim3(bs), 0, s, a); break;
+      case 6: hipLaunchKernelGGL((k_merkle_levels<false, 512>), grid, dim3(bs), 0, s, a); break;
       case 4:
         if (fold_here) hipLaunchKernelGGL((k_merkle_levels<true, 512, true>), grid, dim3(bs), 0, s, a);
         else hipLaunchKernelGGL((k_merkle_levels<true, 512>), grid, dim3(bs), 0, s, a);

@@ -55,7 +55,19 @@ struct FoldLeaves {
   const fe* Thi;
   int shift;
   fe K;
+  const fe* Kp = nullptr;  // != nullptr: K read from device memory (k_fri_fs) instead
 };
+// FRI commit's Fiat-Shamir continued on the device (k_fri_fs): the SHAKE256 sponge lanes with the
+// current partial block already XORed in, and the number of bytes in that block
+struct DevTranscript {
+  uint64_t st[25];
+  uint32_t plen;
+  uint32_t pad_;
+};
+// absorb the Root object of `root` (a tree's root digest, 8 u64), copy the digest to root_out,
+// squeeze 32 bytes and store K = Montgomery(sample(bytes) * C), C = Montgomery(offset_r^-1 2^-1)
+hipError_t launch_fri_fs(DevTranscript* fs, const uint64_t* root, uint64_t* root_out, fe* k_out, const fe& C,
+                         const fe& r2, hipStream_t s);
 // root_flag (optional, with root_host): set to root_seq after the root is visible to the host.
 hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, int batch, uint64_t n,
                               uint64_t* const* root_host, hipStream_t s, uint64_t leaves_ys = 0,
@@ -63,6 +75,9 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
                               uint64_t root_seq = 0, const FoldLeaves* fold = nullptr);
 hipError_t launch_gather_digests(const uint64_t* tree, const uint64_t* idx, uint64_t* out, uint32_t count,
                                  hipStream_t s);
+// HBM probe: dst[0, bytes) = src (16-byte units, bytes % 16 == 0); blocks = 0: one element per
+// lane, else `blocks` x 256 lanes grid-stride
+hipError_t launch_copy16(const void* src, void* dst, uint64_t bytes, unsigned blocks, hipStream_t s);
 hipError_t launch_gather_fe(const fe* src, const uint64_t* idx, fe* out, uint32_t count, hipStream_t s);
 
 // Proof-stream objects serialized on the device (the tail of a proof: FRI query phase and the

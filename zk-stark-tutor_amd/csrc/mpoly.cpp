@@ -1,4 +1,6 @@
 // MPolynomial (m_polynomial.rs) in grouped form, and its C ABI.  See mpoly.hpp.
+#include <atomic>
+#include <mutex>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -151,17 +153,20 @@ MPoly mp_pow(sg_ctx* ctx, const MPoly& a, unsigned __int128 e) {
   return acc;
 }
 
-RescueXPolys::~RescueXPolys() {
-  for (auto& kv : coset) (void)hipFree(kv.second);
+uint64_t next_constraint_id() {
+  static std::atomic<uint64_t> next{1};
+  return next.fetch_add(1);
 }
 
 MPolyDevice::~MPolyDevice() {
   for (void* p : ptr)
     if (p) (void)hipFree(p);
-  for (auto& kv : coset) (void)hipFree(kv.second);
 }
 
 const MPolyDevice& mp_device(sg_ctx* ctx, const MPoly& a) {
+  // contexts on several host threads may share a constraint: its device copy is made once
+  static std::mutex mu;
+  std::lock_guard<std::mutex> lk(mu);
   if (a.dev && a.dev->device == ctx->device) return *a.dev;
   auto d = std::make_shared<MPolyDevice>();
   d->device = ctx->device;

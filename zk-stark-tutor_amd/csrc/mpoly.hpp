@@ -23,18 +23,22 @@
 
 namespace sg {
 
+// identity of a constraint's device data: the key of its coset values in a context's domain tables
+uint64_t next_constraint_id();
+
 // device-resident copies of the group x-vectors (trimmed at their degree), uploaded on first
 // use by the prover: the constraints are an input of every proof, like the trace
 struct MPolyDevice {
   int device = -1;
+  uint64_t id = next_constraint_id();
   std::vector<void*> ptr;       // distinct x-polynomials up to a scalar (first non-zero coefficient 1)
   std::vector<uint64_t> len;    // their degree + 1
   std::vector<HPoly> small;     // host copy of those with len <= kSmallPolyMax (else empty)
   std::vector<int32_t> qidx;    // per group (map order): index into ptr, -1 for an all-zero group
   std::vector<fe> scale;        // per group: x-polynomial = scale * ptr[qidx]
-  // values of x-polynomial q on a coset {q, L, offset limbs} -> L elements: public (the AIR and the
-  // domain), kept like the context's domain tables (stark.cpp transition_values)
-  mutable std::map<std::vector<uint64_t>, void*> coset;
+  // (the values of x-polynomial q on a coset are public -- the AIR and the domain -- and live in
+  // the proving context's domain tables under {kDomainMpolyCoset, id, q, L, offset}: per context,
+  // so two contexts never share a table filled on another stream, and sg_ctx_trim frees them)
   ~MPolyDevice();
 };
 
@@ -42,9 +46,9 @@ struct MPolyDevice {
 // second_0..m-1) and their values on the cosets the prover evaluates it on (public, kept like the
 // context's domain tables; the key carries the device).
 struct RescueXPolys {
+  uint64_t id = next_constraint_id();
   std::vector<HPoly> polys;  // first_0 .. first_{m-1}, second_0 .. second_{m-1}
-  mutable std::map<std::vector<uint64_t>, void*> coset;  // {device, poly, L, offset lo, hi} -> L values
-  ~RescueXPolys();
+  // (their coset values: the context's domain tables, {kDomainRescueCoset, id, poly, L, offset})
 };
 
 // A transition constraint built by the native Rescue-Prime AIR (rescue_prime.rs:246-283) also

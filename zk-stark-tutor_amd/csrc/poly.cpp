@@ -321,7 +321,7 @@ DPoly fast_coset_divide_dev(sg_ctx* ctx, fe root, uint64_t root_order, const fe&
         (void)hipFree(t);
         throw;
       }
-      ctx->domain_table_put(key, t);
+      ctx->domain_table_put_bounded(key, t);
       inv = static_cast<const fe*>(t);
     }
     return coset_divide_finish(ctx, pl, offset, vl.as<fe>(), inv, true);

@@ -437,11 +437,9 @@ DPoly transition_values_rescue(sg_ctx* ctx, const RescueAirForm& f, const AirCos
   const int m = f.m;
   const bool kept = ctx->domain_cache_on();
   auto xvals = [&](int idx) -> const fe* {
-    const std::vector<uint64_t> key = {(uint64_t)ctx->device, (uint64_t)idx, L, fe_lo(offset), fe_hi(offset)};
-    if (kept) {
-      auto it = f.xp->coset.find(key);
-      if (it != f.xp->coset.end()) return static_cast<const fe*>(it->second);
-    }
+    const std::vector<uint64_t> key = {kDomainRescueCoset, f.xp->id, (uint64_t)idx, L, fe_lo(offset), fe_hi(offset)};
+    if (kept)
+      if (void* t = ctx->domain_table(key)) return static_cast<const fe*>(t);
     const HPoly& hp = f.xp->polys[(size_t)idx];
     const int64_t deg = hp_degree(hp);
     void* t = nullptr;
@@ -466,7 +464,7 @@ DPoly transition_values_rescue(sg_ctx* ctx, const RescueAirForm& f, const AirCos
       if (t) (void)hipFree(t);
       throw;
     }
-    if (kept) f.xp->coset[key] = t;
+    if (kept) ctx->domain_table_put(key, t);
     return out;
   };
   AirRescueArgs a{};
@@ -507,11 +505,10 @@ DPoly transition_values(sg_ctx* ctx, const MPoly& tc, const AirCoset& co, const 
   std::vector<const fe*> qp;   // per distinct x-polynomial: its values on the coset
   const bool kept = ctx->domain_cache_on();
   for (size_t q = 0; q < xd.ptr.size(); ++q) {
-    const std::vector<uint64_t> key = {q, L, fe_lo(offset), fe_hi(offset)};
+    const std::vector<uint64_t> key = {kDomainMpolyCoset, xd.id, q, L, fe_lo(offset), fe_hi(offset)};
     if (kept) {
-      auto it = xd.coset.find(key);
-      if (it != xd.coset.end()) {
-        qp.push_back(static_cast<const fe*>(it->second));
+      if (void* t = ctx->domain_table(key)) {
+        qp.push_back(static_cast<const fe*>(t));
         continue;
       }
     }
@@ -532,7 +529,7 @@ DPoly transition_values(sg_ctx* ctx, const MPoly& tc, const AirCoset& co, const 
       void* t = nullptr;
       SG_HIP(hipMalloc(&t, L * sizeof(fe)));
       SG_HIP(hipMemcpyAsync(t, out, L * sizeof(fe), hipMemcpyDeviceToDevice, ctx->stream));
-      xd.coset[key] = t;
+      ctx->domain_table_put(key, t);
       qp.push_back(static_cast<const fe*>(t));
     } else {
       qp.push_back(out);

@@ -172,7 +172,8 @@ void Stream::fiat_shamir(size_t cnt, size_t num_bytes, uint8_t* out) const {
   shake256(in.data(), in.size(), out, num_bytes);
 }
 
-void Stream::fiat_shamir_all(size_t num_bytes, uint8_t* out) {
+// absorbs every complete block of fs_head || body not yet absorbed; returns the byte total
+size_t Stream::fs_absorb_full() {
   const size_t R = 136;  // SHAKE256 rate
   if (!fs_valid || fs_field != field) {
     fs_head.clear();
@@ -188,22 +189,11 @@ void Stream::fiat_shamir_all(size_t num_bytes, uint8_t* out) {
     fs_valid = true;
   }
   const size_t H = fs_head.size(), total = H + body.n;
-  // bytes [off, off + len) of fs_head || body
-  auto gather = [&](size_t off, size_t len, uint8_t* dst) {
-    if (off < H) {
-      const size_t a = len < H - off ? len : H - off;
-      memcpy(dst, fs_head.data() + off, a);
-      dst += a;
-      off += a;
-      len -= a;
-    }
-    if (len) memcpy(dst, body.data() + (off - H), len);
-  };
   uint8_t tmp[R];
   size_t b = fs_absorbed / R;
   const size_t full = total / R;
   for (; b < full && b * R < H; ++b) {  // blocks that start in the head
-    gather(b * R, R, tmp);
+    fs_gather(b * R, R, tmp);
     fs_sponge.absorb_blocks(tmp, 1);
   }
   if (b < full) {  // the rest straight from the body
@@ -211,9 +201,35 @@ void Stream::fiat_shamir_all(size_t num_bytes, uint8_t* out) {
     b = full;
   }
   fs_absorbed = full * R;
+  return total;
+}
+
+// bytes [off, off + len) of fs_head || body
+void Stream::fs_gather(size_t off, size_t len, uint8_t* dst) const {
+  const size_t H = fs_head.size();
+  if (off < H) {
+    const size_t a = len < H - off ? len : H - off;
+    memcpy(dst, fs_head.data() + off, a);
+    dst += a;
+    off += a;
+    len -= a;
+  }
+  if (len) memcpy(dst, body.data() + (off - H), len);
+}
+
+void Stream::fiat_shamir_all(size_t num_bytes, uint8_t* out) {
+  const size_t total = fs_absorb_full();
+  uint8_t tmp[136];
   const size_t tail = total - fs_absorbed;
-  gather(fs_absorbed, tail, tmp);
+  fs_gather(fs_absorbed, tail, tmp);
   fs_sponge.finish(tmp, tail, out, num_bytes);
+}
+
+void Stream::fs_snapshot(uint64_t lanes[25], uint8_t* pending, size_t* pending_len) {
+  const size_t total = fs_absorb_full();
+  memcpy(lanes, fs_sponge.st, sizeof(fs_sponge.st));
+  *pending_len = total - fs_absorbed;
+  fs_gather(fs_absorbed, *pending_len, pending);
 }
 
 bool deserialize_stream(const uint8_t* b, size_t len, Stream& s, std::string& err) {

@@ -132,6 +132,12 @@ class Context:
     def trim(self) -> None:
         self.check(self._lib.sg_ctx_trim(self.handle))
 
+    def hbm_copy_gbs(self, nbytes: int = 1 << 30, iters: int = 10, blocks: int = 0) -> float:
+        """Read + write GB/s of the library's dwordx4 streaming copy kernel (best of `iters`)."""
+        out = ctypes.c_double()
+        self.check(self._lib.sg_hbm_copy_probe(self.handle, nbytes, iters, blocks, ctypes.byref(out)))
+        return out.value
+
     def close(self) -> None:
         if self.handle:
             self._lib.sg_ctx_destroy(self.handle)
