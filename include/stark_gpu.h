@@ -368,6 +368,18 @@ int sg_stark_prove_dev(sg_ctx* ctx, const sg_stark* st, const sg_fe* d_trace, si
                        const sg_mpoly* const* tcs, size_t ntcs, const sg_boundary* boundary, size_t nb,
                        const sg_fe* d_trace_randomizers, const sg_fe* d_randomizer_coeffs, size_t n_rc,
                        const sg_proof_stream* ps);
+/* stark.rs:276-562 Stark::prove with the codeword domain sharded over the communicator (replaces
+ * Stark::prove when the FRI domain is split across GPUs).  Every rank passes the same arguments
+ * (st and tcs created on the communicator's context, sg_dist_ctx) and writes the same proof-stream
+ * bytes as sg_stark_prove: the trace-domain algebra is replicated, the four LDEs, the three
+ * commitments, FRI::prove and the openings run on run shards of N_fri / world elements. */
+int sg_dist_stark_prove(sg_dist* d, const sg_stark* st, const sg_fe* trace, size_t rows, const sg_mpoly* const* tcs,
+                        size_t ntcs, const sg_boundary* boundary, size_t nb, const sg_fe* trace_randomizers,
+                        const sg_fe* randomizer_coeffs, size_t n_rc, const sg_proof_stream* ps);
+int sg_dist_stark_prove_dev(sg_dist* d, const sg_stark* st, const sg_fe* d_trace, size_t rows,
+                            const sg_mpoly* const* tcs, size_t ntcs, const sg_boundary* boundary, size_t nb,
+                            const sg_fe* d_trace_randomizers, const sg_fe* d_randomizer_coeffs, size_t n_rc,
+                            const sg_proof_stream* ps);
 
 #ifdef __cplusplus
 }

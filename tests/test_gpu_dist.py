@@ -10,6 +10,7 @@
   suite pins to the oracle).
 """
 import ctypes
+import json
 import os
 import socket
 
@@ -393,3 +394,123 @@ def test_north_star_sharded_lde_fri_prove(north_star_reference, world):
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     mp.spawn(_north_star_worker, args=(world, port, north_star_reference), nprocs=world, join=True)
+
+
+# ------------------------------------------------------------------ sharded Stark::prove
+
+# (N, expansion, colinearity checks, security, transition degree): FRI domains 2^9 .. 2^21
+STARK_CASES = [(40, 4, 3, 4, 2), (27, 8, 4, 8, 3), (100, 8, 8, 16, 3), (65278, 8, 64, 128, 3)]
+
+
+@pytest.fixture(scope="module")
+def stark_reference():
+    """Rescue-Prime Stark::prove inputs and expected proof bytes per case: the oracle's bytes for
+    the small cases, the single-GPU bytes at C4 (pinned to the CPU checker by
+    test_gpu_fullsize.py::test_c4_proof_bytes_equal_checker).  Plus one false witness."""
+    import shutil
+    import tempfile
+    import stark_prove_oracle as e
+    import starkgpu as sg
+    tmp = tempfile.mkdtemp(prefix="sg_dstark_")
+    try:
+        for k, (N, exp, c, sec, tcd) in enumerate(STARK_CASES):
+            seed = b"dist-stark-%d" % k
+            rp_o = e.RescuePrime(2, 1, sec, N)
+            st_g = sg.Stark(exp, c, sec, 2, N + 1, tcd)
+            rp_g = sg.RescuePrime(2, 1, sec, N)
+            air_g = rp_g.transition_constraints(st_g.omicron, st_g.omicron_domain_length)
+            inp = o.sample(seed)
+            trace = rp_g.trace_array(inp)
+            if k == 1:  # a false witness: the reference still writes a (rejected) proof
+                t = sg.to_ints(trace)
+                t[9] = o.add_mod(t[9], 3)
+                trace = sg.fe_array(t)
+            nrc = st_g.num_randomizer_coefficients(air_g)
+            r = e.randomness_from_seed(seed, 2 * st_g.num_randomizers + nrc)
+            tr, rc = sg.fe_array(r[:2 * st_g.num_randomizers]), sg.fe_array(r[2 * st_g.num_randomizers:])
+            bnd = rp_o.boundary_constraints(rp_o.hash(inp))
+            if N < 1000:
+                st_o = e.Stark(exp, c, sec, 2, N + 1, tcd)
+                air_o = rp_o.transition_constraints(st_o.omicron, st_o.omicron_domain_length)
+                rows = sg.to_ints(trace)
+                want = st_o.prove([rows[2 * i:2 * i + 2] for i in range(len(rows) // 2)], air_o, bnd,
+                                  o.IndependentProofStream(), [r[2 * i:2 * i + 2] for i in range(st_g.num_randomizers)],
+                                  r[2 * st_g.num_randomizers:])
+            else:
+                want = st_g.prove(trace, air_g, bnd, sg.IndependentProofStream(), tr, rc)
+            np.save(os.path.join(tmp, "trace%d.npy" % k), trace)
+            np.save(os.path.join(tmp, "tr%d.npy" % k), tr)
+            np.save(os.path.join(tmp, "rc%d.npy" % k), rc)
+            with open(os.path.join(tmp, "bnd%d.json" % k), "w") as f:
+                json.dump([[int(a), int(b), str(v)] for (a, b, v) in bnd], f)
+            with open(os.path.join(tmp, "proof%d.bin" % k), "wb") as f:
+                f.write(want)
+        yield tmp
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
+
+
+def _stark_checks(nd, world, rank, tmp, cases, gather):
+    """Every case proved with sg_dist_stark_prove on this rank: bytes == expected on every rank."""
+    import starkgpu as sg
+    ok = []
+    for k in cases:
+        N, exp, c, sec, tcd = STARK_CASES[k]
+        st = sg.Stark(exp, c, sec, 2, N + 1, tcd, ctx=nd.ctx)
+        air = sg.RescuePrime(2, 1, sec, N, ctx=nd.ctx).transition_constraints(st.omicron, st.omicron_domain_length)
+        with open(os.path.join(tmp, "bnd%d.json" % k)) as f:
+            bnd = [(a, b, int(v)) for (a, b, v) in json.load(f)]
+        trace = np.load(os.path.join(tmp, "trace%d.npy" % k))
+        tr, rc = np.load(os.path.join(tmp, "tr%d.npy" % k)), np.load(os.path.join(tmp, "rc%d.npy" % k))
+        got = st.prove(trace, air, bnd, sg.IndependentProofStream(), tr, rc, dist=nd)
+        ok.append((k, got == open(os.path.join(tmp, "proof%d.bin" % k), "rb").read()))
+    flags = gather(ok)
+    assert all(f for per_rank in flags for (_, f) in per_rank), f"world {world}: sharded proof bytes differ: {flags}"
+
+
+def test_dist_stark_prove_world1_rccl(stark_reference):
+    """sg_dist_stark_prove over a 1-rank RCCL communicator: the single-GPU / oracle proof bytes."""
+    import starkgpu as sg
+    from starkgpu import dist as D
+    ctx = sg.Context(0)
+    nd = D.NativeDist(ctx, transport="rccl")
+    try:
+        _stark_checks(nd, 1, 0, stark_reference, range(len(STARK_CASES)), lambda a: [a])
+        st = sg.Stark(4, 3, 4, 2, 41, 2)  # created on another context
+        with pytest.raises(ValueError):
+            st.prove([[0, 0]], [], [], sg.IndependentProofStream(), [[0, 0]] * st.num_randomizers, [0], dist=nd)
+    finally:
+        nd.close()
+
+
+def _stark_worker(rank, world, port, tmp, cases):
+    import torch.distributed as dist
+    import starkgpu as sg
+    from starkgpu import dist as D
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        nd = D.NativeDist(sg.Context(0), transport="host")
+
+        def gather(a):
+            out = [None] * world
+            dist.all_gather_object(out, a)
+            return out
+
+        _stark_checks(nd, world, rank, tmp, cases, gather)
+        nd.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("world,cases", [(2, (0, 1, 2, 3)), (4, (1, 2)), (8, (0, 1, 2, 3))])
+def test_dist_stark_prove_one_gpu_host_transport(stark_reference, world, cases):
+    """Stark::prove (stark.rs:276-562) with the FRI domain sharded over `world` ranks on this box's
+    GPU (host transport over gloo): every rank writes the expected proof bytes, C4 included."""
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.spawn(_stark_worker, args=(world, port, stark_reference, cases), nprocs=world, join=True)

@@ -32,6 +32,7 @@
 #include <memory>
 #include <vector>
 
+#include "dist.hpp"
 #include "host_field.hpp"
 #include "internal.hpp"
 
@@ -169,6 +170,8 @@ void four_step(sg_dist* d, const fe& root, const fe* in, uint64_t row_len, uint6
   }
 }
 
+}  // namespace
+
 void dist_ntt(sg_dist* d, const fe& root, const fe* cols, uint64_t row_len, uint64_t n, fe* runs) {
   uint64_t n1, n2;
   plan(n, d->G, n1, n2);
@@ -208,21 +211,11 @@ void dist_coset_evaluate(sg_dist* d, const fe& gen, uint64_t n, const fe& offset
   dist_ntt(d, gen, sc.as<fe>(), row_len, n, runs);
 }
 
-// A sharded FRI round kept for the query phase: the rank's runs, its forest (one subtree of R
-// leaves per run) and the top tree over the G k1s run roots in global run order (every rank).
-struct ShardedRound {
-  uint64_t k1s = 0, m = 0, per = 0;  // runs per rank, run roots overall, u64 per subtree
-  const fe* cw = nullptr;            // [k1s][R]
-  DevBuf cw_own;
-  DevBuf forest;
-  DevBuf top;                        // m leaves' tree (absent for m == 1)
-};
-
 // root of the natural-order codeword held as runs [k1s][R] on every rank (merkle_root.rs:21-32):
 // a forest of k1s subtrees per rank, the run roots all-gathered (64 B each), the top on every rank.
 // With `keep`, the forest and the top tree move into it (openings).
 void dist_merkle_root(sg_dist* d, const fe* runs, uint64_t k1s, uint64_t R, uint8_t root[64],
-                      ShardedRound* keep = nullptr) {
+                      ShardedRound* keep) {
   sg_ctx* ctx = d->ctx;
   SG_REQUIRE(R >= 1 && (R & (R - 1)) == 0 && k1s >= 1 && (k1s & (k1s - 1)) == 0, "Leafs len must be power of two");
   const uint64_t per = merkle_tree_digests(R) * 8;  // u64 per subtree
@@ -262,15 +255,18 @@ void dist_merkle_root(sg_dist* d, const fe* runs, uint64_t k1s, uint64_t R, uint
   }
 }
 
-// What FRI::prove's query phase (fri.rs:174-248) reads after a sharded commit: the sharded rounds
-// (runs, forests, top trees) and, when the commit finished on the gathered codeword, the
-// single-GPU state of the remaining rounds (identical on every rank).
-struct DistFriState {
-  uint64_t n2 = 0, R = 0;
-  std::vector<ShardedRound> sharded;
-  sg_fri_state tail;
-  std::vector<uint64_t> lengths;  // every round's codeword length
-};
+void dist_lde_replicated(sg_dist* d, const fe& gen, uint64_t n, const fe& offset, const fe* coeffs, uint64_t len,
+                         fe* runs) {
+  uint64_t n1, n2;
+  plan(n, d->G, n1, n2);
+  SG_REQUIRE(len <= n, "fast_coset_evaluate: polynomial longer than root_order");
+  const uint64_t rows = n1 / d->G;
+  const uint64_t row_len = std::max<uint64_t>((len + n1 - 1) / n1, 1);
+  // column shard: row r = coefficients (g rows + r) + N1 j, zero past len
+  DevBuf cols(d->ctx, rows * row_len * sizeof(fe));
+  SG_HIP(launch_gather_cols(cols.as<fe>(), coeffs, len, rows, row_len, n1, (uint64_t)d->g * rows, d->ctx->stream));
+  dist_coset_evaluate(d, gen, n, offset, cols.as<fe>(), row_len, runs);
+}
 
 // fri.rs:115-172 on a run-sharded codeword.  The fold partner of i is i + n/2: same k2,
 // k1 + N1/2, i.e. on the same rank, so folds stay local while more than one run per rank is
@@ -391,8 +387,14 @@ void dist_open(sg_dist* d, const DistFriState& s, size_t r, const std::vector<ui
     gather_digests(ctx, tree, pidx, paths.data());  // synchronizes the stream
     return;
   }
-  const ShardedRound& sr = s.sharded[r];
-  const uint64_t R = s.R, n2 = s.n2;
+  dist_open_round(d, s.sharded[r], s.R, s.n2, I, vals, paths, depth);
+}
+
+void dist_open_round(sg_dist* d, const ShardedRound& sr, uint64_t R, uint64_t n2, const std::vector<uint64_t>& I,
+                     std::vector<fe>& vals, std::vector<uint8_t>& paths, int& depth) {
+  sg_ctx* ctx = d->ctx;
+  const size_t q = I.size();
+  vals.assign(q, fe_zero());
   const int lr = ilog2_exact(R), lm = ilog2_exact(sr.m);
   depth = lr + lm;
   const size_t slot = 16 + 64 * (size_t)lr;
@@ -462,7 +464,7 @@ void dist_open(sg_dist* d, const DistFriState& s, size_t r, const std::vector<ui
 // sample_indices over len(codewords[1]) reduced by len(codewords[-1]) (fri.rs:88-113), then per
 // round the c Leafs objects and 3c Path objects (fri.rs:174-208) -- every rank writes the same bytes.
 void dist_fri_prove(sg_dist* d, const sg_fri* f, const fe* runs, uint64_t n, const sg_proof_stream* ps,
-                    size_t* top) {
+                    size_t* top, const std::function<void(const size_t* top)>& extra) {
   DistFriState s;
   dist_fri_commit(d, f, runs, n, ps, &s);
   SG_REQUIRE(s.lengths.size() >= 2, "FRI prove needs at least two rounds (reference indexes codewords[1])");
@@ -505,6 +507,7 @@ void dist_fri_prove(sg_dist* d, const sg_fri* f, const fe* runs, uint64_t n, con
       put_path(pc.data() + k * (size_t)dc * 64, dc);
     }
   }
+  if (extra) extra(top);
 }
 
 sg_dist* checked(sg_dist* d) {
@@ -512,7 +515,10 @@ sg_dist* checked(sg_dist* d) {
   return d;
 }
 
-}  // namespace
+sg_ctx* dist_ctx(sg_dist* d) { return d->ctx; }
+int dist_world(const sg_dist* d) { return d->G; }
+void dist_plan(uint64_t n, int G, uint64_t& n1, uint64_t& n2) { plan(n, G, n1, n2); }
+
 }  // namespace sg
 
 using namespace sg;

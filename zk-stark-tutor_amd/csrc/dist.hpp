@@ -1,0 +1,51 @@
+// Library-internal multi-GPU pieces shared by dist.cpp and the sharded Stark::prove (stark.cpp).
+#pragma once
+#include <cstdint>
+#include <functional>
+#include <vector>
+
+#include "internal.hpp"
+
+namespace sg {
+
+// A sharded FRI round kept for the query phase: the rank's runs, its forest (one subtree of R
+// leaves per run) and the top tree over the G k1s run roots in global run order (every rank).
+struct ShardedRound {
+  uint64_t k1s = 0, m = 0, per = 0;  // runs per rank, run roots overall, u64 per subtree
+  const fe* cw = nullptr;            // [k1s][R]
+  DevBuf cw_own;
+  DevBuf forest;
+  DevBuf top;                        // m leaves' tree (absent for m == 1)
+};
+
+// What FRI::prove's query phase (fri.rs:174-248) reads after a sharded commit: the sharded rounds
+// (runs, forests, top trees) and, when the commit finished on the gathered codeword, the
+// single-GPU state of the remaining rounds (identical on every rank).
+struct DistFriState {
+  uint64_t n2 = 0, R = 0;
+  std::vector<ShardedRound> sharded;
+  sg_fri_state tail;
+  std::vector<uint64_t> lengths;  // every round's codeword length
+};
+
+sg_ctx* dist_ctx(sg_dist* d);
+int dist_world(const sg_dist* d);
+// sg_dist_plan: n = N1 N2, N1 = 2^floor(log2 n / 2); run shards hold N1 runs of N2 / G elements
+void dist_plan(uint64_t n, int G, uint64_t& n1, uint64_t& n2);
+// fft/ntt_arithmetics.rs:161-170 of a coefficient vector every rank holds (device, len <= n) into
+// this rank's run shard [N1][N2 / G] (its column shard gathered first)
+void dist_lde_replicated(sg_dist* d, const fe& gen, uint64_t n, const fe& offset, const fe* coeffs, uint64_t len,
+                         fe* runs);
+// merkle_root.rs:21-32 of a run-sharded codeword; with `keep`, the forest and top tree are retained
+void dist_merkle_root(sg_dist* d, const fe* runs, uint64_t k1s, uint64_t R, uint8_t root[64],
+                      ShardedRound* keep = nullptr);
+// values and authentication paths (leaf level first) of global indices I of a sharded codeword,
+// identical on every rank: one all-gather of the owners' slots plus the local top tree
+void dist_open_round(sg_dist* d, const ShardedRound& sr, uint64_t R, uint64_t n2, const std::vector<uint64_t>& I,
+                     std::vector<fe>& vals, std::vector<uint8_t>& paths, int& depth);
+// fri.rs:210-248 on a run-sharded codeword; `extra` (optional) pushes further objects after the
+// query phase, given the top-level indices
+void dist_fri_prove(sg_dist* d, const sg_fri* f, const fe* runs, uint64_t n, const sg_proof_stream* ps, size_t* top,
+                    const std::function<void(const size_t* top)>& extra = {});
+
+}  // namespace sg

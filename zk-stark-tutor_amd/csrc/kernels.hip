@@ -908,6 +908,15 @@ __global__ void k_gather_digests(const uint64_t* __restrict__ tree, const uint64
   st_digest(out + (uint64_t)i * 8, d);
 }
 
+// column shard of a replicated coefficient vector: out[r][j] = in[base + r + n1 j] (0 past len)
+__global__ void k_gather_cols(fe* __restrict__ out, const fe* __restrict__ in, uint64_t len, uint64_t rows,
+                              uint64_t row_len, uint64_t n1, uint64_t base) {
+  const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (t >= rows * row_len) return;
+  const uint64_t r = t / row_len, j = t % row_len, src = base + r + n1 * j;
+  st_fe(out + t, src < len ? ld_fe(in + src) : fe_zero());
+}
+
 __global__ void k_gather_fe(const fe* __restrict__ src, const uint64_t* __restrict__ idx, fe* __restrict__ out,
                             uint32_t count) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1124,6 +1133,17 @@ hipError_t launch_serialize_tail(const TailItem* items, uint32_t count, uint8_t*
   if (!count) return hipSuccess;
   ProfScope ps("serialize_tail", bytes, s);
   hipLaunchKernelGGL(k_serialize_tail, dim3(count), dim3(64), 0, s, items, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_gather_cols(fe* out, const fe* in, uint64_t len, uint64_t rows, uint64_t row_len, uint64_t n1,
+                              uint64_t base, hipStream_t s) {
+  const uint64_t total = rows * row_len;
+  if (!total) return hipSuccess;
+  if ((total + 255) / 256 > 0x7FFFFFFFull) return hipErrorInvalidValue;
+  ProfScope ps("gather_cols", 32 * total, s);
+  hipLaunchKernelGGL(k_gather_cols, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, out, in, len, rows, row_len,
+                     n1, base);
   return hipGetLastError();
 }
 

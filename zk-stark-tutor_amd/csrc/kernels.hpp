@@ -79,6 +79,9 @@ hipError_t launch_gather_digests(const uint64_t* tree, const uint64_t* idx, uint
 // lane, else `blocks` x 256 lanes grid-stride
 hipError_t launch_copy16(const void* src, void* dst, uint64_t bytes, unsigned blocks, hipStream_t s);
 hipError_t launch_gather_fe(const fe* src, const uint64_t* idx, fe* out, uint32_t count, hipStream_t s);
+// out[r][j] = in[base + r + n1 j] for r < rows, j < row_len (0 past len): a column shard
+hipError_t launch_gather_cols(fe* out, const fe* in, uint64_t len, uint64_t rows, uint64_t row_len, uint64_t n1,
+                              uint64_t base, hipStream_t s);
 
 // Proof-stream objects serialized on the device (the tail of a proof: FRI query phase and the
 // Stark openings): [code u8][len u64 BE][payload] at byte offset `dst` of the output, with

@@ -18,6 +18,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <array>
 #include <cstdio>
 #include <map>
 #include <cstring>
@@ -26,6 +27,7 @@
 #include <string>
 #include <vector>
 
+#include "dist.hpp"
 #include "host_field.hpp"
 #include "host_hash.hpp"
 #include "internal.hpp"
@@ -632,61 +634,26 @@ struct AsyncScope {
   ~AsyncScope() { ctx->async_dev = prev; }
 };
 
-// stark.rs:276-562
-// d_trace: rows x m (row-major), d_trace_rand: num_randomizers x m, d_rcoef: nrc -- all on the device
-void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows,
-                 const std::vector<const MPoly*>& tcs, const std::vector<Boundary>& bnd, const fe* d_trace_rand,
-                 const fe* d_rcoef, size_t nrc, const sg_proof_stream* ps) {
-  SG_REQUIRE(ps && ps->push && ps->fiat_shamir_prover, "proof stream callbacks required");
+// The algebra of Stark::prove (stark.rs:285-512) on one context, in phases: the trace polynomials,
+// the boundary quotients, the transition quotients with every quotient's degree, and the
+// combination polynomial.  The single-GPU prover interleaves its codeword LDEs and side-stream
+// trees between these phases; the sharded prover (sg_dist_stark_prove) runs them as they are on
+// every rank (the trace-domain work is replicated, the codeword-domain work sharded).
+struct ProveAlgebra {
+  uint64_t Tp = 0;                     // randomized trace length
+  std::vector<DPoly> trace_polys, bqs, tqs;
+  std::vector<HPoly> bz;               // boundary zerofiers (host)
+  std::vector<int64_t> qdeg;           // transition quotients' degrees, then the boundary quotients'
+  std::vector<DPoly> wrapped;          // products that wrap the omicron domain (alive for the combination)
+};
+
+// randomized trace (stark.rs:285-324): columns gathered on the device, geometric interpolation
+void prove_trace_polys(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows, const fe* d_trace_rand,
+                       ProveAlgebra& A) {
   const size_t m = st.m;
-  const uint64_t D = st.D;
-  const fe g = st.generator;
-  const uint64_t Nf = st.fri.domain_length;
-  AsyncScope async_scope(ctx);
-  PhaseMarks mark;
-  const uint64_t Tp = rows + st.num_randomizers;
-  SG_REQUIRE(Tp <= D, "randomized trace longer than the omicron domain");
-  const uint64_t tcd = max_degree(st, tcs);
-  SG_REQUIRE(nrc == tcd + 1, "randomizer polynomial must have max_degree(transition_constraints) + 1 coefficients");
-  SG_REQUIRE(nrc <= Nf, "fast_coset_evaluate: polynomial longer than root_order");
-  // The Merkle trees of the boundary-quotient and randomizer codewords (VALU-bound BLAKE2b)
-  // run on the side stream, overlapped with the main stream's transforms and quotients
-  // (which mostly wait on memory).  Everything a side-stream kernel touches is allocated
-  // here, with the main stream drained: a pool buffer released by queued main-stream work
-  // can then never be handed to a side-stream kernel.
-  SG_REQUIRE(m <= 4, "at most 4 registers are supported by the AIR kernel");  // root slots 0..m-1, 4
-  SG_HIP(hipStreamSynchronize(ctx->stream));
-  std::vector<DPoly> bq_cw;
-  std::vector<std::unique_ptr<sg_tree>> bq_trees(m);
-  for (size_t s = 0; s < m; ++s) bq_cw.push_back(dpoly_alloc(ctx, Nf));
-  DPoly r_cw = dpoly_alloc(ctx, Nf);
-  for (size_t s = 0; s < m; ++s) bq_trees[s] = new_tree(ctx, Nf);
-  std::unique_ptr<sg_tree> r_tree = new_tree(ctx, Nf);
-  SideDrain side_drain{ctx};
-  // randomizer codeword (stark.rs:424-445) first: it depends on nothing else, so its LDE and
-  // its tree run on the side stream while the main stream interpolates the trace.  The tables
-  // the LDE reads are created (cached) on the main stream before the fork: the side stream
-  // allocates nothing and only launches the transform passes and the tree.
-  constexpr int kRandSlot = 4;
-  uint64_t r_seq, bq_seq;
-  {
-    (void)ctx->stage_twiddles(st.omega, ilog2_exact(next_pow2(Nf)));
-    (void)ctx->pow_table(g, 4096);
-    (void)ctx->pow_table(fe_pow(g, 4096), (std::max<uint64_t>(nrc, 1) + 4095) / 4096);
-    SG_HIP(hipEventRecord(ctx->ev_fork, ctx->stream));
-    SG_HIP(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
-    const fe* in = d_rcoef;
-    fe* out = r_cw.p();
-    {
-      StreamSwap on_side(ctx, ctx->side);
-      coset_evaluate_batch(ctx, st.omega, Nf, g, &in, nrc, &out, 1);
-    }
-    const fe* leaves = r_cw.p();
-    sg_tree* t = r_tree.get();
-    r_seq = launch_trees(ctx, &leaves, 1, &t, kRandSlot, ctx->side);
-  }
+  const uint64_t D = st.D, Tp = A.Tp;
   // randomized trace (stark.rs:285-301), columns on the device
-  std::vector<DPoly> trace_polys;
+  std::vector<DPoly>& trace_polys = A.trace_polys;
   {
     DPoly col = dpoly_alloc(ctx, Tp);
     GeoInterpCache zc;  // Z(omicron^m), Z'(omicron^i) shared by the register columns
@@ -696,10 +663,19 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
       trace_polys.push_back(interpolate_geometric_dev(ctx, st.omicron, D, col.p(), Tp, &zc));
     }
   }
-  mark("trace_interpolation");
+}
+
+// boundary quotients (stark.rs:326-362)
+void prove_boundary_quotients(sg_ctx* ctx, const sg_stark& st, const std::vector<Boundary>& bnd, ProveAlgebra& A) {
+  const size_t m = st.m;
+  const uint64_t D = st.D;
+  const fe g = st.generator;
   // boundary quotients (stark.rs:326-362)
-  std::vector<HPoly> bi = boundary_interpolants(st, bnd), bz = boundary_zerofiers(st, bnd);
-  std::vector<DPoly> bqs;
+  std::vector<HPoly> bi = boundary_interpolants(st, bnd);
+  A.bz = boundary_zerofiers(st, bnd);
+  const std::vector<HPoly>& bz = A.bz;
+  std::vector<DPoly>& bqs = A.bqs;
+  const std::vector<DPoly>& trace_polys = A.trace_polys;
   {
     // every register's numerator first, then their degrees in one host round trip
     std::vector<DPoly> Zs, diffs;
@@ -716,31 +692,16 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
       bqs.push_back(fast_coset_divide_dev(ctx, st.omicron, D, g, diffs[s].p(), diffs[s].len, Zs[s].p(), Zs[s].len,
                                           hp_degree(bz[s]), bz[s].data(), dnum[s]));
   }
-  mark("boundary_quotients");
-  // boundary-quotient codewords (stark.rs:367-386); their trees hash on the side stream
-  // while the main stream computes the transition quotients
-  for (size_t s = 0; s < m; ++s) {
-    SG_REQUIRE(bqs[s].len <= Nf, "fast_coset_evaluate: polynomial longer than root_order");
-    const fe* in = bqs[s].p();
-    fe* out = bq_cw[s].p();
-    if (bqs[s].len)
-      coset_evaluate_batch(ctx, st.omega, Nf, g, &in, bqs[s].len, &out, 1);
-    else
-      SG_HIP(hipMemsetAsync(out, 0, Nf * sizeof(fe), ctx->stream));
-  }
-  {
-    SG_HIP(hipEventRecord(ctx->ev_fork, ctx->stream));
-    SG_HIP(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
-    const fe* leaves[4];
-    sg_tree* t[4];
-    for (size_t s = 0; s < m; ++s) {
-      leaves[s] = bq_cw[s].p();
-      t[s] = bq_trees[s].get();
-    }
-    bq_seq = launch_trees(ctx, leaves, (int)m, t, 0, ctx->side);
-    SG_HIP(hipEventRecord(ctx->ev_join, ctx->side));
-  }
-  mark("bq_lde");
+}
+
+// transition quotients (stark.rs:388-422) and every quotient's degree (one host round trip; a zero
+// divisor is reported here, before any root is pushed)
+void prove_transition_quotients(sg_ctx* ctx, const sg_stark& st, const std::vector<const MPoly*>& tcs,
+                                ProveAlgebra& A) {
+  const uint64_t D = st.D, Tp = A.Tp;
+  const fe g = st.generator;
+  const std::vector<DPoly>& trace_polys = A.trace_polys;
+  const std::vector<DPoly>& bqs = A.bqs;
   // transition quotients (stark.rs:388-422): evaluate_symbolic's polynomial from its values on a
   // coset of size L > its length, then fast_coset_divide by the transition zerofier.  When the
   // division's order equals L its lhs NTT IS those coset values (same offset, same root), so
@@ -771,7 +732,7 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
   std::vector<DevBuf> air_keep;  // AIR tables and x-polynomial values, alive until the quotients are done
   std::map<uint64_t, AirCoset> cosets;
   std::map<uint64_t, std::pair<DevBuf, uint64_t>> tz_ntt;  // order -> NTT of scale(tz, g)
-  std::vector<DPoly> tqs;
+  std::vector<DPoly>& tqs = A.tqs;
   auto tz_key_at = [&](uint64_t tag, const DivPlan& pl) {
     return std::vector<uint64_t>{tag, fe_lo(st.omicron), fe_hi(st.omicron), D, T, pl.order, fe_lo(pl.root),
                                  fe_hi(pl.root), fe_lo(g), fe_hi(g)};
@@ -865,7 +826,6 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
     }
     tqs.push_back(general_quotient(vals, len, L));
   }
-  mark("transition_quotients");
   // every quotient's degree with one host round trip (checked after the weights, as the
   // reference does, and used again by the terms below); it drains the main stream past
   // every division, so a zero divisor is reported before any root is pushed
@@ -875,7 +835,8 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
     for (const DPoly& q : bqs) qpolys.emplace_back(q.p(), q.len);
     return dev_degrees(ctx, qpolys);
   };
-  std::vector<int64_t> qdeg = quotient_degrees();
+  std::vector<int64_t>& qdeg = A.qdeg;
+  qdeg = quotient_degrees();
   check_div_zero(ctx);
   bool redone = false;
   for (Pending& pd : pending) {
@@ -892,23 +853,17 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
     qdeg = quotient_degrees();
     check_div_zero(ctx);
   }
-  // roots in the reference's order: boundary quotients (stark.rs:373-386), randomizer (:443)
-  {
-    sg_tree* t[4];
-    for (size_t s = 0; s < m; ++s) t[s] = bq_trees[s].get();
-    finish_trees(ctx, t, (int)m, bq_seq, 0, ctx->side);
-    sg_tree* rt = r_tree.get();
-    finish_trees(ctx, &rt, 1, r_seq, kRandSlot, ctx->side);
-    SG_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));  // openings read the trees
-  }
-  for (size_t s = 0; s < m; ++s) push_obj(ps, SG_OBJ_ROOT, bq_trees[s]->root, 64);
-  push_obj(ps, SG_OBJ_ROOT, r_tree->root, 64);
-  mark("trees_joined");
-  // weights (stark.rs:447-450)
-  uint8_t fs[32];
-  if (ps->fiat_shamir_prover(ps->user, 32, fs) != 0)
-    throw Error{SG_ERR_CALLBACK, "proof stream fiat_shamir callback failed"};
-  std::vector<fe> weights = sample_weights(1 + 2 * tqs.size() + 2 * bqs.size(), fs, 32);
+}
+
+// the degree check (stark.rs:451-465) and the combination polynomial (stark.rs:467-512)
+DPoly prove_combination(sg_ctx* ctx, const sg_stark& st, const std::vector<const MPoly*>& tcs, ProveAlgebra& A,
+                        const std::vector<fe>& weights, const fe* d_rcoef, size_t nrc, uint64_t tcd) {
+  const size_t m = st.m;
+  const uint64_t D = st.D, Tp = A.Tp;
+  const std::vector<DPoly>& tqs = A.tqs;
+  const std::vector<DPoly>& bqs = A.bqs;
+  const std::vector<HPoly>& bz = A.bz;
+  const std::vector<int64_t>& qdeg = A.qdeg;
   // degree check (stark.rs:451-465)
   std::vector<uint64_t> tqdb = transition_quotient_degree_bounds(st, tcs);
   for (size_t i = 0; i < tqs.size(); ++i) {
@@ -924,7 +879,7 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
     bqdb.push_back(Tp - 1 - (uint64_t)dz);
   }
   std::vector<DevTerm> terms;
-  std::vector<DPoly> wrapped;  // products that wrap the omicron domain (kept alive for the combination)
+  std::vector<DPoly>& wrapped = A.wrapped;  // products that wrap the omicron domain (alive for the combination)
   wrapped.reserve(2 * (tqs.size() + bqs.size()));
   size_t wi = 0;
   terms.push_back({d_rcoef, 0, nrc, weights[wi++]});
@@ -946,7 +901,113 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
   };
   for (size_t i = 0; i < tqs.size(); ++i) add_pair(tqs[i], tcd - tqdb[i], qdeg[i]);
   for (size_t s = 0; s < m; ++s) add_pair(bqs[s], tcd - bqdb[s], qdeg[tqs.size() + s]);
-  DPoly comb = lincomb(ctx, terms);
+  return lincomb(ctx, terms);
+}
+
+// stark.rs:276-562
+// d_trace: rows x m (row-major), d_trace_rand: num_randomizers x m, d_rcoef: nrc -- all on the device
+void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows,
+                 const std::vector<const MPoly*>& tcs, const std::vector<Boundary>& bnd, const fe* d_trace_rand,
+                 const fe* d_rcoef, size_t nrc, const sg_proof_stream* ps) {
+  SG_REQUIRE(ps && ps->push && ps->fiat_shamir_prover, "proof stream callbacks required");
+  const size_t m = st.m;
+  const uint64_t D = st.D;
+  const fe g = st.generator;
+  const uint64_t Nf = st.fri.domain_length;
+  AsyncScope async_scope(ctx);
+  PhaseMarks mark;
+  const uint64_t Tp = rows + st.num_randomizers;
+  SG_REQUIRE(Tp <= D, "randomized trace longer than the omicron domain");
+  const uint64_t tcd = max_degree(st, tcs);
+  SG_REQUIRE(nrc == tcd + 1, "randomizer polynomial must have max_degree(transition_constraints) + 1 coefficients");
+  SG_REQUIRE(nrc <= Nf, "fast_coset_evaluate: polynomial longer than root_order");
+  // The Merkle trees of the boundary-quotient and randomizer codewords (VALU-bound BLAKE2b)
+  // run on the side stream, overlapped with the main stream's transforms and quotients
+  // (which mostly wait on memory).  Everything a side-stream kernel touches is allocated
+  // here, with the main stream drained: a pool buffer released by queued main-stream work
+  // can then never be handed to a side-stream kernel.
+  SG_REQUIRE(m <= 4, "at most 4 registers are supported by the AIR kernel");  // root slots 0..m-1, 4
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  std::vector<DPoly> bq_cw;
+  std::vector<std::unique_ptr<sg_tree>> bq_trees(m);
+  for (size_t s = 0; s < m; ++s) bq_cw.push_back(dpoly_alloc(ctx, Nf));
+  DPoly r_cw = dpoly_alloc(ctx, Nf);
+  for (size_t s = 0; s < m; ++s) bq_trees[s] = new_tree(ctx, Nf);
+  std::unique_ptr<sg_tree> r_tree = new_tree(ctx, Nf);
+  SideDrain side_drain{ctx};
+  // randomizer codeword (stark.rs:424-445) first: it depends on nothing else, so its LDE and
+  // its tree run on the side stream while the main stream interpolates the trace.  The tables
+  // the LDE reads are created (cached) on the main stream before the fork: the side stream
+  // allocates nothing and only launches the transform passes and the tree.
+  constexpr int kRandSlot = 4;
+  uint64_t r_seq, bq_seq;
+  {
+    (void)ctx->stage_twiddles(st.omega, ilog2_exact(next_pow2(Nf)));
+    (void)ctx->pow_table(g, 4096);
+    (void)ctx->pow_table(fe_pow(g, 4096), (std::max<uint64_t>(nrc, 1) + 4095) / 4096);
+    SG_HIP(hipEventRecord(ctx->ev_fork, ctx->stream));
+    SG_HIP(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
+    const fe* in = d_rcoef;
+    fe* out = r_cw.p();
+    {
+      StreamSwap on_side(ctx, ctx->side);
+      coset_evaluate_batch(ctx, st.omega, Nf, g, &in, nrc, &out, 1);
+    }
+    const fe* leaves = r_cw.p();
+    sg_tree* t = r_tree.get();
+    r_seq = launch_trees(ctx, &leaves, 1, &t, kRandSlot, ctx->side);
+  }
+  ProveAlgebra A;
+  A.Tp = Tp;
+  prove_trace_polys(ctx, st, d_trace, rows, d_trace_rand, A);
+  mark("trace_interpolation");
+  prove_boundary_quotients(ctx, st, bnd, A);
+  mark("boundary_quotients");
+  const std::vector<DPoly>& bqs = A.bqs;
+  // boundary-quotient codewords (stark.rs:367-386); their trees hash on the side stream
+  // while the main stream computes the transition quotients
+  for (size_t s = 0; s < m; ++s) {
+    SG_REQUIRE(bqs[s].len <= Nf, "fast_coset_evaluate: polynomial longer than root_order");
+    const fe* in = bqs[s].p();
+    fe* out = bq_cw[s].p();
+    if (bqs[s].len)
+      coset_evaluate_batch(ctx, st.omega, Nf, g, &in, bqs[s].len, &out, 1);
+    else
+      SG_HIP(hipMemsetAsync(out, 0, Nf * sizeof(fe), ctx->stream));
+  }
+  {
+    SG_HIP(hipEventRecord(ctx->ev_fork, ctx->stream));
+    SG_HIP(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
+    const fe* leaves[4];
+    sg_tree* t[4];
+    for (size_t s = 0; s < m; ++s) {
+      leaves[s] = bq_cw[s].p();
+      t[s] = bq_trees[s].get();
+    }
+    bq_seq = launch_trees(ctx, leaves, (int)m, t, 0, ctx->side);
+    SG_HIP(hipEventRecord(ctx->ev_join, ctx->side));
+  }
+  mark("bq_lde");
+  prove_transition_quotients(ctx, st, tcs, A);
+  mark("transition_quotients");
+  // roots in the reference's order: boundary quotients (stark.rs:373-386), randomizer (:443)
+  {
+    sg_tree* t[4];
+    for (size_t s = 0; s < m; ++s) t[s] = bq_trees[s].get();
+    finish_trees(ctx, t, (int)m, bq_seq, 0, ctx->side);
+    sg_tree* rt = r_tree.get();
+    finish_trees(ctx, &rt, 1, r_seq, kRandSlot, ctx->side);
+    SG_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));  // openings read the trees
+  }
+  for (size_t s = 0; s < m; ++s) push_obj(ps, SG_OBJ_ROOT, bq_trees[s]->root, 64);
+  push_obj(ps, SG_OBJ_ROOT, r_tree->root, 64);
+  mark("trees_joined");
+  // weights (stark.rs:447-450)
+  uint8_t fs[32];
+  if (ps->fiat_shamir_prover(ps->user, 32, fs) != 0)
+    throw Error{SG_ERR_CALLBACK, "proof stream fiat_shamir callback failed"};
+  std::vector<fe> weights = sample_weights(1 + 2 * A.tqs.size() + 2 * bqs.size(), fs, 32);
+  DPoly comb = prove_combination(ctx, st, tcs, A, weights, d_rcoef, nrc, tcd);
   SG_REQUIRE(comb.len <= Nf, "fast_coset_evaluate: polynomial longer than root_order");
   DPoly comb_cw = dpoly_alloc(ctx, Nf);
   {
@@ -980,6 +1041,100 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
   SG_HIP(hipStreamSynchronize(ctx->stream));
   check_div_zero(ctx);
   mark("openings");
+}
+
+// Stark::prove (stark.rs:276-562) with its codeword-domain work sharded over a communicator
+// (the domain can outgrow one GPU): every rank runs the trace-domain algebra
+// (interpolation, quotients, the combination polynomial -- size D = N_fri / expansion) on its own
+// copy, and the N_fri-sized work on its run shards: the four LDEs (from the replicated
+// coefficients), the three commitments (forests + top trees, kept), FRI::prove (sg_dist_fri_prove)
+// and the openings, each from the rank that owns the leaf.  Every rank writes the single-GPU bytes.
+void stark_prove_dist(sg_dist* dd, const sg_stark& st, const fe* d_trace, size_t rows,
+                      const std::vector<const MPoly*>& tcs, const std::vector<Boundary>& bnd, const fe* d_trace_rand,
+                      const fe* d_rcoef, size_t nrc, const sg_proof_stream* ps) {
+  SG_REQUIRE(ps && ps->push && ps->fiat_shamir_prover, "proof stream callbacks required");
+  sg_ctx* ctx = dist_ctx(dd);
+  const size_t m = st.m;
+  const uint64_t D = st.D;
+  const fe g = st.generator;
+  const uint64_t Nf = st.fri.domain_length;
+  const uint64_t Tp = rows + st.num_randomizers;
+  SG_REQUIRE(Tp <= D, "randomized trace longer than the omicron domain");
+  const uint64_t tcd = max_degree(st, tcs);
+  SG_REQUIRE(nrc == tcd + 1, "randomizer polynomial must have max_degree(transition_constraints) + 1 coefficients");
+  SG_REQUIRE(nrc <= Nf, "fast_coset_evaluate: polynomial longer than root_order");
+  SG_REQUIRE(m <= 4, "at most 4 registers are supported by the AIR kernel");
+  uint64_t n1, n2;
+  dist_plan(Nf, dist_world(dd), n1, n2);
+  const uint64_t R = n2 / dist_world(dd), shard = n1 * R;
+  PhaseMarks mark;
+  ProveAlgebra A;
+  A.Tp = Tp;
+  prove_trace_polys(ctx, st, d_trace, rows, d_trace_rand, A);
+  prove_boundary_quotients(ctx, st, bnd, A);
+  mark("dist_algebra_boundary");
+  // boundary-quotient codewords + commitments (stark.rs:364-386), sharded
+  auto commit = [&](const fe* coeffs, uint64_t len, DevBuf& runs, ShardedRound& sr, uint8_t root[64]) {
+    SG_REQUIRE(len <= Nf, "fast_coset_evaluate: polynomial longer than root_order");
+    runs = DevBuf(ctx, shard * sizeof(fe));
+    if (len) dist_lde_replicated(dd, st.omega, Nf, g, coeffs, len, runs.as<fe>());
+    else SG_HIP(hipMemsetAsync(runs.get(), 0, shard * sizeof(fe), ctx->stream));
+    dist_merkle_root(dd, runs.as<fe>(), n1, R, root, &sr);
+    sr.cw = runs.as<fe>();
+  };
+  std::vector<DevBuf> runs(m + 1);
+  std::vector<ShardedRound> rounds(m + 1);
+  std::vector<std::array<uint8_t, 64>> roots(m + 1);
+  for (size_t s = 0; s < m; ++s) commit(A.bqs[s].p(), A.bqs[s].len, runs[s], rounds[s], roots[s].data());
+  mark("dist_bq_commit");
+  prove_transition_quotients(ctx, st, tcs, A);
+  mark("dist_transition_quotients");
+  // randomizer codeword + commitment (stark.rs:424-445)
+  commit(d_rcoef, nrc, runs[m], rounds[m], roots[m].data());
+  for (size_t s = 0; s <= m; ++s) push_obj(ps, SG_OBJ_ROOT, roots[s].data(), 64);
+  uint8_t fs[32];
+  if (ps->fiat_shamir_prover(ps->user, 32, fs) != 0)
+    throw Error{SG_ERR_CALLBACK, "proof stream fiat_shamir callback failed"};
+  std::vector<fe> weights = sample_weights(1 + 2 * A.tqs.size() + 2 * A.bqs.size(), fs, 32);
+  DPoly comb = prove_combination(ctx, st, tcs, A, weights, d_rcoef, nrc, tcd);
+  SG_REQUIRE(comb.len <= Nf, "fast_coset_evaluate: polynomial longer than root_order");
+  DevBuf comb_runs(ctx, shard * sizeof(fe));
+  dist_lde_replicated(dd, st.omega, Nf, g, comb.p(), comb.len, comb_runs.as<fe>());
+  mark("dist_combination_lde");
+  // FRI (stark.rs:514-522), then the openings (stark.rs:524-560) of the boundary-quotient and
+  // randomizer codewords at the quadrupled indices, each value + path from the leaf's owner
+  std::vector<size_t> top(st.fri.num_colinearity_tests);
+  dist_fri_prove(dd, &st.fri, comb_runs.as<fe>(), Nf, ps, top.data(), [&](const size_t* tp) {
+    const size_t c = st.fri.num_colinearity_tests;
+    std::vector<uint64_t> dup;
+    for (size_t k = 0; k < c; ++k) dup.push_back(tp[k]);
+    for (size_t k = 0; k < c; ++k) dup.push_back((tp[k] + st.expansion) % Nf);
+    std::vector<uint64_t> quad = dup;
+    for (uint64_t i : dup) quad.push_back((i + Nf / 2) % Nf);
+    std::sort(quad.begin(), quad.end());
+    for (size_t s = 0; s <= m; ++s) {
+      std::vector<fe> vals;
+      std::vector<uint8_t> paths;
+      int depth = 0;
+      dist_open_round(dd, rounds[s], R, n2, quad, vals, paths, depth);
+      std::vector<uint8_t> pl(72 * (size_t)depth);
+      for (size_t k = 0; k < quad.size(); ++k) {
+        uint8_t v[16];
+        put_u128_be_at(v, vals[k]);
+        push_obj(ps, SG_OBJ_VALUE, v, 16);
+        for (int l = 0; l < depth; ++l) {
+          uint8_t* o = pl.data() + 72 * (size_t)l;
+          memset(o, 0, 8);
+          o[7] = 64;
+          memcpy(o + 8, paths.data() + (k * (size_t)depth + (size_t)l) * 64, 64);
+        }
+        push_obj(ps, SG_OBJ_PATH, pl.data(), pl.size());
+      }
+    }
+  });
+  mark("dist_fri_prove_and_openings");
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  check_div_zero(ctx);
 }
 
 std::vector<const MPoly*> tc_list(const sg_mpoly* const* tcs, size_t n) {
@@ -1177,4 +1332,55 @@ extern "C" int sg_stark_prove_dev(sg_ctx* ctx, const sg_stark* st, const sg_fe* 
                 reinterpret_cast<const fe*>(d_trace_randomizers), reinterpret_cast<const fe*>(d_randomizer_coeffs),
                 n_rc, ps);
   });
+}
+
+// ====================================================================== C ABI: sharded STARK
+
+namespace {
+int dist_prove_entry(sg_dist* d, const sg_stark* st, const sg_fe* trace, size_t rows, const sg_mpoly* const* tcs,
+                     size_t ntcs, const sg_boundary* boundary, size_t nb, const sg_fe* trace_randomizers,
+                     const sg_fe* randomizer_coeffs, size_t n_rc, const sg_proof_stream* ps, bool host) {
+  sg_ctx* ctx = d ? dist_ctx(d) : nullptr;
+  return guard(ctx, [&] {
+    SG_REQUIRE(d && ctx && st && (trace || !rows) && (tcs || !ntcs) && (boundary || !nb), "null argument");
+    SG_REQUIRE(trace_randomizers || !st->num_randomizers, "null argument");
+    set_device(ctx);
+    std::vector<Boundary> bnd;
+    for (size_t i = 0; i < nb; ++i) {
+      check_canonical(&boundary[i].value, 1, "boundary value");
+      SG_REQUIRE(boundary[i].reg < st->m, "boundary register out of range");
+      bnd.push_back({boundary[i].cycle, boundary[i].reg, to_fe(boundary[i].value)});
+    }
+    if (!host) {
+      stark_prove_dist(d, *st, reinterpret_cast<const fe*>(trace), rows, tc_list(tcs, ntcs), bnd,
+                       reinterpret_cast<const fe*>(trace_randomizers), reinterpret_cast<const fe*>(randomizer_coeffs),
+                       n_rc, ps);
+      return;
+    }
+    check_canonical(trace, rows * st->m, "trace");
+    check_canonical(trace_randomizers, st->num_randomizers * st->m, "trace randomizers");
+    check_canonical(randomizer_coeffs, n_rc, "randomizer coefficients");
+    DPoly dt = dpoly_upload(ctx, reinterpret_cast<const fe*>(trace), rows * st->m);
+    DPoly dr = dpoly_upload(ctx, reinterpret_cast<const fe*>(trace_randomizers), st->num_randomizers * st->m);
+    DPoly dc = dpoly_upload(ctx, reinterpret_cast<const fe*>(randomizer_coeffs), n_rc);
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+    stark_prove_dist(d, *st, dt.p(), rows, tc_list(tcs, ntcs), bnd, dr.p(), dc.p(), n_rc, ps);
+  });
+}
+}  // namespace
+
+extern "C" int sg_dist_stark_prove(sg_dist* d, const sg_stark* st, const sg_fe* trace, size_t rows,
+                                   const sg_mpoly* const* tcs, size_t ntcs, const sg_boundary* boundary, size_t nb,
+                                   const sg_fe* trace_randomizers, const sg_fe* randomizer_coeffs, size_t n_rc,
+                                   const sg_proof_stream* ps) {
+  return dist_prove_entry(d, st, trace, rows, tcs, ntcs, boundary, nb, trace_randomizers, randomizer_coeffs, n_rc, ps,
+                          true);
+}
+
+extern "C" int sg_dist_stark_prove_dev(sg_dist* d, const sg_stark* st, const sg_fe* d_trace, size_t rows,
+                                       const sg_mpoly* const* tcs, size_t ntcs, const sg_boundary* boundary, size_t nb,
+                                       const sg_fe* d_trace_randomizers, const sg_fe* d_randomizer_coeffs, size_t n_rc,
+                                       const sg_proof_stream* ps) {
+  return dist_prove_entry(d, st, d_trace, rows, tcs, ntcs, boundary, nb, d_trace_randomizers, d_randomizer_coeffs,
+                          n_rc, ps, false);
 }

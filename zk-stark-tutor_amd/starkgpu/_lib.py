@@ -185,6 +185,10 @@ PROTOTYPES = {
                                       _P(sg_proof_stream)]),
     "sg_stark_prove_dev": (ctypes.c_int, [_vp, _vp, _vp, _sz, _vp, _sz, _vp, _sz, _vp, _vp, _sz,
                                           _P(sg_proof_stream)]),
+    "sg_dist_stark_prove": (ctypes.c_int, [_vp, _vp, _vp, _sz, _vp, _sz, _vp, _sz, _vp, _vp, _sz,
+                                           _P(sg_proof_stream)]),
+    "sg_dist_stark_prove_dev": (ctypes.c_int, [_vp, _vp, _vp, _sz, _vp, _sz, _vp, _sz, _vp, _vp, _sz,
+                                               _P(sg_proof_stream)]),
 }
 
 _lib = None

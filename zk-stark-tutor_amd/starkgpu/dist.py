@@ -528,7 +528,6 @@ class NativeDist:
             raise adapter.error
         self.ctx.check(rc)
 
-
     def fri_prove(self, offset: int, omega: int, runs: torch.Tensor, n: int, expansion: int, c: int,
                   proof_stream) -> List[int]:
         """fri.rs:210-248 on a run-sharded codeword: the same proof-stream bytes and top-level indices

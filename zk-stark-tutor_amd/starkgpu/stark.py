@@ -222,51 +222,71 @@ class Stark:
     def num_randomizer_coefficients(self, tcs: Sequence[MPolynomial]) -> int:
         return self.max_degree(tcs) + 1
 
-    def prove(self, trace, transition_constraints: Sequence[MPolynomial], boundary: Sequence[Tuple[int, int, int]],
-              proof_stream, trace_randomizers, randomizer_coefficients) -> bytes:
-        """stark.rs:276-562; `trace` is rows x registers (list of lists or an (rows*m, 2) array)."""
+    def _stream(self, proof_stream):
+        if isinstance(proof_stream, IndependentProofStream):
+            return proof_stream.callbacks(), None
+        adapter = CallbackProofStream(proof_stream)
+        return adapter.callbacks(), adapter
+
+    def _host_args(self, trace, boundary, trace_randomizers, randomizer_coefficients):
         m = self.num_registers
         if isinstance(trace, np.ndarray):
             t = fe_array(trace)
         else:
             t = fe_array([v for row in trace for v in row])
-        rows = len(t) // m
         tr = fe_array([v for row in trace_randomizers for v in row]) if not isinstance(trace_randomizers, np.ndarray) \
             else fe_array(trace_randomizers)
         rc = fe_array(randomizer_coefficients)
         bnd = (sg_boundary * max(len(boundary), 1))(*[sg_boundary(c, r, _fe(v)) for (c, r, v) in boundary])
-        if isinstance(proof_stream, IndependentProofStream):
-            cb, adapter = proof_stream.callbacks(), None
-        else:
-            adapter = CallbackProofStream(proof_stream)
-            cb = adapter.callbacks()
-        rcode = self.ctx._lib.sg_stark_prove(self.ctx.handle, self.handle, _ptr(t), rows,
-                                             self._tcs(transition_constraints), len(transition_constraints), bnd,
-                                             len(boundary), _ptr(tr), _ptr(rc), len(rc), ctypes.byref(cb))
+        return t, len(t) // m, tr, rc, bnd
+
+    def _finish(self, rcode, adapter):
         if adapter is not None and adapter.error is not None:
             raise adapter.error
         self.ctx.check(rcode)
+
+    def prove(self, trace, transition_constraints: Sequence[MPolynomial], boundary: Sequence[Tuple[int, int, int]],
+              proof_stream, trace_randomizers, randomizer_coefficients, dist=None) -> bytes:
+        """stark.rs:276-562; `trace` is rows x registers (list of lists or an (rows*m, 2) array).
+
+        With `dist` (a starkgpu.dist.NativeDist whose context this Stark and the constraints were
+        created on) the codeword domain is sharded over the communicator (sg_dist_stark_prove):
+        every rank calls with the same arguments and gets the single-GPU proof bytes."""
+        t, rows, tr, rc, bnd = self._host_args(trace, boundary, trace_randomizers, randomizer_coefficients)
+        cb, adapter = self._stream(proof_stream)
+        tcs = self._tcs(transition_constraints)
+        if dist is None:
+            rcode = self.ctx._lib.sg_stark_prove(self.ctx.handle, self.handle, _ptr(t), rows, tcs,
+                                                 len(transition_constraints), bnd, len(boundary), _ptr(tr),
+                                                 _ptr(rc), len(rc), ctypes.byref(cb))
+        else:
+            if dist.ctx is not self.ctx:
+                raise ValueError("the Stark must be created on the communicator's context")
+            dist._torch_ready()
+            rcode = self.ctx._lib.sg_dist_stark_prove(dist.handle, self.handle, _ptr(t), rows, tcs,
+                                                      len(transition_constraints), bnd, len(boundary), _ptr(tr),
+                                                      _ptr(rc), len(rc), ctypes.byref(cb))
+        self._finish(rcode, adapter)
         return proof_stream.digest()
 
     def prove_dev(self, d_trace: int, rows: int, transition_constraints: Sequence[MPolynomial],
                   boundary: Sequence[Tuple[int, int, int]], proof_stream, d_trace_randomizers: int,
-                  d_randomizer_coefficients: int, n_randomizer_coefficients: int) -> None:
+                  d_randomizer_coefficients: int, n_randomizer_coefficients: int, dist=None) -> None:
         """prove() with the trace (rows x registers, row-major), the trace randomizers and the
         randomizer coefficients already in device memory (e.g. torch tensor data_ptr())."""
         bnd = (sg_boundary * max(len(boundary), 1))(*[sg_boundary(c, r, _fe(v)) for (c, r, v) in boundary])
-        if isinstance(proof_stream, IndependentProofStream):
-            cb, adapter = proof_stream.callbacks(), None
+        cb, adapter = self._stream(proof_stream)
+        args = (self.handle, ctypes.c_void_p(d_trace), rows, self._tcs(transition_constraints),
+                len(transition_constraints), bnd, len(boundary), ctypes.c_void_p(d_trace_randomizers),
+                ctypes.c_void_p(d_randomizer_coefficients), n_randomizer_coefficients, ctypes.byref(cb))
+        if dist is None:
+            rcode = self.ctx._lib.sg_stark_prove_dev(self.ctx.handle, *args)
         else:
-            adapter = CallbackProofStream(proof_stream)
-            cb = adapter.callbacks()
-        rcode = self.ctx._lib.sg_stark_prove_dev(self.ctx.handle, self.handle, ctypes.c_void_p(d_trace), rows,
-                                                 self._tcs(transition_constraints), len(transition_constraints), bnd,
-                                                 len(boundary), ctypes.c_void_p(d_trace_randomizers),
-                                                 ctypes.c_void_p(d_randomizer_coefficients),
-                                                 n_randomizer_coefficients, ctypes.byref(cb))
-        if adapter is not None and adapter.error is not None:
-            raise adapter.error
-        self.ctx.check(rcode)
+            if dist.ctx is not self.ctx:
+                raise ValueError("the Stark must be created on the communicator's context")
+            dist._torch_ready()
+            rcode = self.ctx._lib.sg_dist_stark_prove_dev(dist.handle, *args)
+        self._finish(rcode, adapter)
 
     def __del__(self):
         try:
