@@ -390,6 +390,30 @@ def side_sharded(ctx: sg.Context, device, world: int, rank: int, iters: int = 3)
         out["sharded_lde_fri_prove_2p24_ms"] = round(timed(lde_fri_prove) * 1e3, 3)
     except Exception as e:  # noqa: BLE001
         out["sharded_lde_fri_error"] = f"{type(e).__name__}: {e}"
+    try:
+        # the headline Stark::prove with its FRI domain sharded over the ranks (sg_dist_stark_prove):
+        # trace-domain algebra replicated, LDEs / commitments / FRI / openings on run shards; every
+        # rank proves the same statement and must write the single-GPU proof bytes
+        wl = ProveWorkload(0, device, ctx, LOG_TRACE)
+        single = wl.step().digest()
+
+        def prove():
+            ps = sg.IndependentProofStream()
+            wl.stark.prove_dev(wl.trace.data_ptr(), wl.rows, wl.air, wl.boundary, ps, wl.trace_rand.data_ptr(),
+                               wl.rcoef.data_ptr(), wl.nrc, dist=ds)
+            state["bytes"] = ps.digest()
+
+        state = {}
+        t = timed(prove)
+        same = -allreduce_max(-1.0 if state["bytes"] == single else 0.0, device) == 1.0
+        out["sharded_prove_ms"] = round(t * 1e3, 3)
+        out["sharded_prove_gelem_s"] = round(wl.elements_per_step() / t / 1e9, 4)
+        out["sharded_prove_bytes_equal_single_gpu"] = same
+        out["sharded_prove_workload"] = f"the headline proof (trace 2^{LOG_TRACE}, FRI domain " \
+                                        f"2^{wl.fri_len.bit_length() - 1}) sharded over {world} ranks"
+        del wl
+    except Exception as e:  # noqa: BLE001
+        out["sharded_prove_error"] = f"{type(e).__name__}: {e}"
     ds.close()
     ctx.trim()
     return out

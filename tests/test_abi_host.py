@@ -25,6 +25,16 @@ def test_exports_every_declared_symbol():
     assert set(syms) == set(_lib.PROTOTYPES), "ctypes prototypes out of sync with the header"
 
 
+def test_one_rccl_and_one_hip_runtime_in_a_torch_process():
+    """libstarkgpu's NEEDED librccl.so.1 / libamdhip64.so.7 carry the same sonames as the copies
+    torch ships; loaded after torch (starkgpu._lib does that), the loader reuses torch's, so the
+    library's communicator and torch.distributed's share one RCCL and one HIP runtime."""
+    sg.lib()
+    for tag in ("librccl", "libamdhip64"):
+        paths = {line.split()[-1] for line in open("/proc/self/maps") if tag in line and "/" in line}
+        assert len(paths) <= 1, f"{tag} mapped from more than one file: {paths}"
+
+
 def test_host_field_matches_oracle(kats):
     assert sg.generator() == o.GENERATOR
     for v in kats["fe_mul"]:
