@@ -102,7 +102,8 @@ def test_zerofier_and_interpolate_generic_domains():
         assert sg.fast_interpolate_domain(w, n, dom, vals).coefficients == e.fast_interpolate_domain(w, n, dom, vals)
 
 
-@pytest.mark.parametrize("D,ns", [(1 << 6, [1, 2, 3, 28, 36, 63, 64]), (1 << 8, [200, 255])])
+@pytest.mark.parametrize("D,ns", [(1 << 6, [1, 2, 3, 28, 36, 63, 64]), (1 << 8, [200, 255]),
+                                  (1 << 8, [5, 33, 64, 65, 127, 128]), (1 << 10, [7, 60, 64, 65, 256])])
 def test_interpolate_geometric_vs_oracle(D, ns):
     rng = random.Random(5)
     q = o.primitive_nth_root(D)
@@ -128,6 +129,27 @@ def test_interpolate_geometric_large(logD, n):
     assert len(p) == n
     cw = sg.fast_coset_evaluate(q, D, 1, p.array())
     assert sg.to_ints(cw[:n]) == vals
+
+
+@pytest.mark.parametrize("logD", [14, 17])
+def test_interpolate_geometric_decimated_vs_checker(logD, monkeypatch):
+    """n <= D / f: the interpolant comes from its values on the subgroup of order D / f (f residue-class
+    convolutions sharing one inverse transform) -- equal to the CPU checker (fast_cpu, pinned to the
+    oracle) and to the full-group form (SG_GEO_DECIMATE=0), for f = 16, 4, 2 and none."""
+    import torch
+    import fast_cpu as fc
+    D = 1 << logD
+    q = o.primitive_nth_root(D)
+    dev = torch.device("cuda", 0)
+    for n in (D // 16 - 5, D // 4 - 1, D // 4, D // 4 + 1, D // 2, D - 3):
+        vals = o.synthetic_elements(n, b"decimated", n)
+        y = torch.from_numpy(sg.fe_array(vals).view(np.int64)).to(dev)
+        want = fc.ints(fc.geo_interpolate(q, D, vals))
+        monkeypatch.delenv("SG_GEO_DECIMATE", raising=False)
+        got = sg.fast_interpolate_geometric_dev(q, D, y.data_ptr(), n)
+        assert got.coefficients == want, n
+        monkeypatch.setenv("SG_GEO_DECIMATE", "0")
+        assert sg.fast_interpolate_geometric_dev(q, D, y.data_ptr(), n).coefficients == want, n
 
 
 # ---- arbitrary (non-geometric) domains of any size (ntt_arithmetics.rs:66-113, 172-237) ----

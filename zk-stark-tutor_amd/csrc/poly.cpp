@@ -14,6 +14,7 @@
 //     its values on the whole group: y_i for i < n and, for m >= n,
 //     Z(q^m) sum_i y_i / (Z'(q^i) (q^m - q^i)) -- one cyclic convolution with
 //     1 / (1 - q^-j) (3 NTTs), Z = the zerofier above.
+#include <cstdlib>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -356,11 +357,8 @@ DPoly zerofier_geometric_dev(sg_ctx* ctx, const fe& q, uint64_t D, uint64_t n) {
 }
 
 namespace {
-// NTT_D of b[j] = 1 / (1 - q^-j) (j >= 1), b[0] = 0; cached per (q, D)
-const fe* interp_kernel(sg_ctx* ctx, const fe& q, uint64_t D) {
-  auto key = std::make_pair(std::make_pair(fe_lo(q), fe_hi(q)), D);
-  auto it = ctx->interp_tables.find(key);
-  if (it != ctx->interp_tables.end()) return reinterpret_cast<const fe*>(it->second);
+// b[j] = 1 / (1 - q^-j) (j >= 1), b[0] = 0, j < D
+DevBuf interp_b(sg_ctx* ctx, const fe& q, uint64_t D) {
   const fe qinv = fe_inv(q);
   const fe *A, *B;
   pow_tables2(ctx, qinv, D, &A, &B);
@@ -368,47 +366,93 @@ const fe* interp_kernel(sg_ctx* ctx, const fe& q, uint64_t D) {
   SG_HIP(hipMemsetAsync(b.get(), 0, sizeof(fe), ctx->stream));
   SG_HIP(launch_one_minus_pow(b.as<fe>() + 1, D - 1, 1, A, B, ctx->stream));
   dev_div(ctx, b.as<fe>() + 1, nullptr, b.as<fe>() + 1, D - 1);
+  return b;
+}
+
+// logf = 0: NTT_D(b).  logf > 0: the f = 2^logf rows K_r[j] = b[(f j - r) mod D] (j < M = D / f),
+// each transformed with q^f (order M).  Cached per (q, D, f), like a twiddle plan.
+const fe* interp_kernel(sg_ctx* ctx, const fe& q, uint64_t D, int logf) {
+  auto key = std::make_pair(std::make_pair(fe_lo(q), fe_hi(q)), D | ((uint64_t)logf << 58));
+  auto it = ctx->interp_tables.find(key);
+  if (it != ctx->interp_tables.end()) return reinterpret_cast<const fe*>(it->second);
+  DevBuf b = interp_b(ctx, q, D);
   void* t = nullptr;
   SG_HIP(hipMalloc(&t, D * sizeof(fe)));
-  ntt_sized(ctx, q, b.as<fe>(), D, ilog2_exact(D), reinterpret_cast<fe*>(t));
+  if (logf == 0) {
+    ntt_sized(ctx, q, b.as<fe>(), D, ilog2_exact(D), reinterpret_cast<fe*>(t));
+  } else {
+    const uint64_t M = D >> logf;
+    DevBuf rows(ctx, D * sizeof(fe));
+    SG_HIP(launch_geo_krows(rows.as<fe>(), b.as<fe>(), logf, M, D, ctx->stream));
+    ntt_rows_dev(ctx, fe_pow(q, (uint64_t)1 << logf), rows.as<fe>(), (uint64_t)1 << logf, ilog2_exact(M),
+                 reinterpret_cast<fe*>(t), nullptr);
+  }
   ctx->interp_tables[key] = t;
   return reinterpret_cast<const fe*>(t);
 }
+
+// decimation of the geometric interpolation: the largest f = 2^logf with n <= D / f, so the
+// interpolant (degree < n) is recovered from its values on the subgroup of order M = D / f
+// (SG_GEO_DECIMATE=0: the full-group form, f = 1)
+int geo_logf(uint64_t n, uint64_t D) {
+  const char* e = getenv("SG_GEO_DECIMATE");
+  if (e && e[0] == '0') return 0;
+  // M = D / f >= n, M >= 64, M / f >= 1 (rows of M / f inputs), f <= 16
+  const int logD = ilog2_exact(D);
+  int logf = 0;
+  while (logf < 4 && (D >> (logf + 1)) >= n && logD - (logf + 1) >= 6 && logD >= 2 * (logf + 1)) ++logf;
+  return logf;
+}
 }  // namespace
 
-DPoly interpolate_geometric_dev(sg_ctx* ctx, const fe& q, uint64_t D, const fe* y, uint64_t n, GeoInterpCache* cache) {
+std::vector<DPoly> interpolate_geometric_batch_dev(sg_ctx* ctx, const fe& q, uint64_t D, const fe* y, uint64_t ys,
+                                                   size_t cols, uint64_t n, GeoInterpCache* cache) {
   SG_REQUIRE(n <= D, "interpolate: more points than the order of the root");
   SG_REQUIRE(D && (D & (D - 1)) == 0, "interpolate: root order must be a power of two");
-  if (n == 0) return DPoly{};
-  if (n == 1) return dpoly_copy(ctx, y, 1);
-  const int logD = ilog2_exact(D);
-  if (n == D) {
-    DPoly out = dpoly_alloc(ctx, D);
-    intt_sized(ctx, q, y, logD, out.p());
-      return out;
+  std::vector<DPoly> outs;
+  if (n <= 1 || n == D) {
+    for (size_t c = 0; c < cols; ++c) {
+      if (n == 0) {
+        outs.emplace_back();
+      } else if (n == 1) {
+        outs.push_back(dpoly_copy(ctx, y + c * ys, 1));
+      } else {
+        DPoly out = dpoly_alloc(ctx, D);
+        intt_sized(ctx, q, y + c * ys, ilog2_exact(D), out.p());
+        outs.push_back(std::move(out));
+      }
+    }
+    return outs;
   }
-  // Z, Z(q^m) and 1 / Z'(q^i): they depend on the domain only, so the context keeps them like a
-  // twiddle plan (else `cache` shares them between the calls of one prove)
-  const std::vector<uint64_t> key = {kDomainGeoInterp, fe_lo(q), fe_hi(q), D, n};
+  const int logD = ilog2_exact(D);
+  const int logf = geo_logf(n, D);
+  const uint64_t M = D >> logf, f = (uint64_t)1 << logf;
+  const int logM = logD - logf;
+  const fe qf = fe_pow(q, f);  // order M
+  // Z(q^(f k)) (k < M) and 1 / Z'(q^i) (i < n): they depend on the domain only, so the context keeps
+  // them like a twiddle plan (else `cache` shares them between the calls of one prove)
+  const std::vector<uint64_t> key = {kDomainGeoInterp, fe_lo(q), fe_hi(q), D, n, (uint64_t)logf};
   const fe* Zv = ctx->domain_cache_on() ? static_cast<const fe*>(ctx->domain_table(key)) : nullptr;
-  const fe* Zdi = Zv ? Zv + D : nullptr;
+  const fe* Zdi = Zv ? Zv + M : nullptr;
   GeoInterpCache local;
   GeoInterpCache& zc = cache ? *cache : local;
   if (!Zv) {
-    if (!(zc.n == n && zc.D == D && fe_eq(zc.q, q))) {
+    if (!(zc.n == n && zc.D == D && zc.logf == logf && fe_eq(zc.q, q))) {
       DPoly Z = zerofier_geometric_dev(ctx, q, D, n);
       DevBuf Zd(ctx, n * sizeof(fe));
-      zc.Zv = DevBuf(ctx, D * sizeof(fe));
+      DevBuf Zfull(ctx, D * sizeof(fe));
+      ntt_sized(ctx, q, Z.p(), n + 1, logD, Zfull.as<fe>());
+      zc.Zv = DevBuf(ctx, M * sizeof(fe));
+      SG_HIP(launch_gather_stride(zc.Zv.as<fe>(), Zfull.as<fe>(), M, f, ctx->stream));  // Z(q^(f k))
       zc.Zdi = DevBuf(ctx, n * sizeof(fe));
-      ntt_sized(ctx, q, Z.p(), n + 1, logD, zc.Zv.as<fe>());
       SG_HIP(launch_deriv(Zd.as<fe>(), Z.p(), n, fe_r2(), ctx->stream));
       // Z'(q^i) for i < n (the first n values of its size-D transform), inverted once
-      DevBuf Zdfull(ctx, D * sizeof(fe));
-      ntt_sized(ctx, q, Zd.as<fe>(), n, logD, Zdfull.as<fe>());
-      dev_div(ctx, zc.Zdi.as<fe>(), nullptr, Zdfull.as<fe>(), n);
+      ntt_sized(ctx, q, Zd.as<fe>(), n, logD, Zfull.as<fe>());
+      dev_div(ctx, zc.Zdi.as<fe>(), nullptr, Zfull.as<fe>(), n);
       zc.q = q;
       zc.D = D;
       zc.n = n;
+      zc.logf = logf;
     }
     Zv = zc.Zv.as<fe>();
     Zdi = zc.Zdi.as<fe>();
@@ -418,27 +462,57 @@ DPoly interpolate_geometric_dev(sg_ctx* ctx, const fe& q, uint64_t D, const fe* 
       SG_HIP(hipStreamSynchronize(ctx->stream));
       check_div_zero(ctx);
       void* t = nullptr;
-      SG_HIP(hipMalloc(&t, (D + n) * sizeof(fe)));
-      SG_HIP(hipMemcpyAsync(t, Zv, D * sizeof(fe), hipMemcpyDeviceToDevice, ctx->stream));
-      SG_HIP(hipMemcpyAsync(static_cast<fe*>(t) + D, Zdi, n * sizeof(fe), hipMemcpyDeviceToDevice, ctx->stream));
+      SG_HIP(hipMalloc(&t, (M + n) * sizeof(fe)));
+      SG_HIP(hipMemcpyAsync(t, Zv, M * sizeof(fe), hipMemcpyDeviceToDevice, ctx->stream));
+      SG_HIP(hipMemcpyAsync(static_cast<fe*>(t) + M, Zdi, n * sizeof(fe), hipMemcpyDeviceToDevice, ctx->stream));
       ctx->domain_table_put(key, t);
     }
   }
-  // a_i = y_i / Z'(q^i) as a product by the kept inverse; S = a (*) b cyclically, b[j] = 1 / (1 - q^-j)
-  DevBuf a(ctx, n * sizeof(fe)), va(ctx, D * sizeof(fe)), S(ctx, D * sizeof(fe));
-  dev_mul(ctx, a.as<fe>(), y, Zdi, n);
-  ntt_sized(ctx, q, a.as<fe>(), n, logD, va.as<fe>());
-  dev_mul(ctx, va.as<fe>(), va.as<fe>(), interp_kernel(ctx, q, D), D);
-  intt_sized(ctx, q, va.as<fe>(), logD, S.as<fe>());
-  // values on the whole group, then the coefficients
+  // a_i = y_i / Z'(q^i); S(m) = sum_i a_i b[m - i] cyclically, b[j] = 1 / (1 - q^-j).  At m = f k the f
+  // residue classes i = f j + r each give a cyclic convolution of length M (root q^f) against the
+  // row K_r: their transforms are summed pointwise and share one inverse transform.
+  const fe* Khat = interp_kernel(ctx, q, D, logf);
+  DevBuf va(ctx, cols * D * sizeof(fe)), S(ctx, cols * M * sizeof(fe));
+  if (logf == 0) {
+    DevBuf a(ctx, n * sizeof(fe));
+    for (size_t c = 0; c < cols; ++c) {
+      dev_mul(ctx, a.as<fe>(), y + c * ys, Zdi, n);
+      ntt_sized(ctx, q, a.as<fe>(), n, logD, va.as<fe>() + c * D);
+      dev_mul(ctx, va.as<fe>() + c * D, va.as<fe>() + c * D, Khat, D);
+    }
+    S = std::move(va);
+    va = DevBuf(ctx, cols * M * sizeof(fe));
+  } else {
+    const uint64_t Mf = M >> logf;  // every residue class has < n / f + 1 <= Mf entries
+    DevBuf rows(ctx, cols * M * sizeof(fe));
+    SG_HIP(launch_geo_rows(rows.as<fe>(), y, ys, Zdi, n, logf, M, cols, fe_r2(), ctx->stream));
+    // cols * f transforms of length M from Mf inputs each (the first logf stages are copies)
+    const fe* tw = ctx->stage_twiddles(qf, logM);
+    const fe* in0 = rows.as<fe>();
+    fe* out0 = va.as<fe>();
+    SG_HIP(launch_ntt_fused(&out0, &in0, (int)(cols * f), Mf, logM, tw, nullptr, nullptr, logf, nullptr, ctx->stream,
+                            Mf, M));
+    SG_HIP(launch_geo_dot(S.as<fe>(), va.as<fe>(), Khat, logf, M, cols, fe_r2(), ctx->stream));
+  }
+  // S(f k) for every column (one batched inverse transform), then P(q^(f k)), then the coefficients
+  ntt_rows_inverse(ctx, qf, S.as<fe>(), cols, logM, va.as<fe>());
   const fe *iA, *iB;
   pow_tables2(ctx, fe_inv(q), D, &iA, &iB);
-  SG_HIP(launch_interp_assemble(va.as<fe>(), y, Zv, S.as<fe>(), n, D, iA, iB, fe_r2(), ctx->stream));
-  // the coefficients land in the result's own buffer (D >= n slots): no copy of the n kept
-  DPoly out = dpoly_alloc(ctx, D);
-  intt_sized(ctx, q, va.as<fe>(), logD, out.p());
-  out.len = n;
-  return out;
+  SG_HIP(launch_interp_assemble(S.as<fe>(), y, ys, Zv, va.as<fe>(), n, M, logf, cols, iA, iB, fe_r2(),
+                                ctx->stream));
+  // the coefficients land in each result's own buffer (D >= n slots, zero above M: degree < n <= M)
+  for (size_t c = 0; c < cols; ++c) {
+    DPoly out = dpoly_alloc(ctx, D);
+    intt_sized(ctx, qf, S.as<fe>() + c * M, logM, out.p());
+    if (M < D) SG_HIP(hipMemsetAsync(out.p() + M, 0, (D - M) * sizeof(fe), ctx->stream));
+    out.len = n;
+    outs.push_back(std::move(out));
+  }
+  return outs;
+}
+
+DPoly interpolate_geometric_dev(sg_ctx* ctx, const fe& q, uint64_t D, const fe* y, uint64_t n, GeoInterpCache* cache) {
+  return std::move(interpolate_geometric_batch_dev(ctx, q, D, y, 0, 1, n, cache)[0]);
 }
 
 void coset_interpolate_dev(sg_ctx* ctx, const fe* values, uint64_t L, const fe& offset, fe* out) {
@@ -475,6 +549,12 @@ void ntt_rows_dev(sg_ctx* ctx, const fe& root, const fe* in, uint64_t rows, int 
     const fe* i = in + r0 * n;
     SG_HIP(launch_ntt_fused(&o, &i, cnt, n, logn, tw, nullptr, nullptr, 0, post, ctx->stream, n, n));
   }
+}
+
+// `rows` contiguous inverse transforms of 2^logn (intt per row, n^-1 folded into the last pass)
+void ntt_rows_inverse(sg_ctx* ctx, const fe& root, const fe* in, uint64_t rows, int logn, fe* out) {
+  const fe ninv_m = to_mont(fe_inv(fe_from_u64((uint64_t)1 << logn)));
+  ntt_rows_dev(ctx, fe_inv(root), in, rows, logn, out, &ninv_m);
 }
 
 // Bottom-up product tree over d_dom[0..n) (see poly_kernels.hip): Z = prod (x - d_i), length n + 1,

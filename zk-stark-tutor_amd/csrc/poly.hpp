@@ -92,11 +92,15 @@ enum : uint64_t { kDomainGeoInterp = 1, kDomainTzCoeffs = 2, kDomainTzValues = 3
 struct GeoInterpCache {
   fe q;
   uint64_t D = 0, n = 0;
+  int logf = 0;     // Zv holds Z(q^(f k)), k < D / f (decimated interpolation, f = 2^logf)
   DevBuf Zv, Zdi;
 };
 // the interpolant of degree < n through (q^i, y_i), i < n <= D (ntt_arithmetics.rs:172-237), length n
 DPoly interpolate_geometric_dev(sg_ctx* ctx, const fe& q, uint64_t D, const fe* y, uint64_t n,
                                 GeoInterpCache* cache = nullptr);
+// the same for `cols` columns y + c * ys (batched transforms)
+std::vector<DPoly> interpolate_geometric_batch_dev(sg_ctx* ctx, const fe& q, uint64_t D, const fe* y, uint64_t ys,
+                                                   size_t cols, uint64_t n, GeoInterpCache* cache = nullptr);
 // coefficients (length L) of the polynomial of degree < L with P(offset w^k) = values[k], w of order L
 void coset_interpolate_dev(sg_ctx* ctx, const fe* values, uint64_t L, const fe& offset, fe* out);
 // out (length L, a power of two >= len) = [P(offset w^k)], w of order L
@@ -104,6 +108,7 @@ void coset_values_dev(sg_ctx* ctx, const fe* coeffs, uint64_t len, uint64_t L, c
 
 // arbitrary (non-geometric) domains: ntt_arithmetics.rs:66-113 / 172-237 on the device
 void ntt_rows_dev(sg_ctx* ctx, const fe& root, const fe* in, uint64_t rows, int logn, fe* out, const fe* post_host);
+void ntt_rows_inverse(sg_ctx* ctx, const fe& root, const fe* in, uint64_t rows, int logn, fe* out);
 void tree_exact(sg_ctx* ctx, const fe* d_dom, uint64_t n, const fe* d_c, DPoly* Zout, DPoly* Nout);
 DPoly zerofier_any_dev(sg_ctx* ctx, const fe& root, uint64_t root_order, const fe* d_dom, uint64_t n);
 DPoly interpolate_any_dev(sg_ctx* ctx, const fe& root, uint64_t root_order, const fe* d_dom, const fe* d_val,

@@ -324,21 +324,60 @@ __global__ __launch_bounds__(kBlock) void k_qbinom(fe* __restrict__ c, const fe*
   }
 }
 
-// V[m] = y[m] for m < n, else Zv[m] * q^-m * S[m]   (q^-m from the two-level table)
-__global__ __launch_bounds__(kBlock) void k_interp_assemble(fe* __restrict__ V, const fe* __restrict__ y,
+// V[c M + k] = P_c(q^m) at m = f k (k < M): y_c[m] for m < n, else Zv[k] * q^-m * S[c M + k]
+// (q^-m from the two-level table; f = 1, M = D: every point of the group)
+__global__ __launch_bounds__(kBlock) void k_interp_assemble(fe* __restrict__ V, const fe* __restrict__ y, uint64_t ys,
                                                             const fe* __restrict__ Zv, const fe* __restrict__ S,
-                                                            uint64_t n, uint64_t D, const fe* __restrict__ iA,
-                                                            const fe* __restrict__ iB, fe r2) {
-  for (uint64_t m = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; m < D; m += (uint64_t)gridDim.x * blockDim.x) {
+                                                            uint64_t n, uint64_t M, uint32_t logf, uint64_t total,
+                                                            const fe* __restrict__ iA, const fe* __restrict__ iB, fe r2) {
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t c = t / M, k = t - c * M, m = k << logf;
     fe v;
     if (m < n) {
-      v = ld_fe(y + m);
+      v = ld_fe(y + c * ys + m);
     } else {
       fe im = mont_mul(ld_fe(iA + (m & 4095)), ld_fe(iB + (m >> 12)));  // Montgomery(q^-m)
-      v = mont_mul(ld_fe(Zv + m), im);                                   // Zv q^-m
-      v = mont_mul(mont_mul(v, ld_fe(S + m)), r2);                       // * S
+      v = mont_mul(ld_fe(Zv + k), im);                                   // Zv q^-m
+      v = mont_mul(mont_mul(v, ld_fe(S + t)), r2);                       // * S
     }
-    st_fe(V + m, v);
+    st_fe(V + t, v);
+  }
+}
+
+// Decimated interpolation, residue classes of a_i = y_i / Z'(q^i) (i < n <= M = D / f):
+// rows[(c f + r) Mf + j] = a_(c, f j + r) for f j + r < n, else 0  (Mf = M / f rows of column c)
+__global__ __launch_bounds__(kBlock) void k_geo_rows(fe* __restrict__ rows, const fe* __restrict__ y, uint64_t ys,
+                                                     const fe* __restrict__ Zdi, uint64_t n, uint32_t logf,
+                                                     uint64_t M, uint64_t total, fe r2) {
+  const uint64_t Mf = M >> logf, f = (uint64_t)1 << logf;
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t c = t / M, m = t - c * M;
+    const fe v = m < n ? mont_mul(mont_mul(ld_fe(y + c * ys + m), ld_fe(Zdi + m)), r2) : fe_zero();
+    st_fe(rows + (c * f + (m & (f - 1))) * Mf + (m >> logf), v);
+  }
+}
+
+// K rows of the decimated convolution: out[r M + j] = b[(f j - r) mod D], b[j] = 1 / (1 - q^-j), b[0] = 0
+__global__ __launch_bounds__(kBlock) void k_geo_krows(fe* __restrict__ out, const fe* __restrict__ b, uint32_t logf,
+                                                      uint64_t M, uint64_t D) {
+  const uint64_t total = D;  // f rows of M
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t r = t / M, j = t - r * M;
+    st_fe(out + t, ld_fe(b + (((j << logf) + D - r) & (D - 1))));
+  }
+}
+
+// S_hat[c M + k] = sum_r A_hat[(c f + r) M + k] * K_hat[r M + k]  (one pointwise product per
+// residue class, summed: the f convolutions share one inverse transform)
+__global__ __launch_bounds__(kBlock) void k_geo_dot(fe* __restrict__ S, const fe* __restrict__ A,
+                                                    const fe* __restrict__ K, uint32_t logf, uint64_t M,
+                                                    uint64_t total, fe r2) {
+  const uint64_t f = (uint64_t)1 << logf;
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t c = t / M, k = t - c * M;
+    fe acc = fe_zero();
+    for (uint64_t r = 0; r < f; ++r) acc = fe_add(acc, mont_mul(ld_fe(A + (c * f + r) * M + k), ld_fe(K + r * M + k)));
+    st_fe(S + t, mont_mul(acc, r2));
   }
 }
 
@@ -604,11 +643,36 @@ hipError_t launch_qbinom(fe* c, const fe* F, const fe* invF, uint64_t n, uint64_
   return hipGetLastError();
 }
 
-hipError_t launch_interp_assemble(fe* V, const fe* y, const fe* Zv, const fe* S, uint64_t n, uint64_t D,
-                                  const fe* iA, const fe* iB, const fe& r2, hipStream_t s) {
-  ProfScope ps("interp_assemble", 64 * D, s);
-  hipLaunchKernelGGL(k_interp_assemble, dim3((unsigned)grid_for(D)), dim3(kBlock), 0, s, V, y, Zv, S, n, D, iA,
-                     iB, r2);
+hipError_t launch_interp_assemble(fe* V, const fe* y, uint64_t ys, const fe* Zv, const fe* S, uint64_t n, uint64_t M,
+                                  int logf, uint64_t cols, const fe* iA, const fe* iB, const fe& r2, hipStream_t s) {
+  const uint64_t total = cols * M;
+  ProfScope ps("interp_assemble", 64 * total, s);
+  hipLaunchKernelGGL(k_interp_assemble, dim3((unsigned)grid_for(total)), dim3(kBlock), 0, s, V, y, ys, Zv, S, n, M,
+                     (uint32_t)logf, total, iA, iB, r2);
+  return hipGetLastError();
+}
+
+hipError_t launch_geo_rows(fe* rows, const fe* y, uint64_t ys, const fe* Zdi, uint64_t n, int logf, uint64_t M,
+                           uint64_t cols, const fe& r2, hipStream_t s) {
+  const uint64_t total = cols * M;
+  ProfScope ps("geo_rows", 48 * total, s);
+  hipLaunchKernelGGL(k_geo_rows, dim3((unsigned)grid_for(total)), dim3(kBlock), 0, s, rows, y, ys, Zdi, n,
+                     (uint32_t)logf, M, total, r2);
+  return hipGetLastError();
+}
+
+hipError_t launch_geo_krows(fe* out, const fe* b, int logf, uint64_t M, uint64_t D, hipStream_t s) {
+  ProfScope ps("geo_krows", 32 * D, s);
+  hipLaunchKernelGGL(k_geo_krows, dim3((unsigned)grid_for(D)), dim3(kBlock), 0, s, out, b, (uint32_t)logf, M, D);
+  return hipGetLastError();
+}
+
+hipError_t launch_geo_dot(fe* S, const fe* A, const fe* K, int logf, uint64_t M, uint64_t cols, const fe& r2,
+                          hipStream_t s) {
+  const uint64_t total = cols * M;
+  ProfScope ps("geo_dot", (32 * ((uint64_t)1 << logf) + 16) * total, s);
+  hipLaunchKernelGGL(k_geo_dot, dim3((unsigned)grid_for(total)), dim3(kBlock), 0, s, S, A, K, (uint32_t)logf, M,
+                     total, r2);
   return hipGetLastError();
 }
 

@@ -50,8 +50,16 @@ hipError_t launch_scan_tile(fe* data, uint64_t n, fe* tile_tot, const fe& r2, co
 hipError_t launch_scan_fix(fe* data, uint64_t n, const fe* scanned_tot, const fe& r2, hipStream_t s);
 hipError_t launch_qbinom(fe* c, const fe* F, const fe* invF, uint64_t n, uint64_t D, const fe* qA, const fe* qB,
                          const fe& r2, hipStream_t s);
-hipError_t launch_interp_assemble(fe* V, const fe* y, const fe* Zv, const fe* S, uint64_t n, uint64_t D,
-                                  const fe* iA, const fe* iB, const fe& r2, hipStream_t s);
+// V[c M + k] = P_c(q^(k f)), f = 2^logf (y_c at ys stride; Zv[k] = Z(q^(k f)))
+hipError_t launch_interp_assemble(fe* V, const fe* y, uint64_t ys, const fe* Zv, const fe* S, uint64_t n, uint64_t M,
+                                  int logf, uint64_t cols, const fe* iA, const fe* iB, const fe& r2, hipStream_t s);
+// decimated geometric interpolation (poly.cpp interpolate_geometric_*): residue-class rows of
+// y / Z', the K rows, and the summed pointwise products
+hipError_t launch_geo_rows(fe* rows, const fe* y, uint64_t ys, const fe* Zdi, uint64_t n, int logf, uint64_t M,
+                           uint64_t cols, const fe& r2, hipStream_t s);
+hipError_t launch_geo_krows(fe* out, const fe* b, int logf, uint64_t M, uint64_t D, hipStream_t s);
+hipError_t launch_geo_dot(fe* S, const fe* A, const fe* K, int logf, uint64_t M, uint64_t cols, const fe& r2,
+                          hipStream_t s);
 hipError_t launch_last_nonzero(const fe* a, uint64_t n, unsigned long long* last, hipStream_t s);
 hipError_t launch_air_eval(const AirEvalArgs& a, hipStream_t s);
 // the Rescue-Prime AIR row in its factored form (mpoly.hpp RescueAirForm), pointwise on a coset:

@@ -655,13 +655,13 @@ void prove_trace_polys(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_
   // randomized trace (stark.rs:285-301), columns on the device
   std::vector<DPoly>& trace_polys = A.trace_polys;
   {
-    DPoly col = dpoly_alloc(ctx, Tp);
-    GeoInterpCache zc;  // Z(omicron^m), Z'(omicron^i) shared by the register columns
+    // the m columns side by side (column stride Tp), interpolated as one batch
+    DPoly cols = dpoly_alloc(ctx, m * Tp);
     for (size_t s = 0; s < m; ++s) {
-      SG_HIP(launch_gather_stride(col.p(), d_trace + s, rows, m, ctx->stream));
-      SG_HIP(launch_gather_stride(col.p() + rows, d_trace_rand + s, st.num_randomizers, m, ctx->stream));
-      trace_polys.push_back(interpolate_geometric_dev(ctx, st.omicron, D, col.p(), Tp, &zc));
+      SG_HIP(launch_gather_stride(cols.p() + s * Tp, d_trace + s, rows, m, ctx->stream));
+      SG_HIP(launch_gather_stride(cols.p() + s * Tp + rows, d_trace_rand + s, st.num_randomizers, m, ctx->stream));
     }
+    trace_polys = interpolate_geometric_batch_dev(ctx, st.omicron, D, cols.p(), Tp, m, Tp);
   }
 }
 
