@@ -1,0 +1,53 @@
+#!/usr/bin/env python3
+"""The headline Stark::prove through sg_dist_stark_prove on a one-rank RCCL communicator next to the
+single-GPU sg_stark_prove on the same box: the sharded path's own cost (four-step LDEs, forests +
+top trees, sharded FRI rounds, owner-rank openings) without peers.
+
+usage: dist_prove_time.py [steps] [log_trace]
+"""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+
+sg = bench.sg
+
+
+def main():
+    steps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
+    log_trace = int(sys.argv[2]) if len(sys.argv) > 2 else bench.LOG_TRACE
+    from starkgpu import dist as D
+    dev = torch.device("cuda", 0)
+    ctx = sg.Context(0)
+    nd = D.NativeDist(ctx, transport="rccl")
+    wl = bench.ProveWorkload(0, dev, ctx, log_trace)
+
+    def single():
+        return wl.step().digest()
+
+    def sharded():
+        ps = sg.IndependentProofStream()
+        wl.stark.prove_dev(wl.trace.data_ptr(), wl.rows, wl.air, wl.boundary, ps, wl.trace_rand.data_ptr(),
+                           wl.rcoef.data_ptr(), wl.nrc, dist=nd)
+        return ps.digest()
+
+    a, b = single(), sharded()
+    assert a == b, "sharded proof bytes differ from the single-GPU proof"
+    for name, fn in (("single", single), ("sharded_world1", sharded), ("single", single),
+                     ("sharded_world1", sharded)):
+        torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        torch.cuda.synchronize(dev)
+        print(f"{name}: {(time.perf_counter() - t0) / steps * 1e3:.3f} ms/prove", flush=True)
+    nd.close()
+
+
+if __name__ == "__main__":
+    main()

@@ -1478,13 +1478,22 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
         fuse = count >= ((uint64_t)1 << env_fmin) ? env_fuse : 1;
         if (bs < lbs) kind = 0;
       }
-    } else if (count >= kQuadBelow) {
+    } else if (count * (uint64_t)batch >= kQuadBelow && count >= 2) {
       // 3 levels per launch: same-box A/Bs (profiles/r03_ab_merkle_nodes.log, r03_ab_nodes.log) put 3
       // ahead of 4 on the 2^25 tree (4.03-4.09 vs 4.12-4.16 ms) and in the prove; coalesced child
-      // loads staged through LDS were slower (4.22-4.27 ms) and were dropped
+      // loads staged through LDS were slower (4.22-4.27 ms) and were dropped.  The level is
+      // throughput-bound when all its trees together have >= kQuadBelow nodes (a forest of many
+      // small subtrees included): one lane per node, blocks no larger than a tree's level.
       static const int env_nfuse = env_int("SG_MERKLE_NODE_FUSE", 3);
       static const int env_nbs = env_int("SG_MERKLE_NODE_BS", 256);  // A/B knob: 256 or 512
       kind = env_nbs == 512 ? 6 : 2; bs = env_nbs == 512 ? 512u : 256u; fuse = env_nfuse;
+      if (count < bs) {
+        kind = 2;
+        bs = (unsigned)count;  // a power of two (tree levels)
+        int lg = 0;
+        while ((1u << lg) < bs) ++lg;
+        if (fuse > lg + 1) fuse = lg + 1;
+      }
     } else {
       // the last <= 256 nodes of a tree go to the root in one 1024-lane block
       // (SG_MERKLE_QUAD_TOP=0: 64-node blocks only)

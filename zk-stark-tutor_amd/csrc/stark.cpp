@@ -940,11 +940,16 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
   // the LDE reads are created (cached) on the main stream before the fork: the side stream
   // allocates nothing and only launches the transform passes and the tree.
   constexpr int kRandSlot = 4;
-  uint64_t r_seq, bq_seq;
-  {
-    (void)ctx->stage_twiddles(st.omega, ilog2_exact(next_pow2(Nf)));
-    (void)ctx->pow_table(g, 4096);
-    (void)ctx->pow_table(fe_pow(g, 4096), (std::max<uint64_t>(nrc, 1) + 4095) / 4096);
+  uint64_t r_seq = 0, bq_seq;
+  // where the side stream forks off the randomizer LDE + tree: 0 = at the start (beside the trace
+  // interpolation), 1 = after the interpolation, 2 = after the boundary quotients
+  // (SG_PROVE_R_FORK, scheduling experiments; the bytes are the same)
+  const char* rf = getenv("SG_PROVE_R_FORK");
+  const int r_fork = rf ? atoi(rf) : 0;
+  (void)ctx->stage_twiddles(st.omega, ilog2_exact(next_pow2(Nf)));
+  (void)ctx->pow_table(g, 4096);
+  (void)ctx->pow_table(fe_pow(g, 4096), (std::max<uint64_t>(nrc, 1) + 4095) / 4096);
+  auto fork_randomizer = [&]() {
     SG_HIP(hipEventRecord(ctx->ev_fork, ctx->stream));
     SG_HIP(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
     const fe* in = d_rcoef;
@@ -956,13 +961,16 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
     const fe* leaves = r_cw.p();
     sg_tree* t = r_tree.get();
     r_seq = launch_trees(ctx, &leaves, 1, &t, kRandSlot, ctx->side);
-  }
+  };
+  if (r_fork <= 0) fork_randomizer();
   ProveAlgebra A;
   A.Tp = Tp;
   prove_trace_polys(ctx, st, d_trace, rows, d_trace_rand, A);
   mark("trace_interpolation");
+  if (r_fork == 1) fork_randomizer();
   prove_boundary_quotients(ctx, st, bnd, A);
   mark("boundary_quotients");
+  if (r_fork >= 2) fork_randomizer();
   const std::vector<DPoly>& bqs = A.bqs;
   // boundary-quotient codewords (stark.rs:367-386); their trees hash on the side stream
   // while the main stream computes the transition quotients
