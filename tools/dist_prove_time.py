@@ -3,7 +3,7 @@
 single-GPU sg_stark_prove on the same box: the sharded path's own cost (four-step LDEs, forests +
 top trees, sharded FRI rounds, owner-rank openings) without peers.
 
-usage: dist_prove_time.py [steps] [log_trace]
+usage: dist_prove_time.py [steps] [log_trace] [only]   (only = single | sharded_world1)
 """
 import os
 import sys
@@ -21,6 +21,7 @@ sg = bench.sg
 def main():
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 5
     log_trace = int(sys.argv[2]) if len(sys.argv) > 2 else bench.LOG_TRACE
+    only = sys.argv[3] if len(sys.argv) > 3 else None
     from starkgpu import dist as D
     dev = torch.device("cuda", 0)
     ctx = sg.Context(0)
@@ -40,6 +41,8 @@ def main():
     assert a == b, "sharded proof bytes differ from the single-GPU proof"
     for name, fn in (("single", single), ("sharded_world1", sharded), ("single", single),
                      ("sharded_world1", sharded)):
+        if only and name != only:
+            continue
         torch.cuda.synchronize(dev)
         t0 = time.perf_counter()
         for _ in range(steps):

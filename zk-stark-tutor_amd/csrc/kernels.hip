@@ -1473,10 +1473,16 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
         unsigned lbs = env_bs == 512 ? 512u : 256u;
         kind = lbs == 512 ? 4 : 0;
         bs = count < lbs ? (unsigned)count : lbs;
-        // leaf levels of >= 2^SG_MERKLE_LEAF_FUSE_MIN leaves fuse node levels (A/B knob)
+        // leaf levels of >= 2^SG_MERKLE_LEAF_FUSE_MIN leaves (all trees of the launch together, a
+        // forest's subtrees included) fuse node levels (A/B knob)
         static const int env_fmin = env_int("SG_MERKLE_LEAF_FUSE_MIN", 18);
-        fuse = count >= ((uint64_t)1 << env_fmin) ? env_fuse : 1;
+        fuse = count * (uint64_t)batch >= ((uint64_t)1 << env_fmin) ? env_fuse : 1;
         if (bs < lbs) kind = 0;
+        {
+          int lg = 0;  // a block's fused levels end at its single digest
+          while ((1u << lg) < bs) ++lg;
+          if (fuse > lg + 1) fuse = lg + 1;
+        }
       }
     } else if (count * (uint64_t)batch >= kQuadBelow && count >= 2) {
       // 3 levels per launch: same-box A/Bs (profiles/r03_ab_merkle_nodes.log, r03_ab_nodes.log) put 3
