@@ -264,20 +264,31 @@ def _native_checks(nd, ctx, world, rank, logn, gather):
     assert np.array_equal(cw_full, sg.fast_coset_evaluate(root, n, sg.generator(), x[:d], ctx=ctx)), "lde"
     assert nd.merkle_root(cw, n) == sg.MerkleRoot.commit(cw_full, ctx=ctx), "merkle"
     # FRI: c = 16 folds down to one run per rank and finishes on the gathered codeword; c = n/16
-    # (two rounds) ends while still sharded and gathers the last codeword
-    for c in (16, n // 16):
-        ref = sg.IndependentProofStream()
-        sg.FRI(sg.generator(), root, n, 8, c, ctx=ctx).commit(cw_full, ref)
-        got = sg.IndependentProofStream()
-        nd.fri_commit(sg.generator(), root, cw, n, 8, c, got)
-        assert got.digest() == ref.digest(), f"fri stream c={c}"
-        # FRI::prove (fri.rs:210-248): openings gathered from the ranks that own the leaves
-        ref = sg.IndependentProofStream()
-        top = sg.FRI(sg.generator(), root, n, 8, c, ctx=ctx).prove(cw_full, ref)
-        got = sg.IndependentProofStream()
-        gtop = nd.fri_prove(sg.generator(), root, cw, n, 8, c, got)
-        assert gtop == top, f"fri prove top indices c={c}"
-        assert got.digest() == ref.digest(), f"fri prove stream c={c}"
+    # (two rounds) ends while still sharded and gathers the last codeword.  SG_DIST_FRI_TAIL: the
+    # codeword size at which the sharded rounds hand over to the single-GPU commit (0: never
+    # early; logn - 2: after two sharded rounds, with several runs per rank left; logn: at once)
+    old_tail = os.environ.get("SG_DIST_FRI_TAIL")
+    try:
+        for tail in ("0", str(logn - 2), str(logn)):
+            os.environ["SG_DIST_FRI_TAIL"] = tail
+            for c in (16, n // 16):
+                ref = sg.IndependentProofStream()
+                sg.FRI(sg.generator(), root, n, 8, c, ctx=ctx).commit(cw_full, ref)
+                got = sg.IndependentProofStream()
+                nd.fri_commit(sg.generator(), root, cw, n, 8, c, got)
+                assert got.digest() == ref.digest(), f"fri stream c={c} tail={tail}"
+                # FRI::prove (fri.rs:210-248): openings gathered from the ranks that own the leaves
+                ref = sg.IndependentProofStream()
+                top = sg.FRI(sg.generator(), root, n, 8, c, ctx=ctx).prove(cw_full, ref)
+                got = sg.IndependentProofStream()
+                gtop = nd.fri_prove(sg.generator(), root, cw, n, 8, c, got)
+                assert gtop == top, f"fri prove top indices c={c} tail={tail}"
+                assert got.digest() == ref.digest(), f"fri prove stream c={c} tail={tail}"
+    finally:
+        if old_tail is None:
+            os.environ.pop("SG_DIST_FRI_TAIL", None)
+        else:
+            os.environ["SG_DIST_FRI_TAIL"] = old_tail
 
 
 def test_native_dist_world1_rccl():
@@ -462,7 +473,12 @@ def _stark_checks(nd, world, rank, tmp, cases, gather):
             bnd = [(a, b, int(v)) for (a, b, v) in json.load(f)]
         trace = np.load(os.path.join(tmp, "trace%d.npy" % k))
         tr, rc = np.load(os.path.join(tmp, "tr%d.npy" % k)), np.load(os.path.join(tmp, "rc%d.npy" % k))
-        got = st.prove(trace, air, bnd, sg.IndependentProofStream(), tr, rc, dist=nd)
+        # small domains: every FRI round sharded (SG_DIST_FRI_TAIL=0); C4: the default hand-over
+        os.environ["SG_DIST_FRI_TAIL"] = "0" if N < 1000 else "20"
+        try:
+            got = st.prove(trace, air, bnd, sg.IndependentProofStream(), tr, rc, dist=nd)
+        finally:
+            os.environ.pop("SG_DIST_FRI_TAIL", None)
         ok.append((k, got == open(os.path.join(tmp, "proof%d.bin" % k), "rb").read()))
     flags = gather(ok)
     assert all(f for per_rank in flags for (_, f) in per_rank), f"world {world}: sharded proof bytes differ: {flags}"

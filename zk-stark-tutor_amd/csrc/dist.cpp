@@ -295,7 +295,15 @@ void dist_fri_commit(sg_dist* d, const sg_fri* f, const fe* runs, uint64_t n, co
   DevBuf owned;
   uint64_t k1s = n1, length = n;
   size_t r = 0;
+  // once the whole codeword is small (<= 2^SG_DIST_FRI_TAIL elements, default 2^20 = 16 MiB) the
+  // remaining rounds are latency-bound: every rank gathers it and continues with the single-GPU
+  // commit instead of paying a forest, a collective and a host round trip per sharded round
+  const char* te = getenv("SG_DIST_FRI_TAIL");
+  const int tail_log = te ? atoi(te) : 20;
+  const uint64_t tail_below = tail_log <= 0 ? 0 : (uint64_t)1 << std::min(tail_log, 62);
+  bool all_sharded = false;
   while (k1s > 1 && r < rounds) {
+    if (length <= tail_below) break;
     const fe winv = fe_inv(omega);
     SG_REQUIRE(fe_eq(fe_pow(omega, length - 1), winv), "error in commit: omega does not have the right order!");
     uint8_t root[64];
@@ -309,7 +317,10 @@ void dist_fri_commit(sg_dist* d, const sg_fri* f, const fe* runs, uint64_t n, co
     }
     dist_merkle_root(d, cur, k1s, R, root, sr);
     push_obj(ps, SG_OBJ_ROOT, root, 64);
-    if (r == rounds - 1) break;
+    if (r == rounds - 1) {
+      all_sharded = true;
+      break;
+    }
     uint8_t chal[32];
     if (ps->fiat_shamir_prover(ps->user, 32, chal) != 0)
       throw Error{SG_ERR_CALLBACK, "proof stream fiat_shamir callback failed"};
@@ -330,7 +341,7 @@ void dist_fri_commit(sg_dist* d, const sg_fri* f, const fe* runs, uint64_t n, co
     offset = fe_mul(offset, offset);
     ++r;
   }
-  if (r == rounds - 1 && k1s > 1) {
+  if (all_sharded && k1s > 1) {
     // every round done while still sharded: gather the last codeword (fri.rs:166) in natural order
     DevBuf all(ctx, d->G * k1s * R * sizeof(fe)), nat(ctx, d->G * k1s * R * sizeof(fe));
     exchange(d, cur, all.get(), k1s * R * sizeof(fe), /*a2a=*/false);          // [g][k1][c]
@@ -345,9 +356,16 @@ void dist_fri_commit(sg_dist* d, const sg_fri* f, const fe* runs, uint64_t n, co
     push_obj(ps, SG_OBJ_CODEWORD, payload.data(), payload.size());
     return;
   }
-  // one run per rank left: [g][c] is the natural order of the N2-element codeword
-  DevBuf full(ctx, d->G * R * sizeof(fe));
-  exchange(d, cur, full.get(), R * sizeof(fe), /*a2a=*/false);
+  // the rest on the gathered codeword: [g][k1][c] -> [k1][g][c] is its natural order (with one
+  // run per rank left, [g][c] already is)
+  DevBuf full(ctx, d->G * k1s * R * sizeof(fe));
+  if (k1s == 1) {
+    exchange(d, cur, full.get(), R * sizeof(fe), /*a2a=*/false);
+  } else {
+    DevBuf all(ctx, d->G * k1s * R * sizeof(fe));
+    exchange(d, cur, all.get(), k1s * R * sizeof(fe), /*a2a=*/false);
+    SG_HIP(launch_swap01(all.as<fe>(), full.as<fe>(), d->G, k1s, R, ctx->stream));
+  }
   sg_fri sub = *f;
   sub.offset = from_fe(offset);
   sub.omega = from_fe(omega);
