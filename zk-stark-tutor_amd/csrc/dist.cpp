@@ -214,32 +214,48 @@ void dist_coset_evaluate(sg_dist* d, const fe& gen, uint64_t n, const fe& offset
 // root of the natural-order codeword held as runs [k1s][R] on every rank (merkle_root.rs:21-32):
 // a forest of k1s subtrees per rank, the run roots all-gathered (64 B each), the top on every rank.
 // With `keep`, the forest and the top tree move into it (openings).
-void dist_merkle_root(sg_dist* d, const fe* runs, uint64_t k1s, uint64_t R, uint8_t root[64],
-                      ShardedRound* keep) {
-  sg_ctx* ctx = d->ctx;
+//
+// Split in two so the hashing can overlap other work: the forest and its run roots on any stream
+// (no collective), then the all-gather and the top tree on the context's stream (every collective
+// of a communicator stays on one stream, in the same order on every rank).
+void dist_forest_alloc(sg_dist* d, uint64_t k1s, uint64_t R, PendingForest& pf) {
   SG_REQUIRE(R >= 1 && (R & (R - 1)) == 0 && k1s >= 1 && (k1s & (k1s - 1)) == 0, "Leafs len must be power of two");
-  const uint64_t per = merkle_tree_digests(R) * 8;  // u64 per subtree
-  DevBuf forest(ctx, k1s * per * 8), roots(ctx, k1s * 64), all(ctx, d->G * k1s * 64), ordered(ctx, d->G * k1s * 64);
-  for (uint64_t t0 = 0; t0 < k1s; t0 += kRows) {
-    const int cnt = (int)std::min<uint64_t>(kRows, k1s - t0);
-    const fe* lv = runs + t0 * R;
-    uint64_t* tr = forest.as<uint64_t>() + t0 * per;
-    SG_HIP(launch_merkle_tree(&lv, &tr, cnt, R, nullptr, ctx->stream, R, per, 0));
+  pf.k1s = k1s;
+  pf.R = R;
+  pf.per = merkle_tree_digests(R) * 8;  // u64 per subtree
+  pf.forest = DevBuf(d->ctx, k1s * pf.per * 8);
+  pf.roots = DevBuf(d->ctx, k1s * 64);
+}
+
+void dist_forest_launch(sg_dist* d, const fe* runs, PendingForest& pf, hipStream_t s) {
+  (void)d;
+  for (uint64_t t0 = 0; t0 < pf.k1s; t0 += kRows) {
+    const int cnt = (int)std::min<uint64_t>(kRows, pf.k1s - t0);
+    const fe* lv = runs + t0 * pf.R;
+    uint64_t* tr = pf.forest.as<uint64_t>() + t0 * pf.per;
+    SG_HIP(launch_merkle_tree(&lv, &tr, cnt, pf.R, nullptr, s, pf.R, pf.per, 0));
   }
-  SG_HIP(launch_gather_roots(forest.as<uint64_t>(), per, (2 * R - 2) * 8, roots.as<uint64_t>(), k1s, ctx->stream));
-  exchange(d, roots.get(), all.get(), k1s * 64, /*a2a=*/false);  // [g][k1]
+  SG_HIP(launch_gather_roots(pf.forest.as<uint64_t>(), pf.per, (2 * pf.R - 2) * 8, pf.roots.as<uint64_t>(), pf.k1s,
+                             s));
+}
+
+void dist_forest_finish(sg_dist* d, PendingForest& pf, uint8_t root[64], ShardedRound* keep) {
+  sg_ctx* ctx = d->ctx;
+  const uint64_t k1s = pf.k1s;
+  DevBuf all(ctx, d->G * k1s * 64), ordered(ctx, d->G * k1s * 64);
+  exchange(d, pf.roots.get(), all.get(), k1s * 64, /*a2a=*/false);  // [g][k1]
   // [g][k1] -> [k1][g]: global run order (a digest is 4 field-element slots)
   SG_HIP(launch_swap01(all.as<fe>(), ordered.as<fe>(), d->G, k1s, 4, ctx->stream));
   const uint64_t m = d->G * k1s;
   if (keep) {
     keep->k1s = k1s;
     keep->m = m;
-    keep->per = per;
+    keep->per = pf.per;
   }
   if (m == 1) {
     SG_HIP(hipMemcpyAsync(root, ordered.get(), 64, hipMemcpyDeviceToHost, ctx->stream));
     SG_HIP(hipStreamSynchronize(ctx->stream));
-    if (keep) keep->forest = std::move(forest);
+    if (keep) keep->forest = std::move(pf.forest);
     return;
   }
   DevBuf top(ctx, merkle_tree_digests(m) * 64);
@@ -250,9 +266,17 @@ void dist_merkle_root(sg_dist* d, const fe* runs, uint64_t k1s, uint64_t R, uint
   SG_HIP(hipStreamSynchronize(ctx->stream));
   memcpy(root, ctx->pinned_roots, 64);
   if (keep) {
-    keep->forest = std::move(forest);
+    keep->forest = std::move(pf.forest);
     keep->top = std::move(top);
   }
+}
+
+void dist_merkle_root(sg_dist* d, const fe* runs, uint64_t k1s, uint64_t R, uint8_t root[64],
+                      ShardedRound* keep) {
+  PendingForest pf;
+  dist_forest_alloc(d, k1s, R, pf);
+  dist_forest_launch(d, runs, pf, d->ctx->stream);
+  dist_forest_finish(d, pf, root, keep);
 }
 
 void dist_lde_replicated(sg_dist* d, const fe& gen, uint64_t n, const fe& offset, const fe* coeffs, uint64_t len,

@@ -39,6 +39,15 @@ void dist_lde_replicated(sg_dist* d, const fe& gen, uint64_t n, const fe& offset
 // merkle_root.rs:21-32 of a run-sharded codeword; with `keep`, the forest and top tree are retained
 void dist_merkle_root(sg_dist* d, const fe* runs, uint64_t k1s, uint64_t R, uint8_t root[64],
                       ShardedRound* keep = nullptr);
+// the same in two parts: the forest + run roots on any stream (no collective; buffers allocated
+// beforehand), then the all-gather of the run roots and the top tree on the context's stream
+struct PendingForest {
+  uint64_t k1s = 0, R = 0, per = 0;
+  DevBuf forest, roots;
+};
+void dist_forest_alloc(sg_dist* d, uint64_t k1s, uint64_t R, PendingForest& pf);
+void dist_forest_launch(sg_dist* d, const fe* runs, PendingForest& pf, hipStream_t s);
+void dist_forest_finish(sg_dist* d, PendingForest& pf, uint8_t root[64], ShardedRound* keep);
 // values and authentication paths (leaf level first) of global indices I of a sharded codeword,
 // identical on every rank: one all-gather of the owners' slots plus the local top tree
 void dist_open_round(sg_dist* d, const ShardedRound& sr, uint64_t R, uint64_t n2, const std::vector<uint64_t>& I,

@@ -1076,29 +1076,53 @@ void stark_prove_dist(sg_dist* dd, const sg_stark& st, const fe* d_trace, size_t
   dist_plan(Nf, dist_world(dd), n1, n2);
   const uint64_t R = n2 / dist_world(dd), shard = n1 * R;
   PhaseMarks mark;
+  // The forests of the boundary-quotient and randomizer codewords hash on the side stream while
+  // the main stream runs the algebra (as in the single-GPU prove); their run-root all-gathers and
+  // top trees follow on the main stream, where every collective of the communicator stays.  The
+  // buffers side-stream kernels touch are allocated here, with the main stream drained.
+  SG_HIP(hipStreamSynchronize(ctx->stream));
+  std::vector<DevBuf> runs;
+  std::vector<PendingForest> forests(m + 1);
+  for (size_t s = 0; s <= m; ++s) {
+    runs.emplace_back(ctx, shard * sizeof(fe));
+    dist_forest_alloc(dd, n1, R, forests[s]);
+  }
+  SideDrain side_drain{ctx};
+  auto fork_forests = [&](size_t s0, size_t s1) {
+    SG_HIP(hipEventRecord(ctx->ev_fork, ctx->stream));
+    SG_HIP(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
+    for (size_t s = s0; s < s1; ++s) dist_forest_launch(dd, runs[s].as<fe>(), forests[s], ctx->side);
+  };
+  auto lde = [&](const fe* coeffs, uint64_t len, DevBuf& out) {
+    SG_REQUIRE(len <= Nf, "fast_coset_evaluate: polynomial longer than root_order");
+    if (len) dist_lde_replicated(dd, st.omega, Nf, g, coeffs, len, out.as<fe>());
+    else SG_HIP(hipMemsetAsync(out.get(), 0, shard * sizeof(fe), ctx->stream));
+  };
+  // randomizer codeword (stark.rs:424-445) first: it depends on nothing else, so its forest hashes
+  // beside the trace interpolation and the boundary quotients
+  lde(d_rcoef, nrc, runs[m]);
+  fork_forests(m, m + 1);
   ProveAlgebra A;
   A.Tp = Tp;
   prove_trace_polys(ctx, st, d_trace, rows, d_trace_rand, A);
   prove_boundary_quotients(ctx, st, bnd, A);
   mark("dist_algebra_boundary");
-  // boundary-quotient codewords + commitments (stark.rs:364-386), sharded
-  auto commit = [&](const fe* coeffs, uint64_t len, DevBuf& runs, ShardedRound& sr, uint8_t root[64]) {
-    SG_REQUIRE(len <= Nf, "fast_coset_evaluate: polynomial longer than root_order");
-    runs = DevBuf(ctx, shard * sizeof(fe));
-    if (len) dist_lde_replicated(dd, st.omega, Nf, g, coeffs, len, runs.as<fe>());
-    else SG_HIP(hipMemsetAsync(runs.get(), 0, shard * sizeof(fe), ctx->stream));
-    dist_merkle_root(dd, runs.as<fe>(), n1, R, root, &sr);
-    sr.cw = runs.as<fe>();
-  };
-  std::vector<DevBuf> runs(m + 1);
-  std::vector<ShardedRound> rounds(m + 1);
-  std::vector<std::array<uint8_t, 64>> roots(m + 1);
-  for (size_t s = 0; s < m; ++s) commit(A.bqs[s].p(), A.bqs[s].len, runs[s], rounds[s], roots[s].data());
-  mark("dist_bq_commit");
+  // boundary-quotient codewords (stark.rs:364-386), their forests on the side stream
+  for (size_t s = 0; s < m; ++s) lde(A.bqs[s].p(), A.bqs[s].len, runs[s]);
+  fork_forests(0, m);
+  mark("dist_bq_lde");
   prove_transition_quotients(ctx, st, tcs, A);
   mark("dist_transition_quotients");
-  // randomizer codeword + commitment (stark.rs:424-445)
-  commit(d_rcoef, nrc, runs[m], rounds[m], roots[m].data());
+  SG_HIP(hipEventRecord(ctx->ev_join, ctx->side));
+  SG_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
+  // run roots all-gathered, top trees, roots in the reference's order
+  std::vector<ShardedRound> rounds(m + 1);
+  std::vector<std::array<uint8_t, 64>> roots(m + 1);
+  for (size_t s = 0; s <= m; ++s) {
+    dist_forest_finish(dd, forests[s], roots[s].data(), &rounds[s]);
+    rounds[s].cw = runs[s].as<fe>();
+  }
+  mark("dist_commitments");
   for (size_t s = 0; s <= m; ++s) push_obj(ps, SG_OBJ_ROOT, roots[s].data(), 64);
   uint8_t fs[32];
   if (ps->fiat_shamir_prover(ps->user, 32, fs) != 0)
