@@ -409,8 +409,9 @@ def test_north_star_sharded_lde_fri_prove(north_star_reference, world):
 
 # ------------------------------------------------------------------ sharded Stark::prove
 
-# (N, expansion, colinearity checks, security, transition degree): FRI domains 2^9 .. 2^21
-STARK_CASES = [(40, 4, 3, 4, 2), (27, 8, 4, 8, 3), (100, 8, 8, 16, 3), (65278, 8, 64, 128, 3)]
+# (N, expansion, colinearity checks, security, transition degree): FRI domains 2^9 .. 2^21, and
+# 2^8 (too small to split over 8 ranks: every rank proves it whole)
+STARK_CASES = [(40, 4, 3, 4, 2), (27, 8, 4, 8, 3), (100, 8, 8, 16, 3), (65278, 8, 64, 128, 3), (9, 4, 2, 2, 2)]
 
 
 @pytest.fixture(scope="module")
@@ -521,7 +522,7 @@ def _stark_worker(rank, world, port, tmp, cases):
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("world,cases", [(2, (0, 1, 2, 3)), (4, (1, 2)), (8, (0, 1, 2, 3))])
+@pytest.mark.parametrize("world,cases", [(2, (0, 1, 2, 3, 4)), (4, (1, 2, 4)), (8, (0, 1, 2, 3, 4))])
 def test_dist_stark_prove_one_gpu_host_transport(stark_reference, world, cases):
     """Stark::prove (stark.rs:276-562) with the FRI domain sharded over `world` ranks on this box's
     GPU (host transport over gloo): every rank writes the expected proof bytes, C4 included."""

@@ -1072,9 +1072,18 @@ void stark_prove_dist(sg_dist* dd, const sg_stark& st, const fe* d_trace, size_t
   SG_REQUIRE(nrc == tcd + 1, "randomizer polynomial must have max_degree(transition_constraints) + 1 coefficients");
   SG_REQUIRE(nrc <= Nf, "fast_coset_evaluate: polynomial longer than root_order");
   SG_REQUIRE(m <= 4, "at most 4 registers are supported by the AIR kernel");
+  // a FRI domain too small to split over this many ranks (N1 >= G, N2 >= 4 G) is proved whole
+  // by every rank: the same bytes, no collective
+  const int G = dist_world(dd);
+  const int logNf = ilog2_exact(Nf);
+  const uint64_t p1 = (uint64_t)1 << (logNf / 2), p2 = Nf / p1;
+  if (p1 % (uint64_t)G != 0 || p2 % (4 * (uint64_t)G) != 0) {
+    stark_prove(ctx, st, d_trace, rows, tcs, bnd, d_trace_rand, d_rcoef, nrc, ps);
+    return;
+  }
   uint64_t n1, n2;
-  dist_plan(Nf, dist_world(dd), n1, n2);
-  const uint64_t R = n2 / dist_world(dd), shard = n1 * R;
+  dist_plan(Nf, G, n1, n2);
+  const uint64_t R = n2 / G, shard = n1 * R;
   PhaseMarks mark;
   // The forests of the boundary-quotient and randomizer codewords hash on the side stream while
   // the main stream runs the algebra (as in the single-GPU prove); their run-root all-gathers and
