@@ -372,7 +372,8 @@ int sg_stark_prove_dev(sg_ctx* ctx, const sg_stark* st, const sg_fe* d_trace, si
  * Stark::prove when the FRI domain is split across GPUs).  Every rank passes the same arguments
  * (st and tcs created on the communicator's context, sg_dist_ctx) and writes the same proof-stream
  * bytes as sg_stark_prove: the trace-domain algebra is replicated, the four LDEs, the three
- * commitments, FRI::prove and the openings run on run shards of N_fri / world elements. */
+ * commitments, FRI::prove and the openings run on run shards of N_fri / world elements.  A FRI
+ * domain too small to split (sg_dist_plan fails) is proved whole by every rank. */
 int sg_dist_stark_prove(sg_dist* d, const sg_stark* st, const sg_fe* trace, size_t rows, const sg_mpoly* const* tcs,
                         size_t ntcs, const sg_boundary* boundary, size_t nb, const sg_fe* trace_randomizers,
                         const sg_fe* randomizer_coeffs, size_t n_rc, const sg_proof_stream* ps);
