@@ -1,0 +1,102 @@
+/*
+ * prove_rescue.c -- a compiled host calling libstarkgpu through its C ABI only (no Python, no
+ * torch): what the reference crate's Stark::prove (stark/stark.rs:276-562) does for the
+ * Rescue-Prime signature statement (rescue_prime/rescue_prime.rs, stark.rs:823-840), with the
+ * two thread_rng draws read from a file so the bytes can be compared with another prover's.
+ *
+ *   prove_rescue N expansion colinearity security tcd input_lo input_hi randomness.bin proof.bin
+ *
+ * randomness.bin: 16-byte little-endian (lo, hi) field elements -- num_randomizers x 2 trace
+ * randomizer rows (stark.rs:285-301), then max_degree + 1 randomizer coefficients
+ * (stark.rs:425-433).  proof.bin receives the proof stream's digest() (stark.rs:562).
+ * Prints "proof <bytes> num_randomizers <r> randomizer_coefficients <k> fri_domain <n>".
+ * Exit status 0 on success; 2 when randomness.bin is too short (it prints how many elements
+ * it needs first, so a caller can size the file); 1 on any library error.
+ */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "stark_gpu.h"
+
+#define CHECK(call)                                                                      \
+  do {                                                                                   \
+    int rc_ = (call);                                                                    \
+    if (rc_ != 0) {                                                                      \
+      fprintf(stderr, "%s failed (%d): %s\n", #call, rc_, ctx ? sg_last_error(ctx) : ""); \
+      return 1;                                                                          \
+    }                                                                                    \
+  } while (0)
+
+int main(int argc, char** argv) {
+  if (argc != 10) {
+    fprintf(stderr, "usage: %s N expansion colinearity security tcd input_lo input_hi randomness.bin proof.bin\n",
+            argv[0]);
+    return 1;
+  }
+  const size_t N = strtoull(argv[1], NULL, 10), exp = strtoull(argv[2], NULL, 10);
+  const size_t c = strtoull(argv[3], NULL, 10), sec = strtoull(argv[4], NULL, 10);
+  const size_t tcd = strtoull(argv[5], NULL, 10);
+  const sg_fe input = {strtoull(argv[6], NULL, 0), strtoull(argv[7], NULL, 0)};
+  sg_ctx* ctx = NULL;
+  CHECK(sg_ctx_create(0, &ctx));
+  sg_rescue* rp = NULL;
+  CHECK(sg_rescue_create(ctx, 2, 1, sec, N, &rp));  /* RescuePrime::new(m = 2, capacity 1, ...) */
+  sg_fe output;
+  CHECK(sg_rescue_hash(ctx, rp, input, &output));
+  sg_fe* trace = malloc((N + 1) * 2 * sizeof(sg_fe));
+  CHECK(sg_rescue_trace(ctx, rp, input, trace));
+  sg_boundary bnd[2];
+  CHECK(sg_rescue_boundary_constraints(rp, output, bnd));
+  sg_stark* st = NULL;
+  CHECK(sg_stark_create(ctx, exp, c, sec, 2, N + 1, tcd, &st));
+  sg_fe omicron;
+  uint64_t D = 0;
+  sg_fri fri;
+  size_t nr = 0;
+  CHECK(sg_stark_params(st, &omicron, &D, &fri, &nr));
+  sg_mpoly* tcs[2] = {NULL, NULL};
+  CHECK(sg_rescue_transition_constraints(ctx, rp, omicron, D, tcs));
+  uint64_t md = 0;
+  CHECK(sg_stark_max_degree(ctx, st, (const sg_mpoly* const*)tcs, 2, &md));
+  const size_t nrc = (size_t)md + 1, need = 2 * nr + nrc;
+  printf("needs %zu randomness elements\n", need);
+  FILE* f = fopen(argv[8], "rb");
+  if (!f) {
+    fprintf(stderr, "cannot open %s\n", argv[8]);
+    return 1;
+  }
+  sg_fe* rnd = malloc(need * sizeof(sg_fe));
+  const size_t got = fread(rnd, sizeof(sg_fe), need, f);
+  fclose(f);
+  if (got != need) {
+    fprintf(stderr, "%s holds %zu elements, %zu needed\n", argv[8], got, need);
+    return 2;
+  }
+  sg_stream* s = sg_stream_create();
+  const sg_proof_stream cb = sg_stream_callbacks(s);
+  CHECK(sg_stark_prove(ctx, st, trace, N + 1, (const sg_mpoly* const*)tcs, 2, bnd, 2, rnd, rnd + 2 * nr, nrc, &cb));
+  size_t len = 0;
+  CHECK(sg_stream_digest(s, NULL, 0, &len));
+  uint8_t* proof = malloc(len);
+  CHECK(sg_stream_digest(s, proof, len, &len));
+  FILE* o = fopen(argv[9], "wb");
+  if (!o || fwrite(proof, 1, len, o) != len) {
+    fprintf(stderr, "cannot write %s\n", argv[9]);
+    return 1;
+  }
+  fclose(o);
+  printf("proof %zu num_randomizers %zu randomizer_coefficients %zu fri_domain %llu\n", len, nr, nrc,
+         (unsigned long long)fri.domain_length);
+  free(proof);
+  free(rnd);
+  free(trace);
+  sg_stream_destroy(s);
+  sg_mpoly_free(tcs[0]);
+  sg_mpoly_free(tcs[1]);
+  sg_stark_free(st);
+  sg_rescue_free(rp);
+  sg_ctx_destroy(ctx);
+  return 0;
+}

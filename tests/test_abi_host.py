@@ -185,3 +185,18 @@ def test_host_mpolynomial_and_degree_bounds_match_oracle():
     air_h = [sg.MPolynomial.new(a.d, ctx=h) for a in air_o]
     assert st_h.transition_degree_bounds(air_h) == st_o.transition_degree_bounds(air_o)
     assert st_h.max_degree(air_h) == st_o.max_degree(air_o)
+
+
+def test_c_host_example_builds_and_links():
+    """examples/prove_rescue.c compiles against include/stark_gpu.h alone and links libstarkgpu.so
+    (no Python in that binary); without arguments it prints its usage (no GPU touched)."""
+    import subprocess
+    import tempfile
+    out = os.path.join(tempfile.mkdtemp(prefix="sg_chost_"), "prove_rescue")
+    pkg = os.path.join(ROOT, "zk-stark-tutor_amd", "starkgpu")
+    subprocess.run(["gcc", "-O2", "-std=c11", "-Wall", "-Wextra", "-Werror", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(ROOT, "examples", "prove_rescue.c"), "-L", pkg, "-lstarkgpu",
+                    "-Wl,-rpath," + pkg, "-Wl,-rpath,/opt/rocm/lib", "-Wl,-rpath-link,/opt/rocm/lib", "-o", out],
+                   check=True)
+    res = subprocess.run([out], capture_output=True, text=True, timeout=60)
+    assert res.returncode == 1 and "usage" in res.stderr
