@@ -378,14 +378,21 @@ const fe* interp_kernel(sg_ctx* ctx, const fe& q, uint64_t D, int logf) {
   DevBuf b = interp_b(ctx, q, D);
   void* t = nullptr;
   SG_HIP(hipMalloc(&t, D * sizeof(fe)));
-  if (logf == 0) {
-    ntt_sized(ctx, q, b.as<fe>(), D, ilog2_exact(D), reinterpret_cast<fe*>(t));
-  } else {
-    const uint64_t M = D >> logf;
-    DevBuf rows(ctx, D * sizeof(fe));
-    SG_HIP(launch_geo_krows(rows.as<fe>(), b.as<fe>(), logf, M, D, ctx->stream));
-    ntt_rows_dev(ctx, fe_pow(q, (uint64_t)1 << logf), rows.as<fe>(), (uint64_t)1 << logf, ilog2_exact(M),
-                 reinterpret_cast<fe*>(t), nullptr);
+  try {
+    if (logf == 0) {
+      ntt_sized(ctx, q, b.as<fe>(), D, ilog2_exact(D), reinterpret_cast<fe*>(t));
+    } else {
+      const uint64_t M = D >> logf;
+      DevBuf rows(ctx, D * sizeof(fe));
+      SG_HIP(launch_geo_krows(rows.as<fe>(), b.as<fe>(), logf, M, D, ctx->stream));
+      ntt_rows_dev(ctx, fe_pow(q, (uint64_t)1 << logf), rows.as<fe>(), (uint64_t)1 << logf, ilog2_exact(M),
+                   reinterpret_cast<fe*>(t), nullptr);
+    }
+    // the table outlives this call's temporaries: complete before they return to the pool
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+  } catch (...) {
+    (void)hipFree(t);
+    throw;
   }
   ctx->interp_tables[key] = t;
   return reinterpret_cast<const fe*>(t);
