@@ -404,102 +404,157 @@ void dist_fri_commit(sg_dist* d, const sg_fri* f, const fe* runs, uint64_t n, co
   fri_commit_dev(ctx, &sub, full.as<fe>(), length, ps, st, /*borrow_input=*/true);
 }
 
-// Openings of round r at global indices I: values and authentication paths (leaf level first),
-// identical on every rank.  A sharded round's value and subtree part come from the rank that owns
-// the run (i = k1 n2 + g R + c: rank g, run k1, leaf c), exchanged in one all-gather of fixed-size
-// slots; its top part (run index i / R in the top tree) is on every rank.
-void dist_open(sg_dist* d, const DistFriState& s, size_t r, const std::vector<uint64_t>& I, std::vector<fe>& vals,
-               std::vector<uint8_t>& paths, int& depth) {
+// Openings at global indices I of many rounds at once: values and authentication paths (leaf level
+// first), identical on every rank.  A sharded round's value and subtree part come from the rank
+// that owns the run (i = k1 n2 + g R + c: rank g, run k1, leaf c); its top part (run index i / R in
+// the top tree) is on every rank; a round of the single-GPU tail is local.  Every request's device
+// gathers are issued together (one host round trip), and the owned slots of all sharded requests
+// travel in ONE all-gather: two round trips for the whole query phase instead of two per round.
+void dist_open_batch(sg_dist* d, uint64_t R, uint64_t n2, std::vector<OpenReq>& reqs) {
   sg_ctx* ctx = d->ctx;
-  const size_t q = I.size();
-  vals.assign(q, fe_zero());
-  if (r >= s.sharded.size()) {  // a round of the single-GPU tail
-    const size_t t = r - s.sharded.size();
-    const sg_tree* tree = s.tail.trees[t].get();
-    depth = tree->logn;
-    std::vector<uint64_t> di;
-    for (uint64_t i : I) di.push_back(i);
-    DevBuf dI(ctx, q * 8), dV(ctx, q * sizeof(fe));
-    SG_HIP(hipMemcpyAsync(dI.get(), di.data(), q * 8, hipMemcpyHostToDevice, ctx->stream));
-    SG_HIP(launch_gather_fe(s.tail.cw[t], dI.as<uint64_t>(), dV.as<fe>(), (uint32_t)q, ctx->stream));
-    SG_HIP(hipMemcpyAsync(vals.data(), dV.get(), q * sizeof(fe), hipMemcpyDeviceToHost, ctx->stream));
-    std::vector<uint64_t> pidx;
-    for (uint64_t i : I) path_indices(tree, i, pidx);
-    paths.assign(pidx.size() * 64, 0);
-    gather_digests(ctx, tree, pidx, paths.data());  // synchronizes the stream
-    return;
+  const int lr = ilog2_exact(R);
+  const size_t slot = 16 + 64 * (size_t)lr;
+  struct Job {
+    const void* src;
+    bool digest;         // 64-byte digests (else 16-byte elements)
+    size_t idx0, count;  // index range in `idx`
+    size_t out0;         // output offset in values (elements) or digests (64-byte units)
+  };
+  std::vector<uint64_t> idx;
+  std::vector<Job> jobs;
+  size_t nvals = 0, ndig = 0;
+  auto add_job = [&](const void* src, bool digest, const std::vector<uint64_t>& ix) -> size_t {
+    const size_t out0 = digest ? ndig : nvals;
+    if (ix.empty()) return out0;
+    jobs.push_back({src, digest, idx.size(), ix.size(), out0});
+    idx.insert(idx.end(), ix.begin(), ix.end());
+    (digest ? ndig : nvals) += ix.size();
+    return out0;
+  };
+  struct Plan {
+    size_t own_vals = 0, own_dig = 0, top_dig = 0, path_dig = 0, vals_at = 0;
+    std::vector<size_t> own;  // positions in I this rank owns (sharded)
+    int lm = 0;
+  };
+  std::vector<Plan> plans(reqs.size());
+  size_t qtot = 0;  // slots of all sharded requests
+  for (size_t j = 0; j < reqs.size(); ++j) {
+    OpenReq& q = reqs[j];
+    Plan& pl = plans[j];
+    if (!q.sr) {  // a local round
+      std::vector<uint64_t> pidx;
+      for (uint64_t i : q.I) path_indices(q.tree, i, pidx);
+      q.depth = q.tree->logn;
+      pl.vals_at = add_job(q.cw, false, q.I);
+      pl.path_dig = add_job(q.tree->buf.get(), true, pidx);
+      continue;
+    }
+    const ShardedRound& sr = *q.sr;
+    pl.lm = ilog2_exact(sr.m);
+    q.depth = lr + pl.lm;
+    std::vector<uint64_t> eidx, didx, tidx;
+    for (size_t k = 0; k < q.I.size(); ++k) {
+      const uint64_t i = q.I[k];
+      for (int lv = 0; lv < pl.lm; ++lv) tidx.push_back(level_offset(sr.m, lv) + (((i / R) >> lv) ^ 1));
+      if ((i % n2) / R != (uint64_t)d->g) continue;
+      const uint64_t k1 = i / n2, c = i % R;
+      pl.own.push_back(k);
+      eidx.push_back(k1 * R + c);
+      for (int lv = 0; lv < lr; ++lv) didx.push_back(k1 * (sr.per / 8) + level_offset(R, lv) + ((c >> lv) ^ 1));
+    }
+    pl.own_vals = add_job(sr.cw, false, eidx);
+    pl.own_dig = add_job(sr.forest.get(), true, didx);
+    if (pl.lm) pl.top_dig = add_job(sr.top.get(), true, tidx);
+    qtot += q.I.size();
   }
-  dist_open_round(d, s.sharded[r], s.R, s.n2, I, vals, paths, depth);
+  // every gather at once, one round trip
+  std::vector<fe> vals(nvals);
+  std::vector<uint8_t> dig(ndig * 64);
+  if (!jobs.empty()) {
+    DevBuf dI(ctx, idx.size() * 8), dV(ctx, std::max<size_t>(nvals, 1) * sizeof(fe)), dD(ctx, std::max<size_t>(ndig, 1) * 64);
+    SG_HIP(hipMemcpyAsync(dI.get(), idx.data(), idx.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+    for (const Job& jb : jobs) {
+      const uint64_t* ix = dI.as<uint64_t>() + jb.idx0;
+      if (jb.digest)
+        SG_HIP(launch_gather_digests(static_cast<const uint64_t*>(jb.src), ix, dD.as<uint64_t>() + jb.out0 * 8,
+                                     (uint32_t)jb.count, ctx->stream));
+      else
+        SG_HIP(launch_gather_fe(static_cast<const fe*>(jb.src), ix, dV.as<fe>() + jb.out0, (uint32_t)jb.count,
+                                ctx->stream));
+    }
+    if (nvals) SG_HIP(hipMemcpyAsync(vals.data(), dV.get(), nvals * sizeof(fe), hipMemcpyDeviceToHost, ctx->stream));
+    if (ndig) SG_HIP(hipMemcpyAsync(dig.data(), dD.get(), ndig * 64, hipMemcpyDeviceToHost, ctx->stream));
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+  }
+  // the owned slots of every sharded request, one all-gather
+  std::vector<uint8_t> all;
+  if (qtot) {
+    std::vector<uint8_t> mine(qtot * slot, 0);
+    size_t base = 0;
+    for (size_t j = 0; j < reqs.size(); ++j) {
+      if (!reqs[j].sr) continue;
+      const Plan& pl = plans[j];
+      for (size_t o = 0; o < pl.own.size(); ++o) {
+        uint8_t* p = mine.data() + (base + pl.own[o]) * slot;
+        memcpy(p, &vals[pl.own_vals + o], 16);
+        memcpy(p + 16, dig.data() + (pl.own_dig + o * (size_t)lr) * 64, 64 * (size_t)lr);
+      }
+      base += reqs[j].I.size();
+    }
+    DevBuf dsend(ctx, qtot * slot), drecv(ctx, d->G * qtot * slot);
+    SG_HIP(hipMemcpyAsync(dsend.get(), mine.data(), qtot * slot, hipMemcpyHostToDevice, ctx->stream));
+    exchange(d, dsend.get(), drecv.get(), qtot * slot, /*a2a=*/false);
+    all.resize((size_t)d->G * qtot * slot);
+    SG_HIP(hipMemcpyAsync(all.data(), drecv.get(), all.size(), hipMemcpyDeviceToHost, ctx->stream));
+    SG_HIP(hipStreamSynchronize(ctx->stream));
+  }
+  size_t base = 0;
+  for (size_t j = 0; j < reqs.size(); ++j) {
+    OpenReq& q = reqs[j];
+    const Plan& pl = plans[j];
+    const size_t nq = q.I.size(), depth = (size_t)q.depth;
+    q.vals.assign(nq, fe_zero());
+    q.paths.assign(nq * depth * 64, 0);
+    if (!q.sr) {
+      for (size_t k = 0; k < nq; ++k) q.vals[k] = vals[pl.vals_at + k];
+      if (depth) memcpy(q.paths.data(), dig.data() + pl.path_dig * 64, nq * depth * 64);
+      continue;
+    }
+    for (size_t k = 0; k < nq; ++k) {
+      const uint64_t owner = (q.I[k] % n2) / R;
+      const uint8_t* p = all.data() + (owner * qtot + base + k) * slot;
+      memcpy(&q.vals[k], p, 16);
+      uint8_t* out = q.paths.data() + k * depth * 64;
+      memcpy(out, p + 16, 64 * (size_t)lr);
+      if (pl.lm) memcpy(out + 64 * (size_t)lr, dig.data() + (pl.top_dig + k * (size_t)pl.lm) * 64, 64 * (size_t)pl.lm);
+    }
+    base += nq;
+  }
 }
 
 void dist_open_round(sg_dist* d, const ShardedRound& sr, uint64_t R, uint64_t n2, const std::vector<uint64_t>& I,
                      std::vector<fe>& vals, std::vector<uint8_t>& paths, int& depth) {
-  sg_ctx* ctx = d->ctx;
-  const size_t q = I.size();
-  vals.assign(q, fe_zero());
-  const int lr = ilog2_exact(R), lm = ilog2_exact(sr.m);
-  depth = lr + lm;
-  const size_t slot = 16 + 64 * (size_t)lr;
-  // owned requests: element offsets [k1][c] and subtree digest indices
-  std::vector<uint64_t> own, eidx, didx;
-  for (size_t j = 0; j < q; ++j) {
-    const uint64_t i = I[j];
-    if ((i % n2) / R != (uint64_t)d->g) continue;
-    const uint64_t k1 = i / n2, c = i % R;
-    own.push_back(j);
-    eidx.push_back(k1 * R + c);
-    for (int lv = 0; lv < lr; ++lv) didx.push_back(k1 * (sr.per / 8) + level_offset(R, lv) + ((c >> lv) ^ 1));
+  std::vector<OpenReq> reqs(1);
+  reqs[0].sr = &sr;
+  reqs[0].I = I;
+  dist_open_batch(d, R, n2, reqs);
+  vals = std::move(reqs[0].vals);
+  paths = std::move(reqs[0].paths);
+  depth = reqs[0].depth;
+}
+
+// round r of a sharded FRI commit as an opening request
+OpenReq fri_open_req(const DistFriState& s, size_t r, std::vector<uint64_t> I) {
+  OpenReq q;
+  if (r >= s.sharded.size()) {
+    const size_t t = r - s.sharded.size();
+    q.cw = s.tail.cw[t];
+    q.tree = s.tail.trees[t].get();
+  } else {
+    q.sr = &s.sharded[r];
   }
-  std::vector<uint8_t> mine(q * slot, 0);
-  if (!own.empty()) {
-    DevBuf dE(ctx, eidx.size() * 8), dV(ctx, eidx.size() * sizeof(fe));
-    std::vector<fe> v(eidx.size());
-    std::vector<uint8_t> dg(didx.size() * 64);
-    SG_HIP(hipMemcpyAsync(dE.get(), eidx.data(), eidx.size() * 8, hipMemcpyHostToDevice, ctx->stream));
-    SG_HIP(launch_gather_fe(sr.cw, dE.as<uint64_t>(), dV.as<fe>(), (uint32_t)eidx.size(), ctx->stream));
-    SG_HIP(hipMemcpyAsync(v.data(), dV.get(), v.size() * sizeof(fe), hipMemcpyDeviceToHost, ctx->stream));
-    if (!didx.empty()) {
-      DevBuf dD(ctx, didx.size() * 8), dO(ctx, didx.size() * 64);
-      SG_HIP(hipMemcpyAsync(dD.get(), didx.data(), didx.size() * 8, hipMemcpyHostToDevice, ctx->stream));
-      SG_HIP(launch_gather_digests(sr.forest.as<uint64_t>(), dD.as<uint64_t>(), dO.as<uint64_t>(),
-                                   (uint32_t)didx.size(), ctx->stream));
-      SG_HIP(hipMemcpyAsync(dg.data(), dO.get(), dg.size(), hipMemcpyDeviceToHost, ctx->stream));
-    }
-    SG_HIP(hipStreamSynchronize(ctx->stream));
-    for (size_t o = 0; o < own.size(); ++o) {
-      uint8_t* p = mine.data() + own[o] * slot;
-      memcpy(p, &v[o], 16);
-      memcpy(p + 16, dg.data() + o * lr * 64, 64 * (size_t)lr);
-    }
-  }
-  // one all-gather of every rank's slots, then each request takes its owner's
-  DevBuf dsend(ctx, q * slot), drecv(ctx, d->G * q * slot);
-  SG_HIP(hipMemcpyAsync(dsend.get(), mine.data(), q * slot, hipMemcpyHostToDevice, ctx->stream));
-  exchange(d, dsend.get(), drecv.get(), q * slot, /*a2a=*/false);
-  std::vector<uint8_t> all((size_t)d->G * q * slot);
-  SG_HIP(hipMemcpyAsync(all.data(), drecv.get(), all.size(), hipMemcpyDeviceToHost, ctx->stream));
-  // the top part from the top tree every rank holds
-  std::vector<uint64_t> tidx;
-  for (uint64_t i : I)
-    for (int lv = 0; lv < lm; ++lv) tidx.push_back(level_offset(sr.m, lv) + (((i / R) >> lv) ^ 1));
-  std::vector<uint8_t> topd(tidx.size() * 64);
-  if (!tidx.empty()) {
-    DevBuf dT(ctx, tidx.size() * 8), dO(ctx, tidx.size() * 64);
-    SG_HIP(hipMemcpyAsync(dT.get(), tidx.data(), tidx.size() * 8, hipMemcpyHostToDevice, ctx->stream));
-    SG_HIP(launch_gather_digests(sr.top.as<uint64_t>(), dT.as<uint64_t>(), dO.as<uint64_t>(), (uint32_t)tidx.size(),
-                                 ctx->stream));
-    SG_HIP(hipMemcpyAsync(topd.data(), dO.get(), topd.size(), hipMemcpyDeviceToHost, ctx->stream));
-  }
-  SG_HIP(hipStreamSynchronize(ctx->stream));
-  paths.assign(q * (size_t)depth * 64, 0);
-  for (size_t j = 0; j < q; ++j) {
-    const uint64_t owner = (I[j] % n2) / R;
-    const uint8_t* p = all.data() + (owner * q + j) * slot;
-    memcpy(&vals[j], p, 16);
-    uint8_t* out = paths.data() + j * (size_t)depth * 64;
-    memcpy(out, p + 16, 64 * (size_t)lr);
-    memcpy(out + 64 * (size_t)lr, topd.data() + j * (size_t)lm * 64, 64 * (size_t)lm);
-  }
+  q.I = std::move(I);
+  return q;
 }
 
 // FRI::prove (fri.rs:210-248) on a run-sharded codeword: the sharded commit with every round kept,
@@ -526,27 +581,34 @@ void dist_fri_prove(sg_dist* d, const sg_fri* f, const fe* runs, uint64_t n, con
     }
     push_obj(ps, SG_OBJ_PATH, pl.data(), pl.size());
   };
-  for (size_t r = 0; r + 1 < s.lengths.size(); ++r) {
+  // every round's indices first (fri.rs:182-186: i mod half, then i + half), all openings in one batch
+  const size_t nr = s.lengths.size() - 1;
+  std::vector<OpenReq> reqs;
+  reqs.reserve(2 * nr);
+  for (size_t r = 0; r < nr; ++r) {
     const uint64_t half = s.lengths[r] / 2;
     for (auto& i : idx) i %= half;
     std::vector<uint64_t> ab(idx);
     for (uint64_t i : idx) ab.push_back(i + half);
-    std::vector<fe> vab, vc;
-    std::vector<uint8_t> pab, pc;
-    int dab = 0, dc = 0;
-    dist_open(d, s, r, ab, vab, pab, dab);
-    dist_open(d, s, r + 1, idx, vc, pc, dc);
+    reqs.push_back(fri_open_req(s, r, std::move(ab)));
+    reqs.push_back(fri_open_req(s, r + 1, idx));
+  }
+  dist_open_batch(d, s.R, s.n2, reqs);
+  for (size_t r = 0; r < nr; ++r) {
+    const OpenReq& qab = reqs[2 * r];
+    const OpenReq& qc = reqs[2 * r + 1];
+    const int dab = qab.depth, dc = qc.depth;
     for (size_t k = 0; k < c; ++k) {
       uint8_t pl[48];
-      put_u128_be_at(pl, vab[k]);
-      put_u128_be_at(pl + 16, vab[c + k]);
-      put_u128_be_at(pl + 32, vc[k]);
+      put_u128_be_at(pl, qab.vals[k]);
+      put_u128_be_at(pl + 16, qab.vals[c + k]);
+      put_u128_be_at(pl + 32, qc.vals[k]);
       push_obj(ps, SG_OBJ_LEAFS, pl, 48);
     }
     for (size_t k = 0; k < c; ++k) {
-      put_path(pab.data() + k * (size_t)dab * 64, dab);
-      put_path(pab.data() + (c + k) * (size_t)dab * 64, dab);
-      put_path(pc.data() + k * (size_t)dc * 64, dc);
+      put_path(qab.paths.data() + k * (size_t)dab * 64, dab);
+      put_path(qab.paths.data() + (c + k) * (size_t)dab * 64, dab);
+      put_path(qc.paths.data() + k * (size_t)dc * 64, dc);
     }
   }
   if (extra) extra(top);

@@ -52,6 +52,20 @@ void dist_forest_finish(sg_dist* d, PendingForest& pf, uint8_t root[64], Sharded
 // identical on every rank: one all-gather of the owners' slots plus the local top tree
 void dist_open_round(sg_dist* d, const ShardedRound& sr, uint64_t R, uint64_t n2, const std::vector<uint64_t>& I,
                      std::vector<fe>& vals, std::vector<uint8_t>& paths, int& depth);
+// one opening request: a sharded round (sr) or a local round (cw + tree), indices I; filled with the
+// values and the paths (I.size() x depth digests, leaf level first)
+struct OpenReq {
+  const ShardedRound* sr = nullptr;
+  const fe* cw = nullptr;
+  const sg_tree* tree = nullptr;
+  std::vector<uint64_t> I;
+  std::vector<fe> vals;
+  std::vector<uint8_t> paths;
+  int depth = 0;
+};
+// many requests with one host round trip for all device gathers and ONE all-gather for every
+// sharded request's owned slots (R, n2: the run length and N2 of the sharded rounds)
+void dist_open_batch(sg_dist* d, uint64_t R, uint64_t n2, std::vector<OpenReq>& reqs);
 // fri.rs:210-248 on a run-sharded codeword; `extra` (optional) pushes further objects after the
 // query phase, given the top-level indices
 void dist_fri_prove(sg_dist* d, const sg_fri* f, const fe* runs, uint64_t n, const sg_proof_stream* ps, size_t* top,

@@ -1153,21 +1153,24 @@ void stark_prove_dist(sg_dist* dd, const sg_stark& st, const fe* d_trace, size_t
     std::vector<uint64_t> quad = dup;
     for (uint64_t i : dup) quad.push_back((i + Nf / 2) % Nf);
     std::sort(quad.begin(), quad.end());
+    std::vector<OpenReq> reqs(m + 1);
     for (size_t s = 0; s <= m; ++s) {
-      std::vector<fe> vals;
-      std::vector<uint8_t> paths;
-      int depth = 0;
-      dist_open_round(dd, rounds[s], R, n2, quad, vals, paths, depth);
+      reqs[s].sr = &rounds[s];
+      reqs[s].I = quad;
+    }
+    dist_open_batch(dd, R, n2, reqs);  // all m + 1 codewords: one all-gather
+    for (size_t s = 0; s <= m; ++s) {
+      const int depth = reqs[s].depth;
       std::vector<uint8_t> pl(72 * (size_t)depth);
       for (size_t k = 0; k < quad.size(); ++k) {
         uint8_t v[16];
-        put_u128_be_at(v, vals[k]);
+        put_u128_be_at(v, reqs[s].vals[k]);
         push_obj(ps, SG_OBJ_VALUE, v, 16);
         for (int l = 0; l < depth; ++l) {
           uint8_t* o = pl.data() + 72 * (size_t)l;
           memset(o, 0, 8);
           o[7] = 64;
-          memcpy(o + 8, paths.data() + (k * (size_t)depth + (size_t)l) * 64, 64);
+          memcpy(o + 8, reqs[s].paths.data() + (k * (size_t)depth + (size_t)l) * 64, 64);
         }
         push_obj(ps, SG_OBJ_PATH, pl.data(), pl.size());
       }
