@@ -311,8 +311,33 @@ def c5_single_gpu(ctx: sg.Context, device, iters: int = 3) -> dict:
     t = (time.perf_counter() - t0) / iters
     out["c5_dist_world1_ms"] = round(t * 1e3, 3)
     out["c5_dist_world1_gelem_s"] = round(n / t / 1e9, 3)
-    nd.close()
     del cols, runs
+    ctx.trim()
+    # the headline proof through sg_dist_stark_prove on the same one-rank communicator: the sharded
+    # prove's own cost (four-step LDEs, forests, sharded FRI rounds, batched openings) without peers;
+    # its bytes must equal the single-GPU proof's
+    try:
+        wl = ProveWorkload(0, device, ctx, LOG_TRACE)
+        single = wl.step().digest()
+
+        def sharded():
+            ps = sg.IndependentProofStream()
+            wl.stark.prove_dev(wl.trace.data_ptr(), wl.rows, wl.air, wl.boundary, ps, wl.trace_rand.data_ptr(),
+                               wl.rcoef.data_ptr(), wl.nrc, dist=nd)
+            return ps.digest()
+
+        same = sharded() == single
+        torch.cuda.synchronize(device)
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            sharded()
+        torch.cuda.synchronize(device)
+        out["sharded_prove_world1_ms"] = round((time.perf_counter() - t0) / iters * 1e3, 3)
+        out["sharded_prove_world1_bytes_equal_single_gpu"] = same
+        del wl
+    except Exception as e:  # noqa: BLE001
+        out["sharded_prove_world1_error"] = f"{type(e).__name__}: {e}"
+    nd.close()
     ctx.trim()
     return out
 
