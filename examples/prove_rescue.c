@@ -5,6 +5,11 @@
  * two thread_rng draws read from a file so the bytes can be compared with another prover's.
  *
  *   prove_rescue N expansion colinearity security tcd input_lo input_hi randomness.bin proof.bin
+ *                [--dist id_file rank nranks]
+ *
+ * With --dist the proof is computed with the FRI domain sharded over `nranks` processes, one GPU
+ * each (sg_dist_stark_prove over RCCL, rank r on GPU r): rank 0 writes the RCCL unique id to
+ * id_file, the other ranks wait for it; every rank writes the same bytes.
  *
  * randomness.bin: 16-byte little-endian (lo, hi) field elements -- num_randomizers x 2 trace
  * randomizer rows (stark.rs:285-301), then max_degree + 1 randomizer coefficients
@@ -13,10 +18,12 @@
  * Exit status 0 on success; 2 when randomness.bin is too short (it prints how many elements
  * it needs first, so a caller can size the file); 1 on any library error.
  */
+#define _POSIX_C_SOURCE 200809L
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "stark_gpu.h"
 
@@ -30,8 +37,11 @@
   } while (0)
 
 int main(int argc, char** argv) {
-  if (argc != 10) {
-    fprintf(stderr, "usage: %s N expansion colinearity security tcd input_lo input_hi randomness.bin proof.bin\n",
+  const int dist = argc == 14 && strcmp(argv[10], "--dist") == 0;
+  if (argc != 10 && !dist) {
+    fprintf(stderr,
+            "usage: %s N expansion colinearity security tcd input_lo input_hi randomness.bin proof.bin"
+            " [--dist id_file rank nranks]\n",
             argv[0]);
     return 1;
   }
@@ -39,8 +49,38 @@ int main(int argc, char** argv) {
   const size_t c = strtoull(argv[3], NULL, 10), sec = strtoull(argv[4], NULL, 10);
   const size_t tcd = strtoull(argv[5], NULL, 10);
   const sg_fe input = {strtoull(argv[6], NULL, 0), strtoull(argv[7], NULL, 0)};
+  const int rank = dist ? atoi(argv[12]) : 0, nranks = dist ? atoi(argv[13]) : 1;
   sg_ctx* ctx = NULL;
-  CHECK(sg_ctx_create(0, &ctx));
+  CHECK(sg_ctx_create(dist ? rank : 0, &ctx));  /* one GPU per rank of the node */
+  sg_dist* comm = NULL;
+  if (dist) {
+    uint8_t id[SG_DIST_ID_BYTES];
+    if (rank == 0) {
+      CHECK(sg_dist_unique_id(id));
+      char tmp[4096];
+      snprintf(tmp, sizeof tmp, "%s.tmp", argv[11]);
+      FILE* f = fopen(tmp, "wb");
+      if (!f || fwrite(id, 1, sizeof id, f) != sizeof id || fclose(f) != 0 || rename(tmp, argv[11]) != 0) {
+        fprintf(stderr, "cannot write %s\n", argv[11]);
+        return 1;
+      }
+    } else {
+      FILE* f = NULL;
+      for (int tries = 0; tries < 6000 && !f; ++tries) {  /* up to 60 s for rank 0 */
+        f = fopen(argv[11], "rb");
+        if (!f) {
+          struct timespec ts = {0, 10000000};
+          nanosleep(&ts, NULL);
+        }
+      }
+      if (!f || fread(id, 1, sizeof id, f) != sizeof id) {
+        fprintf(stderr, "cannot read %s\n", argv[11]);
+        return 1;
+      }
+      fclose(f);
+    }
+    CHECK(sg_dist_create(ctx, id, nranks, rank, &comm));
+  }
   sg_rescue* rp = NULL;
   CHECK(sg_rescue_create(ctx, 2, 1, sec, N, &rp));  /* RescuePrime::new(m = 2, capacity 1, ...) */
   sg_fe output;
@@ -76,7 +116,12 @@ int main(int argc, char** argv) {
   }
   sg_stream* s = sg_stream_create();
   const sg_proof_stream cb = sg_stream_callbacks(s);
-  CHECK(sg_stark_prove(ctx, st, trace, N + 1, (const sg_mpoly* const*)tcs, 2, bnd, 2, rnd, rnd + 2 * nr, nrc, &cb));
+  if (comm)
+    CHECK(sg_dist_stark_prove(comm, st, trace, N + 1, (const sg_mpoly* const*)tcs, 2, bnd, 2, rnd, rnd + 2 * nr, nrc,
+                              &cb));
+  else
+    CHECK(sg_stark_prove(ctx, st, trace, N + 1, (const sg_mpoly* const*)tcs, 2, bnd, 2, rnd, rnd + 2 * nr, nrc,
+                         &cb));
   size_t len = 0;
   CHECK(sg_stream_digest(s, NULL, 0, &len));
   uint8_t* proof = malloc(len);
@@ -97,6 +142,7 @@ int main(int argc, char** argv) {
   sg_mpoly_free(tcs[1]);
   sg_stark_free(st);
   sg_rescue_free(rp);
+  if (comm) sg_dist_destroy(comm);
   sg_ctx_destroy(ctx);
   return 0;
 }

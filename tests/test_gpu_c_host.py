@@ -18,7 +18,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 BIN = os.path.join(ROOT, "examples", "build", "prove_rescue")
 
 
-def _run(tmp_path, N, exp, c, sec, tcd, seed):
+def _run(tmp_path, N, exp, c, sec, tcd, seed, dist=False):
     assert os.path.exists(BIN), "examples/build/prove_rescue missing: run __graft_entry__.build()"
     st = e.Stark(exp, c, sec, 2, N + 1, tcd)
     inp = o.sample(seed)
@@ -38,15 +38,19 @@ def _run(tmp_path, N, exp, c, sec, tcd, seed):
     rnd = np.array([[v & (2**64 - 1), v >> 64] for v in r], dtype=np.uint64)
     rfile, pfile = tmp_path / "randomness.bin", tmp_path / "proof.bin"
     rnd.tofile(rfile)
+    extra = ["--dist", str(tmp_path / "rccl.id"), "0", "1"] if dist else []
     res = subprocess.run([BIN, str(N), str(exp), str(c), str(sec), str(tcd), str(inp & (2**64 - 1)), str(inp >> 64),
-                          str(rfile), str(pfile)], capture_output=True, text=True, timeout=300)
+                          str(rfile), str(pfile)] + extra, capture_output=True, text=True, timeout=300)
     assert res.returncode == 0, res.stderr
     return pfile.read_bytes(), st, rp, air, inp, r
 
 
+@pytest.mark.parametrize("dist", [False, True])
 @pytest.mark.parametrize("N,exp,c,sec,tcd", [(27, 4, 2, 2, 2), (40, 4, 3, 4, 2), (27, 8, 4, 8, 3)])
-def test_c_host_proof_equals_oracle(tmp_path, N, exp, c, sec, tcd):
-    got, st, rp, air, inp, r = _run(tmp_path, N, exp, c, sec, tcd, b"c-host-%d-%d" % (N, exp))
+def test_c_host_proof_equals_oracle(tmp_path, N, exp, c, sec, tcd, dist):
+    """dist: the same through sg_dist_stark_prove on a one-rank RCCL communicator created from a
+    unique id passed through a file (what a multi-process Rust / C caller does)."""
+    got, st, rp, air, inp, r = _run(tmp_path, N, exp, c, sec, tcd, b"c-host-%d-%d" % (N, exp), dist)
     m = 2
     trace = rp.trace(inp)
     bnd = rp.boundary_constraints(rp.hash(inp))
