@@ -366,12 +366,13 @@ def north_star_reference():
         shutil.rmtree(tmp, ignore_errors=True)
 
 
-def _north_star_worker(rank, world, port, tmp):
+def _north_star_worker(rank, world, port, tmp, tail):
     import torch.distributed as dist
     import starkgpu as sg
     from starkgpu import dist as D
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    os.environ["SG_DIST_FRI_TAIL"] = tail
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         ctx = sg.Context(0)
@@ -395,16 +396,18 @@ def _north_star_worker(rank, world, port, tmp):
 
 
 @pytest.mark.timeout(600)
+@pytest.mark.parametrize("tail", ["20", "0"])
 @pytest.mark.parametrize("world", [2, 8])
-def test_north_star_sharded_lde_fri_prove(north_star_reference, world):
+def test_north_star_sharded_lde_fri_prove(north_star_reference, world, tail):
     """The north-star block sharded over `world` ranks on this box's GPU (host transport over gloo):
     sg_dist_coset_evaluate (2^21 -> 2^24) + sg_dist_fri_prove (expansion 8, c = 64) write the
-    single-GPU FRI::prove bytes (fri.rs:210-248) on every rank."""
+    single-GPU FRI::prove bytes (fri.rs:210-248) on every rank -- with the default hand-over of the
+    rounds <= 2^20 to the single-GPU commit, and with every round sharded (SG_DIST_FRI_TAIL=0)."""
     import torch.multiprocessing as mp
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
-    mp.spawn(_north_star_worker, args=(world, port, north_star_reference), nprocs=world, join=True)
+    mp.spawn(_north_star_worker, args=(world, port, north_star_reference, tail), nprocs=world, join=True)
 
 
 # ------------------------------------------------------------------ sharded Stark::prove

@@ -11,7 +11,9 @@ rows.sort(key=lambda r:int(r['Start_Timestamp']))
 def nm(r):
     n=r['Kernel_Name']; n=re.sub(r'\(.*','',n); n=n.replace('void ','').replace('sg::','')
     return n[:34]+f" g={r['Grid_Size_X']}x{r['Grid_Size_Y']} q{r['Queue_Id']}"
-starts=[i for i,r in enumerate(rows) if r['Queue_Id']!='1' and 'k_ntt_first<11>' in r['Kernel_Name'] and r['Grid_Size_X']=='4194304' and (i==0 or True)]
+side=[i for i,r in enumerate(rows) if r['Queue_Id']!='1' and 'k_ntt_first' in r['Kernel_Name']]
+gmax=max((int(rows[i]['Grid_Size_X']) for i in side), default=0)
+starts=[i for i in side if int(rows[i]['Grid_Size_X'])==gmax]
 # step start = side-stream randomizer LDE; keep those followed by gather_stride soon
 print('candidate starts', len(starts))
 step_starts=starts[-3:]
