@@ -19,6 +19,13 @@ step writes a complete proof into a fresh proof stream.
 
 One process per GPU (torchrun); each rank proves its own independent trace
 (weak scaling, no collective on the data path).  Rank 0 prints one JSON line.
+
+Side measurements (not the metric): at N = 1 the other BASELINE configs (C2 2^22 fwd+inv NTT,
+the 2^24 north-star LDE + FRI commit, C4's prove at trace 2^16, C5's 2^27 NTT) and the sharded
+paths on a one-rank RCCL communicator (`c5_dist_world1_ms`, `sharded_prove_world1_ms` with a
+byte check against the single-GPU proof); at N > 1 the same sharded paths over all ranks
+(C2 and C5 NTTs, the north-star block with FRI::prove, and the headline proof through
+sg_dist_stark_prove, `sharded_prove_ms`, bytes checked on every rank).
 """
 import argparse
 import json
@@ -40,8 +47,8 @@ import torch.distributed as dist  # noqa: E402
 import starkgpu as sg  # noqa: E402
 
 P = sg.FIELD_PRIME
-LOG_TRACE = 20      # coefficients per polynomial (trace 2^20)
-EXPANSION = 8       # N = 2^23
+LOG_TRACE = 20      # randomized trace rows + 1 (trace 2^20)
+EXPANSION = 8       # FRI domain = 8 x omicron domain (2^25 at the headline)
 COLINEARITY = 64
 REGISTERS = 2       # Rescue-Prime m = 2
 HBM_PEAK_GBS = 8000.0
