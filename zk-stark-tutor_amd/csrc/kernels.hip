@@ -733,6 +733,35 @@ __device__ __forceinline__ void blake2b_quad(const uint64_t* msg, uint64_t t, in
   out_hi = iv4q ^ b ^ d;
 }
 
+// The `fuse - 1` levels a quad block computes above its first digests (hlo, hhi of node `node`):
+// children through LDS, every digest written to the tree, the root published by the level reaching it.
+template <int NODES>
+__device__ __forceinline__ void quad_upper_levels(const MerkleArgs& a, uint64_t* __restrict__ tree,
+                                                  uint64_t* root_slot, uint64_t (*msg)[16], int node, int q,
+                                                  const SigmaPack& sp, uint32_t count, uint64_t hlo, uint64_t hhi) {
+  for (int lev = 1; lev < a.fuse; ++lev) {
+    __syncthreads();  // everyone finished reading msg
+    if (node < (int)count) {
+      msg[node >> 1][(node & 1) * 8 + q] = hlo;
+      msg[node >> 1][(node & 1) * 8 + 4 + q] = hhi;
+    }
+    __syncthreads();
+    count >>= 1;
+    if (node < (int)count) {
+      blake2b_quad(msg[node], 128, q, sp, hlo, hhi);
+      uint64_t gidx = (uint64_t)blockIdx.x * count + node;
+      uint64_t* dst = tree + (a.off[lev + 1] + gidx) * 8;
+      dst[q] = hlo;
+      dst[4 + q] = hhi;
+      if (a.first_level + lev == a.root_level && root_slot) {
+        root_slot[q] = hlo;
+        root_slot[4 + q] = hhi;
+        merkle_root_publish(a, q == 0);
+      }
+    }
+  }
+}
+
 // Node levels with a quad per node: 4 * NODES threads = NODES nodes at the first level,
 // `fuse` levels computed (NODES -> 1 at most).  Children of the first level are
 // read from HBM (level first_level-1), every produced digest is written to the tree.
@@ -775,27 +804,64 @@ __global__ __launch_bounds__(4 * NODES) void k_merkle_quad(MerkleArgs a) {
       merkle_root_publish(a, q == 0);  // the quad is one wavefront: its fence covers all 4 lanes
     }
   }
-  for (int lev = 1; lev < a.fuse; ++lev) {
-    __syncthreads();  // everyone finished reading msg
-    if (node < (int)count) {
-      msg[node >> 1][(node & 1) * 8 + q] = hlo;
-      msg[node >> 1][(node & 1) * 8 + 4 + q] = hhi;
+  quad_upper_levels<NODES>(a, tree, root_slot, msg, node, q, sp, count, hlo, hhi);
+}
+
+// Leaf level of a latency-bound tree (a late FRI round's codeword, C4's small trees, a forest's
+// small subtrees) with a quad of lanes per leaf: each lane of the quad converts the leaf to its
+// decimal words (the quad shares a wavefront, so the redundant conversion costs no time) and
+// stores its four of the 16 message words (decimal words 0..4, zeros above); the quad then
+// compresses the single block with t = the string length (merkle_root.rs:7-32 on
+// field_element.rs:46-50 bytes), and the node levels above are fused as in k_merkle_quad.
+// FOLD: the leaf is the fold of the previous round's codeword (fri.rs:151-159), stored too.
+template <int NODES, bool FOLD>
+__global__ __launch_bounds__(4 * NODES) void k_merkle_quad_leaves(MerkleArgs a) {
+  __shared__ uint64_t msg[NODES][16];
+  const int tid = threadIdx.x;
+  const int q = tid & 3;
+  const int node = tid >> 2;
+  uint64_t* __restrict__ tree = merkle_tree_ptr(a);
+  uint64_t* const root_slot = merkle_root_slot(a);
+  const SigmaPack sp = sigma_pack(q);
+  uint32_t count = blockDim.x >> 2;  // leaves of this block
+  const uint64_t leaf = (uint64_t)blockIdx.x * count + node;
+  const bool valid = leaf < a.first_count;
+  uint32_t len = 0;
+  if (valid) {
+    fe v;
+    if constexpr (FOLD) {
+      const fe x = ld_fe(a.fold.src + leaf);
+      const fe y = ld_fe(a.fold.src + leaf + a.first_count);
+      const uint64_t e = leaf << a.fold.shift;
+      const fe K = a.fold.Kp ? ld_fe(a.fold.Kp) : a.fold.K;
+      fe t = mont_mul(K, ld_fe(a.fold.Tlo + (e & 4095)));
+      t = mont_mul(t, ld_fe(a.fold.Thi + (e >> 12)));
+      v = fe_add(fe_halve(fe_add(x, y)), mont_mul(fe_sub(x, y), t));
+      if (q == 0) st_fe(a.fold.dst + leaf, v);
+    } else {
+      v = ld_fe(merkle_leaves_ptr(a) + leaf);
     }
-    __syncthreads();
-    count >>= 1;
-    if (node < (int)count) {
-      blake2b_quad(msg[node], 128, q, sp, hlo, hhi);
-      uint64_t gidx = (uint64_t)blockIdx.x * count + node;
-      uint64_t* dst = tree + (a.off[lev + 1] + gidx) * 8;
-      dst[q] = hlo;
-      dst[4 + q] = hhi;
-      if (a.first_level + lev == a.root_level && root_slot) {
-        root_slot[q] = hlo;
-        root_slot[4 + q] = hhi;
-        merkle_root_publish(a, q == 0);
-      }
+    uint64_t m[5];
+    len = fe_decimal_words(v, m);
+    msg[node][4 * q + 0] = q == 0 ? m[0] : q == 1 ? m[4] : 0;
+    msg[node][4 * q + 1] = q == 0 ? m[1] : 0;
+    msg[node][4 * q + 2] = q == 0 ? m[2] : 0;
+    msg[node][4 * q + 3] = q == 0 ? m[3] : 0;
+  }
+  __syncthreads();
+  uint64_t hlo = 0, hhi = 0;
+  if (valid) {
+    blake2b_quad(msg[node], len, q, sp, hlo, hhi);
+    uint64_t* dst = tree + (a.off[1] + leaf) * 8;
+    dst[q] = hlo;
+    dst[4 + q] = hhi;
+    if (a.first_level == a.root_level && root_slot) {
+      root_slot[q] = hlo;
+      root_slot[4 + q] = hhi;
+      merkle_root_publish(a, q == 0);
     }
   }
+  quad_upper_levels<NODES>(a, tree, root_slot, msg, node, q, sp, count, hlo, hhi);
 }
 
 // ---------------------------------------------- row-sharded helpers (four-step)
@@ -1430,7 +1496,9 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
   //  * leaves: one lane per leaf (decimal + hash) in 512-lane blocks; 3 more levels
   //    fused through LDS (512 -> 64 lanes: every active wave full) when the tree is
   //    large enough to be throughput-bound, else the leaf level only;
-  //    a tree of <= 1024 leaves with nothing above runs in one 1024-thread block.
+  //    a tree of <= 1024 leaves with nothing above runs in one 1024-thread block;
+  //    latency-bound leaf levels (< 2^17 leaves over the launch's trees) take a quad of lanes
+  //    per leaf instead, 256 leaves per block, every level up to the block's digest fused;
   //  * node levels with >= kQuadBelow digests: one lane per node, 3 levels fused;
   //  * smaller levels (latency-bound): a quad of lanes per node, up to 7 levels fused.
   // SG_MERKLE_QUAD_BELOW = log2 of the threshold (A/B only)
@@ -1463,8 +1531,21 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
     a.first_count = count;
     int fuse;
     unsigned bs;
-    int kind;  // 0: leaf 256, 1: leaf tail 1024, 2: node 256, 3: quad 64, 4: leaf 512, 5: quad 256, 6: node 512
-    if (level == 0) {
+    int kind;  // 0: leaf 256, 1: leaf tail 1024, 2: node 256, 3: quad 64, 4: leaf 512, 5: quad 256, 6: node 512,
+              // 7: quad leaves 256
+    // SG_MERKLE_QUAD_LEAF_BELOW = log2 of the leaf count (all trees of the launch) under which the
+    // leaf level takes a quad per leaf (k_merkle_quad_leaves); 0 disables it (A/B knob)
+    static const int env_qleaf = env_int("SG_MERKLE_QUAD_LEAF_BELOW", 17);
+    if (level == 0 && env_qleaf > 0 && count * (uint64_t)batch < ((uint64_t)1 << env_qleaf)) {
+      // latency-bound leaf level: up to 256 leaves per 1024-lane block, every level fused up to
+      // the block's single digest (the whole tree when it has <= 256 leaves)
+      kind = 7;
+      const uint64_t nodes = count < 256 ? count : 256;
+      bs = (unsigned)(4 * nodes);
+      int lg = 0;
+      while (((uint64_t)1 << lg) < nodes) ++lg;
+      fuse = lg + 1;
+    } else if (level == 0) {
       if (count <= 64) {
         kind = 1; bs = (unsigned)count; fuse = logn + 1;
       } else {
@@ -1523,11 +1604,12 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
     uint64_t digests = 0;
     for (int k = 0; k < fuse; ++k) digests += count >> k;
     // a fused fold reads 2 source elements and writes the folded one instead of reading the leaf
-    const uint64_t per_block = kind == 3 || kind == 5 ? bs / 4 : bs;  // quad kernels: 4 lanes per node
+    const uint64_t per_block = kind == 3 || kind == 5 || kind == 7 ? bs / 4 : bs;  // quad kernels: 4 lanes per node
     dim3 grid((unsigned)((count + per_block - 1) / per_block), batch);
     // elems = lanes launched (the rocprofv3 Grid_Size of this dispatch), so per-wave PMC
     // instruction counts scale to any launch population
-    ProfScope ps(level == 0 ? (fold_here ? "merkle_fold_leaves" : "merkle_leaves")
+    ProfScope ps(kind == 7  ? "merkle_leaves_quad"
+                 : level == 0 ? (fold_here ? "merkle_fold_leaves" : "merkle_leaves")
                             : (kind == 3 || kind == 5 ? "merkle_nodes_quad" : "merkle_nodes"),
                  batch * ((level == 0 ? (fold_here ? 48 : 16) * count : 0) + 64 * digests), s,
                  (uint64_t)grid.x * grid.y * bs);
@@ -1547,6 +1629,10 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
         else hipLaunchKernelGGL((k_merkle_levels<true, 512>), grid, dim3(bs), 0, s, a);
         break;
       case 5: hipLaunchKernelGGL(k_merkle_quad<256>, grid, dim3(bs), 0, s, a); break;
+      case 7:
+        if (fold_here) hipLaunchKernelGGL((k_merkle_quad_leaves<256, true>), grid, dim3(bs), 0, s, a);
+        else hipLaunchKernelGGL((k_merkle_quad_leaves<256, false>), grid, dim3(bs), 0, s, a);
+        break;
       default: hipLaunchKernelGGL(k_merkle_quad<64>, grid, dim3(bs), 0, s, a); break;
     }
     hipError_t e = hipGetLastError();
