@@ -686,8 +686,8 @@ __device__ __forceinline__ SigmaPack sigma_pack(int q) {
 
 template <int CTRL>
 __device__ __forceinline__ uint64_t quad_perm64(uint64_t x) {
-  uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)x, CTRL, 0xF, 0xF, false);
-  uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(x >> 32), CTRL, 0xF, 0xF, false);
+  uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)x, CTRL, 0xF, 0xF, true);
+  uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(x >> 32), CTRL, 0xF, 0xF, true);
   return ((uint64_t)hi << 32) | lo;
 }
 // quad_perm encodings: lane i takes lane sel[i]
