@@ -614,11 +614,20 @@ void build_trees(sg_ctx* ctx, const fe* const* d_leaves, int batch, uint64_t n, 
 // build into a tree whose buffer is already allocated; with `fold`, the leaves are
 // the FRI fold of fold->src, computed by the leaf kernel and stored to d_leaves
 void fill_tree(sg_ctx* ctx, const fe* d_leaves, sg_tree* t, const FoldLeaves* fold) {
+  fill_tree_finish(ctx, t, fill_tree_launch(ctx, d_leaves, t, fold));
+}
+
+// fill_tree in two halves, so work can be queued behind the tree before the host waits for its root
+uint64_t fill_tree_launch(sg_ctx* ctx, const fe* d_leaves, sg_tree* t, const FoldLeaves* fold) {
   uint64_t* buf = t->buf.as<uint64_t>();
   uint64_t* root_dev = ctx->pinned_roots_dev;
   uint64_t* flag_dev = ctx->pinned_roots_dev + sg_ctx::kFlagIndex;
   const uint64_t seq = ++ctx->root_seq;
   SG_HIP(launch_merkle_tree(&d_leaves, &buf, 1, t->n, &root_dev, ctx->stream, 0, 0, 0, &flag_dev, seq, fold));
+  return seq;
+}
+
+void fill_tree_finish(sg_ctx* ctx, sg_tree* t, uint64_t seq) {
   wait_roots(ctx, 1, seq, 0, ctx->stream);
   memcpy(t->root, ctx->pinned_roots, 64);
 }
@@ -1079,12 +1088,23 @@ void fri_commit_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, co
     push_obj(ps, SG_OBJ_CODEWORD, payload.data(), payload.size());  // fri.rs:166
     return;
   }
+  const uint64_t last_len = st.lengths.back();
+  fe* last = nullptr;  // the last codeword on the host (pinned staging)
   for (size_t r = 0; r < rounds; ++r) {
     const uint64_t len = plan[r].len;
     // assert omega^(n-1) == omega^-1 (fri.rs:133)
     SG_REQUIRE(fe_eq(fe_pow(plan[r].omega, len - 1), plan[r].winv),
                "error in commit: omega does not have the right order!");
-    fill_tree(ctx, st.cw[r], trees[r].get(), r ? &fold : nullptr);
+    if (r + 1 < rounds) {
+      fill_tree(ctx, st.cw[r], trees[r].get(), r ? &fold : nullptr);
+    } else {
+      // the last round's codeword (its leaves, folded by its own leaf kernel) is copied to the
+      // host right behind its tree, so the copy lands while the host waits for the root
+      const uint64_t seq = fill_tree_launch(ctx, st.cw[r], trees[r].get(), r ? &fold : nullptr);
+      last = static_cast<fe*>(ctx->staging(1, last_len * sizeof(fe)));
+      SG_HIP(hipMemcpyAsync(last, st.cw.back(), last_len * sizeof(fe), hipMemcpyDeviceToHost, ctx->stream));
+      fill_tree_finish(ctx, trees[r].get(), seq);
+    }
     st.trees.push_back(std::move(trees[r]));
     push_obj(ps, SG_OBJ_ROOT, st.trees.back()->root, 64);
     if (r == rounds - 1) break;
@@ -1102,15 +1122,11 @@ void fri_commit_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, co
     fold.K = to_mont(fe_mul(fe_mul(alpha, plan[r].oinv), inv2));
   }
   // push last codeword (fri.rs:166)
-  uint64_t last_len = st.lengths.back();
-  std::vector<fe> last(last_len);
-  SG_HIP(hipMemcpyAsync(last.data(), st.cw.back(), last_len * sizeof(fe), hipMemcpyDeviceToHost,
-                        ctx->stream));
   SG_HIP(hipStreamSynchronize(ctx->stream));
-  std::vector<uint8_t> payload;
-  payload.reserve(last_len * 16);
-  for (auto& v : last) put_u128_be(payload, v);
-  push_obj(ps, SG_OBJ_CODEWORD, payload.data(), payload.size());
+  ObjWriter w{ps};
+  uint8_t* payload = w.begin(SG_OBJ_CODEWORD, last_len * 16);
+  for (uint64_t i = 0; i < last_len; ++i) put_u128_be_at(payload + 16 * i, last[i]);
+  w.commit();
 }
 
 // fri.rs:60-86
@@ -1162,6 +1178,10 @@ void fri_prove_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, con
   // in one launch together with the caller's `extra` objects.
   const size_t R = st.codewords.size() - 1;  // query rounds
   TailWriter tw;
+  // the query phase's 4c objects per round, plus room for a STARK's openings (2 objects at up
+  // to 4c indices for up to 4 codewords): one allocation instead of repeated growth
+  tw.items.reserve(R * 4 * c + 32 * c);
+  tw.offs.reserve(R * 4 * c + 32 * c);
   std::vector<size_t> indices(top, top + c);
   for (size_t r = 0; r < R; ++r) {
     const uint64_t len = st.lengths[r];

@@ -108,6 +108,8 @@ uint64_t launch_trees(sg_ctx* ctx, const fe* const* d_leaves, int batch, sg_tree
 void finish_trees(sg_ctx* ctx, sg_tree* const* trees, int batch, uint64_t seq, int slot0, hipStream_t s);
 sg_tree* build_tree(sg_ctx* ctx, const fe* d_leaves, uint64_t n);
 void fill_tree(sg_ctx* ctx, const fe* d_leaves, sg_tree* t, const FoldLeaves* fold = nullptr);
+uint64_t fill_tree_launch(sg_ctx* ctx, const fe* d_leaves, sg_tree* t, const FoldLeaves* fold = nullptr);
+void fill_tree_finish(sg_ctx* ctx, sg_tree* t, uint64_t seq);
 void path_indices(const sg_tree* t, uint64_t index, std::vector<uint64_t>& idx);
 void gather_digests(sg_ctx* ctx, const sg_tree* t, const std::vector<uint64_t>& idx, uint8_t* out);
 

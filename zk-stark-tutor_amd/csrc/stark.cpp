@@ -1005,7 +1005,9 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
     finish_trees(ctx, t, (int)m, bq_seq, 0, ctx->side);
     sg_tree* rt = r_tree.get();
     finish_trees(ctx, &rt, 1, r_seq, kRandSlot, ctx->side);
-    SG_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));  // openings read the trees
+    // the main stream joins the side stream only where it reads the side stream's output (the
+    // openings below): the combination, its LDE and FRI do not, and a cross-stream wait enqueued
+    // here held the combination back ~50 us behind the last tree kernel's completion signal
   }
   for (size_t s = 0; s < m; ++s) push_obj(ps, SG_OBJ_ROOT, bq_trees[s]->root, 64);
   push_obj(ps, SG_OBJ_ROOT, r_tree->root, 64);
@@ -1032,6 +1034,7 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
   for (size_t s = 0; s < m; ++s) cts.emplace_back(bq_cw[s].p(), bq_trees[s].get());
   cts.emplace_back(r_cw.p(), r_tree.get());
   fri_prove_dev(ctx, &st.fri, comb_cw.p(), Nf, ps, top.data(), [&](const size_t* tp, TailWriter& tw) {
+    SG_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));  // the openings read the side-stream trees
     const size_t c = st.fri.num_colinearity_tests;
     std::vector<uint64_t> dup;
     for (size_t k = 0; k < c; ++k) dup.push_back(tp[k]);
