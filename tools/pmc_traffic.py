@@ -13,7 +13,8 @@ import csv
 import json
 import sys
 
-ALIASES = [("k_merkle_levels<true, 256, true>", "merkle_fold_leaves"),
+ALIASES = [("k_merkle_leaf_pairs<512, true>", "merkle_fold_leaves"), ("k_merkle_leaf_pairs", "merkle_leaves"),
+           ("k_merkle_levels<true, 256, true>", "merkle_fold_leaves"),
            ("k_merkle_levels<true, 512, true>", "merkle_fold_leaves"),
            ("k_merkle_levels<true, 1024, true>", "merkle_fold_leaves"), ("k_merkle_levels<true", "merkle_leaves"), ("k_merkle_levels<false", "merkle_nodes"),
            ("k_merkle_quad_leaves", "merkle_leaves_quad"), ("k_merkle_quad", "merkle_nodes_quad"), ("k_ntt_pass", "ntt_pass"), ("k_ntt_first", "ntt_first"),

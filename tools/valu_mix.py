@@ -23,7 +23,7 @@ from asm_mix import kernels  # noqa: E402
 FULL_CLK, HALF_CLK = 4 / 1.65, 4 / 0.90
 FULL = re.compile(r"^v_(add_u32|sub_u32|subrev_u32|xor_b32|and_b32|or_b32|not_b32|bitop3_b32|bitop3_b16|"
                   r"lshrrev_b32|ashrrev_i32|mov_b32|cndmask_b32|max_u32|min_u32)(_e32|_e64)?$")
-KERNELS = {"merkle_leaves": "k_merkle_levelsILb1ELi512ELb0E", "merkle_fold_leaves": "k_merkle_levelsILb1ELi512ELb1E",
+KERNELS = {"merkle_leaves": "k_merkle_leaf_pairsILi512ELb0E", "merkle_fold_leaves": "k_merkle_leaf_pairsILi512ELb1E",
            "merkle_nodes": "k_merkle_levelsILb0ELi256ELb0E", "ntt_pass": "k_ntt_pass_rrILi11E",
            "ntt_first": "k_ntt_firstILi11E"}
 

@@ -647,6 +647,98 @@ __global__ __launch_bounds__(MAXB) void k_merkle_levels(MerkleArgs a) {
   }
 }
 
+// Leaf value `idx` of the launch (merkle_root.rs:25-30); FOLD: the FRI fold of the previous
+// codeword (fri.rs:151-159), also stored to fold.dst.
+template <bool FOLD>
+__device__ __forceinline__ fe leaf_value(const MerkleArgs& a, uint64_t idx) {
+  if constexpr (FOLD) {
+    const fe x = ld_fe(a.fold.src + idx);
+    const fe y = ld_fe(a.fold.src + idx + a.first_count);
+    const uint64_t e = idx << a.fold.shift;
+    const fe K = a.fold.Kp ? ld_fe(a.fold.Kp) : a.fold.K;
+    fe t = mont_mul(K, ld_fe(a.fold.Tlo + (e & 4095)));
+    t = mont_mul(t, ld_fe(a.fold.Thi + (e >> 12)));
+    const fe v = fe_add(fe_halve(fe_add(x, y)), mont_mul(fe_sub(x, y), t));
+    st_fe(a.fold.dst + idx, v);
+    return v;
+  } else {
+    return ld_fe(merkle_leaves_ptr(a) + idx);
+  }
+}
+
+// leaf digest: BLAKE2b-512 of the decimal string (field_element.rs:46-50 bytes)
+__device__ __forceinline__ void leaf_hash(const fe& v, uint64_t d[8]) {
+  uint64_t m[16];
+  uint32_t len = fe_decimal_words(v, m);
+#pragma unroll
+  for (int i = 5; i < 16; ++i) m[i] = 0;
+  blake2b_single_block(m, len, d);
+}
+
+// Leaf level with two leaves per lane: lane p hashes leaves 2p and 2p+1 and their parent (level 1)
+// itself, so the first two levels keep every wave of the block busy and need no LDS hand-over;
+// levels 2 .. fuse-1 follow through LDS as in k_merkle_levels.  first_count (leaves) is a multiple
+// of 2 * blockDim.x (host-checked).  With one leaf per lane, a 512-lane block's fused levels leave
+// 4, 2, 1 of its 8 waves busy (74 VGPRs: 6 waves per SIMD), so the SIMDs run short of ready waves;
+// here the first two levels keep all 8 busy.
+template <int MAXB, bool FOLD>
+__global__ __launch_bounds__(MAXB) void k_merkle_leaf_pairs(MerkleArgs a) {
+  __shared__ uint64_t sm[8][MAXB];
+  const uint32_t tid = threadIdx.x;
+  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + tid;  // level-1 node
+  uint64_t* __restrict__ tree = merkle_tree_ptr(a);
+  uint64_t* const root_slot = merkle_root_slot(a);
+  uint64_t d[8];
+  {
+    // both leaves are read (and folded) up front and both digests stored together, so each lane's
+    // 32-byte leaf pair and 128-byte digest pair move as whole lines (stored one compression apart,
+    // the digest halves were written back to HBM as separate partial lines: 1.19x the algorithmic
+    // bytes in the PMC pass)
+    fe v0 = leaf_value<FOLD>(a, 2 * p);
+    const fe v1 = leaf_value<FOLD>(a, 2 * p + 1);
+    // keep the second leaf's read beside the first: the first compression's input is tied to it
+    // (the scheduler would sink the read past that compression to save 4 VGPRs, re-touching each
+    // lane pair's line ~2000 instructions later)
+    asm("" : "+v"(v0.w[0]), "+v"(v0.w[1]), "+v"(v0.w[2]), "+v"(v0.w[3])
+        : "v"(v1.w[0]), "v"(v1.w[1]), "v"(v1.w[2]), "v"(v1.w[3]));
+    uint64_t l[8], r[8];
+    leaf_hash(v0, l);
+    leaf_hash(v1, r);
+    st_digest(tree + (a.off[1] + 2 * p) * 8, l);
+    st_digest(tree + (a.off[1] + 2 * p + 1) * 8, r);
+    blake2b_node(l, r, d);
+    st_digest(tree + (a.off[2] + p) * 8, d);
+    if (a.first_level + 1 == a.root_level && root_slot) {
+      for (int i = 0; i < 8; ++i) root_slot[i] = d[i];
+      merkle_root_publish(a, true);
+    }
+  }
+  uint32_t count = blockDim.x;  // digests of this block at the current level
+  for (int lev = 2; lev < a.fuse; ++lev) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) sm[i][tid] = d[i];
+    __syncthreads();
+    count >>= 1;
+    if (tid < count) {
+      uint64_t l[8], r[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const ulonglong2 lr = *reinterpret_cast<const ulonglong2*>(&sm[i][2 * tid]);
+        l[i] = lr.x;
+        r[i] = lr.y;
+      }
+      blake2b_node(l, r, d);
+      uint64_t gidx = (uint64_t)blockIdx.x * count + tid;
+      st_digest(tree + (a.off[lev + 1] + gidx) * 8, d);
+      if (a.first_level + lev == a.root_level && root_slot) {
+        for (int i = 0; i < 8; ++i) root_slot[i] = d[i];
+        merkle_root_publish(a, true);
+      }
+    }
+    __syncthreads();
+  }
+}
+
 // ---------------------------------------------------- Merkle: 4 lanes per hash
 //
 // The top of a tree is latency-bound: a level of a few thousand nodes or less
@@ -1531,7 +1623,7 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
     a.first_count = count;
     int fuse;
     unsigned bs;
-    int kind;  // 0: leaf 256, 1: leaf tail 1024, 2: node 256, 3: quad 64, 4: leaf 512, 5: quad 256, 6: node 512,
+    int kind;  // 0: leaf 256, 1: leaf tail 1024, 2: node 256, 3: quad 64, 4: leaf 512, 5: quad 256, 6: node 512, 8: leaf pairs 512,
               // 7: quad leaves 256
     // SG_MERKLE_QUAD_LEAF_BELOW = log2 of the leaf count (all trees of the launch) under which the
     // leaf level takes a quad per leaf (k_merkle_quad_leaves); 0 disables it (A/B knob)
@@ -1563,6 +1655,16 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
           int lg = 0;  // a block's fused levels end at its single digest
           while ((1u << lg) < bs) ++lg;
           if (fuse > lg + 1) fuse = lg + 1;
+        }
+        // two leaves per lane (k_merkle_leaf_pairs), 512 lanes per 1024 leaves, the same levels fused:
+        // 2^25 tree 4.13 -> 4.08 ms, prove -0.15 ms (profiles/r03_ab_leaf_pairs.log).
+        // SG_MERKLE_LEAF_PAIRS = 0 restores one leaf per lane; k > 1 fuses k - 1 levels more (A/B knob)
+        static const int env_pairs = env_int("SG_MERKLE_LEAF_PAIRS", 1);
+        if (env_pairs > 0 && fuse >= 2 && count % 1024 == 0) {
+          kind = 8;
+          bs = 512;
+          fuse = fuse + env_pairs - 1;
+          if (fuse > 11) fuse = 11;  // leaf + level 1 in the lane, then 512 -> 1 through LDS
         }
       }
     } else if (count * (uint64_t)batch >= kQuadBelow && count >= 2) {
@@ -1604,7 +1706,8 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
     uint64_t digests = 0;
     for (int k = 0; k < fuse; ++k) digests += count >> k;
     // a fused fold reads 2 source elements and writes the folded one instead of reading the leaf
-    const uint64_t per_block = kind == 3 || kind == 5 || kind == 7 ? bs / 4 : bs;  // quad kernels: 4 lanes per node
+    // quad kernels: 4 lanes per node; leaf pairs: 2 leaves per lane
+    const uint64_t per_block = kind == 3 || kind == 5 || kind == 7 ? bs / 4 : kind == 8 ? 2 * bs : bs;
     dim3 grid((unsigned)((count + per_block - 1) / per_block), batch);
     // elems = lanes launched (the rocprofv3 Grid_Size of this dispatch), so per-wave PMC
     // instruction counts scale to any launch population
@@ -1629,6 +1732,10 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
         else hipLaunchKernelGGL((k_merkle_levels<true, 512>), grid, dim3(bs), 0, s, a);
         break;
       case 5: hipLaunchKernelGGL(k_merkle_quad<256>, grid, dim3(bs), 0, s, a); break;
+      case 8:
+        if (fold_here) hipLaunchKernelGGL((k_merkle_leaf_pairs<512, true>), grid, dim3(bs), 0, s, a);
+        else hipLaunchKernelGGL((k_merkle_leaf_pairs<512, false>), grid, dim3(bs), 0, s, a);
+        break;
       case 7:
         if (fold_here) hipLaunchKernelGGL((k_merkle_quad_leaves<256, true>), grid, dim3(bs), 0, s, a);
         else hipLaunchKernelGGL((k_merkle_quad_leaves<256, false>), grid, dim3(bs), 0, s, a);
