@@ -30,4 +30,21 @@ __device__ __forceinline__ void st_fe_stream(fe* p, const fe& a, bool nt) {
   __builtin_nontemporal_store(v, reinterpret_cast<sg_u32x4*>(p));
 }
 
+// (a + p) / 2 if a odd else a / 2 -- a * 2^-1 mod p for canonical a
+__device__ __forceinline__ fe fe_halve(const fe& a) {
+  uint64_t a0 = fe_lo(a), a1 = fe_hi(a);
+  uint64_t odd = a0 & 1u;
+  // s = a + odd*p (129 bits)
+  uint64_t s0 = a0 + odd;             // p0 = 1
+  uint64_t c0 = s0 < odd;
+  uint64_t add1 = odd ? ((uint64_t)P3 << 32) : 0;
+  uint64_t s1 = a1 + add1;
+  uint64_t c1 = s1 < add1;
+  uint64_t s1b = s1 + c0;
+  c1 += s1b < c0;
+  uint64_t r0 = (s0 >> 1) | (s1b << 63);
+  uint64_t r1 = (s1b >> 1) | (c1 << 63);
+  return fe_make(r0, r1);
+}
+
 }  // namespace sg

@@ -27,32 +27,15 @@
 #include "leaf_decimal.hpp"
 #include "kernels.hpp"
 #include "profiler.hpp"
+#include "merkle_dev.hpp"
 
 namespace sg {
 
 thread_local KernelProfiler* g_prof = nullptr;
 
-constexpr int kMaxBatch = 4;  // transforms / trees per launch (blockIdx.y)
 
 // ------------------------------------------------------------------ helpers
 
-
-// (a + p) / 2 if a odd else a / 2 -- a * 2^-1 mod p for canonical a
-__device__ __forceinline__ fe fe_halve(const fe& a) {
-  uint64_t a0 = fe_lo(a), a1 = fe_hi(a);
-  uint64_t odd = a0 & 1u;
-  // s = a + odd*p (129 bits)
-  uint64_t s0 = a0 + odd;             // p0 = 1
-  uint64_t c0 = s0 < odd;
-  uint64_t add1 = odd ? ((uint64_t)P3 << 32) : 0;
-  uint64_t s1 = a1 + add1;
-  uint64_t c1 = s1 < add1;
-  uint64_t s1b = s1 + c0;
-  c1 += s1b < c0;
-  uint64_t r0 = (s0 >> 1) | (s1b << 63);
-  uint64_t r1 = (s1b >> 1) | (c1 << 63);
-  return fe_make(r0, r1);
-}
 
 // ------------------------------------------------------------- twiddles
 
@@ -510,234 +493,6 @@ __global__ void k_scale_const(fe* __restrict__ data, uint64_t n, const fe* __res
 }
 
 // ------------------------------------------------------------- Merkle
-
-struct Digest {
-  uint64_t h[8];
-};
-
-__device__ __forceinline__ void st_digest(uint64_t* p, const uint64_t d[8]) {
-  uint4* q = reinterpret_cast<uint4*>(p);
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-    q[i] = make_uint4((uint32_t)d[2 * i], (uint32_t)(d[2 * i] >> 32), (uint32_t)d[2 * i + 1], (uint32_t)(d[2 * i + 1] >> 32));
-}
-__device__ __forceinline__ void ld_digest(const uint64_t* p, uint64_t d[8]) {
-  const uint4* q = reinterpret_cast<const uint4*>(p);
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    uint4 v = q[i];
-    d[2 * i] = (uint64_t)v.x | ((uint64_t)v.y << 32);
-    d[2 * i + 1] = (uint64_t)v.z | ((uint64_t)v.w << 32);
-  }
-}
-
-// Hash the first level of a group (leaves when `leaves` != nullptr, else nodes
-// from the children at `child_level`), then `fuse - 1` further levels in LDS.
-// Level k of the tree starts at digest offset level_off[k] in `tree`.
-constexpr int kMaxFuse = 11;  // 1024 threads: up to 11 levels (1024 -> 1) in one launch
-
-struct MerkleArgs {
-  const fe* leaves[kMaxBatch];  // level 0 input (field elements) per tree (blockIdx.y)
-  uint64_t* tree[kMaxBatch];    // retained trees: 8 u64 per digest
-  uint64_t first_level;     // level hashed first by this launch
-  uint64_t first_count;     // digests at first_level
-  int fuse;                 // levels computed by this launch
-  uint64_t off[kMaxFuse + 1];  // digest offsets of levels first_level-1 .. first_level+fuse-1 (off[0] = child level)
-  uint64_t* root_host[kMaxBatch];  // optional host-coherent copy of the root (written by the launch reaching it)
-  uint64_t root_level;             // log2(n): the level whose single digest is the root
-  uint64_t leaves_ys, tree_ys;     // != 0: strided rows of trees (leaves[0] + y * leaves_ys, tree[0] + y * tree_ys)
-  uint64_t* root_flag[kMaxBatch];  // with root_host: set to root_seq (system scope) once the root is visible
-  uint64_t root_seq;
-  // FRI: the leaves are the fold of the previous round's codeword (fri.rs:151-159),
-  // computed here and also stored (dst) -- one launch instead of fold + leaf hash
-  struct {
-    const fe* src;   // previous codeword (2 * first_count elements)
-    fe* dst;         // this round's codeword
-    const fe* Tlo;   // Montgomery(w^-e) tables of the round-0 omega: e & 4095, e >> 12
-    const fe* Thi;
-    int shift;       // previous round r: exponent = i << r
-    fe K;            // Montgomery(alpha * offset_r^-1 * 2^-1)
-    const fe* Kp;    // != nullptr: K is read from here (written by k_fri_fs on the device)
-  } fold;
-};
-
-__device__ __forceinline__ uint64_t* merkle_tree_ptr(const MerkleArgs& a) {
-  return a.tree_ys ? a.tree[0] + (uint64_t)blockIdx.y * a.tree_ys : a.tree[blockIdx.y];
-}
-__device__ __forceinline__ const fe* merkle_leaves_ptr(const MerkleArgs& a) {
-  return a.leaves_ys ? a.leaves[0] + (uint64_t)blockIdx.y * a.leaves_ys : a.leaves[blockIdx.y];
-}
-__device__ __forceinline__ uint64_t* merkle_root_slot(const MerkleArgs& a) {
-  return a.tree_ys ? nullptr : a.root_host[blockIdx.y];
-}
-// publish: every lane's root stores reach system scope before the ready flag
-__device__ __forceinline__ void merkle_root_publish(const MerkleArgs& a, bool writer) {
-  __threadfence_system();
-  if (writer && a.root_flag[blockIdx.y]) *(volatile uint64_t*)a.root_flag[blockIdx.y] = a.root_seq;
-}
-
-template <bool LEAF, int MAXB, bool FOLD = false>
-__global__ __launch_bounds__(MAXB) void k_merkle_levels(MerkleArgs a) {
-  // fused levels hand digests over through LDS word-major (sm[word][lane]): a lane
-  // writes word i at an 8-byte lane stride and reads its two children's word i as one
-  // 16-byte pair, both conflict-free (a 64-byte digest per lane put every lane of a
-  // ds_read at a 128-byte stride, i.e. on the same banks)
-  __shared__ uint64_t sm[8][MAXB];
-  const uint32_t tid = threadIdx.x;
-  const uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + tid;
-  uint64_t* __restrict__ tree = merkle_tree_ptr(a);
-  uint64_t* const root_slot = merkle_root_slot(a);
-  uint64_t d[8];
-  if (idx < a.first_count) {
-    if (LEAF) {
-      uint64_t m[16];
-      fe v;
-      if constexpr (FOLD) {
-        const fe x = ld_fe(a.fold.src + idx);
-        const fe y = ld_fe(a.fold.src + idx + a.first_count);
-        const uint64_t e = idx << a.fold.shift;
-        const fe K = a.fold.Kp ? ld_fe(a.fold.Kp) : a.fold.K;
-        fe t = mont_mul(K, ld_fe(a.fold.Tlo + (e & 4095)));
-        t = mont_mul(t, ld_fe(a.fold.Thi + (e >> 12)));
-        v = fe_add(fe_halve(fe_add(x, y)), mont_mul(fe_sub(x, y), t));
-        st_fe(a.fold.dst + idx, v);
-      } else {
-        v = ld_fe(merkle_leaves_ptr(a) + idx);
-      }
-      uint32_t len = fe_decimal_words(v, m);
-#pragma unroll
-      for (int i = 5; i < 16; ++i) m[i] = 0;
-      blake2b_single_block(m, len, d);
-    } else {
-      uint64_t l[8], r[8];
-      const uint64_t* child = tree + a.off[0] * 8;
-      ld_digest(child + (2 * idx) * 8, l);
-      ld_digest(child + (2 * idx + 1) * 8, r);
-      blake2b_node(l, r, d);
-    }
-    st_digest(tree + (a.off[1] + idx) * 8, d);
-    if (a.first_level == a.root_level && root_slot) {
-      for (int i = 0; i < 8; ++i) root_slot[i] = d[i];
-      merkle_root_publish(a, true);
-    }
-  }
-  uint32_t count = blockDim.x;  // digests of this block at the current level
-  for (int lev = 1; lev < a.fuse; ++lev) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) sm[i][tid] = d[i];
-    __syncthreads();
-    count >>= 1;
-    if (tid < count) {
-      uint64_t l[8], r[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const ulonglong2 lr = *reinterpret_cast<const ulonglong2*>(&sm[i][2 * tid]);
-        l[i] = lr.x;
-        r[i] = lr.y;
-      }
-      blake2b_node(l, r, d);
-      uint64_t gidx = (uint64_t)blockIdx.x * count + tid;
-      st_digest(tree + (a.off[lev + 1] + gidx) * 8, d);
-      if (a.first_level + lev == a.root_level && root_slot) {
-        for (int i = 0; i < 8; ++i) root_slot[i] = d[i];
-        merkle_root_publish(a, true);
-      }
-    }
-    __syncthreads();
-  }
-}
-
-// Leaf value `idx` of the launch (merkle_root.rs:25-30); FOLD: the FRI fold of the previous
-// codeword (fri.rs:151-159), also stored to fold.dst.
-template <bool FOLD>
-__device__ __forceinline__ fe leaf_value(const MerkleArgs& a, uint64_t idx) {
-  if constexpr (FOLD) {
-    const fe x = ld_fe(a.fold.src + idx);
-    const fe y = ld_fe(a.fold.src + idx + a.first_count);
-    const uint64_t e = idx << a.fold.shift;
-    const fe K = a.fold.Kp ? ld_fe(a.fold.Kp) : a.fold.K;
-    fe t = mont_mul(K, ld_fe(a.fold.Tlo + (e & 4095)));
-    t = mont_mul(t, ld_fe(a.fold.Thi + (e >> 12)));
-    const fe v = fe_add(fe_halve(fe_add(x, y)), mont_mul(fe_sub(x, y), t));
-    st_fe(a.fold.dst + idx, v);
-    return v;
-  } else {
-    return ld_fe(merkle_leaves_ptr(a) + idx);
-  }
-}
-
-// leaf digest: BLAKE2b-512 of the decimal string (field_element.rs:46-50 bytes)
-__device__ __forceinline__ void leaf_hash(const fe& v, uint64_t d[8]) {
-  uint64_t m[16];
-  uint32_t len = fe_decimal_words(v, m);
-#pragma unroll
-  for (int i = 5; i < 16; ++i) m[i] = 0;
-  blake2b_single_block(m, len, d);
-}
-
-// Leaf level with two leaves per lane: lane p hashes leaves 2p and 2p+1 and their parent (level 1)
-// itself, so the first two levels keep every wave of the block busy and need no LDS hand-over;
-// levels 2 .. fuse-1 follow through LDS as in k_merkle_levels.  first_count (leaves) is a multiple
-// of 2 * blockDim.x (host-checked).  With one leaf per lane, a 512-lane block's fused levels leave
-// 4, 2, 1 of its 8 waves busy (74 VGPRs: 6 waves per SIMD), so the SIMDs run short of ready waves;
-// here the first two levels keep all 8 busy.
-template <int MAXB, bool FOLD>
-__global__ __launch_bounds__(MAXB) void k_merkle_leaf_pairs(MerkleArgs a) {
-  __shared__ uint64_t sm[8][MAXB];
-  const uint32_t tid = threadIdx.x;
-  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + tid;  // level-1 node
-  uint64_t* __restrict__ tree = merkle_tree_ptr(a);
-  uint64_t* const root_slot = merkle_root_slot(a);
-  uint64_t d[8];
-  {
-    // both leaves are read (and folded) up front and both digests stored together, so each lane's
-    // 32-byte leaf pair and 128-byte digest pair move as whole lines (stored one compression apart,
-    // the digest halves were written back to HBM as separate partial lines: 1.19x the algorithmic
-    // bytes in the PMC pass)
-    fe v0 = leaf_value<FOLD>(a, 2 * p);
-    const fe v1 = leaf_value<FOLD>(a, 2 * p + 1);
-    // keep the second leaf's read beside the first: the first compression's input is tied to it
-    // (the scheduler would sink the read past that compression to save 4 VGPRs, re-touching each
-    // lane pair's line ~2000 instructions later)
-    asm("" : "+v"(v0.w[0]), "+v"(v0.w[1]), "+v"(v0.w[2]), "+v"(v0.w[3])
-        : "v"(v1.w[0]), "v"(v1.w[1]), "v"(v1.w[2]), "v"(v1.w[3]));
-    uint64_t l[8], r[8];
-    leaf_hash(v0, l);
-    leaf_hash(v1, r);
-    st_digest(tree + (a.off[1] + 2 * p) * 8, l);
-    st_digest(tree + (a.off[1] + 2 * p + 1) * 8, r);
-    blake2b_node(l, r, d);
-    st_digest(tree + (a.off[2] + p) * 8, d);
-    if (a.first_level + 1 == a.root_level && root_slot) {
-      for (int i = 0; i < 8; ++i) root_slot[i] = d[i];
-      merkle_root_publish(a, true);
-    }
-  }
-  uint32_t count = blockDim.x;  // digests of this block at the current level
-  for (int lev = 2; lev < a.fuse; ++lev) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) sm[i][tid] = d[i];
-    __syncthreads();
-    count >>= 1;
-    if (tid < count) {
-      uint64_t l[8], r[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const ulonglong2 lr = *reinterpret_cast<const ulonglong2*>(&sm[i][2 * tid]);
-        l[i] = lr.x;
-        r[i] = lr.y;
-      }
-      blake2b_node(l, r, d);
-      uint64_t gidx = (uint64_t)blockIdx.x * count + tid;
-      st_digest(tree + (a.off[lev + 1] + gidx) * 8, d);
-      if (a.first_level + lev == a.root_level && root_slot) {
-        for (int i = 0; i < 8; ++i) root_slot[i] = d[i];
-        merkle_root_publish(a, true);
-      }
-    }
-    __syncthreads();
-  }
-}
 
 // ---------------------------------------------------- Merkle: 4 lanes per hash
 //
@@ -1717,30 +1472,16 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
                  batch * ((level == 0 ? (fold_here ? 48 : 16) * count : 0) + 64 * digests), s,
                  (uint64_t)grid.x * grid.y * bs);
     switch (kind) {
-      case 0:
-        if (fold_here) hipLaunchKernelGGL((k_merkle_levels<true, 256, true>), grid, dim3(bs), 0, s, a);
-        else hipLaunchKernelGGL((k_merkle_levels<true, 256>), grid, dim3(bs), 0, s, a);
-        break;
-      case 1:
-        if (fold_here) hipLaunchKernelGGL((k_merkle_levels<true, 1024, true>), grid, dim3(bs), 0, s, a);
-        else hipLaunchKernelGGL((k_merkle_levels<true, 1024>), grid, dim3(bs), 0, s, a);
-        break;
-      case 2: hipLaunchKernelGGL((k_merkle_levels<false, 256>), grid, dim3(bs), 0, s, a); break;
-      case 6: hipLaunchKernelGGL((k_merkle_levels<false, 512>), grid, dim3(bs), 0, s, a); break;
-      case 4:
-        if (fold_here) hipLaunchKernelGGL((k_merkle_levels<true, 512, true>), grid, dim3(bs), 0, s, a);
-        else hipLaunchKernelGGL((k_merkle_levels<true, 512>), grid, dim3(bs), 0, s, a);
-        break;
       case 5: hipLaunchKernelGGL(k_merkle_quad<256>, grid, dim3(bs), 0, s, a); break;
-      case 8:
-        if (fold_here) hipLaunchKernelGGL((k_merkle_leaf_pairs<512, true>), grid, dim3(bs), 0, s, a);
-        else hipLaunchKernelGGL((k_merkle_leaf_pairs<512, false>), grid, dim3(bs), 0, s, a);
-        break;
       case 7:
         if (fold_here) hipLaunchKernelGGL((k_merkle_quad_leaves<256, true>), grid, dim3(bs), 0, s, a);
         else hipLaunchKernelGGL((k_merkle_quad_leaves<256, false>), grid, dim3(bs), 0, s, a);
         break;
-      default: hipLaunchKernelGGL(k_merkle_quad<64>, grid, dim3(bs), 0, s, a); break;
+      case 3: hipLaunchKernelGGL(k_merkle_quad<64>, grid, dim3(bs), 0, s, a); break;
+      default: {
+        hipError_t e = launch_merkle_lanes(kind, fold_here, grid, bs, s, a);
+        if (e != hipSuccess) return e;
+      }
     }
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;

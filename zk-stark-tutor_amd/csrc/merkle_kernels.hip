@@ -1,0 +1,173 @@
+// Merkle lane-per-hash kernels: one leaf or node compression per lane (two leaves in
+// k_merkle_leaf_pairs), the levels above fused through LDS (merkle_root.rs:7-32).
+//
+// This translation unit is compiled with LLVM's max-ILP machine scheduler (Makefile): it
+// interleaves the four independent G functions of each BLAKE2b half-round, trading VGPRs
+// (74 -> 104 for the leaf-pair kernel, 6 -> 4 waves per SIMD) for per-wave instruction-level
+// parallelism: 2^25 tree 2.5 % faster (profiles/r03_ab_merkle_max_ilp.log).  The NTT and quad-lane
+// kernels stay on the default scheduler (max-ILP spills them).
+#include "merkle_dev.hpp"
+
+namespace sg {
+
+template <bool LEAF, int MAXB, bool FOLD = false>
+__global__ __launch_bounds__(MAXB) void k_merkle_levels(MerkleArgs a) {
+  // fused levels hand digests over through LDS word-major (sm[word][lane]): a lane
+  // writes word i at an 8-byte lane stride and reads its two children's word i as one
+  // 16-byte pair, both conflict-free (a 64-byte digest per lane put every lane of a
+  // ds_read at a 128-byte stride, i.e. on the same banks)
+  __shared__ uint64_t sm[8][MAXB];
+  const uint32_t tid = threadIdx.x;
+  const uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + tid;
+  uint64_t* __restrict__ tree = merkle_tree_ptr(a);
+  uint64_t* const root_slot = merkle_root_slot(a);
+  uint64_t d[8];
+  if (idx < a.first_count) {
+    if (LEAF) {
+      uint64_t m[16];
+      fe v;
+      if constexpr (FOLD) {
+        const fe x = ld_fe(a.fold.src + idx);
+        const fe y = ld_fe(a.fold.src + idx + a.first_count);
+        const uint64_t e = idx << a.fold.shift;
+        const fe K = a.fold.Kp ? ld_fe(a.fold.Kp) : a.fold.K;
+        fe t = mont_mul(K, ld_fe(a.fold.Tlo + (e & 4095)));
+        t = mont_mul(t, ld_fe(a.fold.Thi + (e >> 12)));
+        v = fe_add(fe_halve(fe_add(x, y)), mont_mul(fe_sub(x, y), t));
+        st_fe(a.fold.dst + idx, v);
+      } else {
+        v = ld_fe(merkle_leaves_ptr(a) + idx);
+      }
+      uint32_t len = fe_decimal_words(v, m);
+#pragma unroll
+      for (int i = 5; i < 16; ++i) m[i] = 0;
+      blake2b_single_block(m, len, d);
+    } else {
+      uint64_t l[8], r[8];
+      const uint64_t* child = tree + a.off[0] * 8;
+      ld_digest(child + (2 * idx) * 8, l);
+      ld_digest(child + (2 * idx + 1) * 8, r);
+      blake2b_node(l, r, d);
+    }
+    st_digest(tree + (a.off[1] + idx) * 8, d);
+    if (a.first_level == a.root_level && root_slot) {
+      for (int i = 0; i < 8; ++i) root_slot[i] = d[i];
+      merkle_root_publish(a, true);
+    }
+  }
+  uint32_t count = blockDim.x;  // digests of this block at the current level
+  for (int lev = 1; lev < a.fuse; ++lev) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) sm[i][tid] = d[i];
+    __syncthreads();
+    count >>= 1;
+    if (tid < count) {
+      uint64_t l[8], r[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const ulonglong2 lr = *reinterpret_cast<const ulonglong2*>(&sm[i][2 * tid]);
+        l[i] = lr.x;
+        r[i] = lr.y;
+      }
+      blake2b_node(l, r, d);
+      uint64_t gidx = (uint64_t)blockIdx.x * count + tid;
+      st_digest(tree + (a.off[lev + 1] + gidx) * 8, d);
+      if (a.first_level + lev == a.root_level && root_slot) {
+        for (int i = 0; i < 8; ++i) root_slot[i] = d[i];
+        merkle_root_publish(a, true);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// Leaf level with two leaves per lane: lane p hashes leaves 2p and 2p+1 and their parent (level 1)
+// itself, so the first two levels keep every wave of the block busy and need no LDS hand-over;
+// levels 2 .. fuse-1 follow through LDS as in k_merkle_levels.  first_count (leaves) is a multiple
+// of 2 * blockDim.x (host-checked).  With one leaf per lane, a 512-lane block's fused levels leave
+// 4, 2, 1 of its 8 waves busy (74 VGPRs: 6 waves per SIMD), so the SIMDs run short of ready waves;
+// here the first two levels keep all 8 busy.
+template <int MAXB, bool FOLD>
+__global__ __launch_bounds__(MAXB) void k_merkle_leaf_pairs(MerkleArgs a) {
+  __shared__ uint64_t sm[8][MAXB];
+  const uint32_t tid = threadIdx.x;
+  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + tid;  // level-1 node
+  uint64_t* __restrict__ tree = merkle_tree_ptr(a);
+  uint64_t* const root_slot = merkle_root_slot(a);
+  uint64_t d[8];
+  {
+    // both leaves are read (and folded) up front and both digests stored together, so each lane's
+    // 32-byte leaf pair and 128-byte digest pair move as whole lines (stored one compression apart,
+    // the digest halves were written back to HBM as separate partial lines: 1.19x the algorithmic
+    // bytes in the PMC pass)
+    fe v0 = leaf_value<FOLD>(a, 2 * p);
+    const fe v1 = leaf_value<FOLD>(a, 2 * p + 1);
+    // keep the second leaf's read beside the first: the first compression's input is tied to it
+    // (the scheduler would sink the read past that compression to save 4 VGPRs, re-touching each
+    // lane pair's line ~2000 instructions later)
+    asm("" : "+v"(v0.w[0]), "+v"(v0.w[1]), "+v"(v0.w[2]), "+v"(v0.w[3])
+        : "v"(v1.w[0]), "v"(v1.w[1]), "v"(v1.w[2]), "v"(v1.w[3]));
+    uint64_t l[8], r[8];
+    leaf_hash(v0, l);
+    leaf_hash(v1, r);
+    st_digest(tree + (a.off[1] + 2 * p) * 8, l);
+    st_digest(tree + (a.off[1] + 2 * p + 1) * 8, r);
+    blake2b_node(l, r, d);
+    st_digest(tree + (a.off[2] + p) * 8, d);
+    if (a.first_level + 1 == a.root_level && root_slot) {
+      for (int i = 0; i < 8; ++i) root_slot[i] = d[i];
+      merkle_root_publish(a, true);
+    }
+  }
+  uint32_t count = blockDim.x;  // digests of this block at the current level
+  for (int lev = 2; lev < a.fuse; ++lev) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) sm[i][tid] = d[i];
+    __syncthreads();
+    count >>= 1;
+    if (tid < count) {
+      uint64_t l[8], r[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const ulonglong2 lr = *reinterpret_cast<const ulonglong2*>(&sm[i][2 * tid]);
+        l[i] = lr.x;
+        r[i] = lr.y;
+      }
+      blake2b_node(l, r, d);
+      uint64_t gidx = (uint64_t)blockIdx.x * count + tid;
+      st_digest(tree + (a.off[lev + 1] + gidx) * 8, d);
+      if (a.first_level + lev == a.root_level && root_slot) {
+        for (int i = 0; i < 8; ++i) root_slot[i] = d[i];
+        merkle_root_publish(a, true);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+hipError_t launch_merkle_lanes(int kind, bool fold, dim3 grid, unsigned bs, hipStream_t s, const MerkleArgs& a) {
+  switch (kind) {
+    case 0:
+      if (fold) hipLaunchKernelGGL((k_merkle_levels<true, 256, true>), grid, dim3(bs), 0, s, a);
+      else hipLaunchKernelGGL((k_merkle_levels<true, 256>), grid, dim3(bs), 0, s, a);
+      break;
+    case 1:
+      if (fold) hipLaunchKernelGGL((k_merkle_levels<true, 1024, true>), grid, dim3(bs), 0, s, a);
+      else hipLaunchKernelGGL((k_merkle_levels<true, 1024>), grid, dim3(bs), 0, s, a);
+      break;
+    case 2: hipLaunchKernelGGL((k_merkle_levels<false, 256>), grid, dim3(bs), 0, s, a); break;
+    case 6: hipLaunchKernelGGL((k_merkle_levels<false, 512>), grid, dim3(bs), 0, s, a); break;
+    case 4:
+      if (fold) hipLaunchKernelGGL((k_merkle_levels<true, 512, true>), grid, dim3(bs), 0, s, a);
+      else hipLaunchKernelGGL((k_merkle_levels<true, 512>), grid, dim3(bs), 0, s, a);
+      break;
+    case 8:
+      if (fold) hipLaunchKernelGGL((k_merkle_leaf_pairs<512, true>), grid, dim3(bs), 0, s, a);
+      else hipLaunchKernelGGL((k_merkle_leaf_pairs<512, false>), grid, dim3(bs), 0, s, a);
+      break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace sg
