@@ -50,6 +50,10 @@ const char* sg_last_error(const sg_ctx* ctx);
 void* sg_ctx_stream(sg_ctx* ctx);
 /* release cached device buffers and twiddle tables */
 int sg_ctx_trim(sg_ctx* ctx);
+/* instrumentation, no reference counterpart: the number of public tables the context keeps
+ * (domain / AIR coset tables, twiddle plans, interpolation kernels) -- constant across proofs
+ * on one (AIR, domain), also when the constraints are rebuilt for every proof */
+int sg_ctx_cached_tables(const sg_ctx* ctx, size_t* domain_tables, size_t* twiddle_tables);
 /* HBM probe (measurement, no reference counterpart): read + write GB/s of a dwordx4 streaming
  * device copy of `bytes` (multiple of 16), best of `iters`; blocks = 0: one 16-byte element per
  * lane, else a grid-stride copy over blocks x 256 lanes */

@@ -419,6 +419,9 @@ void build_tree(const u128* leaves, uint64_t n, Tree& t) {
 struct Stream {
   std::vector<uint8_t> body;  // objects after the 16-byte header
   bool field = false;
+  // Fiat-Shamir input prefix: empty for IndependentProofStream (proof_stream.rs:31-48);
+  // [len u64 BE][blake2b512(document)] for SignatureProofStream (rescue_prime/proof_stream.rs:22-39)
+  std::vector<uint8_t> fs_prefix;
   void push(uint8_t code, const uint8_t* p, size_t len, bool carries_field) {
     body.push_back(code);
     for (int b = 7; b >= 0; --b) body.push_back((uint8_t)((uint64_t)len >> (8 * b)));
@@ -433,7 +436,9 @@ struct Stream {
     return out;
   }
   void fiat_shamir(uint8_t out[32]) const {
-    const std::vector<uint8_t> d = digest();
+    std::vector<uint8_t> d = fs_prefix;
+    const std::vector<uint8_t> b = digest();
+    d.insert(d.end(), b.begin(), b.end());
     shake256(d.data(), d.size(), out, 32);
   }
 };
@@ -999,7 +1004,7 @@ struct StarkArgs {
 
 std::vector<uint8_t> stark_prove(const StarkArgs& A, const Vec& trace, uint64_t rows, const Vec& trace_rand,
                                  const Vec& rcoef, const std::vector<uint64_t>& bcyc, const std::vector<uint64_t>& breg,
-                                 const Vec& bval, double* phase_s) {
+                                 const Vec& bval, double* phase_s, const std::vector<uint8_t>& fs_prefix) {
   auto clk = [] { return omp_get_wtime(); };
   double t0 = clk();
   int ph = 0;
@@ -1011,6 +1016,7 @@ std::vector<uint8_t> stark_prove(const StarkArgs& A, const Vec& trace, uint64_t 
   FC_REQUIRE(T <= D, -1, "randomized trace longer than the omicron domain");
   FC_REQUIRE(rcoef.size() == A.tcd + 1, -1, "randomizer polynomial must have max_degree + 1 coefficients");
   Stream ps;
+  ps.fs_prefix = fs_prefix;
   // trace polynomials (stark.rs:303-324)
   std::vector<Vec> tp(m);
   for (uint64_t s = 0; s < m; ++s) {
@@ -1240,7 +1246,9 @@ const char* fc_last_error(void) { return g_err.c_str(); }
 // randomness (the two thread_rng draws), every argument as the reference's Stark / RescuePrime
 // hold it.  Elements are (lo, hi) u64 pairs; the serialized proof (stark.rs:562) goes to a malloc'd
 // buffer (*out, *out_len; free with fc_free).  phase_s (optional, 8 doubles): cumulative wall
-// seconds at the end of each phase.  Returns 0, or < 0 with fc_last_error().
+// seconds at the end of each phase.  fs_prefix (fs_prefix_len bytes, may be empty): the bytes a
+// SignatureProofStream puts before the digest in every Fiat-Shamir draw
+// (rescue_prime/proof_stream.rs:22-39).  Returns 0, or < 0 with fc_last_error().
 long fc_stark_prove_rescue(uint64_t m, uint64_t original_trace_length, uint64_t num_randomizers, uint64_t D,
                            uint64_t Nf, uint64_t expansion, uint64_t colinearity, const uint64_t* omicron,
                            const uint64_t* omega, const uint64_t* generator, uint64_t alpha, const uint64_t* mds,
@@ -1248,7 +1256,7 @@ long fc_stark_prove_rescue(uint64_t m, uint64_t original_trace_length, uint64_t 
                            const uint64_t* tqdb, uint64_t tcd, const uint64_t* trace, uint64_t trace_rows,
                            const uint64_t* trace_rand, const uint64_t* rcoef, uint64_t nrc, const uint64_t* bcyc,
                            const uint64_t* breg, const uint64_t* bval, uint64_t nb, uint8_t** out, size_t* out_len,
-                           double* phase_s) {
+                           double* phase_s, const uint8_t* fs_prefix, size_t fs_prefix_len) {
   try {
     auto vec = [](const uint64_t* p, uint64_t n) {
       Vec v(n);
@@ -1265,7 +1273,8 @@ long fc_stark_prove_rescue(uint64_t m, uint64_t original_trace_length, uint64_t 
     std::vector<uint64_t> bc(bcyc, bcyc + nb), br(breg, breg + nb);
     const std::vector<uint8_t> d = stark_prove(A, vec(trace, trace_rows * m), trace_rows,
                                                vec(trace_rand, num_randomizers * m), vec(rcoef, nrc), bc, br,
-                                               vec(bval, nb), phase_s);
+                                               vec(bval, nb), phase_s,
+                                               std::vector<uint8_t>(fs_prefix, fs_prefix + fs_prefix_len));
     *out = static_cast<uint8_t*>(malloc(d.size()));
     if (!*out) return -4;
     memcpy(*out, d.data(), d.size());

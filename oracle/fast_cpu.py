@@ -5,6 +5,7 @@ cpu_baseline leg).  Build with `make -C oracle` (done by __graft_entry__.build()
 Arrays are numpy uint64 of shape (n, 2): little-endian (lo, hi) limbs, canonical.
 """
 import ctypes
+import hashlib
 import os
 
 import numpy as np
@@ -50,7 +51,8 @@ def lib():
         l.fc_last_error.restype = ctypes.c_char_p
         l.fc_stark_prove_rescue.argtypes = [u64] * 7 + [vp, vp, vp, u64, vp, vp, vp, u64, vp, u64, vp, u64, vp, vp,
                                                         u64, vp, vp, vp, u64, ctypes.POINTER(ctypes.c_void_p),
-                                                        ctypes.POINTER(ctypes.c_size_t), vp]
+                                                        ctypes.POINTER(ctypes.c_size_t), vp, ctypes.c_char_p,
+                                                        ctypes.c_size_t]
         l.fc_stark_prove_rescue.restype = ctypes.c_long
         l.fc_geo_interpolate.argtypes = [vp, u64, vp, u64, vp]
         l.fc_geo_interpolate.restype = ctypes.c_long
@@ -280,9 +282,11 @@ PHASES = ("trace_interpolation", "boundary_quotients", "bq_codewords_commit", "t
 
 
 def stark_prove_rescue(rp, st, trace, boundary, trace_randomizers, randomizer_coefficients, bounds=None,
-                       phases=None) -> bytes:
+                       phases=None, document=None) -> bytes:
     """Stark::prove (stark.rs:276-562) of a Rescue-Prime trace on the CPU (Montgomery + OpenMP):
-    the serialized proof stream (IndependentProofStream, stark.rs:562).  `rp` / `st` are the
+    the serialized proof stream (IndependentProofStream, stark.rs:562; with `document`, a
+    SignatureProofStream's: every Fiat-Shamir draw hashes [len u64 BE][blake2b512(document)]
+    before the stream, rescue_prime/proof_stream.rs:22-39).  `rp` / `st` are the
     oracle's RescuePrime / Stark (or any objects with the same attributes); `trace` rows x m
     (list of lists or an (rows * m, 2) array); the two thread_rng draws are explicit like the
     oracle's prove.  Raises ValueError with the reference's message where it returns Err/panics."""
@@ -304,12 +308,16 @@ def stark_prove_rescue(rp, st, trace, boundary, trace_randomizers, randomizer_co
     out = ctypes.c_void_p()
     out_len = ctypes.c_size_t()
     ph = np.zeros(8, dtype=np.float64)
+    prefix = b""
+    if document is not None:
+        h = hashlib.blake2b(bytes(document), digest_size=64).digest()
+        prefix = len(h).to_bytes(8, "big") + h
     r = lib().fc_stark_prove_rescue(m, st.original_trace_length, st.num_randomizers, st.omicron_domain_length,
                                     st.fri.domain_length, st.expansion_factor, st.fri.num_colinearity_tests,
                                     _p(_fe(st.omicron)), _p(_fe(st.omega)), _p(_fe(st.generator)), rp.alpha,
                                     _p(mds), _p(mdsi), _p(rcs), rp.N, _p(tq), tcd, _p(t), rows, _p(tr), _p(rc),
                                     len(rc), _p(bc), _p(br), _p(bv), len(boundary), ctypes.byref(out),
-                                    ctypes.byref(out_len), _p(ph))
+                                    ctypes.byref(out_len), _p(ph), prefix, len(prefix))
     if r < 0:
         raise ValueError(lib().fc_last_error().decode())
     try:

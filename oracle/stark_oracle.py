@@ -318,6 +318,37 @@ def serialize(objects: Sequence) -> bytes:
     return _u128be(P if has_field else 0) + b"".join(body)
 
 
+def deserialize(data: bytes) -> list:
+    """stark/stark.rs:30-67 deser_independent_proof_stream + proof_stream_enum.rs:129-159 from_bytes:
+    the objects of a serialized stream (the field order, when present, must be P)."""
+    order = int.from_bytes(data[:16], "big")
+    assert order in (0, P), "serialized field differs from Stark's field"
+    pos, out = 16, []
+    while pos < len(data):
+        code = data[pos]
+        size = int.from_bytes(data[pos + 1:pos + 9], "big")
+        pl = data[pos + 9:pos + 9 + size]
+        assert len(pl) == size, "truncated object"
+        pos += 9 + size
+        if code == ROOT:
+            out.append((ROOT, bytes(pl)))
+        elif code in (CODEWORD, LEAFS):
+            vals = [int.from_bytes(pl[i:i + 16], "big") for i in range(0, size, 16)]
+            out.append((code, vals if code == CODEWORD else tuple(vals)))
+        elif code == PATH:
+            path, q = [], 0
+            while q < size:
+                n = int.from_bytes(pl[q:q + 8], "big")
+                path.append(bytes(pl[q + 8:q + 8 + n]))
+                q += 8 + n
+            out.append((PATH, path))
+        elif code == VALUE:
+            out.append((VALUE, int.from_bytes(pl, "big")))
+        else:
+            raise ValueError("unknown object code")
+    return out
+
+
 class IndependentProofStream:
     """proof_stream.rs:15-78 (the in-memory transcript)."""
 

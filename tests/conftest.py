@@ -6,7 +6,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG_DIR = os.path.join(ROOT, "zk-stark-tutor_amd")
-for p in (ROOT, PKG_DIR, os.path.join(ROOT, "oracle")):
+for p in (ROOT, PKG_DIR, os.path.join(ROOT, "oracle"), os.path.join(ROOT, "tests")):
     if p not in sys.path:
         sys.path.insert(0, p)
 

@@ -149,6 +149,27 @@ def test_stark_prove_domain_tables_cached_and_recomputed(monkeypatch):
     assert st.prove(trace, air, bnd, sg.IndependentProofStream(), tr, rc) == want
 
 
+@pytest.mark.parametrize("generic", ["0", "1"])
+def test_stark_prove_rebuilt_constraints_keep_tables_flat(monkeypatch, generic):
+    """The reference rebuilds the transition constraints for every sign / verify (rpsss.rs:46,57).
+    The AIR's coset tables are keyed by content (the Rescue parameters and domain, or a digest of
+    each x-polynomial for the expanded groups), so rebuilding the constraints for each of 5 proofs
+    leaves the context's table count where the first proof put it; every proof equals the oracle's."""
+    monkeypatch.setenv("SG_AIR_GENERIC", generic)
+    rp, st_o, st_g, air_o, air_g, trace, bnd, tr, rc, out = _case(40, 4, 3, 4, 2, b"rebuilt-air")
+    want = st_o.prove(trace, air_o, bnd, o.IndependentProofStream(), tr, rc)
+    ctx = sg.Context(0)
+    st = sg.Stark(4, 3, 4, 2, 41, 2, ctx=ctx)
+    rpg = sg.RescuePrime(2, 1, 4, 40, ctx=ctx)
+    counts = []
+    for _ in range(5):
+        air = rpg.transition_constraints(st.omicron, st.omicron_domain_length)
+        assert st.prove(trace, air, bnd, sg.IndependentProofStream(), tr, rc) == want
+        counts.append(ctx.cached_tables())
+        del air
+    assert counts[0][0] > 0 and all(c == counts[0] for c in counts), counts
+
+
 def test_stark_prove_constraints_shared_by_two_contexts():
     """Constraint objects built on one context and proved on two (the AIR's coset values live in
     each context's domain tables, not in the shared constraint), with sg_ctx_trim between proofs
@@ -284,3 +305,52 @@ def test_stark_prove_c4_rescue_trace_2p16():
     assert ok, err
     ok, _ = st_o.verify(sair, rp_o.boundary_constraints(o.add_mod(out, 1)), o.IndependentProofStream(objs))
     assert not ok
+
+
+@pytest.fixture(scope="module")
+def rpsss():
+    """The reference's published RPSSS configuration (tests/rpsss_case.py) and the oracle's
+    signature for it (Stark.prove through a SignatureProofStream, ~8 s)."""
+    import rpsss_case as R
+    c = R.Case()
+    return R, c, c.oracle_sign()
+
+
+def test_rpsss_published_configuration_bytes_length_verify(rpsss):
+    """rpsss.rs:89,103,113-131: RPSSS::new(field, 4, 64, 128, 3) signs b"Hello, World!" --
+    Rescue N = 27, Stark(4, 64, 128, 2, 28, 3), FRI domain 4096, c = 64, a SignatureProofStream,
+    randomizers injected.  The GPU proof bytes equal the oracle's, the length is the reference's
+    1 156 888, the oracle verifier accepts the signature for the document and rejects it for
+    b"Malicious document"."""
+    R, c, want = rpsss
+    rp_g = sg.RescuePrime(*R.RESCUE)
+    st_g = sg.Stark(R.EXPANSION, R.CHECKS, R.SECURITY, rp_g.m, R.RESCUE[3] + 1, R.TCD)
+    assert (st_g.omicron_domain_length, st_g.fri_domain_length) == (1024, 4096)
+    assert rp_g.hash(c.sk) == c.pk
+    air_g = rp_g.transition_constraints(st_g.omicron, st_g.omicron_domain_length)
+    assert st_g.transition_degree_bounds(air_g) == c.st.transition_degree_bounds(c.air)
+    got = st_g.prove(rp_g.trace(c.sk), air_g, rp_g.boundary_constraints(c.pk), sg.SignatureProofStream(R.DOCUMENT),
+                     c.trace_randomizers, c.randomizer_coefficients)
+    assert len(got) == R.PROOF_LEN, "rpsss.rs:89"
+    assert got == want
+    assert c.oracle_verify(R.DOCUMENT, got) == (True, "")
+    ok, err = c.oracle_verify(R.FORGED, got)
+    assert not ok, "rpsss.rs:127-131: " + err
+    # the same signature through a foreign (Python) proof stream driven by the callbacks
+    ops = o.SignatureProofStream(R.DOCUMENT)
+    assert st_g.prove(c.trace, air_g, c.boundary, ops, c.trace_randomizers, c.randomizer_coefficients) == want
+
+
+def test_rpsss_published_configuration_signature_roundtrip(rpsss):
+    """The signature deserializes (stark.rs:30-67, sg_stream_deserialize) into the objects the
+    oracle's deserializer reads, and a second document signs to different bytes of the same length."""
+    R, c, want = rpsss
+    back = sg.IndependentProofStream.deserialize(want)
+    assert back.digest() == want
+    rp_g = sg.RescuePrime(*R.RESCUE)
+    st_g = sg.Stark(R.EXPANSION, R.CHECKS, R.SECURITY, rp_g.m, R.RESCUE[3] + 1, R.TCD)
+    air_g = rp_g.transition_constraints(st_g.omicron, st_g.omicron_domain_length)
+    other = st_g.prove(c.trace, air_g, c.boundary, sg.SignatureProofStream(R.FORGED), c.trace_randomizers,
+                       c.randomizer_coefficients)
+    assert len(other) == R.PROOF_LEN and other != want
+    assert c.oracle_verify(R.FORGED, other) == (True, "")

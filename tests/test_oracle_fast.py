@@ -206,3 +206,31 @@ def test_fast_stark_prove_false_witness_and_errors(fc):
             st.prove(bad, air, bnd, o.IndependentProofStream(), tr, rc)
     with pytest.raises(ValueError, match="max_degree"):
         fc.stark_prove_rescue(rp, st, trace, bnd, tr, rc[:-1])
+
+
+def test_fast_stark_prove_rpsss_published_configuration(fc):
+    """The reference's published end-to-end fixture (rpsss.rs:89,103,113-131; tests/rpsss_case.py):
+    RPSSS::new(field, 4, 64, 128, 3) signing b"Hello, World!" through a SignatureProofStream.
+    The CPU checker (with the stream's Fiat-Shamir prefix) writes the oracle's bytes, the length is
+    the reference's 1 156 888, the oracle verifier accepts the document and rejects the forgery,
+    and the bytes are the committed golden digest (tests/golden/make_rpsss.py)."""
+    import hashlib
+    import json
+    import rpsss_case as R
+    with open(os.path.join(ROOT, "tests", "golden", "rpsss_published.json")) as f:
+        g = json.load(f)
+    c = R.Case(g["seed"].encode())
+    assert (c.sk, c.pk) == (int(g["sk"]), int(g["pk"]))
+    want = c.oracle_sign()
+    assert len(want) == R.PROOF_LEN == g["proof_len"], "rpsss.rs:89"
+    assert hashlib.sha256(want).hexdigest() == g["proof_sha256"]
+    got = fc.stark_prove_rescue(c.rp, c.st, c.trace, c.boundary, c.trace_randomizers,
+                                c.randomizer_coefficients, document=R.DOCUMENT)
+    assert got == want
+    # an IndependentProofStream's Fiat-Shamir draws differ: same length, different bytes
+    plain = fc.stark_prove_rescue(c.rp, c.st, c.trace, c.boundary, c.trace_randomizers, c.randomizer_coefficients)
+    assert len(plain) == len(want) and plain != want
+    assert c.oracle_verify(R.DOCUMENT, want) == (True, "")
+    ok, err = c.oracle_verify(R.FORGED, want)
+    assert not ok, "rpsss.rs:127-131"
+    assert o.serialize(o.deserialize(want)) == want

@@ -352,6 +352,13 @@ extern "C" int sg_ctx_trim(sg_ctx* ctx) {
   });
 }
 
+extern "C" int sg_ctx_cached_tables(const sg_ctx* ctx, size_t* domain_tables, size_t* twiddle_tables) {
+  if (!ctx || !domain_tables || !twiddle_tables) return SG_ERR_INVALID;
+  *domain_tables = ctx->domain_tables.size();
+  *twiddle_tables = ctx->pow_tables.size() + ctx->stage_tables.size() + ctx->interp_tables.size();
+  return SG_OK;
+}
+
 // HBM copy probe: the read + write rate of a dwordx4 streaming copy of `bytes` (SURVEY.md 8(d):
 // "measure actual HBM with a copy kernel on the box"), best of `iters` launches, HIP events on the
 // context's stream.  blocks = 0: one 16-byte element per lane (the fastest form); else a

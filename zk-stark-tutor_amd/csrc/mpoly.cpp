@@ -8,6 +8,7 @@
 #include <vector>
 
 #include "host_field.hpp"
+#include "host_hash.hpp"
 #include "internal.hpp"
 #include "mpoly.hpp"
 #include "poly_kernels.hpp"
@@ -98,7 +99,7 @@ MPoly mp_lift(const HPoly& poly, uint32_t vi) {
 
 MPoly mp_neg(const MPoly& a) {
   MPoly r = a;
-  r.dev.reset();
+  r.dev.clear();
   r.rescue.reset();  // the factored form describes +a: the negation is evaluated from its groups
   for (auto& kv : r.g)
     for (auto& c : kv.second) c = fe_neg(c);
@@ -153,21 +154,18 @@ MPoly mp_pow(sg_ctx* ctx, const MPoly& a, unsigned __int128 e) {
   return acc;
 }
 
-uint64_t next_constraint_id() {
-  static std::atomic<uint64_t> next{1};
-  return next.fetch_add(1);
-}
-
 MPolyDevice::~MPolyDevice() {
   for (void* p : ptr)
     if (p) (void)hipFree(p);
 }
 
-const MPolyDevice& mp_device(sg_ctx* ctx, const MPoly& a) {
-  // contexts on several host threads may share a constraint: its device copy is made once
+std::shared_ptr<const MPolyDevice> mp_device(sg_ctx* ctx, const MPoly& a) {
+  // contexts on several host threads may share a constraint: its device copy is made once per
+  // device, and a copy for another device never replaces it
   static std::mutex mu;
   std::lock_guard<std::mutex> lk(mu);
-  if (a.dev && a.dev->device == ctx->device) return *a.dev;
+  auto hit = a.dev.find(ctx->device);
+  if (hit != a.dev.end()) return hit->second;
   auto d = std::make_shared<MPolyDevice>();
   d->device = ctx->device;
   // normalize every group's x-vector (trimmed at its degree) by its first non-zero
@@ -216,9 +214,14 @@ const MPolyDevice& mp_device(sg_ctx* ctx, const MPoly& a) {
     d->small.push_back(v.size() <= (size_t)kSmallPolyMax ? v : HPoly{});
     SG_HIP(hipMemcpyAsync(p, v.data(), v.size() * sizeof(fe), hipMemcpyHostToDevice, ctx->stream));
     SG_HIP(hipStreamSynchronize(ctx->stream));
+    uint8_t h[64];
+    blake2b512(reinterpret_cast<const uint8_t*>(v.data()), v.size() * sizeof(fe), h);
+    std::array<uint64_t, 4> dg{};
+    memcpy(dg.data(), h, sizeof(dg));
+    d->digest.push_back(dg);
   }
-  a.dev = d;
-  return *a.dev;
+  a.dev[ctx->device] = d;
+  return d;
 }
 
 fe mp_evaluate(const MPoly& a, const std::vector<fe>& point) {

@@ -17,38 +17,44 @@
 #include <memory>
 #include <vector>
 
+#include <array>
+
 #include "context.hpp"
 #include "fe128.hpp"
 #include "poly.hpp"
 
 namespace sg {
 
-// identity of a constraint's device data: the key of its coset values in a context's domain tables
-uint64_t next_constraint_id();
-
 // device-resident copies of the group x-vectors (trimmed at their degree), uploaded on first
 // use by the prover: the constraints are an input of every proof, like the trace
 struct MPolyDevice {
   int device = -1;
-  uint64_t id = next_constraint_id();
   std::vector<void*> ptr;       // distinct x-polynomials up to a scalar (first non-zero coefficient 1)
   std::vector<uint64_t> len;    // their degree + 1
   std::vector<HPoly> small;     // host copy of those with len <= kSmallPolyMax (else empty)
   std::vector<int32_t> qidx;    // per group (map order): index into ptr, -1 for an all-zero group
   std::vector<fe> scale;        // per group: x-polynomial = scale * ptr[qidx]
-  // (the values of x-polynomial q on a coset are public -- the AIR and the domain -- and live in
-  // the proving context's domain tables under {kDomainMpolyCoset, id, q, L, offset}: per context,
-  // so two contexts never share a table filled on another stream, and sg_ctx_trim frees them)
+  // per distinct x-polynomial: its content digest (BLAKE2b-512 of the coefficients, first 32
+  // bytes). The values of x-polynomial q on a coset are public -- the AIR and the domain -- and
+  // live in the proving context's domain tables under {kDomainMpolyCoset, len, digest, L, offset}:
+  // per context (two contexts never share a table filled on another stream), keyed by content so
+  // a constraint rebuilt for every proof (the reference rebuilds them per sign / verify,
+  // rpsss.rs:46,57) finds the tables of the last build instead of adding a set per build; and
+  // sg_ctx_trim frees them
+  std::vector<std::array<uint64_t, 4>> digest;
   ~MPolyDevice();
 };
 
 // The x-polynomials of a Rescue-Prime AIR (its round-constant interpolants first_0..m-1,
 // second_0..m-1) and their values on the cosets the prover evaluates it on (public, kept like the
-// context's domain tables; the key carries the device).
+// context's domain tables).
 struct RescueXPolys {
-  uint64_t id = next_constraint_id();
+  // what determines the polynomials: RescuePrime::new's parameters (m, capacity, security, N:
+  // the round constants follow from them, rescue_prime.rs:111-128) and the interpolation domain
+  // (omicron, D). Their coset values live in the context's domain tables under
+  // {kDomainRescueCoset, content..., poly, L, offset}: a rebuilt AIR reuses them.
+  std::vector<uint64_t> content;
   std::vector<HPoly> polys;  // first_0 .. first_{m-1}, second_0 .. second_{m-1}
-  // (their coset values: the context's domain tables, {kDomainRescueCoset, id, poly, L, offset})
 };
 
 // A transition constraint built by the native Rescue-Prime AIR (rescue_prime.rs:246-283) also
@@ -68,11 +74,13 @@ struct RescueAirForm {
 struct MPoly {
   uint32_t nvars = 0;                          // key length (0: empty dictionary)
   std::map<std::vector<uint32_t>, HPoly> g;    // exponents of variables 1..nvars-1 -> x coefficients
-  mutable std::shared_ptr<MPolyDevice> dev;    // lazily built (polynomials are immutable once built)
+  // lazily built device copies, one per device (polynomials are immutable once built); a caller
+  // holds the shared_ptr mp_device returns for as long as its kernels may read the copy
+  mutable std::map<int, std::shared_ptr<const MPolyDevice>> dev;
   std::shared_ptr<const RescueAirForm> rescue; // set by the native Rescue-Prime AIR builder only
 };
 
-const MPolyDevice& mp_device(sg_ctx* ctx, const MPoly& a);
+std::shared_ptr<const MPolyDevice> mp_device(sg_ctx* ctx, const MPoly& a);
 
 MPoly mp_constant(const fe& c);
 std::vector<MPoly> mp_variables(uint32_t n);

@@ -232,6 +232,7 @@ std::vector<MPoly> rescue_transition_constraints(sg_ctx* ctx, const sg_rescue& r
     return dpoly_download(ctx, p.p(), p.len);
   };
   auto xp = std::make_shared<RescueXPolys>();
+  xp->content = {rp.m, rp.capacity, rp.security, rp.N, fe_lo(omicron), fe_hi(omicron), D};
   for (size_t i = 0; i < 2 * m; ++i) xp->polys.push_back(interp(i));  // first_0..m-1, second_0..m-1
   std::vector<MPoly> first(m), second(m);
   for (size_t i = 0; i < m; ++i) first[i] = mp_lift(xp->polys[i], 0);
@@ -439,7 +440,9 @@ DPoly transition_values_rescue(sg_ctx* ctx, const RescueAirForm& f, const AirCos
   const int m = f.m;
   const bool kept = ctx->domain_cache_on();
   auto xvals = [&](int idx) -> const fe* {
-    const std::vector<uint64_t> key = {kDomainRescueCoset, f.xp->id, (uint64_t)idx, L, fe_lo(offset), fe_hi(offset)};
+    std::vector<uint64_t> key = {kDomainRescueCoset};
+    key.insert(key.end(), f.xp->content.begin(), f.xp->content.end());
+    key.insert(key.end(), {(uint64_t)idx, L, fe_lo(offset), fe_hi(offset)});
     if (kept)
       if (void* t = ctx->domain_table(key)) return static_cast<const fe*>(t);
     const HPoly& hp = f.xp->polys[(size_t)idx];
@@ -502,12 +505,15 @@ DPoly transition_values(sg_ctx* ctx, const MPoly& tc, const AirCoset& co, const 
   SG_REQUIRE(tc.nvars <= 1 + (uint32_t)nv, "transition constraint has more variables than the point");
   SG_REQUIRE(nv <= kAirMaxVars, "at most 4 registers are supported by the AIR kernel");
   // distinct group x-polynomials (device-resident, uploaded once per constraint) on the coset
-  const MPolyDevice& xd = mp_device(ctx, tc);
+  const std::shared_ptr<const MPolyDevice> xdp = mp_device(ctx, tc);
+  const MPolyDevice& xd = *xdp;
   std::vector<DPoly> Q;        // values computed by this call (when not kept)
   std::vector<const fe*> qp;   // per distinct x-polynomial: its values on the coset
   const bool kept = ctx->domain_cache_on();
   for (size_t q = 0; q < xd.ptr.size(); ++q) {
-    const std::vector<uint64_t> key = {kDomainMpolyCoset, xd.id, q, L, fe_lo(offset), fe_hi(offset)};
+    const auto& dg = xd.digest[q];
+    const std::vector<uint64_t> key = {kDomainMpolyCoset, xd.len[q], dg[0], dg[1], dg[2], dg[3], L, fe_lo(offset),
+                                       fe_hi(offset)};
     if (kept) {
       if (void* t = ctx->domain_table(key)) {
         qp.push_back(static_cast<const fe*>(t));

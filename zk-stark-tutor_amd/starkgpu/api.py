@@ -132,6 +132,12 @@ class Context:
     def trim(self) -> None:
         self.check(self._lib.sg_ctx_trim(self.handle))
 
+    def cached_tables(self) -> Tuple[int, int]:
+        """(public domain / AIR tables, twiddle tables) the context keeps (sg_ctx_cached_tables)."""
+        d, t = ctypes.c_size_t(), ctypes.c_size_t()
+        self.check(self._lib.sg_ctx_cached_tables(self.handle, ctypes.byref(d), ctypes.byref(t)))
+        return d.value, t.value
+
     def hbm_copy_gbs(self, nbytes: int = 1 << 30, iters: int = 10, blocks: int = 0) -> float:
         """Read + write GB/s of the library's dwordx4 streaming copy kernel (best of `iters`)."""
         out = ctypes.c_double()
