@@ -5,11 +5,14 @@
  * two thread_rng draws read from a file so the bytes can be compared with another prover's.
  *
  *   prove_rescue N expansion colinearity security tcd input_lo input_hi randomness.bin proof.bin
- *                [--dist id_file rank nranks]
+ *                [--dist id_file rank nranks [nonce]]
  *
  * With --dist the proof is computed with the FRI domain sharded over `nranks` processes, one GPU
  * each (sg_dist_stark_prove over RCCL, rank r on GPU r): rank 0 writes the RCCL unique id to
- * id_file, the other ranks wait for it; every rank writes the same bytes.
+ * id_file, the other ranks wait for it; every rank writes the same bytes.  `nonce` (any 64-bit
+ * number the launcher picks per run and passes to every rank) is written before the id, and the
+ * other ranks accept only a file carrying it: an id file left over from an earlier run is never
+ * read as this run's id.
  *
  * randomness.bin: 16-byte little-endian (lo, hi) field elements -- num_randomizers x 2 trace
  * randomizer rows (stark.rs:285-301), then max_degree + 1 randomizer coefficients
@@ -37,11 +40,11 @@
   } while (0)
 
 int main(int argc, char** argv) {
-  const int dist = argc == 14 && strcmp(argv[10], "--dist") == 0;
+  const int dist = (argc == 14 || argc == 15) && strcmp(argv[10], "--dist") == 0;
   if (argc != 10 && !dist) {
     fprintf(stderr,
             "usage: %s N expansion colinearity security tcd input_lo input_hi randomness.bin proof.bin"
-            " [--dist id_file rank nranks]\n",
+            " [--dist id_file rank nranks [nonce]]\n",
             argv[0]);
     return 1;
   }
@@ -55,29 +58,35 @@ int main(int argc, char** argv) {
   sg_dist* comm = NULL;
   if (dist) {
     uint8_t id[SG_DIST_ID_BYTES];
+    const uint64_t nonce = argc == 15 ? strtoull(argv[14], NULL, 0) : 0;
     if (rank == 0) {
       CHECK(sg_dist_unique_id(id));
       char tmp[4096];
       snprintf(tmp, sizeof tmp, "%s.tmp", argv[11]);
       FILE* f = fopen(tmp, "wb");
-      if (!f || fwrite(id, 1, sizeof id, f) != sizeof id || fclose(f) != 0 || rename(tmp, argv[11]) != 0) {
+      if (!f || fwrite(&nonce, 1, sizeof nonce, f) != sizeof nonce || fwrite(id, 1, sizeof id, f) != sizeof id ||
+          fclose(f) != 0 || rename(tmp, argv[11]) != 0) {
         fprintf(stderr, "cannot write %s\n", argv[11]);
         return 1;
       }
     } else {
-      FILE* f = NULL;
-      for (int tries = 0; tries < 6000 && !f; ++tries) {  /* up to 60 s for rank 0 */
-        f = fopen(argv[11], "rb");
-        if (!f) {
+      int have = 0;
+      for (int tries = 0; tries < 6000 && !have; ++tries) {  /* up to 60 s for rank 0 */
+        FILE* f = fopen(argv[11], "rb");
+        uint64_t got = 0;
+        if (f) {
+          have = fread(&got, 1, sizeof got, f) == sizeof got && got == nonce && fread(id, 1, sizeof id, f) == sizeof id;
+          fclose(f);
+        }
+        if (!have) {
           struct timespec ts = {0, 10000000};
           nanosleep(&ts, NULL);
         }
       }
-      if (!f || fread(id, 1, sizeof id, f) != sizeof id) {
-        fprintf(stderr, "cannot read %s\n", argv[11]);
+      if (!have) {
+        fprintf(stderr, "no id for this run (nonce %llu) in %s\n", (unsigned long long)nonce, argv[11]);
         return 1;
       }
-      fclose(f);
     }
     CHECK(sg_dist_create(ctx, id, nranks, rank, &comm));
   }

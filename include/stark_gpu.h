@@ -243,12 +243,30 @@ typedef struct {
   int (*all_to_all)(void* user, const void* send, void* recv, size_t bytes);
   /* send = one block of `bytes`; recv = every rank's block in rank order */
   int (*all_gather)(void* user, const void* send, void* recv, size_t bytes);
+  /* optional (may be NULL): called once when a call fails on this rank and the communicator is
+   * poisoned, so the caller can end the peers' pending exchanges (e.g. tear its group down).
+   * The library cannot interrupt a callback that blocks: a caller transport bounds its own waits. */
+  void (*abort)(void* user);
 } sg_dist_transport;
 int sg_dist_unique_id(uint8_t* id /* SG_DIST_ID_BYTES */);                   /* ncclGetUniqueId */
 int sg_dist_create(sg_ctx* ctx, const uint8_t* id, int nranks, int rank, sg_dist** out); /* RCCL */
 int sg_dist_create_transport(sg_ctx* ctx, int nranks, int rank, const sg_dist_transport* t,
                              sg_dist** out);
 void sg_dist_destroy(sg_dist* d);
+/* Failure containment (no reference counterpart; the reference is single-process).  Every
+ * sg_dist_* call below is collective.  When one fails on a rank -- an error of its own, a failing
+ * proof-stream or transport callback, an RCCL asynchronous error, or a host wait that outlasts the
+ * deadline -- the communicator is POISONED on that rank: RCCL's is aborted (ncclCommAbort ends the
+ * collectives in flight, so the peers' waits fail in turn), a caller transport's abort hook runs,
+ * and every later call on it returns SG_ERR_INVALID.  Destroy it and create a new one.
+ * Deadline: SG_DIST_TIMEOUT_S at creation (default 300 s) or sg_dist_set_timeout (per rank). */
+int sg_dist_set_timeout(sg_dist* d, double seconds);
+int sg_dist_poisoned(const sg_dist* d); /* 1 when poisoned */
+/* Collective: the codeword size (log2 elements, <= 0: never) at which a sharded FRI commit hands
+ * over to the single-GPU rounds (default SG_DIST_FRI_TAIL at creation, else 20).  It decides the
+ * collective schedule, so every rank passes the same value; the call all-gathers it and fails
+ * (poisoning) when they differ.  Creation checks the environment's value the same way. */
+int sg_dist_set_fri_tail(sg_dist* d, int log2_elements);
 /* N1 = 2^floor(log2 n / 2), N2 = n / N1; needs N1 >= G and N2 >= 4 G */
 int sg_dist_plan(size_t n, int nranks, size_t* n1, size_t* n2);
 /* fft/ntt.rs:7-49 over the ranks: column shard in, run shard out */

@@ -38,7 +38,8 @@ def _run(tmp_path, N, exp, c, sec, tcd, seed, dist=False):
     rnd = np.array([[v & (2**64 - 1), v >> 64] for v in r], dtype=np.uint64)
     rfile, pfile = tmp_path / "randomness.bin", tmp_path / "proof.bin"
     rnd.tofile(rfile)
-    extra = ["--dist", str(tmp_path / "rccl.id"), "0", "1"] if dist else []
+    # a fresh id path per run and a per-run nonce: a stale id file is never read as this run's
+    extra = ["--dist", str(tmp_path / "rccl.id"), "0", "1", str(int.from_bytes(os.urandom(7), "big"))] if dist else []
     res = subprocess.run([BIN, str(N), str(exp), str(c), str(sec), str(tcd), str(inp & (2**64 - 1)), str(inp >> 64),
                           str(rfile), str(pfile)] + extra, capture_output=True, text=True, timeout=300)
     assert res.returncode == 0, res.stderr

@@ -267,10 +267,9 @@ def _native_checks(nd, ctx, world, rank, logn, gather):
     # (two rounds) ends while still sharded and gathers the last codeword.  SG_DIST_FRI_TAIL: the
     # codeword size at which the sharded rounds hand over to the single-GPU commit (0: never
     # early; logn - 2: after two sharded rounds, with several runs per rank left; logn: at once)
-    old_tail = os.environ.get("SG_DIST_FRI_TAIL")
     try:
-        for tail in ("0", str(logn - 2), str(logn)):
-            os.environ["SG_DIST_FRI_TAIL"] = tail
+        for tail in (0, logn - 2, logn):
+            nd.set_fri_tail(tail)  # collective: every rank sets the same hand-over size
             for c in (16, n // 16):
                 ref = sg.IndependentProofStream()
                 sg.FRI(sg.generator(), root, n, 8, c, ctx=ctx).commit(cw_full, ref)
@@ -285,10 +284,7 @@ def _native_checks(nd, ctx, world, rank, logn, gather):
                 assert gtop == top, f"fri prove top indices c={c} tail={tail}"
                 assert got.digest() == ref.digest(), f"fri prove stream c={c} tail={tail}"
     finally:
-        if old_tail is None:
-            os.environ.pop("SG_DIST_FRI_TAIL", None)
-        else:
-            os.environ["SG_DIST_FRI_TAIL"] = old_tail
+        nd.set_fri_tail(20)
 
 
 def test_native_dist_world1_rccl():
@@ -477,12 +473,9 @@ def _stark_checks(nd, world, rank, tmp, cases, gather):
             bnd = [(a, b, int(v)) for (a, b, v) in json.load(f)]
         trace = np.load(os.path.join(tmp, "trace%d.npy" % k))
         tr, rc = np.load(os.path.join(tmp, "tr%d.npy" % k)), np.load(os.path.join(tmp, "rc%d.npy" % k))
-        # small domains: every FRI round sharded (SG_DIST_FRI_TAIL=0); C4: the default hand-over
-        os.environ["SG_DIST_FRI_TAIL"] = "0" if N < 1000 else "20"
-        try:
-            got = st.prove(trace, air, bnd, sg.IndependentProofStream(), tr, rc, dist=nd)
-        finally:
-            os.environ.pop("SG_DIST_FRI_TAIL", None)
+        # small domains: every FRI round sharded (hand-over size 0); C4: the default hand-over
+        nd.set_fri_tail(0 if N < 1000 else 20)
+        got = st.prove(trace, air, bnd, sg.IndependentProofStream(), tr, rc, dist=nd)
         ok.append((k, got == open(os.path.join(tmp, "proof%d.bin" % k), "rb").read()))
     flags = gather(ok)
     assert all(f for per_rank in flags for (_, f) in per_rank), f"world {world}: sharded proof bytes differ: {flags}"
@@ -534,3 +527,121 @@ def test_dist_stark_prove_one_gpu_host_transport(stark_reference, world, cases):
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     mp.spawn(_stark_worker, args=(world, port, stark_reference, cases), nprocs=world, join=True)
+
+
+# ----------------------------------------------------------------- failure containment
+
+class _FailingStream(o.IndependentProofStream):
+    """A proof stream whose Fiat-Shamir callback fails: the prover has issued collectives by then
+    (the randomizer LDE's all-to-all, the forests' run-root all-gathers)."""
+
+    def fiat_shamir_prover(self, num_bytes):
+        raise RuntimeError("injected proof-stream failure")
+
+
+def _load_case(tmp, k):
+    N, exp, c, sec, tcd = STARK_CASES[k]
+    with open(os.path.join(tmp, "bnd%d.json" % k)) as f:
+        bnd = [(a, b, int(v)) for (a, b, v) in json.load(f)]
+    return (N, exp, c, sec, tcd), bnd, np.load(os.path.join(tmp, "trace%d.npy" % k)), \
+        np.load(os.path.join(tmp, "tr%d.npy" % k)), np.load(os.path.join(tmp, "rc%d.npy" % k))
+
+
+def test_dist_failure_world1_rccl_poisons(stark_reference):
+    """A call that fails after issuing collectives poisons the RCCL communicator (ncclCommAbort):
+    the prove returns an error, sg_dist_poisoned reports it, and every later call fails with
+    SG_ERR_INVALID at once instead of issuing collectives out of step with the peers."""
+    import starkgpu as sg
+    from starkgpu import dist as D
+    ctx = sg.Context(0)
+    nd = D.NativeDist(ctx, transport="rccl")
+    try:
+        (N, exp, c, sec, tcd), bnd, trace, tr, rc = _load_case(stark_reference, 1)
+        st = sg.Stark(exp, c, sec, 2, N + 1, tcd, ctx=ctx)
+        air = sg.RescuePrime(2, 1, sec, N, ctx=ctx).transition_constraints(st.omicron, st.omicron_domain_length)
+        assert not nd.poisoned
+        with pytest.raises(RuntimeError, match="injected"):
+            st.prove(trace, air, bnd, _FailingStream(), tr, rc, dist=nd)
+        assert nd.poisoned
+        with pytest.raises(sg.StarkGpuError) as ei:
+            st.prove(trace, air, bnd, sg.IndependentProofStream(), tr, rc, dist=nd)
+        assert ei.value.code == -1 and "poisoned" in str(ei.value)
+        with pytest.raises(sg.StarkGpuError):
+            nd.set_fri_tail(20)
+        # a new communicator on the same context works again and proves the expected bytes
+        nd.close()
+        nd = D.NativeDist(ctx, transport="rccl")
+        got = st.prove(trace, air, bnd, sg.IndependentProofStream(), tr, rc, dist=nd)
+        assert got == open(os.path.join(stark_reference, "proof1.bin"), "rb").read()
+    finally:
+        nd.close()
+
+
+def _failure_worker(rank, world, port, tmp):
+    import time
+    from datetime import timedelta
+    import torch.distributed as dist
+    import starkgpu as sg
+    from starkgpu import dist as D
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=timedelta(seconds=60))
+    aborted = []
+
+    def on_abort():  # poisoned on this rank: close its pairs so the peers' exchanges fail now
+        aborted.append(time.time())
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+    out = {"rank": rank}
+    try:
+        ctx = sg.Context(0)
+        nd = D.NativeDist(ctx, transport="host", abort=on_abort)
+        (N, exp, c, sec, tcd), bnd, trace, tr, rc = _load_case(tmp, 1)
+        st = sg.Stark(exp, c, sec, 2, N + 1, tcd, ctx=ctx)
+        air = sg.RescuePrime(2, 1, sec, N, ctx=ctx).transition_constraints(st.omicron, st.omicron_domain_length)
+        stream = _FailingStream() if rank == world - 1 else sg.IndependentProofStream()
+        t0 = time.time()
+        try:
+            st.prove(trace, air, bnd, stream, tr, rc, dist=nd)
+            out["result"] = "ok"
+        except Exception as e:  # noqa: BLE001 - recorded for the parent
+            out["result"] = type(e).__name__ + ": " + str(e)
+        out["seconds"] = time.time() - t0
+        out["poisoned"] = nd.poisoned
+        out["aborted"] = bool(aborted)
+        try:
+            nd.set_fri_tail(20)
+            out["after"] = "ok"
+        except Exception as e:  # noqa: BLE001
+            out["after"] = str(e)
+        nd.close()
+    finally:
+        with open(os.path.join(tmp, "fail_rank%d.json" % rank), "w") as f:
+            json.dump(out, f)
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+def test_dist_failure_one_rank_host_transport(stark_reference):
+    """World 2 on this GPU over the host transport (gloo): rank 1 alone fails mid-prove (its
+    Fiat-Shamir callback raises after the commitments' collectives).  Both ranks return an error
+    well within the deadline -- rank 1 from its callback, rank 0 from the exchange its peer left --
+    both communicators are poisoned, later calls fail at once, and no process is left blocked."""
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    for r in range(2):
+        p = os.path.join(stark_reference, "fail_rank%d.json" % r)
+        if os.path.exists(p):
+            os.remove(p)
+    mp.spawn(_failure_worker, args=(2, port, stark_reference), nprocs=2, join=True)
+    res = [json.load(open(os.path.join(stark_reference, "fail_rank%d.json" % r))) for r in range(2)]
+    for r in res:
+        assert r["result"] != "ok", res
+        assert r["poisoned"] and r["aborted"], res
+        assert "poisoned" in r["after"], res
+        assert r["seconds"] < 60, res
+    assert "injected" in res[1]["result"], res

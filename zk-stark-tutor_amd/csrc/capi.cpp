@@ -3,6 +3,9 @@
 // flow (fri.rs, merkle_root.rs, fft/ntt.rs) around the gfx950 kernels.
 #include <hip/hip_runtime.h>
 
+#include <chrono>
+#include <thread>
+
 #include <algorithm>
 #include <atomic>
 #include <cstring>
@@ -104,16 +107,16 @@ const fe* sg_ctx::pow_table(const fe& root, uint64_t count) {
     SG_HIP(hipMemcpyAsync(dA.get(), A.data(), na * sizeof(fe), hipMemcpyHostToDevice, stream));
     SG_HIP(hipMemcpyAsync(dB.get(), B.data(), nb * sizeof(fe), hipMemcpyHostToDevice, stream));
     SG_HIP(launch_pow_table(reinterpret_cast<fe*>(table), dA.as<fe>(), dB.as<fe>(), count, stream));
-    SG_HIP(hipStreamSynchronize(stream));  // A/B return to the pool below
+    host_wait(this, stream);  // A/B return to the pool below
   }
-  SG_HIP(hipStreamSynchronize(stream));
+  host_wait(this, stream);
   pow_tables[key] = PowTable{table, count};
   return reinterpret_cast<const fe*>(table);
 }
 
 void* sg_ctx::staging(int slot, size_t bytes) {
   if (staging_bytes[slot] < bytes) {
-    SG_HIP(hipStreamSynchronize(stream));  // the old buffer may still be in flight
+    host_wait(this, stream);  // the old buffer may still be in flight
     if (staging_ptr[slot]) (void)hipHostFree(staging_ptr[slot]);
     staging_ptr[slot] = nullptr;
     staging_bytes[slot] = 0;
@@ -133,8 +136,8 @@ void sg_ctx::domain_table_put_bounded(const std::vector<uint64_t>& key, void* p)
   domain_table_put(key, p);
   bounded_keys.push_back(key);
   if (bounded_keys.size() <= kBoundedTables) return;
-  SG_HIP(hipStreamSynchronize(stream));  // queued work may still read the oldest table
-  SG_HIP(hipStreamSynchronize(side));
+  host_wait(this, stream);  // queued work may still read the oldest table
+  host_wait(this, side);
   auto it = domain_tables.find(bounded_keys.front());
   if (it != domain_tables.end()) {
     (void)hipFree(it->second);
@@ -166,7 +169,7 @@ const fe* sg_ctx::stage_twiddles(const fe& root, int logn) {
     SG_HIP(hipMemcpyAsync(tail, A, 4096 * sizeof(fe), hipMemcpyDeviceToDevice, stream));
     SG_HIP(hipMemcpyAsync(tail + 4096, B, nb * sizeof(fe), hipMemcpyDeviceToDevice, stream));
   }
-  SG_HIP(hipStreamSynchronize(stream));
+  host_wait(this, stream);
   stage_tables[key] = t;
   return reinterpret_cast<const fe*>(t);
 }
@@ -197,7 +200,7 @@ void ntt_run(sg_ctx* ctx, fe* const* out, const fe* const* in, int batch, uint64
   }
   SG_HIP(launch_ntt_fused(out, in, batch, n_in, logn, tw, sA, sB, skip, post, ctx->stream));
   // async mode (sg_ctx_set_async): stream-ordered, the caller synchronizes
-  if (!ctx->async_dev) SG_HIP(hipStreamSynchronize(ctx->stream));
+  if (!ctx->async_dev) host_wait(ctx, ctx->stream);
 }
 
 // out (device, next_pow2(n_in)) = ntt(root, in) ; in may alias nothing in out
@@ -291,12 +294,12 @@ extern "C" int sg_ctx_set_async(sg_ctx* ctx, int enable) {
 }
 
 extern "C" int sg_ctx_synchronize(sg_ctx* ctx) {
-  return guard(ctx, [&] { SG_HIP(hipStreamSynchronize(ctx->stream)); });
+  return guard(ctx, [&] { host_wait(ctx, ctx->stream); });
 }
 
 extern "C" int sg_ctx_profile(sg_ctx* ctx, int enable) {
   return guard(ctx, [&] {
-    SG_HIP(hipStreamSynchronize(ctx->stream));
+    host_wait(ctx, ctx->stream);
     ctx->prof.drain();
     ctx->prof.totals.clear();
     ctx->profiling = enable != 0;
@@ -309,7 +312,7 @@ extern "C" int sg_ctx_profile_only(sg_ctx* ctx, const char* kernel) {
 
 extern "C" int sg_ctx_profile_report(sg_ctx* ctx, char* buf, size_t cap, size_t* len) {
   return guard(ctx, [&] {
-    SG_HIP(hipStreamSynchronize(ctx->stream));
+    host_wait(ctx, ctx->stream);
     ctx->prof.drain();
     std::string js = "{";
     bool first = true;
@@ -337,8 +340,8 @@ extern "C" void* sg_ctx_stream(sg_ctx* ctx) { return ctx ? (void*)ctx->stream : 
 extern "C" int sg_ctx_trim(sg_ctx* ctx) {
   return guard(ctx, [&] {
     SG_REQUIRE(ctx, "null context");
-    SG_HIP(hipStreamSynchronize(ctx->stream));  // nothing queued may still read a table freed here
-    SG_HIP(hipStreamSynchronize(ctx->side));
+    host_wait(ctx, ctx->stream);  // nothing queued may still read a table freed here
+    host_wait(ctx, ctx->side);
     ctx->trim();
     for (auto& kv : ctx->pow_tables) (void)hipFree(kv.second.ptr);
     ctx->pow_tables.clear();
@@ -439,7 +442,7 @@ extern "C" int sg_intt_dev(sg_ctx* ctx, sg_fe root, const sg_fe* d_in, size_t n_
     if (n_in < 2) {
       // fft/ntt.rs:56-58: returned unchanged
       if (n_in) SG_HIP(hipMemcpyAsync(d_out, d_in, n_in * sizeof(fe), hipMemcpyDeviceToDevice, ctx->stream));
-      SG_HIP(hipStreamSynchronize(ctx->stream));
+      host_wait(ctx, ctx->stream);
       return;
     }
     uint64_t n = next_pow2(n_in);
@@ -502,7 +505,7 @@ void host_roundtrip(sg_ctx* ctx, const sg_fe* in, size_t n_in, sg_fe* out, size_
   if (n_in) SG_HIP(hipMemcpyAsync(din.get(), in, n_in * sizeof(fe), hipMemcpyHostToDevice, ctx->stream));
   dev_fn(din.as<sg_fe>(), dout.as<sg_fe>());
   if (n_out) SG_HIP(hipMemcpyAsync(out, dout.get(), n_out * sizeof(fe), hipMemcpyDeviceToHost, ctx->stream));
-  SG_HIP(hipStreamSynchronize(ctx->stream));
+  host_wait(ctx, ctx->stream);
 }
 void throw_if(int rc, sg_ctx* ctx) {
   if (rc != SG_OK) throw Error{rc, ctx->last_error};
@@ -546,15 +549,34 @@ extern "C" int sg_fast_coset_evaluate(sg_ctx* ctx, sg_fe generator, uint64_t roo
 
 namespace sg {
 
+void host_wait(sg_ctx* ctx, hipStream_t s) {
+  if (!ctx->watch) {
+    SG_HIP(hipStreamSynchronize(s));
+    return;
+  }
+  const auto t0 = std::chrono::steady_clock::now();
+  for (uint32_t spins = 0;; ++spins) {
+    const hipError_t q = hipStreamQuery(s);
+    if (q == hipSuccess) return;
+    if (q != hipErrorNotReady) SG_HIP(q);
+    if ((spins & 63) == 0)
+      ctx->watch(std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+    if (spins < 4096) __builtin_ia32_pause();
+    else std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
+}
+
 // Spin until the tree kernels have published `batch` roots (flag == seq) in slots
 // slot0.. .  `s` (the stream the trees run on) is queried now and then so a
 // finished-without-flag stream or a kernel error surfaces instead of spinning forever.
 void wait_roots(sg_ctx* ctx, int batch, uint64_t seq, int slot0, hipStream_t s) {
   volatile uint64_t* flags = ctx->pinned_roots + sg_ctx::kFlagIndex + slot0;
+  const auto t0 = std::chrono::steady_clock::now();
   for (int b = 0; b < batch; ++b) {
     uint32_t spins = 0;
     while (flags[b] != seq) {
       if ((++spins & 255) == 0) {
+        if (ctx->watch) ctx->watch(std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
         hipError_t q = hipStreamQuery(s);
         if (q == hipSuccess) {
           if (flags[b] != seq) throw Error{SG_ERR_HIP, "tree root was not published"};
@@ -657,7 +679,7 @@ void gather_digests(sg_ctx* ctx, const sg_tree* t, const std::vector<uint64_t>& 
   SG_HIP(launch_gather_digests(t->buf.as<uint64_t>(), di.as<uint64_t>(), dout.as<uint64_t>(), (uint32_t)idx.size(),
                                ctx->stream));
   SG_HIP(hipMemcpyAsync(out, dout.get(), idx.size() * 64, hipMemcpyDeviceToHost, ctx->stream));
-  SG_HIP(hipStreamSynchronize(ctx->stream));
+  host_wait(ctx, ctx->stream);
 }
 }  // namespace sg
 
@@ -943,17 +965,17 @@ void TailWriter::flush(sg_ctx* ctx, const sg_proof_stream* ps) {
     uint8_t* dst = st.append_block(bytes, offs, field);
     if (pinned) {
       SG_HIP(hipMemcpyAsync(dst, dout.get(), bytes, hipMemcpyDeviceToHost, ctx->stream));
-      SG_HIP(hipStreamSynchronize(ctx->stream));
+      host_wait(ctx, ctx->stream);
     } else {
       uint8_t* stg = static_cast<uint8_t*>(ctx->staging(1, bytes));
       SG_HIP(hipMemcpyAsync(stg, dout.get(), bytes, hipMemcpyDeviceToHost, ctx->stream));
-      SG_HIP(hipStreamSynchronize(ctx->stream));
+      host_wait(ctx, ctx->stream);
       memcpy(dst, stg, bytes);
     }
   } else {
     uint8_t* stg = static_cast<uint8_t*>(ctx->staging(1, bytes));
     SG_HIP(hipMemcpyAsync(stg, dout.get(), bytes, hipMemcpyDeviceToHost, ctx->stream));
-    SG_HIP(hipStreamSynchronize(ctx->stream));
+    host_wait(ctx, ctx->stream);
     for (const TailItem& it : items)
       push_obj(ps, (uint8_t)it.code, stg + it.dst + 9, (it.code == SG_OBJ_PATH ? 72 : 16) * (size_t)it.count);
   }
@@ -1083,7 +1105,7 @@ void fri_commit_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, co
     std::vector<fe> last(last_len);
     SG_HIP(hipMemcpyAsync(roots.data(), droots.get(), roots.size(), hipMemcpyDeviceToHost, ctx->stream));
     SG_HIP(hipMemcpyAsync(last.data(), st.cw.back(), last_len * sizeof(fe), hipMemcpyDeviceToHost, ctx->stream));
-    SG_HIP(hipStreamSynchronize(ctx->stream));
+    host_wait(ctx, ctx->stream);
     for (size_t r = 0; r < rounds; ++r) {
       memcpy(trees[r]->root, roots.data() + 64 * r, 64);
       st.trees.push_back(std::move(trees[r]));
@@ -1129,7 +1151,7 @@ void fri_commit_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, co
     fold.K = to_mont(fe_mul(fe_mul(alpha, plan[r].oinv), inv2));
   }
   // push last codeword (fri.rs:166)
-  SG_HIP(hipStreamSynchronize(ctx->stream));
+  host_wait(ctx, ctx->stream);
   ObjWriter w{ps};
   uint8_t* payload = w.begin(SG_OBJ_CODEWORD, last_len * 16);
   for (uint64_t i = 0; i < last_len; ++i) put_u128_be_at(payload + 16 * i, last[i]);
@@ -1315,7 +1337,7 @@ extern "C" int sg_ntt_rows_dev(sg_ctx* ctx, sg_fe root, const sg_fe* d_in, size_
       const fe* i = in + r0 * n_in;
       SG_HIP(launch_ntt_fused(&o, &i, cnt, n_in, logn, tw, nullptr, nullptr, skip, nullptr, ctx->stream, n_in, n));
     }
-    SG_HIP(hipStreamSynchronize(ctx->stream));
+    host_wait(ctx, ctx->stream);
   });
 }
 
@@ -1328,7 +1350,7 @@ extern "C" int sg_scale_dev(sg_ctx* ctx, sg_fe* d_data, size_t n, sg_fe c) {
     DevBuf dc(ctx, sizeof(fe));
     SG_HIP(hipMemcpyAsync(dc.get(), &cm, sizeof(fe), hipMemcpyHostToDevice, ctx->stream));
     SG_HIP(launch_scale_const(reinterpret_cast<fe*>(d_data), n, dc.as<fe>(), ctx->stream));
-    SG_HIP(hipStreamSynchronize(ctx->stream));
+    host_wait(ctx, ctx->stream);
   });
 }
 
@@ -1346,7 +1368,7 @@ extern "C" int sg_mul_pow_dev(sg_ctx* ctx, sg_fe base, sg_fe* d_data, size_t row
     const fe* T[3];
     pow_tables3(ctx, b, T);
     SG_HIP(launch_mul_pow(reinterpret_cast<fe*>(d_data), rows, cols, a0, a1, b0, b1, T[0], T[1], T[2], ctx->stream));
-    SG_HIP(hipStreamSynchronize(ctx->stream));
+    host_wait(ctx, ctx->stream);
   });
 }
 
@@ -1358,7 +1380,7 @@ extern "C" int sg_transpose_dev(sg_ctx* ctx, const sg_fe* d_in, sg_fe* d_out, si
     SG_REQUIRE(!ranges_overlap(reinterpret_cast<const fe*>(d_in), total, reinterpret_cast<const fe*>(d_out), total),
                "transpose: output must not alias the input");
     SG_HIP(launch_swap01(reinterpret_cast<const fe*>(d_in), reinterpret_cast<fe*>(d_out), A, B, C, ctx->stream));
-    SG_HIP(hipStreamSynchronize(ctx->stream));
+    host_wait(ctx, ctx->stream);
   });
 }
 
@@ -1381,7 +1403,7 @@ extern "C" int sg_merkle_forest_dev(sg_ctx* ctx, const sg_fe* d_leaves, size_t r
       uint64_t* tr = f->buf.as<uint64_t>() + r0 * per;
       SG_HIP(launch_merkle_tree(&lv, &tr, cnt, run, nullptr, ctx->stream, run, per, 0));
     }
-    SG_HIP(hipStreamSynchronize(ctx->stream));
+    host_wait(ctx, ctx->stream);
     *out = f.release();
   });
 }
@@ -1394,7 +1416,7 @@ extern "C" int sg_forest_roots_dev(sg_ctx* ctx, const sg_forest* f, uint8_t* d_r
     const uint64_t root_off = (2 * f->run - 2) * 8;
     SG_HIP(launch_gather_roots(f->buf.as<uint64_t>(), per, root_off, reinterpret_cast<uint64_t*>(d_roots), f->runs,
                                ctx->stream));
-    SG_HIP(hipStreamSynchronize(ctx->stream));
+    host_wait(ctx, ctx->stream);
   });
 }
 
@@ -1411,7 +1433,7 @@ extern "C" int sg_forest_open(sg_ctx* ctx, const sg_forest* f, size_t tree, size
       SG_HIP(launch_gather_digests(f->buf.as<uint64_t>(), di.as<uint64_t>(), dout.as<uint64_t>(),
                                    (uint32_t)idx.size(), ctx->stream));
       SG_HIP(hipMemcpyAsync(path, dout.get(), idx.size() * 64, hipMemcpyDeviceToHost, ctx->stream));
-      SG_HIP(hipStreamSynchronize(ctx->stream));
+      host_wait(ctx, ctx->stream);
     }
     if (path_len) *path_len = idx.size();
   });
@@ -1435,7 +1457,7 @@ extern "C" int sg_merkle_top_dev(sg_ctx* ctx, const uint8_t* d_digests, size_t n
     uint64_t* tr = t->buf.as<uint64_t>();
     uint64_t* root_dev = ctx->pinned_roots_dev;
     if (n > 1) SG_HIP(launch_merkle_tree(nullptr, &tr, 1, n, &root_dev, ctx->stream, 0, 0, 1));
-    SG_HIP(hipStreamSynchronize(ctx->stream));
+    host_wait(ctx, ctx->stream);
     if (n > 1)
       memcpy(t->root, ctx->pinned_roots, 64);
     else
@@ -1469,6 +1491,6 @@ extern "C" int sg_fri_fold_runs_dev(sg_ctx* ctx, sg_fe omega, sg_fe offset, sg_f
                "fold: output must not alias the input");
     SG_HIP(launch_fri_fold_runs(reinterpret_cast<fe*>(d_out), reinterpret_cast<const fe*>(d_in), half, run, run_stride,
                                 run_off, T[0], T[1], T[2], K, ctx->stream));
-    SG_HIP(hipStreamSynchronize(ctx->stream));
+    host_wait(ctx, ctx->stream);
   });
 }

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <deque>
+#include <functional>
 #include <map>
 #include <string>
 #include <utility>
@@ -67,6 +68,11 @@ struct sg_ctx {
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   std::string last_error;
+  // set while a communicator call runs on this context (dist.cpp DistWatch): every host wait
+  // (sg::host_wait, the tree-root spin) polls it; it throws -- after aborting the communicator --
+  // on an RCCL asynchronous error or when one wait outlasts the communicator's deadline (the
+  // argument: seconds this wait has lasted)
+  std::function<void(double)> watch;
   // pool: rounded size -> free pointers
   std::multimap<size_t, void*> free_bufs;
   size_t pooled_bytes = 0;

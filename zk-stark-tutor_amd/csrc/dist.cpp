@@ -28,8 +28,10 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
+#include <string>
 #include <vector>
 
 #include "dist.hpp"
@@ -46,6 +48,17 @@ struct sg_dist {
   void* hsend = nullptr;
   void* hrecv = nullptr;
   size_t hsend_bytes = 0, hrecv_bytes = 0;
+  // failure containment: a call that fails on this rank may leave its peers inside (or on their
+  // way into) a collective this rank never joins.  The communicator is then poisoned: RCCL's is
+  // aborted (ncclCommAbort ends the collectives in flight), a caller transport gets its abort hook,
+  // and every later call returns SG_ERR_INVALID.  A host wait that outlasts timeout_s
+  // (SG_DIST_TIMEOUT_S, default 300 s) or an RCCL asynchronous error poisons it the same way.
+  bool dead = false;
+  std::string dead_reason;
+  double timeout_s = 300.0;
+  // codeword size (log2 elements) at which a sharded FRI commit hands over to the single-GPU
+  // rounds: part of the collective schedule, so it is agreed by all ranks (sg_dist_set_fri_tail)
+  int fri_tail_log = 20;
   ~sg_dist() {
     if (comm) (void)ncclCommDestroy(comm);
     if (hsend) (void)hipHostFree(hsend);
@@ -54,6 +67,65 @@ struct sg_dist {
 };
 
 namespace sg {
+
+void dist_poison(sg_dist* d, const std::string& why) {
+  if (d->dead) return;
+  d->dead = true;
+  d->dead_reason = why;
+  if (d->comm) {
+    (void)ncclCommAbort(d->comm);  // ends the collectives in flight on this rank
+    d->comm = nullptr;
+  }
+  if (d->staged && d->tr.abort) d->tr.abort(d->tr.user);
+}
+
+int dist_run(sg_dist* d, const std::function<void()>& body) {
+  sg_ctx* ctx = d ? d->ctx : nullptr;
+  if (d && ctx && d->dead) {
+    ctx->last_error = "communicator poisoned by an earlier failure: " + d->dead_reason;
+    return SG_ERR_INVALID;
+  }
+  struct WatchScope {
+    sg_ctx* ctx;
+    WatchScope(sg_dist* dd, sg_ctx* c) : ctx(c) {
+      if (!c) return;
+      c->watch = [dd](double waited_s) {
+        if (dd->comm) {
+          ncclResult_t e = ncclSuccess;
+          if (ncclCommGetAsyncError(dd->comm, &e) == ncclSuccess && e != ncclSuccess && e != ncclInProgress) {
+            const std::string m = std::string("RCCL asynchronous error: ") + ncclGetErrorString(e);
+            dist_poison(dd, m);
+            throw Error{SG_ERR_HIP, m};
+          }
+        }
+        if (waited_s > dd->timeout_s) {
+          const std::string m = "a wait on this communicator outlasted its deadline (SG_DIST_TIMEOUT_S = " +
+                                std::to_string(dd->timeout_s) + " s): a peer failed or stalled";
+          dist_poison(dd, m);
+          throw Error{SG_ERR_HIP, m};
+        }
+      };
+    }
+    ~WatchScope() {
+      if (ctx) ctx->watch = nullptr;
+    }
+  } watch(d, ctx);
+  return guard(ctx, [&] {
+    if (!d || !ctx) throw Error{SG_ERR_INVALID, "null communicator"};
+    set_device(ctx);
+    try {
+      body();
+    } catch (const Error& e) {
+      // before guard drains the stream: collectives queued on it may wait for peers forever
+      dist_poison(d, e.msg);
+      throw;
+    } catch (...) {
+      dist_poison(d, "a call failed on this rank");
+      throw;
+    }
+  });
+}
+
 namespace {
 
 #define SG_NCCL(call)                                                                          \
@@ -92,7 +164,7 @@ void exchange(sg_dist* d, const void* dsend, void* drecv, size_t bytes, bool a2a
   grow_pinned(d->hsend, d->hsend_bytes, sbytes);
   grow_pinned(d->hrecv, d->hrecv_bytes, total);
   SG_HIP(hipMemcpyAsync(d->hsend, dsend, sbytes, hipMemcpyDeviceToHost, ctx->stream));
-  SG_HIP(hipStreamSynchronize(ctx->stream));
+  host_wait(ctx, ctx->stream);
   const int rc = a2a ? d->tr.all_to_all(d->tr.user, d->hsend, d->hrecv, bytes)
                      : d->tr.all_gather(d->tr.user, d->hsend, d->hrecv, bytes);
   if (rc != 0) throw Error{SG_ERR_CALLBACK, a2a ? "all_to_all transport callback failed"
@@ -254,7 +326,7 @@ void dist_forest_finish(sg_dist* d, PendingForest& pf, uint8_t root[64], Sharded
   }
   if (m == 1) {
     SG_HIP(hipMemcpyAsync(root, ordered.get(), 64, hipMemcpyDeviceToHost, ctx->stream));
-    SG_HIP(hipStreamSynchronize(ctx->stream));
+    host_wait(ctx, ctx->stream);
     if (keep) keep->forest = std::move(pf.forest);
     return;
   }
@@ -263,7 +335,7 @@ void dist_forest_finish(sg_dist* d, PendingForest& pf, uint8_t root[64], Sharded
   uint64_t* tr = top.as<uint64_t>();
   uint64_t* root_dev = ctx->pinned_roots_dev;
   SG_HIP(launch_merkle_tree(nullptr, &tr, 1, m, &root_dev, ctx->stream, 0, 0, 1));
-  SG_HIP(hipStreamSynchronize(ctx->stream));
+  host_wait(ctx, ctx->stream);
   memcpy(root, ctx->pinned_roots, 64);
   if (keep) {
     keep->forest = std::move(pf.forest);
@@ -322,8 +394,7 @@ void dist_fri_commit(sg_dist* d, const sg_fri* f, const fe* runs, uint64_t n, co
   // once the whole codeword is small (<= 2^SG_DIST_FRI_TAIL elements, default 2^20 = 16 MiB) the
   // remaining rounds are latency-bound: every rank gathers it and continues with the single-GPU
   // commit instead of paying a forest, a collective and a host round trip per sharded round
-  const char* te = getenv("SG_DIST_FRI_TAIL");
-  const int tail_log = te ? atoi(te) : 20;
+  const int tail_log = d->fri_tail_log;
   const uint64_t tail_below = tail_log <= 0 ? 0 : (uint64_t)1 << std::min(tail_log, 62);
   bool all_sharded = false;
   while (k1s > 1 && r < rounds) {
@@ -373,7 +444,7 @@ void dist_fri_commit(sg_dist* d, const sg_fri* f, const fe* runs, uint64_t n, co
     const uint64_t len = d->G * k1s * R;
     std::vector<fe> last(len);
     SG_HIP(hipMemcpyAsync(last.data(), nat.get(), len * sizeof(fe), hipMemcpyDeviceToHost, ctx->stream));
-    SG_HIP(hipStreamSynchronize(ctx->stream));
+    host_wait(ctx, ctx->stream);
     std::vector<uint8_t> payload;
     payload.reserve(len * 16);
     for (auto& v : last) put_u128_be(payload, v);
@@ -484,7 +555,7 @@ void dist_open_batch(sg_dist* d, uint64_t R, uint64_t n2, std::vector<OpenReq>& 
     }
     if (nvals) SG_HIP(hipMemcpyAsync(vals.data(), dV.get(), nvals * sizeof(fe), hipMemcpyDeviceToHost, ctx->stream));
     if (ndig) SG_HIP(hipMemcpyAsync(dig.data(), dD.get(), ndig * 64, hipMemcpyDeviceToHost, ctx->stream));
-    SG_HIP(hipStreamSynchronize(ctx->stream));
+    host_wait(ctx, ctx->stream);
   }
   // the owned slots of every sharded request, one all-gather
   std::vector<uint8_t> all;
@@ -506,7 +577,7 @@ void dist_open_batch(sg_dist* d, uint64_t R, uint64_t n2, std::vector<OpenReq>& 
     exchange(d, dsend.get(), drecv.get(), qtot * slot, /*a2a=*/false);
     all.resize((size_t)d->G * qtot * slot);
     SG_HIP(hipMemcpyAsync(all.data(), drecv.get(), all.size(), hipMemcpyDeviceToHost, ctx->stream));
-    SG_HIP(hipStreamSynchronize(ctx->stream));
+    host_wait(ctx, ctx->stream);
   }
   size_t base = 0;
   for (size_t j = 0; j < reqs.size(); ++j) {
@@ -614,11 +685,6 @@ void dist_fri_prove(sg_dist* d, const sg_fri* f, const fe* runs, uint64_t n, con
   if (extra) extra(top);
 }
 
-sg_dist* checked(sg_dist* d) {
-  if (!d || !d->ctx) throw Error{SG_ERR_INVALID, "null communicator"};
-  return d;
-}
-
 sg_ctx* dist_ctx(sg_dist* d) { return d->ctx; }
 int dist_world(const sg_dist* d) { return d->G; }
 void dist_plan(uint64_t n, int G, uint64_t& n1, uint64_t& n2) { plan(n, G, n1, n2); }
@@ -636,39 +702,92 @@ extern "C" int sg_dist_unique_id(uint8_t* id) {
   });
 }
 
+namespace {
+
+// settings every rank must share, read from the environment at creation
+void dist_defaults(sg_dist* d) {
+  if (const char* t = getenv("SG_DIST_TIMEOUT_S")) {
+    const double v = atof(t);
+    if (v > 0) d->timeout_s = v;
+  }
+  if (const char* te = getenv("SG_DIST_FRI_TAIL")) d->fri_tail_log = atoi(te);
+}
+
+// all-gathers v over the communicator; every rank throws the same error when the values differ
+void agree(sg_dist* d, int64_t v, const char* what) {
+  sg_ctx* ctx = d->ctx;
+  DevBuf one(ctx, sizeof(int64_t)), all(ctx, sizeof(int64_t) * (size_t)d->G);
+  std::vector<int64_t> h((size_t)d->G);
+  SG_HIP(hipMemcpyAsync(one.get(), &v, sizeof(v), hipMemcpyHostToDevice, ctx->stream));
+  exchange(d, one.get(), all.get(), sizeof(int64_t), /*a2a=*/false);
+  SG_HIP(hipMemcpyAsync(h.data(), all.get(), h.size() * sizeof(int64_t), hipMemcpyDeviceToHost, ctx->stream));
+  host_wait(ctx, ctx->stream);
+  for (int64_t x : h)
+    if (x != h[0]) throw Error{SG_ERR_INVALID, std::string(what) + " differs between ranks"};
+}
+
+}  // namespace
+
 extern "C" int sg_dist_create(sg_ctx* ctx, const uint8_t* id, int nranks, int rank, sg_dist** out) {
-  return guard(ctx, [&] {
+  std::unique_ptr<sg_dist> d;
+  int rc = guard(ctx, [&] {
     SG_REQUIRE(out && id, "null argument");
     SG_REQUIRE(nranks >= 1 && rank >= 0 && rank < nranks, "bad rank / rank count");
     set_device(ctx);
-    std::unique_ptr<sg_dist> d(new sg_dist());
+    d.reset(new sg_dist());
     d->ctx = ctx;
     d->G = nranks;
     d->g = rank;
+    dist_defaults(d.get());
     ncclUniqueId u;
     memcpy(u.internal, id, SG_DIST_ID_BYTES);
     SG_NCCL(ncclCommInitRank(&d->comm, nranks, u, rank));
-    *out = d.release();
   });
+  if (rc != SG_OK) return rc;
+  rc = dist_run(d.get(), [&] { agree(d.get(), d->fri_tail_log, "SG_DIST_FRI_TAIL"); });
+  if (rc != SG_OK) return rc;
+  *out = d.release();
+  return SG_OK;
 }
 
 extern "C" int sg_dist_create_transport(sg_ctx* ctx, int nranks, int rank, const sg_dist_transport* t,
                                         sg_dist** out) {
-  return guard(ctx, [&] {
+  std::unique_ptr<sg_dist> d;
+  int rc = guard(ctx, [&] {
     SG_REQUIRE(out && t && t->all_to_all && t->all_gather, "transport callbacks required");
     SG_REQUIRE(nranks >= 1 && rank >= 0 && rank < nranks, "bad rank / rank count");
     set_device(ctx);
-    std::unique_ptr<sg_dist> d(new sg_dist());
+    d.reset(new sg_dist());
     d->ctx = ctx;
     d->G = nranks;
     d->g = rank;
     d->tr = *t;
     d->staged = true;
-    *out = d.release();
+    dist_defaults(d.get());
   });
+  if (rc != SG_OK) return rc;
+  rc = dist_run(d.get(), [&] { agree(d.get(), d->fri_tail_log, "SG_DIST_FRI_TAIL"); });
+  if (rc != SG_OK) return rc;
+  *out = d.release();
+  return SG_OK;
 }
 
 extern "C" void sg_dist_destroy(sg_dist* d) { delete d; }
+
+extern "C" int sg_dist_set_fri_tail(sg_dist* d, int log2_elements) {
+  return dist_run(d, [&] {
+    agree(d, log2_elements, "the FRI hand-over size");
+    d->fri_tail_log = log2_elements;
+  });
+}
+
+extern "C" int sg_dist_set_timeout(sg_dist* d, double seconds) {
+  if (!d || !d->ctx || !(seconds > 0)) return SG_ERR_INVALID;
+  d->timeout_s = seconds;
+  return SG_OK;
+}
+
+extern "C" int sg_dist_poisoned(const sg_dist* d) { return d && d->dead ? 1 : 0; }
 
 extern "C" int sg_dist_plan(size_t n, int nranks, size_t* n1, size_t* n2) {
   return guard(nullptr, [&] {
@@ -681,47 +800,38 @@ extern "C" int sg_dist_plan(size_t n, int nranks, size_t* n1, size_t* n2) {
 }
 
 extern "C" int sg_dist_ntt(sg_dist* d, sg_fe root, const sg_fe* d_cols, size_t row_len, size_t n, sg_fe* d_runs) {
-  sg_ctx* ctx = d ? d->ctx : nullptr;
-  return guard(ctx, [&] {
-    checked(d);
-    set_device(ctx);
+  return dist_run(d, [&] {
+    sg_ctx* ctx = d->ctx;
     SG_REQUIRE(d_cols && d_runs, "null buffer");
     dist_ntt(d, to_fe(root), reinterpret_cast<const fe*>(d_cols), row_len, n, reinterpret_cast<fe*>(d_runs));
-    SG_HIP(hipStreamSynchronize(ctx->stream));
+    host_wait(ctx, ctx->stream);
   });
 }
 
 extern "C" int sg_dist_intt(sg_dist* d, sg_fe root, const sg_fe* d_runs, size_t n, sg_fe* d_cols) {
-  sg_ctx* ctx = d ? d->ctx : nullptr;
-  return guard(ctx, [&] {
-    checked(d);
-    set_device(ctx);
+  return dist_run(d, [&] {
+    sg_ctx* ctx = d->ctx;
     SG_REQUIRE(d_cols && d_runs, "null buffer");
     dist_intt(d, to_fe(root), reinterpret_cast<const fe*>(d_runs), n, reinterpret_cast<fe*>(d_cols));
-    SG_HIP(hipStreamSynchronize(ctx->stream));
+    host_wait(ctx, ctx->stream);
   });
 }
 
 extern "C" int sg_dist_coset_evaluate(sg_dist* d, sg_fe generator, size_t root_order, sg_fe offset,
                                       const sg_fe* d_cols, size_t row_len, sg_fe* d_runs) {
-  sg_ctx* ctx = d ? d->ctx : nullptr;
-  return guard(ctx, [&] {
-    checked(d);
-    set_device(ctx);
+  return dist_run(d, [&] {
+    sg_ctx* ctx = d->ctx;
     SG_REQUIRE(d_cols && d_runs, "null buffer");
     const fe off = to_fe(offset);
     SG_REQUIRE(fe_is_canonical(off), "offset must be canonical");
     dist_coset_evaluate(d, to_fe(generator), root_order, off, reinterpret_cast<const fe*>(d_cols), row_len,
                         reinterpret_cast<fe*>(d_runs));
-    SG_HIP(hipStreamSynchronize(ctx->stream));
+    host_wait(ctx, ctx->stream);
   });
 }
 
 extern "C" int sg_dist_merkle_root(sg_dist* d, const sg_fe* d_runs, size_t n, uint8_t* root) {
-  sg_ctx* ctx = d ? d->ctx : nullptr;
-  return guard(ctx, [&] {
-    checked(d);
-    set_device(ctx);
+  return dist_run(d, [&] {
     SG_REQUIRE(d_runs && root, "null argument");
     uint64_t n1, n2;
     plan(n, d->G, n1, n2);
@@ -731,24 +841,20 @@ extern "C" int sg_dist_merkle_root(sg_dist* d, const sg_fe* d_runs, size_t n, ui
 
 extern "C" int sg_dist_fri_prove(sg_dist* d, const sg_fri* fri, const sg_fe* d_runs, size_t n,
                                  const sg_proof_stream* ps, size_t* top) {
-  sg_ctx* ctx = d ? d->ctx : nullptr;
-  return guard(ctx, [&] {
-    checked(d);
-    set_device(ctx);
+  return dist_run(d, [&] {
+    sg_ctx* ctx = d->ctx;
     SG_REQUIRE(fri && d_runs && top, "null argument");
     dist_fri_prove(d, fri, reinterpret_cast<const fe*>(d_runs), n, ps, top);
-    SG_HIP(hipStreamSynchronize(ctx->stream));
+    host_wait(ctx, ctx->stream);
   });
 }
 
 extern "C" int sg_dist_fri_commit(sg_dist* d, const sg_fri* fri, const sg_fe* d_runs, size_t n,
                                   const sg_proof_stream* ps) {
-  sg_ctx* ctx = d ? d->ctx : nullptr;
-  return guard(ctx, [&] {
-    checked(d);
-    set_device(ctx);
+  return dist_run(d, [&] {
+    sg_ctx* ctx = d->ctx;
     SG_REQUIRE(fri && d_runs, "null argument");
     dist_fri_commit(d, fri, reinterpret_cast<const fe*>(d_runs), n, ps);
-    SG_HIP(hipStreamSynchronize(ctx->stream));
+    host_wait(ctx, ctx->stream);
   });
 }

@@ -2,6 +2,7 @@
 #pragma once
 #include <cstdint>
 #include <functional>
+#include <string>
 #include <vector>
 
 #include "internal.hpp"
@@ -29,6 +30,11 @@ struct DistFriState {
 };
 
 sg_ctx* dist_ctx(sg_dist* d);
+// runs a communicator call: a poisoned communicator fails at once (SG_ERR_INVALID); while the body
+// runs, the context's host waits watch the communicator (RCCL async errors, SG_DIST_TIMEOUT_S);
+// any failure poisons the communicator before the error is returned (dist.cpp sg_dist::dead)
+int dist_run(sg_dist* d, const std::function<void()>& body);
+void dist_poison(sg_dist* d, const std::string& why);
 int dist_world(const sg_dist* d);
 // sg_dist_plan: n = N1 N2, N1 = 2^floor(log2 n / 2); run shards hold N1 runs of N2 / G elements
 void dist_plan(uint64_t n, int G, uint64_t& n1, uint64_t& n2);

@@ -43,6 +43,11 @@ inline std::string& host_last_error() {
   return s;
 }
 
+// Host wait for everything queued on stream s: hipStreamSynchronize, or -- while a communicator
+// call runs on the context (ctx->watch) -- a polling wait that lets the watch abort a collective
+// that never completes (a peer failed) instead of blocking forever.
+void host_wait(sg_ctx* ctx, hipStream_t s);
+
 // Runs f, mapping library errors to the C-ABI return code (+ ctx->last_error).
 template <class F>
 int guard(sg_ctx* ctx, F&& f) {

@@ -213,7 +213,7 @@ std::shared_ptr<const MPolyDevice> mp_device(sg_ctx* ctx, const MPoly& a) {
     d->len.push_back(v.size());
     d->small.push_back(v.size() <= (size_t)kSmallPolyMax ? v : HPoly{});
     SG_HIP(hipMemcpyAsync(p, v.data(), v.size() * sizeof(fe), hipMemcpyHostToDevice, ctx->stream));
-    SG_HIP(hipStreamSynchronize(ctx->stream));
+    host_wait(ctx, ctx->stream);
     uint8_t h[64];
     blake2b512(reinterpret_cast<const uint8_t*>(v.data()), v.size() * sizeof(fe), h);
     std::array<uint64_t, 4> dg{};

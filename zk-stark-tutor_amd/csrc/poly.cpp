@@ -58,7 +58,7 @@ DPoly dpoly_upload(sg_ctx* ctx, const fe* host, uint64_t len) {
 std::vector<fe> dpoly_download(sg_ctx* ctx, const fe* d, uint64_t len) {
   std::vector<fe> out(len);
   if (len) SG_HIP(hipMemcpyAsync(out.data(), d, len * sizeof(fe), hipMemcpyDeviceToHost, ctx->stream));
-  SG_HIP(hipStreamSynchronize(ctx->stream));
+  host_wait(ctx, ctx->stream);
   return out;
 }
 
@@ -75,7 +75,7 @@ int64_t dev_degree(sg_ctx* ctx, const fe* d, uint64_t len) {
   SG_HIP(launch_last_nonzero(d, len, last.as<unsigned long long>(), ctx->stream));
   unsigned long long h = 0;
   SG_HIP(hipMemcpyAsync(&h, last.get(), 8, hipMemcpyDeviceToHost, ctx->stream));
-  SG_HIP(hipStreamSynchronize(ctx->stream));
+  host_wait(ctx, ctx->stream);
   return (int64_t)h - 1;
 }
 
@@ -88,7 +88,7 @@ std::vector<int64_t> dev_degrees(sg_ctx* ctx, const std::vector<std::pair<const 
     SG_HIP(launch_last_nonzero(polys[i].first, polys[i].second, last.as<unsigned long long>() + i, ctx->stream));
   std::vector<unsigned long long> h(polys.size());
   SG_HIP(hipMemcpyAsync(h.data(), last.get(), 8 * polys.size(), hipMemcpyDeviceToHost, ctx->stream));
-  SG_HIP(hipStreamSynchronize(ctx->stream));  // one round trip for the whole batch
+  host_wait(ctx, ctx->stream);  // one round trip for the whole batch
   for (size_t i = 0; i < polys.size(); ++i) out[i] = (int64_t)h[i] - 1;
   return out;
 }
@@ -188,7 +188,7 @@ DPoly poly_mul_exact(sg_ctx* ctx, const fe* a, uint64_t la, const fe* b, uint64_
     std::vector<fe> ha = dpoly_download(ctx, a, la), hb = dpoly_download(ctx, b, lb);
     HPoly r = hp_mul(ha, hb);
     SG_HIP(hipMemcpyAsync(out.p(), r.data(), lr * sizeof(fe), hipMemcpyHostToDevice, ctx->stream));
-    SG_HIP(hipStreamSynchronize(ctx->stream));
+    host_wait(ctx, ctx->stream);
     return out;
   }
   const uint64_t n = next_pow2(lr);
@@ -216,7 +216,7 @@ void ref_inner_ntt(sg_ctx* ctx, const fe& root, uint64_t order, const fe* p, uin
       memcpy(sp.c, host_copy, len * sizeof(fe));
     } else {
       SG_HIP(hipMemcpyAsync(sp.c, p, len * sizeof(fe), hipMemcpyDeviceToHost, ctx->stream));
-      SG_HIP(hipStreamSynchronize(ctx->stream));
+      host_wait(ctx, ctx->stream);
     }
     const fe *A, *B;
     pow_tables2(ctx, root, order, &A, &B);
@@ -315,7 +315,7 @@ DPoly fast_coset_divide_dev(sg_ctx* ctx, fe root, uint64_t root_order, const fe&
       void* t = nullptr;
       SG_HIP(hipMalloc(&t, pl.order * sizeof(fe)));
       dev_div(ctx, static_cast<fe*>(t), nullptr, vr.as<fe>(), pl.order);
-      SG_HIP(hipStreamSynchronize(ctx->stream));
+      host_wait(ctx, ctx->stream);
       try {
         check_div_zero(ctx);  // a zero divisor is reported now and the table is not kept
       } catch (...) {
@@ -389,7 +389,7 @@ const fe* interp_kernel(sg_ctx* ctx, const fe& q, uint64_t D, int logf) {
                    reinterpret_cast<fe*>(t), nullptr);
     }
     // the table outlives this call's temporaries: complete before they return to the pool
-    SG_HIP(hipStreamSynchronize(ctx->stream));
+    host_wait(ctx, ctx->stream);
   } catch (...) {
     (void)hipFree(t);
     throw;
@@ -466,7 +466,7 @@ std::vector<DPoly> interpolate_geometric_batch_dev(sg_ctx* ctx, const fe& q, uin
     if (ctx->domain_cache_on()) {
       // kept only once the inversion is known to have met no zero (the points are distinct, so
       // Z'(q^i) != 0; a table is never cached unchecked)
-      SG_HIP(hipStreamSynchronize(ctx->stream));
+      host_wait(ctx, ctx->stream);
       check_div_zero(ctx);
       void* t = nullptr;
       SG_HIP(hipMalloc(&t, (M + n) * sizeof(fe)));
@@ -763,7 +763,7 @@ sg_poly* wrap(DPoly&& d) {
 const fe* dptr(const sg_poly* p) { return p ? p->d.p() : nullptr; }
 // ABI calls return after their device work: drain the stream, then report a zero divisor
 void done(sg_ctx* ctx) {
-  SG_HIP(hipStreamSynchronize(ctx->stream));
+  host_wait(ctx, ctx->stream);
   check_div_zero(ctx);
 }
 uint64_t dlen(const sg_poly* p) { return p ? p->d.len : 0; }
@@ -775,7 +775,7 @@ extern "C" int sg_poly_create(sg_ctx* ctx, const sg_fe* coeffs, size_t len, sg_p
     set_device(ctx);
     check_canonical(coeffs, len, "coefficients");
     DPoly d = dpoly_upload(ctx, reinterpret_cast<const fe*>(coeffs), len);
-    SG_HIP(hipStreamSynchronize(ctx->stream));
+    host_wait(ctx, ctx->stream);
     *out = wrap(std::move(d));
   });
 }
@@ -785,7 +785,7 @@ extern "C" int sg_poly_create_dev(sg_ctx* ctx, const sg_fe* d_coeffs, size_t len
     SG_REQUIRE(out && (d_coeffs || !len), "null argument");
     set_device(ctx);
     DPoly d = dpoly_copy(ctx, reinterpret_cast<const fe*>(d_coeffs), len);
-    SG_HIP(hipStreamSynchronize(ctx->stream));
+    host_wait(ctx, ctx->stream);
     *out = wrap(std::move(d));
   });
 }
@@ -801,7 +801,7 @@ extern "C" int sg_poly_read(sg_ctx* ctx, const sg_poly* p, sg_fe* out) {
     set_device(ctx);
     if (p->d.len)
       SG_HIP(hipMemcpyAsync(out, p->d.p(), p->d.len * sizeof(fe), hipMemcpyDeviceToHost, ctx->stream));
-    SG_HIP(hipStreamSynchronize(ctx->stream));
+    host_wait(ctx, ctx->stream);
   });
 }
 

@@ -772,7 +772,7 @@ void prove_transition_quotients(sg_ctx* ctx, const sg_stark& st, const std::vect
     void* t = nullptr;
     SG_HIP(hipMalloc(&t, pl.order * sizeof(fe)));
     dev_div(ctx, static_cast<fe*>(t), nullptr, tz_values(pl), pl.order);
-    SG_HIP(hipStreamSynchronize(ctx->stream));
+    host_wait(ctx, ctx->stream);
     try {
       check_div_zero(ctx);
     } catch (...) {
@@ -933,7 +933,7 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
   // here, with the main stream drained: a pool buffer released by queued main-stream work
   // can then never be handed to a side-stream kernel.
   SG_REQUIRE(m <= 4, "at most 4 registers are supported by the AIR kernel");  // root slots 0..m-1, 4
-  SG_HIP(hipStreamSynchronize(ctx->stream));
+  host_wait(ctx, ctx->stream);
   std::vector<DPoly> bq_cw;
   std::vector<std::unique_ptr<sg_tree>> bq_trees(m);
   for (size_t s = 0; s < m; ++s) bq_cw.push_back(dpoly_alloc(ctx, Nf));
@@ -1055,7 +1055,7 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
       }
   });
   mark("fri_prove_and_openings");
-  SG_HIP(hipStreamSynchronize(ctx->stream));
+  host_wait(ctx, ctx->stream);
   check_div_zero(ctx);
   mark("openings");
 }
@@ -1098,7 +1098,7 @@ void stark_prove_dist(sg_dist* dd, const sg_stark& st, const fe* d_trace, size_t
   // the main stream runs the algebra (as in the single-GPU prove); their run-root all-gathers and
   // top trees follow on the main stream, where every collective of the communicator stays.  The
   // buffers side-stream kernels touch are allocated here, with the main stream drained.
-  SG_HIP(hipStreamSynchronize(ctx->stream));
+  host_wait(ctx, ctx->stream);
   std::vector<DevBuf> runs;
   std::vector<PendingForest> forests(m + 1);
   for (size_t s = 0; s <= m; ++s) {
@@ -1186,7 +1186,7 @@ void stark_prove_dist(sg_dist* dd, const sg_stark& st, const fe* d_trace, size_t
     }
   });
   mark("dist_fri_prove_and_openings");
-  SG_HIP(hipStreamSynchronize(ctx->stream));
+  host_wait(ctx, ctx->stream);
   check_div_zero(ctx);
 }
 
@@ -1258,7 +1258,7 @@ extern "C" int sg_rescue_transition_constraints(sg_ctx* ctx, const sg_rescue* rp
     SG_REQUIRE(ctx && rp && out, "a GPU context is required (interpolation on the device)");
     set_device(ctx);
     std::vector<MPoly> tcs = rescue_transition_constraints(ctx, *rp, to_fe(omicron), omicron_domain_length);
-    SG_HIP(hipStreamSynchronize(ctx->stream));
+    host_wait(ctx, ctx->stream);
     check_div_zero(ctx);
     for (size_t i = 0; i < tcs.size(); ++i) {
       out[i] = new sg_mpoly();
@@ -1362,7 +1362,7 @@ extern "C" int sg_stark_prove(sg_ctx* ctx, const sg_stark* st, const sg_fe* trac
     DPoly dt = dpoly_upload(ctx, reinterpret_cast<const fe*>(trace), rows * st->m);
     DPoly dr = dpoly_upload(ctx, reinterpret_cast<const fe*>(trace_randomizers), st->num_randomizers * st->m);
     DPoly dc = dpoly_upload(ctx, reinterpret_cast<const fe*>(randomizer_coeffs), n_rc);
-    SG_HIP(hipStreamSynchronize(ctx->stream));
+    host_wait(ctx, ctx->stream);
     stark_prove(ctx, *st, dt.p(), rows, tc_list(tcs, ntcs), bnd, dr.p(), dc.p(), n_rc, ps);
   });
 }
@@ -1393,11 +1393,10 @@ namespace {
 int dist_prove_entry(sg_dist* d, const sg_stark* st, const sg_fe* trace, size_t rows, const sg_mpoly* const* tcs,
                      size_t ntcs, const sg_boundary* boundary, size_t nb, const sg_fe* trace_randomizers,
                      const sg_fe* randomizer_coeffs, size_t n_rc, const sg_proof_stream* ps, bool host) {
-  sg_ctx* ctx = d ? dist_ctx(d) : nullptr;
-  return guard(ctx, [&] {
-    SG_REQUIRE(d && ctx && st && (trace || !rows) && (tcs || !ntcs) && (boundary || !nb), "null argument");
+  return dist_run(d, [&] {
+    sg_ctx* ctx = dist_ctx(d);
+    SG_REQUIRE(st && (trace || !rows) && (tcs || !ntcs) && (boundary || !nb), "null argument");
     SG_REQUIRE(trace_randomizers || !st->num_randomizers, "null argument");
-    set_device(ctx);
     std::vector<Boundary> bnd;
     for (size_t i = 0; i < nb; ++i) {
       check_canonical(&boundary[i].value, 1, "boundary value");
@@ -1416,7 +1415,7 @@ int dist_prove_entry(sg_dist* d, const sg_stark* st, const sg_fe* trace, size_t 
     DPoly dt = dpoly_upload(ctx, reinterpret_cast<const fe*>(trace), rows * st->m);
     DPoly dr = dpoly_upload(ctx, reinterpret_cast<const fe*>(trace_randomizers), st->num_randomizers * st->m);
     DPoly dc = dpoly_upload(ctx, reinterpret_cast<const fe*>(randomizer_coeffs), n_rc);
-    SG_HIP(hipStreamSynchronize(ctx->stream));
+    host_wait(ctx, ctx->stream);
     stark_prove_dist(d, *st, dt.p(), rows, tc_list(tcs, ntcs), bnd, dr.p(), dc.p(), n_rc, ps);
   });
 }

@@ -49,8 +49,11 @@ class sg_proof_stream(ctypes.Structure):
 A2A_CB = ctypes.CFUNCTYPE(ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t)
 
 
+ABORT_CB = ctypes.CFUNCTYPE(None, ctypes.c_void_p)
+
+
 class sg_dist_transport(ctypes.Structure):
-    _fields_ = [("user", ctypes.c_void_p), ("all_to_all", A2A_CB), ("all_gather", A2A_CB)]
+    _fields_ = [("user", ctypes.c_void_p), ("all_to_all", A2A_CB), ("all_gather", A2A_CB), ("abort", ABORT_CB)]
 
 
 # name -> (restype, argtypes)
@@ -131,6 +134,9 @@ PROTOTYPES = {
     "sg_dist_create": (ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int, _P(_vp)]),
     "sg_dist_create_transport": (ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _P(sg_dist_transport), _P(_vp)]),
     "sg_dist_destroy": (None, [_vp]),
+    "sg_dist_set_timeout": (ctypes.c_int, [_vp, ctypes.c_double]),
+    "sg_dist_poisoned": (ctypes.c_int, [_vp]),
+    "sg_dist_set_fri_tail": (ctypes.c_int, [_vp, ctypes.c_int]),
     "sg_dist_plan": (ctypes.c_int, [_sz, ctypes.c_int, _P(_sz), _P(_sz)]),
     "sg_dist_ntt": (ctypes.c_int, [_vp, sg_fe, _vp, _sz, _sz, _vp]),
     "sg_dist_intt": (ctypes.c_int, [_vp, sg_fe, _vp, _sz, _vp]),

@@ -409,8 +409,11 @@ class NativeDist:
     Shards are int64 device tensors (2 words per element) in the layouts of ``DistStark``:
     column shard in, run shard out (ntt / coset_evaluate), the reverse for intt."""
 
-    def __init__(self, ctx: Optional[api.Context] = None, transport: str = "rccl", group=None):
-        from ._lib import A2A_CB, sg_dist_transport
+    def __init__(self, ctx: Optional[api.Context] = None, transport: str = "rccl", group=None, abort=None):
+        """``abort`` (host transport, optional): called with no arguments when a call fails on this
+        rank and the library poisons the communicator, e.g. to tear the group down so the peers'
+        pending exchanges fail instead of waiting (sg_dist_transport.abort)."""
+        from ._lib import A2A_CB, ABORT_CB, sg_dist_transport
         self.ctx = api._ctx(ctx)
         self._lib = lib()
         self.group = group
@@ -448,13 +451,34 @@ class NativeDist:
                 except Exception:  # noqa: BLE001
                     return 1
 
-            self._cbs = (A2A_CB(a2a), A2A_CB(ag))  # keep the thunks alive
-            self._tr = sg_dist_transport(None, self._cbs[0], self._cbs[1])
+            def on_abort(_user):
+                if abort is not None:
+                    try:
+                        abort()
+                    except Exception:  # noqa: BLE001 - the library is already returning an error
+                        pass
+
+            self._cbs = (A2A_CB(a2a), A2A_CB(ag), ABORT_CB(on_abort))  # keep the thunks alive
+            self._tr = sg_dist_transport(None, self._cbs[0], self._cbs[1], self._cbs[2])
             self.ctx.check(self._lib.sg_dist_create_transport(self.ctx.handle, self.G, self.g, ctypes.byref(self._tr),
                                                               ctypes.byref(h)))
         else:
             raise ValueError(f"unknown transport {transport!r}")
         self.handle = h
+
+    def set_fri_tail(self, log2_elements: int) -> None:
+        """Collective (every rank, same value): the codeword size at which a sharded FRI commit
+        hands over to the single-GPU rounds (sg_dist_set_fri_tail)."""
+        self.ctx.check(self._lib.sg_dist_set_fri_tail(self.handle, int(log2_elements)))
+
+    def set_timeout(self, seconds: float) -> None:
+        """Deadline of one host wait inside a communicator call (sg_dist_set_timeout)."""
+        self.ctx.check(self._lib.sg_dist_set_timeout(self.handle, float(seconds)))
+
+    @property
+    def poisoned(self) -> bool:
+        """True once a call failed on this rank: every later call fails (sg_dist_poisoned)."""
+        return bool(self._lib.sg_dist_poisoned(self.handle))
 
     def close(self) -> None:
         if self.handle:
