@@ -475,10 +475,18 @@ def _stark_checks(nd, world, rank, tmp, cases, gather):
         tr, rc = np.load(os.path.join(tmp, "tr%d.npy" % k)), np.load(os.path.join(tmp, "rc%d.npy" % k))
         # small domains: every FRI round sharded (hand-over size 0); C4: the default hand-over
         nd.set_fri_tail(0 if N < 1000 else 20)
+        before = nd.counters()[1]
         got = st.prove(trace, air, bnd, sg.IndependentProofStream(), tr, rc, dist=nd)
-        ok.append((k, got == open(os.path.join(tmp, "proof%d.bin" % k), "rb").read()))
+        ok.append((k, got == open(os.path.join(tmp, "proof%d.bin" % k), "rb").read(), nd.counters()[1] - before))
     flags = gather(ok)
-    assert all(f for per_rank in flags for (_, f) in per_rank), f"world {world}: sharded proof bytes differ: {flags}"
+    assert all(f for per_rank in flags for (_, f, _) in per_rank), f"world {world}: sharded proof bytes differ: {flags}"
+    # the transition quotients' coset work ran on run shards (2 constraints) wherever the coset
+    # splits over the ranks: C4 (coset 2^18) at every world, the false witness (coset 2^8,
+    # redone from the gathered values) up to 4 ranks
+    for per_rank in flags:
+        for (k, _, sq) in per_rank:
+            if k == 3 or (k == 1 and world <= 4):
+                assert sq == 2, f"world {world} case {k}: {sq} sharded quotients"
 
 
 def test_dist_stark_prove_world1_rccl(stark_reference):

@@ -59,6 +59,8 @@ struct sg_dist {
   // codeword size (log2 elements) at which a sharded FRI commit hands over to the single-GPU
   // rounds: part of the collective schedule, so it is agreed by all ranks (sg_dist_set_fri_tail)
   int fri_tail_log = 20;
+  // counters (sg_dist_counters): collectives issued, transition quotients computed sharded
+  uint64_t collectives = 0, sharded_quotients = 0;
   ~sg_dist() {
     if (comm) (void)ncclCommDestroy(comm);
     if (hsend) (void)hipHostFree(hsend);
@@ -149,6 +151,7 @@ void grow_pinned(void*& p, size_t& have, size_t need) {
 void exchange(sg_dist* d, const void* dsend, void* drecv, size_t bytes, bool a2a) {
   sg_ctx* ctx = d->ctx;
   const size_t total = bytes * d->G;
+  ++d->collectives;
   if (d->comm) {  // RCCL over xGMI, stream-ordered (a 1-rank communicator runs the same calls)
     if (a2a)
       SG_NCCL(ncclAllToAll(dsend, drecv, bytes, ncclUint8, d->comm, ctx->stream));
@@ -362,6 +365,48 @@ void dist_lde_replicated(sg_dist* d, const fe& gen, uint64_t n, const fe& offset
   DevBuf cols(d->ctx, rows * row_len * sizeof(fe));
   SG_HIP(launch_gather_cols(cols.as<fe>(), coeffs, len, rows, row_len, n1, (uint64_t)d->g * rows, d->ctx->stream));
   dist_coset_evaluate(d, gen, n, offset, cols.as<fe>(), row_len, runs);
+}
+
+// Coset interpolation of a run-sharded codeword (the values of a polynomial of degree < n on
+// offset * <gen>, ntt_arithmetics.rs:172-181): its coefficients as this rank's column shard
+// [N1/G][N2] -- the distributed INTT, then coefficient i = (g rows + r) + N1 j times offset^-i.
+void dist_coset_interpolate(sg_dist* d, const fe& gen, uint64_t n, const fe& offset, const fe* runs, fe* cols) {
+  uint64_t n1, n2;
+  plan(n, d->G, n1, n2);
+  dist_intt(d, gen, runs, n, cols);
+  const uint64_t rows = n1 / d->G;
+  const fe* T[3];
+  tables3(d->ctx, fe_inv(offset), T);
+  SG_HIP(launch_mul_pow(cols, rows, n2, n1, 0, (uint64_t)d->g * rows, 1, T[0], T[1], T[2], d->ctx->stream));
+}
+
+// every rank's column shard [N1/G][N2] -> the whole vector in natural order on every rank: one
+// all-gather ([g][r][j] = [j1][j]) and one transpose to [j][j1] (index j1 + N1 j)
+void dist_gather_columns(sg_dist* d, const fe* cols, uint64_t n, fe* out) {
+  uint64_t n1, n2;
+  plan(n, d->G, n1, n2);
+  DevBuf all(d->ctx, n * sizeof(fe));
+  exchange(d, cols, all.get(), (n1 / d->G) * n2 * sizeof(fe), /*a2a=*/false);
+  SG_HIP(launch_swap01(all.as<fe>(), out, n1, n2, 1, d->ctx->stream));
+}
+
+// every rank's run shard [N1][N2/G] -> the whole codeword in natural order on every rank
+void dist_gather_runs(sg_dist* d, const fe* runs, uint64_t n, fe* out) {
+  uint64_t n1, n2;
+  plan(n, d->G, n1, n2);
+  const uint64_t R = n2 / d->G;
+  DevBuf all(d->ctx, n * sizeof(fe));
+  exchange(d, runs, all.get(), n1 * R * sizeof(fe), /*a2a=*/false);                  // [g][k1][c]
+  SG_HIP(launch_swap01(all.as<fe>(), out, d->G, n1, R, d->ctx->stream));              // [k1][g][c]
+}
+
+// this rank's run shard of a natural-order vector every rank holds (no exchange)
+void dist_take_runs(sg_dist* d, const fe* full, uint64_t n, fe* runs) {
+  uint64_t n1, n2;
+  plan(n, d->G, n1, n2);
+  const uint64_t R = n2 / d->G;
+  SG_HIP(hipMemcpy2DAsync(runs, R * sizeof(fe), full + (uint64_t)d->g * R, n2 * sizeof(fe), R * sizeof(fe), n1,
+                          hipMemcpyDeviceToDevice, d->ctx->stream));
 }
 
 // fri.rs:115-172 on a run-sharded codeword.  The fold partner of i is i + n/2: same k2,
@@ -687,6 +732,15 @@ void dist_fri_prove(sg_dist* d, const sg_fri* f, const fe* runs, uint64_t n, con
 
 sg_ctx* dist_ctx(sg_dist* d) { return d->ctx; }
 int dist_world(const sg_dist* d) { return d->G; }
+int dist_rank(const sg_dist* d) { return d->g; }
+void dist_count_sharded_quotient(sg_dist* d) { ++d->sharded_quotients; }
+bool dist_can_shard(uint64_t n, int G) {
+  if (n < 2 || (n & (n - 1)) || G < 1 || (G & (G - 1))) return false;
+  const uint64_t n1 = (uint64_t)1 << (ilog2_exact(n) / 2), n2 = n / n1;
+  // sg_dist_plan (ntt) and the inverse's interleaved first pass (intt)
+  return n1 % (uint64_t)G == 0 && n2 % (4 * (uint64_t)G) == 0 && n2 % (uint64_t)G == 0 && n1 / G >= 4 &&
+         (n1 / G) % 4 == 0;
+}
 void dist_plan(uint64_t n, int G, uint64_t& n1, uint64_t& n2) { plan(n, G, n1, n2); }
 
 }  // namespace sg
@@ -788,6 +842,13 @@ extern "C" int sg_dist_set_timeout(sg_dist* d, double seconds) {
 }
 
 extern "C" int sg_dist_poisoned(const sg_dist* d) { return d && d->dead ? 1 : 0; }
+
+extern "C" int sg_dist_counters(const sg_dist* d, uint64_t* collectives, uint64_t* sharded_quotients) {
+  if (!d || !collectives || !sharded_quotients) return SG_ERR_INVALID;
+  *collectives = d->collectives;
+  *sharded_quotients = d->sharded_quotients;
+  return SG_OK;
+}
 
 extern "C" int sg_dist_plan(size_t n, int nranks, size_t* n1, size_t* n2) {
   return guard(nullptr, [&] {

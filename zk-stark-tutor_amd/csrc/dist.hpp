@@ -36,12 +36,24 @@ sg_ctx* dist_ctx(sg_dist* d);
 int dist_run(sg_dist* d, const std::function<void()>& body);
 void dist_poison(sg_dist* d, const std::string& why);
 int dist_world(const sg_dist* d);
+int dist_rank(const sg_dist* d);
+void dist_count_sharded_quotient(sg_dist* d);
+// n splits over G ranks for both the forward transform (sg_dist_plan) and the inverse
+bool dist_can_shard(uint64_t n, int G);
 // sg_dist_plan: n = N1 N2, N1 = 2^floor(log2 n / 2); run shards hold N1 runs of N2 / G elements
 void dist_plan(uint64_t n, int G, uint64_t& n1, uint64_t& n2);
 // fft/ntt_arithmetics.rs:161-170 of a coefficient vector every rank holds (device, len <= n) into
 // this rank's run shard [N1][N2 / G] (its column shard gathered first)
 void dist_lde_replicated(sg_dist* d, const fe& gen, uint64_t n, const fe& offset, const fe* coeffs, uint64_t len,
                          fe* runs);
+// coset interpolation of a run-sharded codeword of n points on offset * <gen> into the column shard
+// [N1/G][N2] of its coefficients (distributed INTT + offset^-i)
+void dist_coset_interpolate(sg_dist* d, const fe& gen, uint64_t n, const fe& offset, const fe* runs, fe* cols);
+// all-gathers: column shards / run shards of an n-vector -> the whole vector, natural order, every rank
+void dist_gather_columns(sg_dist* d, const fe* cols, uint64_t n, fe* out);
+void dist_gather_runs(sg_dist* d, const fe* runs, uint64_t n, fe* out);
+// this rank's run shard [N1][N2/G] of a natural-order n-vector (a strided copy, no exchange)
+void dist_take_runs(sg_dist* d, const fe* full, uint64_t n, fe* runs);
 // merkle_root.rs:21-32 of a run-sharded codeword; with `keep`, the forest and top tree are retained
 void dist_merkle_root(sg_dist* d, const fe* runs, uint64_t k1s, uint64_t R, uint8_t root[64],
                       ShardedRound* keep = nullptr);

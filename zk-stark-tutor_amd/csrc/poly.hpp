@@ -86,7 +86,9 @@ DPoly fast_coset_divide_dev(sg_ctx* ctx, fe root, uint64_t root_order, const fe&
 DPoly zerofier_geometric_dev(sg_ctx* ctx, const fe& q, uint64_t D, uint64_t n);
 // tags of the context's domain tables (sg_ctx::domain_tables keys start with one)
 enum : uint64_t { kDomainGeoInterp = 1, kDomainTzCoeffs = 2, kDomainTzValues = 3, kDomainTzInverse = 4,
-                  kDomainDivisorInverse = 5, kDomainMpolyCoset = 6, kDomainRescueCoset = 7 };
+                  kDomainDivisorInverse = 5, kDomainMpolyCoset = 6, kDomainRescueCoset = 7,
+                  // run-shard slices of public coset tables for a sharded prove (key carries G, g)
+                  kDomainShard = 8 };
 // Z(q^m) (m < D) and 1 / Z'(q^i) (i < n) of the domain q^0..q^(n-1), reusable across
 // interpolations on one domain
 struct GeoInterpCache {

@@ -434,43 +434,89 @@ bool air_generic() {
 // A Rescue-Prime row in its factored form (mpoly.hpp RescueAirForm) on the coset: the same values
 // as the expanded polynomial.  Its round-constant interpolants' coset values are public and kept
 // with the AIR (like the x-polynomial values of the generic path).
+// values of a Rescue AIR x-polynomial (first_i / second_k) on offset * <w_L>, kept in the
+// context's domain tables (content-keyed) unless SG_NO_DOMAIN_CACHE=1 (then owned by `keep`)
+const fe* rescue_xvals(sg_ctx* ctx, const RescueAirForm& f, int idx, uint64_t L, const fe& offset,
+                       std::vector<DevBuf>& keep) {
+  const bool kept = ctx->domain_cache_on();
+  std::vector<uint64_t> key = {kDomainRescueCoset};
+  key.insert(key.end(), f.xp->content.begin(), f.xp->content.end());
+  key.insert(key.end(), {(uint64_t)idx, L, fe_lo(offset), fe_hi(offset)});
+  if (kept)
+    if (void* t = ctx->domain_table(key)) return static_cast<const fe*>(t);
+  const HPoly& hp = f.xp->polys[(size_t)idx];
+  const int64_t deg = hp_degree(hp);
+  void* t = nullptr;
+  fe* out = nullptr;
+  if (kept) {
+    SG_HIP(hipMalloc(&t, L * sizeof(fe)));
+    out = static_cast<fe*>(t);
+  } else {
+    keep.emplace_back(ctx, L * sizeof(fe));
+    out = keep.back().as<fe>();
+  }
+  try {
+    if (deg < 0) {
+      SG_HIP(hipMemsetAsync(out, 0, L * sizeof(fe), ctx->stream));
+    } else {
+      DPoly in = dpoly_upload(ctx, hp.data(), (uint64_t)deg + 1);
+      const fe* ip = in.p();
+      coset_evaluate_batch(ctx, root_of_order(L), L, offset, &ip, (size_t)deg + 1, &out, 1);
+      keep.push_back(std::move(in.buf));
+    }
+  } catch (...) {
+    if (t) (void)hipFree(t);
+    throw;
+  }
+  if (kept) ctx->domain_table_put(key, t);
+  return out;
+}
+
+// This rank's run shard of a public table of L coset values (`full`, computed by every rank
+// locally: no collective, so ranks whose caches differ stay in step), kept under `key` + (G, g).
+const fe* shard_table(sg_dist* dd, std::vector<uint64_t> key, const fe* full, uint64_t L, std::vector<DevBuf>& keep) {
+  sg_ctx* ctx = dist_ctx(dd);
+  const bool kept = ctx->domain_cache_on();
+  key.insert(key.begin(), kDomainShard);
+  key.push_back((uint64_t)dist_world(dd));
+  key.push_back((uint64_t)dist_rank(dd));
+  if (kept)
+    if (void* t = ctx->domain_table(key)) return static_cast<const fe*>(t);
+  const uint64_t n = L / (uint64_t)dist_world(dd);
+  fe* out = nullptr;
+  void* t = nullptr;
+  if (kept) {
+    SG_HIP(hipMalloc(&t, n * sizeof(fe)));
+    out = static_cast<fe*>(t);
+  } else {
+    keep.emplace_back(ctx, n * sizeof(fe));
+    out = keep.back().as<fe>();
+  }
+  try {
+    dist_take_runs(dd, full, L, out);
+  } catch (...) {
+    if (t) (void)hipFree(t);
+    throw;
+  }
+  if (kept) ctx->domain_table_put(key, t);
+  return out;
+}
+
+// A Rescue-Prime row in its factored form (mpoly.hpp RescueAirForm) on the coset: the same values
+// as the expanded polynomial.  Its round-constant interpolants' coset values are public and kept
+// with the AIR (like the x-polynomial values of the generic path).  With `dd`, co holds this rank's
+// run shards (co.L = L / G points, full_L = L) and the x-polynomial values are sliced to them.
 DPoly transition_values_rescue(sg_ctx* ctx, const RescueAirForm& f, const AirCoset& co, const fe& offset,
-                               std::vector<DevBuf>& keep) {
+                               std::vector<DevBuf>& keep, sg_dist* dd = nullptr, uint64_t full_L = 0) {
   const uint64_t L = co.L;
   const int m = f.m;
-  const bool kept = ctx->domain_cache_on();
   auto xvals = [&](int idx) -> const fe* {
+    if (!dd) return rescue_xvals(ctx, f, idx, L, offset, keep);
+    const fe* full = rescue_xvals(ctx, f, idx, full_L, offset, keep);
     std::vector<uint64_t> key = {kDomainRescueCoset};
     key.insert(key.end(), f.xp->content.begin(), f.xp->content.end());
-    key.insert(key.end(), {(uint64_t)idx, L, fe_lo(offset), fe_hi(offset)});
-    if (kept)
-      if (void* t = ctx->domain_table(key)) return static_cast<const fe*>(t);
-    const HPoly& hp = f.xp->polys[(size_t)idx];
-    const int64_t deg = hp_degree(hp);
-    void* t = nullptr;
-    fe* out = nullptr;
-    if (kept) {
-      SG_HIP(hipMalloc(&t, L * sizeof(fe)));
-      out = static_cast<fe*>(t);
-    } else {
-      keep.emplace_back(ctx, L * sizeof(fe));
-      out = keep.back().as<fe>();
-    }
-    try {
-      if (deg < 0) {
-        SG_HIP(hipMemsetAsync(out, 0, L * sizeof(fe), ctx->stream));
-      } else {
-        DPoly in = dpoly_upload(ctx, hp.data(), (uint64_t)deg + 1);
-        const fe* ip = in.p();
-        coset_evaluate_batch(ctx, root_of_order(L), L, offset, &ip, (size_t)deg + 1, &out, 1);
-        keep.push_back(std::move(in.buf));
-      }
-    } catch (...) {
-      if (t) (void)hipFree(t);
-      throw;
-    }
-    if (kept) ctx->domain_table_put(key, t);
-    return out;
+    key.insert(key.end(), {(uint64_t)idx, full_L, fe_lo(offset), fe_hi(offset)});
+    return shard_table(dd, key, full, full_L, keep);
   };
   AirRescueArgs a{};
   DPoly vals = dpoly_alloc(ctx, L);
@@ -702,8 +748,16 @@ void prove_boundary_quotients(sg_ctx* ctx, const sg_stark& st, const std::vector
 
 // transition quotients (stark.rs:388-422) and every quotient's degree (one host round trip; a zero
 // divisor is reported here, before any root is pushed)
+//
+// With `dd` (the sharded prove) and a native Rescue-Prime AIR, the coset work is
+// split over the communicator: each rank evaluates the trace polynomials on its run shard of the
+// coset (2m distributed LDEs: current rows at offset g, next rows at g * omicron), the factored AIR
+// and the division by the zerofier there, and the quotient's coset interpolation (distributed INTT);
+// one all-gather then hands every rank the whole quotient, so the degree checks, the combination
+// and the proof bytes are those of the replicated path.  The public tables (x-polynomial and
+// zerofier values) are computed whole by every rank with no collective and sliced to its shard.
 void prove_transition_quotients(sg_ctx* ctx, const sg_stark& st, const std::vector<const MPoly*>& tcs,
-                                ProveAlgebra& A) {
+                                ProveAlgebra& A, sg_dist* dd = nullptr) {
   const uint64_t D = st.D, Tp = A.Tp;
   const fe g = st.generator;
   const std::vector<DPoly>& trace_polys = A.trace_polys;
@@ -806,13 +860,65 @@ void prove_transition_quotients(sg_ctx* ctx, const sg_stark& st, const std::vect
   // reference's way.
   struct Pending {
     size_t idx;
-    DPoly vals;
+    DPoly vals;  // the transition values on the coset (sharded: this rank's run shard)
     uint64_t len, L;
+    bool sharded = false;
   };
   std::vector<Pending> pending;
+  // the sharded coset work applies when every constraint carries the factored Rescue form, all
+  // share one coset size Ls on the fast path (L <= D, deg Z < len), and Ls splits over the ranks;
+  // the decision depends only on inputs every rank shares, so all ranks take the same branch
+  uint64_t Ls = 0;
+  bool sharded = dd && !tcs.empty();
+  for (const MPoly* tc : tcs) {
+    if (!sharded) break;
+    const uint64_t len = symbolic_degree_bound(*tc, Tp - 1) + 1;
+    const uint64_t L = next_pow2(len);
+    if (!tc->rescue || (size_t)tc->rescue->m != trace_polys.size() || !(L <= D && (uint64_t)dtz < len) ||
+        (Ls && L != Ls))
+      sharded = false;
+    Ls = L;
+  }
+  if (sharded) sharded = dist_can_shard(Ls, dist_world(dd));
+  AirCoset sco;  // this rank's run shards of the coset values (sharded)
+  const fe* tz_shard = nullptr;
+  bool tz_shard_inverse = false;
+  if (sharded) {
+    const int G = dist_world(dd);
+    const fe wL = root_of_order(Ls);
+    sco.L = Ls / (uint64_t)G;
+    for (int pass = 0; pass < 2; ++pass)
+      for (size_t s = 0; s < trace_polys.size(); ++s) {
+        sco.V.push_back(dpoly_alloc(ctx, sco.L));
+        dist_lde_replicated(dd, wL, Ls, pass ? fe_mul(g, st.omicron) : g, trace_polys[s].p(), trace_polys[s].len,
+                            sco.V.back().p());
+        sco.var.push_back((int)sco.V.size() - 1);
+        sco.shift.push_back(0);
+      }
+    DivPlan pl;
+    pl.root = wL;
+    pl.order = Ls;
+    tz_shard_inverse = dcache;
+    tz_shard = dcache ? shard_table(dd, tz_key_at(kDomainTzInverse, pl), tz_inverse(pl), Ls, air_keep)
+                      : shard_table(dd, tz_key_at(kDomainTzValues, pl), tz_values(pl), Ls, air_keep);
+  }
   for (const MPoly* tc : tcs) {
     const uint64_t len = symbolic_degree_bound(*tc, Tp - 1) + 1;
     const uint64_t L = next_pow2(len);
+    if (sharded) {
+      const uint64_t nl = sco.L;
+      DPoly vals = transition_values_rescue(ctx, *tc->rescue, sco, g, air_keep, dd, Ls);
+      DevBuf qv(ctx, nl * sizeof(fe)), cols(ctx, nl * sizeof(fe));
+      if (tz_shard_inverse) dev_mul(ctx, qv.as<fe>(), vals.p(), tz_shard, nl);
+      else dev_div(ctx, qv.as<fe>(), vals.p(), tz_shard, nl);
+      dist_coset_interpolate(dd, root_of_order(Ls), Ls, g, qv.as<fe>(), cols.as<fe>());
+      DPoly out = dpoly_alloc(ctx, Ls);  // all Ls coefficients, on every rank
+      dist_gather_columns(dd, cols.as<fe>(), Ls, out.p());
+      pending.push_back(Pending{tqs.size(), std::move(vals), len, Ls, true});
+      dist_count_sharded_quotient(dd);
+      tqs.push_back(std::move(out));
+      continue;
+    }
     auto cit = cosets.find(L);
     if (cit == cosets.end()) cit = cosets.emplace(L, air_coset(ctx, trace_polys, L, st.omicron, g, st.D)).first;
     DPoly vals = transition_values(ctx, *tc, cit->second, g, air_keep);
@@ -851,6 +957,11 @@ void prove_transition_quotients(sg_ctx* ctx, const sg_stark& st, const std::vect
     if (dq >= 0 && dl <= pd.len - 1 && std::max<uint64_t>(dl, (uint64_t)dtz) >= pd.L / 2) {
       tqs[pd.idx].len = (uint64_t)dq + 1;  // the reference's truncated quotient
     } else {
+      if (pd.sharded) {  // the reference's steps on the whole coset: every rank gathers the values
+        DPoly full = dpoly_alloc(ctx, pd.L);
+        dist_gather_runs(dd, pd.vals.p(), pd.L, full.p());
+        pd.vals = std::move(full);
+      }
       tqs[pd.idx] = general_quotient(pd.vals, pd.len, pd.L);
       redone = true;
     }
@@ -1129,7 +1240,7 @@ void stark_prove_dist(sg_dist* dd, const sg_stark& st, const fe* d_trace, size_t
   for (size_t s = 0; s < m; ++s) lde(A.bqs[s].p(), A.bqs[s].len, runs[s]);
   fork_forests(0, m);
   mark("dist_bq_lde");
-  prove_transition_quotients(ctx, st, tcs, A);
+  prove_transition_quotients(ctx, st, tcs, A, dd);
   mark("dist_transition_quotients");
   SG_HIP(hipEventRecord(ctx->ev_join, ctx->side));
   SG_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));
