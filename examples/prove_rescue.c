@@ -5,7 +5,12 @@
  * two thread_rng draws read from a file so the bytes can be compared with another prover's.
  *
  *   prove_rescue N expansion colinearity security tcd input_lo input_hi randomness.bin proof.bin
- *                [--dist id_file rank nranks [nonce]]
+ *                [--dist id_file rank nranks [nonce]] [--document text]
+ *
+ * With --document the proof goes through a SignatureProofStream of that document
+ * (rescue_prime/proof_stream.rs:9-52: every Fiat-Shamir draw is prefixed by blake2b(document)):
+ * RPSSS::sign (rpsss.rs:74-78), e.g. the reference's published configuration
+ * `27 4 64 128 3 ... --document "Hello, World!"` (rpsss.rs:103-108, 1 156 888 bytes).
  *
  * With --dist the proof is computed with the FRI domain sharded over `nranks` processes, one GPU
  * each (sg_dist_stark_prove over RCCL, rank r on GPU r): rank 0 writes the RCCL unique id to
@@ -40,11 +45,29 @@
   } while (0)
 
 int main(int argc, char** argv) {
-  const int dist = (argc == 14 || argc == 15) && strcmp(argv[10], "--dist") == 0;
-  if (argc != 10 && !dist) {
+  int dist = 0, bad = argc < 10;
+  const char *id_path = NULL, *document = NULL;
+  int rank = 0, nranks = 1;
+  uint64_t nonce = 0;
+  for (int i = 10; i < argc && !bad;) {
+    if (strcmp(argv[i], "--document") == 0 && i + 1 < argc) {
+      document = argv[i + 1];
+      i += 2;
+    } else if (strcmp(argv[i], "--dist") == 0 && i + 3 < argc) {
+      dist = 1;
+      id_path = argv[i + 1];
+      rank = atoi(argv[i + 2]);
+      nranks = atoi(argv[i + 3]);
+      i += 4;
+      if (i < argc && strncmp(argv[i], "--", 2) != 0) nonce = strtoull(argv[i++], NULL, 0);
+    } else {
+      bad = 1;
+    }
+  }
+  if (bad) {
     fprintf(stderr,
             "usage: %s N expansion colinearity security tcd input_lo input_hi randomness.bin proof.bin"
-            " [--dist id_file rank nranks [nonce]]\n",
+            " [--dist id_file rank nranks [nonce]] [--document text]\n",
             argv[0]);
     return 1;
   }
@@ -52,27 +75,25 @@ int main(int argc, char** argv) {
   const size_t c = strtoull(argv[3], NULL, 10), sec = strtoull(argv[4], NULL, 10);
   const size_t tcd = strtoull(argv[5], NULL, 10);
   const sg_fe input = {strtoull(argv[6], NULL, 0), strtoull(argv[7], NULL, 0)};
-  const int rank = dist ? atoi(argv[12]) : 0, nranks = dist ? atoi(argv[13]) : 1;
   sg_ctx* ctx = NULL;
   CHECK(sg_ctx_create(dist ? rank : 0, &ctx));  /* one GPU per rank of the node */
   sg_dist* comm = NULL;
   if (dist) {
     uint8_t id[SG_DIST_ID_BYTES];
-    const uint64_t nonce = argc == 15 ? strtoull(argv[14], NULL, 0) : 0;
     if (rank == 0) {
       CHECK(sg_dist_unique_id(id));
       char tmp[4096];
-      snprintf(tmp, sizeof tmp, "%s.tmp", argv[11]);
+      snprintf(tmp, sizeof tmp, "%s.tmp", id_path);
       FILE* f = fopen(tmp, "wb");
       if (!f || fwrite(&nonce, 1, sizeof nonce, f) != sizeof nonce || fwrite(id, 1, sizeof id, f) != sizeof id ||
-          fclose(f) != 0 || rename(tmp, argv[11]) != 0) {
-        fprintf(stderr, "cannot write %s\n", argv[11]);
+          fclose(f) != 0 || rename(tmp, id_path) != 0) {
+        fprintf(stderr, "cannot write %s\n", id_path);
         return 1;
       }
     } else {
       int have = 0;
       for (int tries = 0; tries < 6000 && !have; ++tries) {  /* up to 60 s for rank 0 */
-        FILE* f = fopen(argv[11], "rb");
+        FILE* f = fopen(id_path, "rb");
         uint64_t got = 0;
         if (f) {
           have = fread(&got, 1, sizeof got, f) == sizeof got && got == nonce && fread(id, 1, sizeof id, f) == sizeof id;
@@ -84,7 +105,7 @@ int main(int argc, char** argv) {
         }
       }
       if (!have) {
-        fprintf(stderr, "no id for this run (nonce %llu) in %s\n", (unsigned long long)nonce, argv[11]);
+        fprintf(stderr, "no id for this run (nonce %llu) in %s\n", (unsigned long long)nonce, id_path);
         return 1;
       }
     }
@@ -123,7 +144,8 @@ int main(int argc, char** argv) {
     fprintf(stderr, "%s holds %zu elements, %zu needed\n", argv[8], got, need);
     return 2;
   }
-  sg_stream* s = sg_stream_create();
+  sg_stream* s = document ? sg_stream_create_signature((const uint8_t*)document, strlen(document))
+                          : sg_stream_create();
   const sg_proof_stream cb = sg_stream_callbacks(s);
   if (comm)
     CHECK(sg_dist_stark_prove(comm, st, trace, N + 1, (const sg_mpoly* const*)tcs, 2, bnd, 2, rnd, rnd + 2 * nr, nrc,

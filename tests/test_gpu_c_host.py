@@ -73,3 +73,26 @@ def test_c_host_c4_equals_python_binding(tmp_path):
     want = st_g.prove(rp_g.trace_array(inp), air_g, rp.boundary_constraints(rp.hash(inp)),
                       sg.IndependentProofStream(), sg.fe_array(r[:2 * nr]), sg.fe_array(r[2 * nr:]))
     assert got == want
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("dist", [False, True])
+def test_c_host_rpsss_signature_equals_oracle(tmp_path, dist):
+    """RPSSS::sign at the reference's published configuration (rpsss.rs:103-108; tests/rpsss_case.py)
+    from the compiled host: `--document "Hello, World!"` puts the proof through a
+    SignatureProofStream; the bytes equal the oracle's signature and its length is the reference's
+    1 156 888 (rpsss.rs:89).  dist: the same through sg_dist_stark_prove (one-rank RCCL)."""
+    import rpsss_case as R
+    c = R.Case()
+    want = c.oracle_sign()
+    r = [v for row in c.trace_randomizers for v in row] + list(c.randomizer_coefficients)
+    rnd = np.array([[v & (2**64 - 1), v >> 64] for v in r], dtype=np.uint64)
+    rfile, pfile = tmp_path / "randomness.bin", tmp_path / "sig.bin"
+    rnd.tofile(rfile)
+    extra = ["--dist", str(tmp_path / "rccl.id"), "0", "1", str(int.from_bytes(os.urandom(7), "big"))] if dist else []
+    res = subprocess.run([BIN, str(R.RESCUE[3]), str(R.EXPANSION), str(R.CHECKS), str(R.SECURITY), str(R.TCD),
+                          str(c.sk & (2**64 - 1)), str(c.sk >> 64), str(rfile), str(pfile), "--document",
+                          R.DOCUMENT.decode()] + extra, capture_output=True, text=True, timeout=300)
+    assert res.returncode == 0, res.stderr
+    got = pfile.read_bytes()
+    assert len(got) == R.PROOF_LEN and got == want
