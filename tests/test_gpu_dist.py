@@ -481,12 +481,14 @@ def _stark_checks(nd, world, rank, tmp, cases, gather):
     flags = gather(ok)
     assert all(f for per_rank in flags for (_, f, _) in per_rank), f"world {world}: sharded proof bytes differ: {flags}"
     # the transition quotients' coset work ran on run shards (2 constraints) wherever the coset
-    # splits over the ranks: C4 (coset 2^18) at every world, the false witness (coset 2^8,
-    # redone from the gathered values) up to 4 ranks
+    # splits over the ranks: C4 (coset 2^18) at every world > 1, the false witness (coset 2^8,
+    # redone from the gathered values) at 2 and 4 ranks; one rank runs the replicated path
     for per_rank in flags:
         for (k, _, sq) in per_rank:
-            if k == 3 or (k == 1 and world <= 4):
+            if world > 1 and (k == 3 or (k == 1 and world <= 4)):
                 assert sq == 2, f"world {world} case {k}: {sq} sharded quotients"
+            if world == 1:
+                assert sq == 0, f"world 1 case {k}: {sq} sharded quotients"
 
 
 def test_dist_stark_prove_world1_rccl(stark_reference):

@@ -1431,6 +1431,10 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
       static const int env_nfuse = env_int("SG_MERKLE_NODE_FUSE", 3);
       static const int env_nbs = env_int("SG_MERKLE_NODE_BS", 256);  // A/B knob: 256 or 512
       kind = env_nbs == 512 ? 6 : 2; bs = env_nbs == 512 ? 512u : 256u; fuse = env_nfuse;
+      // SG_MERKLE_NODE_PIPE=1: blocks walk several groups, the next group's children loaded while
+      // the current one hashes (k_merkle_nodes_pipe; A/B knob)
+      static const int env_pipe = env_int("SG_MERKLE_NODE_PIPE", 0);
+      if (env_pipe && kind == 2 && count % 256 == 0 && level + fuse - 1 < logn) kind = 9;
       if (count < bs) {
         kind = 2;
         bs = (unsigned)count;  // a power of two (tree levels)

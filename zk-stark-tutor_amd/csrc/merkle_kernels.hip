@@ -6,6 +6,8 @@
 // (74 -> 104 for the leaf-pair kernel, 6 -> 4 waves per SIMD) for per-wave instruction-level
 // parallelism: 2^25 tree 2.5 % faster (profiles/r03_ab_merkle_max_ilp.log).  The NTT and quad-lane
 // kernels stay on the default scheduler (max-ILP spills them).
+#include <cstdlib>
+
 #include "merkle_dev.hpp"
 
 namespace sg {
@@ -100,8 +102,8 @@ __global__ __launch_bounds__(MAXB) void k_merkle_leaf_pairs(MerkleArgs a) {
     // 32-byte leaf pair and 128-byte digest pair move as whole lines (stored one compression apart,
     // the digest halves were written back to HBM as separate partial lines: 1.19x the algorithmic
     // bytes in the PMC pass)
-    fe v0 = leaf_value<FOLD>(a, 2 * p);
-    const fe v1 = leaf_value<FOLD>(a, 2 * p + 1);
+    fe v0, v1;
+    leaf_value_pair<FOLD>(a, 2 * p, v0, v1);
     // keep the second leaf's read beside the first: the first compression's input is tied to it
     // (the scheduler would sink the read past that compression to save 4 VGPRs, re-touching each
     // lane pair's line ~2000 instructions later)
@@ -145,6 +147,63 @@ __global__ __launch_bounds__(MAXB) void k_merkle_leaf_pairs(MerkleArgs a) {
   }
 }
 
+// Node levels as k_merkle_levels<false, MAXB>, but each block walks groups g = blockIdx.x,
+// blockIdx.x + gridDim.x, ... (MAXB first-level nodes and their fused levels each) and issues the
+// NEXT group's child loads before hashing the current one: the 128 B of children per lane arrive
+// while the lane compresses, instead of every block starting with a full HBM round trip (the SQ
+// pass of the one-group kernel shows its waves parked on s_waitcnt / barriers 36 % of their
+// lifetime, against 25 % for the leaf kernel).  groups = first_count / MAXB (host-checked exact).
+template <int MAXB>
+__global__ __launch_bounds__(MAXB) void k_merkle_nodes_pipe(MerkleArgs a, uint64_t groups) {
+  __shared__ uint64_t sm[8][MAXB];
+  const uint32_t tid = threadIdx.x;
+  uint64_t* __restrict__ tree = merkle_tree_ptr(a);
+  const uint64_t* child = tree + a.off[0] * 8;
+  uint64_t nl[8], nr[8];
+  uint64_t g = blockIdx.x;
+  if (g < groups) {
+    const uint64_t idx = g * MAXB + tid;
+    ld_digest(child + (2 * idx) * 8, nl);
+    ld_digest(child + (2 * idx + 1) * 8, nr);
+  }
+  for (; g < groups; g += gridDim.x) {
+    uint64_t l[8], r[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      l[i] = nl[i];
+      r[i] = nr[i];
+    }
+    const uint64_t gn = g + gridDim.x;
+    if (gn < groups) {
+      const uint64_t idxn = gn * MAXB + tid;
+      ld_digest(child + (2 * idxn) * 8, nl);
+      ld_digest(child + (2 * idxn + 1) * 8, nr);
+    }
+    uint64_t d[8];
+    blake2b_node(l, r, d);
+    st_digest(tree + (a.off[1] + g * MAXB + tid) * 8, d);
+    uint32_t count = MAXB;
+    for (int lev = 1; lev < a.fuse; ++lev) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) sm[i][tid] = d[i];
+      __syncthreads();
+      count >>= 1;
+      if (tid < count) {
+        uint64_t cl[8], cr[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const ulonglong2 lr = *reinterpret_cast<const ulonglong2*>(&sm[i][2 * tid]);
+          cl[i] = lr.x;
+          cr[i] = lr.y;
+        }
+        blake2b_node(cl, cr, d);
+        st_digest(tree + (a.off[lev + 1] + g * count + tid) * 8, d);
+      }
+      __syncthreads();
+    }
+  }
+}
+
 hipError_t launch_merkle_lanes(int kind, bool fold, dim3 grid, unsigned bs, hipStream_t s, const MerkleArgs& a) {
   switch (kind) {
     case 0:
@@ -156,6 +215,17 @@ hipError_t launch_merkle_lanes(int kind, bool fold, dim3 grid, unsigned bs, hipS
       else hipLaunchKernelGGL((k_merkle_levels<true, 1024>), grid, dim3(bs), 0, s, a);
       break;
     case 2: hipLaunchKernelGGL((k_merkle_levels<false, 256>), grid, dim3(bs), 0, s, a); break;
+    case 9: {
+      // pipelined node levels: grid.x = the groups, run by at most `cap` resident blocks per tree
+      const uint64_t groups = grid.x;
+      static const uint64_t cap = [] {
+        const char* v = getenv("SG_MERKLE_NODE_PIPE_BLOCKS");  // blocks per launch row (A/B knob)
+        return (uint64_t)(v && atoi(v) > 0 ? atoi(v) : 1024);
+      }();
+      dim3 g2((unsigned)(groups < cap ? groups : cap), grid.y);
+      hipLaunchKernelGGL((k_merkle_nodes_pipe<256>), g2, dim3(bs), 0, s, a, groups);
+      break;
+    }
     case 6: hipLaunchKernelGGL((k_merkle_levels<false, 512>), grid, dim3(bs), 0, s, a); break;
     case 4:
       if (fold) hipLaunchKernelGGL((k_merkle_levels<true, 512, true>), grid, dim3(bs), 0, s, a);

@@ -868,8 +868,10 @@ void prove_transition_quotients(sg_ctx* ctx, const sg_stark& st, const std::vect
   // the sharded coset work applies when every constraint carries the factored Rescue form, all
   // share one coset size Ls on the fast path (L <= D, deg Z < len), and Ls splits over the ranks;
   // the decision depends only on inputs every rank shares, so all ranks take the same branch
+  // (one rank: its "shard" is the whole coset, which the replicated path evaluates with half the
+  // transforms -- the next-row values are a rotation there)
   uint64_t Ls = 0;
-  bool sharded = dd && !tcs.empty();
+  bool sharded = dd && dist_world(dd) > 1 && !tcs.empty();
   for (const MPoly* tc : tcs) {
     if (!sharded) break;
     const uint64_t len = symbolic_degree_bound(*tc, Tp - 1) + 1;
