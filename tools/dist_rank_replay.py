@@ -144,11 +144,14 @@ def replay(world, rank, out, steps):
     want = open(os.path.join(out, "proof.bin"), "rb").read()
     assert _prove(wl, nd) == want, "replayed proof bytes differ (first prove)"
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
+    dt = 0.0
     for _ in range(steps):
+        time.sleep(0.1)  # idle gaps separate the proves in a kernel trace (tools/trace_sum.py)
+        t0 = time.perf_counter()
         assert _prove(wl, nd) == want, "replayed proof bytes differ"
-    torch.cuda.synchronize()
-    dt = (time.perf_counter() - t0) / steps
+        torch.cuda.synchronize()
+        dt += time.perf_counter() - t0
+    dt /= steps
     print(f"world {world} rank {rank} alone: {dt * 1e3:.3f} ms/prove (host wall; exchanges replayed from host "
           f"memory through the staged transport); {seq[0]} collectives", flush=True)
     lib.sg_dist_destroy(h)

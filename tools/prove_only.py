@@ -23,11 +23,16 @@ def main():
     wl.step()
     torch.cuda.synchronize(dev)
     time.sleep(0.05)  # a gap that separates the warmup from the traced steps
-    t0 = time.perf_counter()
+    gap = os.environ.get("SG_PROVE_GAPS") == "1"  # idle gaps between proves (tools/trace_sum.py)
+    dt = 0.0
     for _ in range(steps):
+        if gap:
+            time.sleep(0.1)
+        t0 = time.perf_counter()
         wl.step()
-    torch.cuda.synchronize(dev)
-    print(f"{(time.perf_counter() - t0) / steps * 1e3:.3f} ms/prove")
+        torch.cuda.synchronize(dev)
+        dt += time.perf_counter() - t0
+    print(f"{dt / steps * 1e3:.3f} ms/prove")
 
 
 if __name__ == "__main__":
