@@ -262,9 +262,10 @@ void sg_dist_destroy(sg_dist* d);
  * Deadline: SG_DIST_TIMEOUT_S at creation (default 300 s) or sg_dist_set_timeout (per rank). */
 int sg_dist_set_timeout(sg_dist* d, double seconds);
 int sg_dist_poisoned(const sg_dist* d); /* 1 when poisoned */
-/* instrumentation: collectives this communicator issued, transition quotients sg_dist_stark_prove
- * computed on run shards (the rest ran replicated) */
-int sg_dist_counters(const sg_dist* d, uint64_t* collectives, uint64_t* sharded_quotients);
+/* instrumentation: collectives this communicator issued, transition quotients and trace columns
+ * whose coset work / interpolation sg_dist_stark_prove ran on run shards (the rest ran replicated) */
+int sg_dist_counters(const sg_dist* d, uint64_t* collectives, uint64_t* sharded_quotients,
+                     uint64_t* sharded_interpolations);
 /* Collective: the codeword size (log2 elements, <= 0: never) at which a sharded FRI commit hands
  * over to the single-GPU rounds (default SG_DIST_FRI_TAIL at creation, else 20).  It decides the
  * collective schedule, so every rank passes the same value; the call all-gathers it and fails

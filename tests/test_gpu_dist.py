@@ -475,20 +475,27 @@ def _stark_checks(nd, world, rank, tmp, cases, gather):
         tr, rc = np.load(os.path.join(tmp, "tr%d.npy" % k)), np.load(os.path.join(tmp, "rc%d.npy" % k))
         # small domains: every FRI round sharded (hand-over size 0); C4: the default hand-over
         nd.set_fri_tail(0 if N < 1000 else 20)
-        before = nd.counters()[1]
+        before = nd.counters()
         got = st.prove(trace, air, bnd, sg.IndependentProofStream(), tr, rc, dist=nd)
-        ok.append((k, got == open(os.path.join(tmp, "proof%d.bin" % k), "rb").read(), nd.counters()[1] - before))
+        after = nd.counters()
+        ok.append((k, got == open(os.path.join(tmp, "proof%d.bin" % k), "rb").read(), after[1] - before[1],
+                   after[2] - before[2]))
     flags = gather(ok)
-    assert all(f for per_rank in flags for (_, f, _) in per_rank), f"world {world}: sharded proof bytes differ: {flags}"
+    assert all(f for per_rank in flags for (_, f, _, _) in per_rank), \
+        f"world {world}: sharded proof bytes differ: {flags}"
     # the transition quotients' coset work ran on run shards (2 constraints) wherever the coset
     # splits over the ranks: C4 (coset 2^18) at every world > 1, the false witness (coset 2^8,
     # redone from the gathered values) at 2 and 4 ranks; one rank runs the replicated path
+    # The trace interpolation's transforms ran on run shards (both register columns) where its
+    # subgroup (order M = D / f) splits: C4 (M = 2^16) at every world > 1.
     for per_rank in flags:
-        for (k, _, sq) in per_rank:
+        for (k, _, sq, si) in per_rank:
             if world > 1 and (k == 3 or (k == 1 and world <= 4)):
                 assert sq == 2, f"world {world} case {k}: {sq} sharded quotients"
+            if world > 1 and k == 3:
+                assert si == 2, f"world {world} case {k}: {si} sharded interpolation columns"
             if world == 1:
-                assert sq == 0, f"world 1 case {k}: {sq} sharded quotients"
+                assert sq == 0 and si == 0, f"world 1 case {k}: {sq} / {si} sharded quotients / columns"
 
 
 def test_dist_stark_prove_world1_rccl(stark_reference):

@@ -60,7 +60,7 @@ struct sg_dist {
   // rounds: part of the collective schedule, so it is agreed by all ranks (sg_dist_set_fri_tail)
   int fri_tail_log = 20;
   // counters (sg_dist_counters): collectives issued, transition quotients computed sharded
-  uint64_t collectives = 0, sharded_quotients = 0;
+  uint64_t collectives = 0, sharded_quotients = 0, sharded_interpolations = 0;
   ~sg_dist() {
     if (comm) (void)ncclCommDestroy(comm);
     if (hsend) (void)hipHostFree(hsend);
@@ -734,6 +734,7 @@ sg_ctx* dist_ctx(sg_dist* d) { return d->ctx; }
 int dist_world(const sg_dist* d) { return d->G; }
 int dist_rank(const sg_dist* d) { return d->g; }
 void dist_count_sharded_quotient(sg_dist* d) { ++d->sharded_quotients; }
+void dist_count_sharded_interpolation(sg_dist* d, uint64_t columns) { d->sharded_interpolations += columns; }
 bool dist_can_shard(uint64_t n, int G) {
   if (n < 2 || (n & (n - 1)) || G < 1 || (G & (G - 1))) return false;
   const uint64_t n1 = (uint64_t)1 << (ilog2_exact(n) / 2), n2 = n / n1;
@@ -843,10 +844,12 @@ extern "C" int sg_dist_set_timeout(sg_dist* d, double seconds) {
 
 extern "C" int sg_dist_poisoned(const sg_dist* d) { return d && d->dead ? 1 : 0; }
 
-extern "C" int sg_dist_counters(const sg_dist* d, uint64_t* collectives, uint64_t* sharded_quotients) {
-  if (!d || !collectives || !sharded_quotients) return SG_ERR_INVALID;
+extern "C" int sg_dist_counters(const sg_dist* d, uint64_t* collectives, uint64_t* sharded_quotients,
+                                uint64_t* sharded_interpolations) {
+  if (!d || !collectives || !sharded_quotients || !sharded_interpolations) return SG_ERR_INVALID;
   *collectives = d->collectives;
   *sharded_quotients = d->sharded_quotients;
+  *sharded_interpolations = d->sharded_interpolations;
   return SG_OK;
 }
 

@@ -38,6 +38,7 @@ void dist_poison(sg_dist* d, const std::string& why);
 int dist_world(const sg_dist* d);
 int dist_rank(const sg_dist* d);
 void dist_count_sharded_quotient(sg_dist* d);
+void dist_count_sharded_interpolation(sg_dist* d, uint64_t columns);
 // n splits over G ranks for both the forward transform (sg_dist_plan) and the inverse
 bool dist_can_shard(uint64_t n, int G);
 // sg_dist_plan: n = N1 N2, N1 = 2^floor(log2 n / 2); run shards hold N1 runs of N2 / G elements
@@ -46,6 +47,10 @@ void dist_plan(uint64_t n, int G, uint64_t& n1, uint64_t& n2);
 // this rank's run shard [N1][N2 / G] (its column shard gathered first)
 void dist_lde_replicated(sg_dist* d, const fe& gen, uint64_t n, const fe& offset, const fe* coeffs, uint64_t len,
                          fe* runs);
+// fft/ntt.rs:7-68 over the ranks (a root of order exactly n): column shard [N1/G][row_len] in, run
+// shard [N1][N2/G] out; the inverse from a run shard into the column shard [N1/G][N2]
+void dist_ntt(sg_dist* d, const fe& root, const fe* cols, uint64_t row_len, uint64_t n, fe* runs);
+void dist_intt(sg_dist* d, const fe& root, const fe* runs, uint64_t n, fe* cols);
 // coset interpolation of a run-sharded codeword of n points on offset * <gen> into the column shard
 // [N1/G][N2] of its coefficients (distributed INTT + offset^-i)
 void dist_coset_interpolate(sg_dist* d, const fe& gen, uint64_t n, const fe& offset, const fe* runs, fe* cols);

@@ -401,8 +401,8 @@ const fe* interp_kernel(sg_ctx* ctx, const fe& q, uint64_t D, int logf) {
 // decimation of the geometric interpolation: the largest f = 2^logf with n <= D / f, so the
 // interpolant (degree < n) is recovered from its values on the subgroup of order M = D / f
 // (SG_GEO_DECIMATE=0: the full-group form, f = 1)
-int geo_logf(uint64_t n, uint64_t D) {
-  const char* e = getenv("SG_GEO_DECIMATE");
+int geo_logf(uint64_t n, uint64_t D, bool env = true) {
+  const char* e = env ? getenv("SG_GEO_DECIMATE") : nullptr;
   if (e && e[0] == '0') return 0;
   // M = D / f >= n, M >= 64, M / f >= 1 (rows of M / f inputs), f <= 16
   const int logD = ilog2_exact(D);
@@ -412,37 +412,22 @@ int geo_logf(uint64_t n, uint64_t D) {
 }
 }  // namespace
 
-std::vector<DPoly> interpolate_geometric_batch_dev(sg_ctx* ctx, const fe& q, uint64_t D, const fe* y, uint64_t ys,
-                                                   size_t cols, uint64_t n, GeoInterpCache* cache) {
-  SG_REQUIRE(n <= D, "interpolate: more points than the order of the root");
-  SG_REQUIRE(D && (D & (D - 1)) == 0, "interpolate: root order must be a power of two");
-  std::vector<DPoly> outs;
-  if (n <= 1 || n == D) {
-    for (size_t c = 0; c < cols; ++c) {
-      if (n == 0) {
-        outs.emplace_back();
-      } else if (n == 1) {
-        outs.push_back(dpoly_copy(ctx, y + c * ys, 1));
-      } else {
-        DPoly out = dpoly_alloc(ctx, D);
-        intt_sized(ctx, q, y + c * ys, ilog2_exact(D), out.p());
-        outs.push_back(std::move(out));
-      }
-    }
-    return outs;
-  }
+GeoPlan geo_plan(sg_ctx* ctx, const fe& q, uint64_t D, uint64_t n, GeoInterpCache* cache, bool env) {
+  SG_REQUIRE(n > 1 && n < D && D && (D & (D - 1)) == 0, "geo_plan: 1 < n < D, D a power of two");
+  GeoPlan P;
   const int logD = ilog2_exact(D);
-  const int logf = geo_logf(n, D);
+  const int logf = geo_logf(n, D, env);
   const uint64_t M = D >> logf, f = (uint64_t)1 << logf;
-  const int logM = logD - logf;
   const fe qf = fe_pow(q, f);  // order M
+  P.logf = logf;
+  P.M = M;
+  P.qf = qf;
   // Z(q^(f k)) (k < M) and 1 / Z'(q^i) (i < n): they depend on the domain only, so the context keeps
   // them like a twiddle plan (else `cache` shares them between the calls of one prove)
   const std::vector<uint64_t> key = {kDomainGeoInterp, fe_lo(q), fe_hi(q), D, n, (uint64_t)logf};
   const fe* Zv = ctx->domain_cache_on() ? static_cast<const fe*>(ctx->domain_table(key)) : nullptr;
   const fe* Zdi = Zv ? Zv + M : nullptr;
-  GeoInterpCache local;
-  GeoInterpCache& zc = cache ? *cache : local;
+  GeoInterpCache& zc = *cache;
   if (!Zv) {
     if (!(zc.n == n && zc.D == D && zc.logf == logf && fe_eq(zc.q, q))) {
       DPoly Z = zerofier_geometric_dev(ctx, q, D, n);
@@ -475,10 +460,44 @@ std::vector<DPoly> interpolate_geometric_batch_dev(sg_ctx* ctx, const fe& q, uin
       ctx->domain_table_put(key, t);
     }
   }
+  P.Zv = Zv;
+  P.Zdi = Zdi;
+  P.Khat = interp_kernel(ctx, q, D, logf);
+  return P;
+}
+
+std::vector<DPoly> interpolate_geometric_batch_dev(sg_ctx* ctx, const fe& q, uint64_t D, const fe* y, uint64_t ys,
+                                                   size_t cols, uint64_t n, GeoInterpCache* cache) {
+  SG_REQUIRE(n <= D, "interpolate: more points than the order of the root");
+  SG_REQUIRE(D && (D & (D - 1)) == 0, "interpolate: root order must be a power of two");
+  std::vector<DPoly> outs;
+  if (n <= 1 || n == D) {
+    for (size_t c = 0; c < cols; ++c) {
+      if (n == 0) {
+        outs.emplace_back();
+      } else if (n == 1) {
+        outs.push_back(dpoly_copy(ctx, y + c * ys, 1));
+      } else {
+        DPoly out = dpoly_alloc(ctx, D);
+        intt_sized(ctx, q, y + c * ys, ilog2_exact(D), out.p());
+        outs.push_back(std::move(out));
+      }
+    }
+    return outs;
+  }
+  const int logD = ilog2_exact(D);
+  GeoInterpCache local;
+  const GeoPlan P = geo_plan(ctx, q, D, n, cache ? cache : &local);
+  const int logf = P.logf;
+  const uint64_t M = P.M, f = (uint64_t)1 << P.logf;
+  const int logM = logD - logf;
+  const fe qf = P.qf;
+  const fe* Zv = P.Zv;
+  const fe* Zdi = P.Zdi;
   // a_i = y_i / Z'(q^i); S(m) = sum_i a_i b[m - i] cyclically, b[j] = 1 / (1 - q^-j).  At m = f k the f
   // residue classes i = f j + r each give a cyclic convolution of length M (root q^f) against the
   // row K_r: their transforms are summed pointwise and share one inverse transform.
-  const fe* Khat = interp_kernel(ctx, q, D, logf);
+  const fe* Khat = P.Khat;
   DevBuf va(ctx, cols * D * sizeof(fe)), S(ctx, cols * M * sizeof(fe));
   if (logf == 0) {
     DevBuf a(ctx, n * sizeof(fe));

@@ -97,6 +97,19 @@ struct GeoInterpCache {
   int logf = 0;     // Zv holds Z(q^(f k)), k < D / f (decimated interpolation, f = 2^logf)
   DevBuf Zv, Zdi;
 };
+// the decimated geometric interpolation's public tables for (q, D, n), 1 < n < D (context-cached):
+// f = 2^logf, M = D / f, qf = q^f (order M), Zv[k] = Z(q^(f k)) (k < M), Zdi[i] = 1 / Z'(q^i) (i < n),
+// Khat = the f rows (M each) of the transformed convolution kernel (f = 1: NTT_D(b), one row)
+struct GeoPlan {
+  int logf = 0;
+  uint64_t M = 0;
+  fe qf;
+  const fe* Zv = nullptr;
+  const fe* Zdi = nullptr;
+  const fe* Khat = nullptr;
+};
+// env = false: ignore SG_GEO_DECIMATE (a sharded prove: every rank must take the same plan)
+GeoPlan geo_plan(sg_ctx* ctx, const fe& q, uint64_t D, uint64_t n, GeoInterpCache* cache, bool env = true);
 // the interpolant of degree < n through (q^i, y_i), i < n <= D (ntt_arithmetics.rs:172-237), length n
 DPoly interpolate_geometric_dev(sg_ctx* ctx, const fe& q, uint64_t D, const fe* y, uint64_t n,
                                 GeoInterpCache* cache = nullptr);

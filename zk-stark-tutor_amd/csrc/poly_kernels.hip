@@ -344,6 +344,32 @@ __global__ __launch_bounds__(kBlock) void k_interp_assemble(fe* __restrict__ V, 
   }
 }
 
+// k_interp_assemble on a column shard [rows][n2] of S (a sharded prove): local element p = r n2 + j
+// is subgroup index k = row0 + r + n1 j; every value is also multiplied by M^-1 (minv = M^-1 R,
+// minv_r2 = M^-1 R^2 for the Montgomery products), so the forward transform with root qf^-1 that
+// follows is the inverse transform
+__global__ __launch_bounds__(kBlock) void k_interp_assemble_cols(fe* __restrict__ V, const fe* __restrict__ y,
+                                                                 uint64_t ys, const fe* __restrict__ Zv,
+                                                                 const fe* __restrict__ S, uint64_t n, uint32_t logf,
+                                                                 uint64_t local, uint64_t total, uint64_t n2,
+                                                                 uint64_t n1, uint64_t row0, const fe* __restrict__ iA,
+                                                                 const fe* __restrict__ iB, fe minv, fe minv_r2) {
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t c = t / local, p = t - c * local;
+    const uint64_t r = p / n2, j = p - r * n2;
+    const uint64_t k = row0 + r + n1 * j, m = k << logf;
+    fe v;
+    if (m < n) {
+      v = mont_mul(ld_fe(y + c * ys + m), minv);
+    } else {
+      fe im = mont_mul(ld_fe(iA + (m & 4095)), ld_fe(iB + (m >> 12)));  // Montgomery(q^-m)
+      v = mont_mul(ld_fe(Zv + k), im);                                   // Zv q^-m
+      v = mont_mul(mont_mul(v, ld_fe(S + t)), minv_r2);                  // * S / M
+    }
+    st_fe(V + t, v);
+  }
+}
+
 // Decimated interpolation, residue classes of a_i = y_i / Z'(q^i) (i < n <= M = D / f):
 // rows[(c f + r) Mf + j] = a_(c, f j + r) for f j + r < n, else 0  (Mf = M / f rows of column c)
 __global__ __launch_bounds__(kBlock) void k_geo_rows(fe* __restrict__ rows, const fe* __restrict__ y, uint64_t ys,
@@ -649,6 +675,17 @@ hipError_t launch_interp_assemble(fe* V, const fe* y, uint64_t ys, const fe* Zv,
   ProfScope ps("interp_assemble", 64 * total, s);
   hipLaunchKernelGGL(k_interp_assemble, dim3((unsigned)grid_for(total)), dim3(kBlock), 0, s, V, y, ys, Zv, S, n, M,
                      (uint32_t)logf, total, iA, iB, r2);
+  return hipGetLastError();
+}
+
+hipError_t launch_interp_assemble_cols(fe* V, const fe* y, uint64_t ys, const fe* Zv, const fe* S, uint64_t n,
+                                       int logf, uint64_t cols, uint64_t rows, uint64_t n2, uint64_t n1, uint64_t row0,
+                                       const fe* iA, const fe* iB, const fe& minv_m, const fe& minv_r2,
+                                       hipStream_t s) {
+  const uint64_t local = rows * n2, total = cols * local;
+  ProfScope ps("interp_assemble", 64 * total, s);
+  hipLaunchKernelGGL(k_interp_assemble_cols, dim3((unsigned)grid_for(total)), dim3(kBlock), 0, s, V, y, ys, Zv, S, n,
+                     (uint32_t)logf, local, total, n2, n1, row0, iA, iB, minv_m, minv_r2);
   return hipGetLastError();
 }
 

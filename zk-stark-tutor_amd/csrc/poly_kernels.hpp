@@ -55,6 +55,12 @@ hipError_t launch_interp_assemble(fe* V, const fe* y, uint64_t ys, const fe* Zv,
                                   int logf, uint64_t cols, const fe* iA, const fe* iB, const fe& r2, hipStream_t s);
 // decimated geometric interpolation (poly.cpp interpolate_geometric_*): residue-class rows of
 // y / Z', the K rows, and the summed pointwise products
+// the same on a column shard [rows][n2] (subgroup index row0 + r + n1 j), every value times M^-1
+// (minv_m = Montgomery(M^-1), minv_r2 = Montgomery(Montgomery(M^-1)))
+hipError_t launch_interp_assemble_cols(fe* V, const fe* y, uint64_t ys, const fe* Zv, const fe* S, uint64_t n,
+                                       int logf, uint64_t cols, uint64_t rows, uint64_t n2, uint64_t n1, uint64_t row0,
+                                       const fe* iA, const fe* iB, const fe& minv_m, const fe& minv_r2,
+                                       hipStream_t s);
 hipError_t launch_geo_rows(fe* rows, const fe* y, uint64_t ys, const fe* Zdi, uint64_t n, int logf, uint64_t M,
                            uint64_t cols, const fe& r2, hipStream_t s);
 hipError_t launch_geo_krows(fe* out, const fe* b, int logf, uint64_t M, uint64_t D, hipStream_t s);

@@ -699,9 +699,94 @@ struct ProveAlgebra {
   std::vector<DPoly> wrapped;          // products that wrap the omicron domain (alive for the combination)
 };
 
+// interpolate_geometric_batch_dev (ntt_arithmetics.rs:172-237 on q^0..q^(n-1)) with its transforms
+// on run shards: the f residue-class rows of every column (gathered from the replicated values as
+// column shards) go through the distributed NTT, the pointwise products with the kernel rows and
+// their sum run on the run shards, the inverse transform of the sum lands as column shards, the
+// subgroup values are assembled there (scaled by 1/M) and one more distributed transform (root
+// qf^-1) gives the coefficients as run shards, all-gathered into every rank's polynomial.  The
+// public tables are the replicated path's (every rank builds them locally: no collective); the
+// kernel rows are sliced to the rank's run shards.  Returns false (nothing done) where the plan
+// does not split over the ranks; the caller then runs the replicated path.
+bool interpolate_geometric_batch_dist(sg_dist* dd, const fe& q, uint64_t D, const fe* y, uint64_t ys, size_t cols,
+                                      uint64_t n, std::vector<DPoly>& outs, std::vector<DevBuf>& keep) {
+  sg_ctx* ctx = dist_ctx(dd);
+  const int G = dist_world(dd);
+  if (G < 2 || n <= 1 || n >= D) return false;
+  GeoInterpCache local;
+  const GeoPlan P = geo_plan(ctx, q, D, n, &local, /*env=*/false);
+  const uint64_t M = P.M, f = (uint64_t)1 << P.logf, Mf = M >> P.logf;
+  if (P.logf < 1 || !dist_can_shard(M, G)) return false;
+  uint64_t n1, n2;
+  dist_plan(M, G, n1, n2);
+  const uint64_t rows = n1 / (uint64_t)G, Ml = M / (uint64_t)G, row0 = (uint64_t)dist_rank(dd) * rows;
+  const uint64_t row_len = std::max<uint64_t>((Mf + n1 - 1) / n1, 1);
+  // residue-class rows of a_i = y_i / Z'(q^i) (replicated: cols * M elements), then their transforms
+  DevBuf rowsbuf(ctx, cols * M * sizeof(fe));
+  SG_HIP(launch_geo_rows(rowsbuf.as<fe>(), y, ys, P.Zdi, n, P.logf, M, cols, fe_r2(), ctx->stream));
+  DevBuf A(ctx, cols * f * Ml * sizeof(fe)), colsbuf(ctx, rows * row_len * sizeof(fe));
+  for (uint64_t t = 0; t < cols * f; ++t) {
+    SG_HIP(launch_gather_cols(colsbuf.as<fe>(), rowsbuf.as<fe>() + t * Mf, Mf, rows, row_len, n1, row0, ctx->stream));
+    dist_ntt(dd, P.qf, colsbuf.as<fe>(), row_len, M, A.as<fe>() + t * Ml);
+  }
+  // the kernel rows on this rank's run shards ([r][Ml], kept with the domain tables)
+  std::vector<uint64_t> kkey = {kDomainGeoInterp, fe_lo(q), fe_hi(q), D, (uint64_t)P.logf, 0xB0B};
+  const fe* K = nullptr;
+  {
+    std::vector<uint64_t> key = kkey;
+    key.insert(key.begin(), kDomainShard);
+    key.push_back((uint64_t)G);
+    key.push_back((uint64_t)dist_rank(dd));
+    const bool kept = ctx->domain_cache_on();
+    if (kept) K = static_cast<const fe*>(ctx->domain_table(key));
+    if (!K) {
+      fe* out = nullptr;
+      void* tbl = nullptr;
+      if (kept) {
+        SG_HIP(hipMalloc(&tbl, f * Ml * sizeof(fe)));
+        out = static_cast<fe*>(tbl);
+      } else {
+        keep.emplace_back(ctx, f * Ml * sizeof(fe));
+        out = keep.back().as<fe>();
+      }
+      try {
+        for (uint64_t r = 0; r < f; ++r) dist_take_runs(dd, P.Khat + r * M, M, out + r * Ml);
+      } catch (...) {
+        if (tbl) (void)hipFree(tbl);
+        throw;
+      }
+      if (kept) ctx->domain_table_put(key, tbl);
+      K = out;
+    }
+  }
+  DevBuf Shat(ctx, cols * Ml * sizeof(fe)), Scol(ctx, cols * Ml * sizeof(fe));
+  SG_HIP(launch_geo_dot(Shat.as<fe>(), A.as<fe>(), K, P.logf, Ml, cols, fe_r2(), ctx->stream));
+  for (size_t c = 0; c < cols; ++c) dist_intt(dd, P.qf, Shat.as<fe>() + c * Ml, M, Scol.as<fe>() + c * Ml);
+  // P(q^(f k)) / M on the column shards, then the coefficients (run shards) and every rank's copy
+  const fe *iA, *iB;
+  pow_tables2(ctx, fe_inv(q), D, &iA, &iB);
+  const fe minv_m = to_mont(fe_inv(fe_from_u64(M)));
+  DevBuf V(ctx, cols * Ml * sizeof(fe)), runs(ctx, Ml * sizeof(fe));
+  SG_HIP(launch_interp_assemble_cols(V.as<fe>(), y, ys, P.Zv, Scol.as<fe>(), n, P.logf, cols, rows, n2, n1, row0, iA, iB,
+                                     minv_m, to_mont(minv_m), ctx->stream));
+  const fe qfi = fe_inv(P.qf);
+  for (size_t c = 0; c < cols; ++c) {
+    dist_ntt(dd, qfi, V.as<fe>() + c * Ml, n2, M, runs.as<fe>());
+    DPoly out = dpoly_alloc(ctx, D);
+    dist_gather_runs(dd, runs.as<fe>(), M, out.p());
+    if (M < D) SG_HIP(hipMemsetAsync(out.p() + M, 0, (D - M) * sizeof(fe), ctx->stream));
+    out.len = n;
+    outs.push_back(std::move(out));
+  }
+  dist_count_sharded_interpolation(dd, cols);
+  return true;
+}
+
 // randomized trace (stark.rs:285-324): columns gathered on the device, geometric interpolation
+// With `dd` (two ranks or more), the interpolation's transforms run on run shards
+// (interpolate_geometric_batch_dist) where its plan splits over the ranks.
 void prove_trace_polys(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows, const fe* d_trace_rand,
-                       ProveAlgebra& A) {
+                       ProveAlgebra& A, sg_dist* dd = nullptr) {
   const size_t m = st.m;
   const uint64_t D = st.D, Tp = A.Tp;
   // randomized trace (stark.rs:285-301), columns on the device
@@ -713,7 +798,9 @@ void prove_trace_polys(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_
       SG_HIP(launch_gather_stride(cols.p() + s * Tp, d_trace + s, rows, m, ctx->stream));
       SG_HIP(launch_gather_stride(cols.p() + s * Tp + rows, d_trace_rand + s, st.num_randomizers, m, ctx->stream));
     }
-    trace_polys = interpolate_geometric_batch_dev(ctx, st.omicron, D, cols.p(), Tp, m, Tp);
+    std::vector<DevBuf> keep;
+    if (!(dd && interpolate_geometric_batch_dist(dd, st.omicron, D, cols.p(), Tp, m, Tp, trace_polys, keep)))
+      trace_polys = interpolate_geometric_batch_dev(ctx, st.omicron, D, cols.p(), Tp, m, Tp);
   }
 }
 
@@ -1235,7 +1322,7 @@ void stark_prove_dist(sg_dist* dd, const sg_stark& st, const fe* d_trace, size_t
   fork_forests(m, m + 1);
   ProveAlgebra A;
   A.Tp = Tp;
-  prove_trace_polys(ctx, st, d_trace, rows, d_trace_rand, A);
+  prove_trace_polys(ctx, st, d_trace, rows, d_trace_rand, A, dd);
   prove_boundary_quotients(ctx, st, bnd, A);
   mark("dist_algebra_boundary");
   // boundary-quotient codewords (stark.rs:364-386), their forests on the side stream

@@ -136,7 +136,7 @@ PROTOTYPES = {
     "sg_dist_destroy": (None, [_vp]),
     "sg_dist_set_timeout": (ctypes.c_int, [_vp, ctypes.c_double]),
     "sg_dist_poisoned": (ctypes.c_int, [_vp]),
-    "sg_dist_counters": (ctypes.c_int, [_vp, _P(ctypes.c_uint64), _P(ctypes.c_uint64)]),
+    "sg_dist_counters": (ctypes.c_int, [_vp, _P(ctypes.c_uint64), _P(ctypes.c_uint64), _P(ctypes.c_uint64)]),
     "sg_dist_set_fri_tail": (ctypes.c_int, [_vp, ctypes.c_int]),
     "sg_dist_plan": (ctypes.c_int, [_sz, ctypes.c_int, _P(_sz), _P(_sz)]),
     "sg_dist_ntt": (ctypes.c_int, [_vp, sg_fe, _vp, _sz, _sz, _vp]),

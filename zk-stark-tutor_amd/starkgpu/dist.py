@@ -475,11 +475,12 @@ class NativeDist:
         """Deadline of one host wait inside a communicator call (sg_dist_set_timeout)."""
         self.ctx.check(self._lib.sg_dist_set_timeout(self.handle, float(seconds)))
 
-    def counters(self) -> Tuple[int, int]:
-        """(collectives issued, transition quotients computed on run shards) (sg_dist_counters)."""
-        a, b = ctypes.c_uint64(), ctypes.c_uint64()
-        self.ctx.check(self._lib.sg_dist_counters(self.handle, ctypes.byref(a), ctypes.byref(b)))
-        return a.value, b.value
+    def counters(self) -> Tuple[int, int, int]:
+        """(collectives issued, transition quotients and trace columns whose coset work /
+        interpolation ran on run shards) (sg_dist_counters)."""
+        a, b, c = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        self.ctx.check(self._lib.sg_dist_counters(self.handle, ctypes.byref(a), ctypes.byref(b), ctypes.byref(c)))
+        return a.value, b.value, c.value
 
     @property
     def poisoned(self) -> bool:
