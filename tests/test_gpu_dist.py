@@ -486,12 +486,14 @@ def _stark_checks(nd, world, rank, tmp, cases, gather):
     # the transition quotients' coset work ran on run shards (2 constraints) wherever the coset
     # splits over the ranks: C4 (coset 2^18) at every world > 1, the false witness (coset 2^8,
     # redone from the gathered values) at 2 and 4 ranks; one rank runs the replicated path
-    # The trace interpolation's transforms ran on run shards (both register columns) where its
-    # subgroup (order M = D / f) splits: C4 (M = 2^16) at every world > 1.
+    # The boundary quotients' division (order 2^16 at C4, 2^6 for case 1) likewise, and the trace
+    # interpolation's transforms (both register columns) where its subgroup (order M = D / f)
+    # splits: C4 (M = 2^16) at every world > 1.
+    want_sq = {(3, 2): 4, (3, 4): 4, (3, 8): 4, (1, 2): 4, (1, 4): 2}
     for per_rank in flags:
         for (k, _, sq, si) in per_rank:
-            if world > 1 and (k == 3 or (k == 1 and world <= 4)):
-                assert sq == 2, f"world {world} case {k}: {sq} sharded quotients"
+            if (k, world) in want_sq:
+                assert sq == want_sq[(k, world)], f"world {world} case {k}: {sq} sharded quotients"
             if world > 1 and k == 3:
                 assert si == 2, f"world {world} case {k}: {si} sharded interpolation columns"
             if world == 1:

@@ -282,6 +282,47 @@ DPoly fast_multiply_dev(sg_ctx* ctx, fe root, uint64_t root_order, const fe* a, 
   return out;
 }
 
+const fe* divisor_inverse_values(sg_ctx* ctx, const DivPlan& pl, const fe& offset, const fe* rhs, uint64_t lr,
+                                 const fe* rhs_host, std::vector<DevBuf>* keep) {
+  if (keep && !ctx->domain_cache_on()) {  // recomputed per call, owned by the caller's scope
+    DevBuf vr;
+    uint64_t nr;
+    ref_inner_ntt(ctx, pl.root, pl.order, rhs, lr, &offset, vr, nr, rhs_host);
+    keep->emplace_back(ctx, pl.order * sizeof(fe));
+    dev_div(ctx, keep->back().as<fe>(), nullptr, vr.as<fe>(), pl.order);
+    host_wait(ctx, ctx->stream);
+    check_div_zero(ctx);
+    return keep->back().as<fe>();
+  }
+  // a small divisor known on the host (a boundary zerofier: public): 1 / its coset values is
+  // kept in the context, keyed by its coefficients and the coset, so the division is a product
+  std::vector<uint64_t> key = {kDomainDivisorInverse, pl.order, fe_lo(pl.root), fe_hi(pl.root), fe_lo(offset),
+                               fe_hi(offset), lr};
+  for (uint64_t i = 0; i < lr; ++i) {
+    key.push_back(fe_lo(rhs_host[i]));
+    key.push_back(fe_hi(rhs_host[i]));
+  }
+  const fe* inv = static_cast<const fe*>(ctx->domain_table(key));
+  if (!inv) {
+    DevBuf vr;
+    uint64_t nr;
+    ref_inner_ntt(ctx, pl.root, pl.order, rhs, lr, &offset, vr, nr, rhs_host);
+    void* t = nullptr;
+    SG_HIP(hipMalloc(&t, pl.order * sizeof(fe)));
+    dev_div(ctx, static_cast<fe*>(t), nullptr, vr.as<fe>(), pl.order);
+    host_wait(ctx, ctx->stream);
+    try {
+      check_div_zero(ctx);  // a zero divisor is reported now and the table is not kept
+    } catch (...) {
+      (void)hipFree(t);
+      throw;
+    }
+    ctx->domain_table_put_bounded(key, t);
+    inv = static_cast<const fe*>(t);
+  }
+  return inv;
+}
+
 DPoly fast_coset_divide_dev(sg_ctx* ctx, fe root, uint64_t root_order, const fe& offset, const fe* lhs, uint64_t ll,
                             const fe* rhs, uint64_t lr, int64_t rhs_degree, const fe* rhs_host, int64_t lhs_degree) {
   check_root(root, root_order);
@@ -300,33 +341,9 @@ DPoly fast_coset_divide_dev(sg_ctx* ctx, fe root, uint64_t root_order, const fe&
   DevBuf vl, vr;
   uint64_t nl, nr;
   ref_inner_ntt(ctx, pl.root, pl.order, lhs, ll, &offset, vl, nl);
-  if (rhs_host && lr <= 64 && ctx->domain_cache_on()) {
-    // a small divisor known on the host (a boundary zerofier: public): 1 / its coset values is
-    // kept in the context, keyed by its coefficients and the coset, so the division is a product
-    std::vector<uint64_t> key = {kDomainDivisorInverse, pl.order, fe_lo(pl.root), fe_hi(pl.root), fe_lo(offset),
-                                 fe_hi(offset), lr};
-    for (uint64_t i = 0; i < lr; ++i) {
-      key.push_back(fe_lo(rhs_host[i]));
-      key.push_back(fe_hi(rhs_host[i]));
-    }
-    const fe* inv = static_cast<const fe*>(ctx->domain_table(key));
-    if (!inv) {
-      ref_inner_ntt(ctx, pl.root, pl.order, rhs, lr, &offset, vr, nr, rhs_host);
-      void* t = nullptr;
-      SG_HIP(hipMalloc(&t, pl.order * sizeof(fe)));
-      dev_div(ctx, static_cast<fe*>(t), nullptr, vr.as<fe>(), pl.order);
-      host_wait(ctx, ctx->stream);
-      try {
-        check_div_zero(ctx);  // a zero divisor is reported now and the table is not kept
-      } catch (...) {
-        (void)hipFree(t);
-        throw;
-      }
-      ctx->domain_table_put_bounded(key, t);
-      inv = static_cast<const fe*>(t);
-    }
-    return coset_divide_finish(ctx, pl, offset, vl.as<fe>(), inv, true);
-  }
+  if (rhs_host && lr <= 64 && ctx->domain_cache_on())
+    return coset_divide_finish(ctx, pl, offset, vl.as<fe>(), divisor_inverse_values(ctx, pl, offset, rhs, lr, rhs_host),
+                               true);
   ref_inner_ntt(ctx, pl.root, pl.order, rhs, lr, &offset, vr, nr, rhs_host);
   return coset_divide_finish(ctx, pl, offset, vl.as<fe>(), vr.as<fe>());
 }

@@ -75,6 +75,11 @@ void ref_inner_ntt(sg_ctx* ctx, const fe& root, uint64_t order, const fe* p, uin
 // rhs_is_inverse: rhs_v holds 1 / (the divisor's coset values), so the division is a product
 DPoly coset_divide_finish(sg_ctx* ctx, const DivPlan& pl, const fe& offset, fe* lhs_v, const fe* rhs_v,
                           bool rhs_is_inverse = false);
+// 1 / the coset values (order pl.order, offset) of a small divisor known on the host (<= 64
+// coefficients), kept in the context's bounded content-keyed tables (with `keep` and
+// SG_NO_DOMAIN_CACHE=1: recomputed into a buffer `keep` owns); a zero value throws
+const fe* divisor_inverse_values(sg_ctx* ctx, const DivPlan& pl, const fe& offset, const fe* rhs, uint64_t lr,
+                                 const fe* rhs_host, std::vector<DevBuf>* keep = nullptr);
 // ntt_arithmetics.rs:239-310
 // rhs_degree / lhs_degree: the divisor's / dividend's degree when the caller knows it (-1 = zero
 // polynomial), -2 = query the device

@@ -804,8 +804,13 @@ void prove_trace_polys(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_
   }
 }
 
-// boundary quotients (stark.rs:326-362)
-void prove_boundary_quotients(sg_ctx* ctx, const sg_stark& st, const std::vector<Boundary>& bnd, ProveAlgebra& A) {
+// boundary quotients (stark.rs:326-362).  With `dd` (two ranks or more) a quotient whose division
+// plan splits over the ranks runs its coset work on run shards: the numerator's distributed LDE on
+// the coset, the product by 1 / the divisor's coset values (public: computed whole by every rank,
+// sliced), the distributed coset interpolation and one all-gather -- the reference's truncated
+// quotient, the same coefficients as fast_coset_divide_dev.
+void prove_boundary_quotients(sg_ctx* ctx, const sg_stark& st, const std::vector<Boundary>& bnd, ProveAlgebra& A,
+                              sg_dist* dd = nullptr) {
   const size_t m = st.m;
   const uint64_t D = st.D;
   const fe g = st.generator;
@@ -827,9 +832,37 @@ void prove_boundary_quotients(sg_ctx* ctx, const sg_stark& st, const std::vector
       nums.emplace_back(diffs.back().p(), diffs.back().len);
     }
     const std::vector<int64_t> dnum = dev_degrees(ctx, nums);
-    for (size_t s = 0; s < m; ++s)
+    for (size_t s = 0; s < m; ++s) {
+      const int64_t dz = hp_degree(bz[s]);
+      // (the branch depends only on what every rank shares -- never on a per-rank environment)
+      if (dd && dist_world(dd) > 1 && dz >= 0 && dnum[s] >= dz && bz[s].size() <= 64) {
+        const DivPlan pl = coset_divide_plan(st.omicron, D, dnum[s], dz);
+        if (diffs[s].len <= pl.order && dist_can_shard(pl.order, dist_world(dd))) {
+          const uint64_t nl = pl.order / (uint64_t)dist_world(dd);
+          std::vector<DevBuf> keep;
+          const fe* inv = divisor_inverse_values(ctx, pl, g, Zs[s].p(), Zs[s].len, bz[s].data(), &keep);
+          std::vector<uint64_t> key = {kDomainDivisorInverse, pl.order, fe_lo(pl.root), fe_hi(pl.root), fe_lo(g),
+                                       fe_hi(g), bz[s].size()};
+          for (const fe& c : bz[s]) {
+            key.push_back(fe_lo(c));
+            key.push_back(fe_hi(c));
+          }
+          const fe* inv_shard = shard_table(dd, key, inv, pl.order, keep);
+          DevBuf vals(ctx, nl * sizeof(fe)), cols(ctx, nl * sizeof(fe));
+          dist_lde_replicated(dd, pl.root, pl.order, g, diffs[s].p(), diffs[s].len, vals.as<fe>());
+          dev_mul(ctx, vals.as<fe>(), vals.as<fe>(), inv_shard, nl);
+          dist_coset_interpolate(dd, pl.root, pl.order, g, vals.as<fe>(), cols.as<fe>());
+          DPoly full = dpoly_alloc(ctx, pl.order);
+          dist_gather_columns(dd, cols.as<fe>(), pl.order, full.p());
+          full.len = std::min(pl.result_len, pl.order);  // the reference's truncation (coset_divide_finish)
+          bqs.push_back(std::move(full));
+          dist_count_sharded_quotient(dd);
+          continue;
+        }
+      }
       bqs.push_back(fast_coset_divide_dev(ctx, st.omicron, D, g, diffs[s].p(), diffs[s].len, Zs[s].p(), Zs[s].len,
-                                          hp_degree(bz[s]), bz[s].data(), dnum[s]));
+                                          dz, bz[s].data(), dnum[s]));
+    }
   }
 }
 
@@ -1323,7 +1356,7 @@ void stark_prove_dist(sg_dist* dd, const sg_stark& st, const fe* d_trace, size_t
   ProveAlgebra A;
   A.Tp = Tp;
   prove_trace_polys(ctx, st, d_trace, rows, d_trace_rand, A, dd);
-  prove_boundary_quotients(ctx, st, bnd, A);
+  prove_boundary_quotients(ctx, st, bnd, A, dd);
   mark("dist_algebra_boundary");
   // boundary-quotient codewords (stark.rs:364-386), their forests on the side stream
   for (size_t s = 0; s < m; ++s) lde(A.bqs[s].p(), A.bqs[s].len, runs[s]);
