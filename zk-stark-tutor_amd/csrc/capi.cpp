@@ -554,15 +554,20 @@ void host_wait(sg_ctx* ctx, hipStream_t s) {
     SG_HIP(hipStreamSynchronize(s));
     return;
   }
+  // a spin like hipStreamSynchronize's own (a sleep would add its timer slack, tens of us, to every
+  // wait of a prove); the watch runs about once per millisecond
   const auto t0 = std::chrono::steady_clock::now();
-  for (uint32_t spins = 0;; ++spins) {
+  auto next = t0;
+  for (;;) {
     const hipError_t q = hipStreamQuery(s);
     if (q == hipSuccess) return;
     if (q != hipErrorNotReady) SG_HIP(q);
-    if ((spins & 63) == 0)
-      ctx->watch(std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
-    if (spins < 4096) __builtin_ia32_pause();
-    else std::this_thread::sleep_for(std::chrono::microseconds(20));
+    const auto now = std::chrono::steady_clock::now();
+    if (now >= next) {
+      ctx->watch(std::chrono::duration<double>(now - t0).count());
+      next = now + std::chrono::milliseconds(1);
+    }
+    __builtin_ia32_pause();
   }
 }
 
