@@ -461,7 +461,7 @@ def stark_reference():
         shutil.rmtree(tmp, ignore_errors=True)
 
 
-def _stark_checks(nd, world, rank, tmp, cases, gather):
+def _stark_checks(nd, world, rank, tmp, cases, gather, sharded_algebra=True):
     """Every case proved with sg_dist_stark_prove on this rank: bytes == expected on every rank."""
     import starkgpu as sg
     ok = []
@@ -492,6 +492,9 @@ def _stark_checks(nd, world, rank, tmp, cases, gather):
     want_sq = {(3, 2): 4, (3, 4): 4, (3, 8): 4, (1, 2): 4, (1, 4): 2}
     for per_rank in flags:
         for (k, _, sq, si) in per_rank:
+            if not sharded_algebra:
+                assert sq == 0 and si == 0, f"world {world} case {k}: algebra sharded although switched off"
+                continue
             if (k, world) in want_sq:
                 assert sq == want_sq[(k, world)], f"world {world} case {k}: {sq} sharded quotients"
             if world > 1 and k == 3:
@@ -515,12 +518,13 @@ def test_dist_stark_prove_world1_rccl(stark_reference):
         nd.close()
 
 
-def _stark_worker(rank, world, port, tmp, cases):
+def _stark_worker(rank, world, port, tmp, cases, shard="1"):
     import torch.distributed as dist
     import starkgpu as sg
     from starkgpu import dist as D
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
+    os.environ["SG_DIST_SHARD_ALGEBRA"] = shard
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         nd = D.NativeDist(sg.Context(0), transport="host")
@@ -530,22 +534,24 @@ def _stark_worker(rank, world, port, tmp, cases):
             dist.all_gather_object(out, a)
             return out
 
-        _stark_checks(nd, world, rank, tmp, cases, gather)
+        _stark_checks(nd, world, rank, tmp, cases, gather, sharded_algebra=shard != "0")
         nd.close()
     finally:
         dist.destroy_process_group()
 
 
 @pytest.mark.timeout(900)
-@pytest.mark.parametrize("world,cases", [(2, (0, 1, 2, 3, 4)), (4, (1, 2, 4)), (8, (0, 1, 2, 3, 4))])
-def test_dist_stark_prove_one_gpu_host_transport(stark_reference, world, cases):
+@pytest.mark.parametrize("world,cases,shard", [(2, (0, 1, 2, 3, 4), "1"), (4, (1, 2, 4), "1"), (8, (0, 1, 2, 3, 4), "1"),
+                                               (2, (1, 3), "0")])
+def test_dist_stark_prove_one_gpu_host_transport(stark_reference, world, cases, shard):
     """Stark::prove (stark.rs:276-562) with the FRI domain sharded over `world` ranks on this box's
-    GPU (host transport over gloo): every rank writes the expected proof bytes, C4 included."""
+    GPU (host transport over gloo): every rank writes the expected proof bytes, C4 included.
+    shard = "0": SG_DIST_SHARD_ALGEBRA=0, the trace-domain algebra replicated (no sharded counts)."""
     import torch.multiprocessing as mp
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
-    mp.spawn(_stark_worker, args=(world, port, stark_reference, cases), nprocs=world, join=True)
+    mp.spawn(_stark_worker, args=(world, port, stark_reference, cases, shard), nprocs=world, join=True)
 
 
 # ----------------------------------------------------------------- failure containment

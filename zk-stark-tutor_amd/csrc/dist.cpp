@@ -59,6 +59,10 @@ struct sg_dist {
   // codeword size (log2 elements) at which a sharded FRI commit hands over to the single-GPU
   // rounds: part of the collective schedule, so it is agreed by all ranks (sg_dist_set_fri_tail)
   int fri_tail_log = 20;
+  // sg_dist_stark_prove shards the trace-domain algebra (transition / boundary quotients, trace
+  // interpolation) from two ranks up; 0 keeps it replicated (SG_DIST_SHARD_ALGEBRA at creation,
+  // agreed by every rank like the FRI hand-over)
+  int shard_algebra = 1;
   // counters (sg_dist_counters): collectives issued, transition quotients computed sharded
   uint64_t collectives = 0, sharded_quotients = 0, sharded_interpolations = 0;
   ~sg_dist() {
@@ -733,6 +737,7 @@ void dist_fri_prove(sg_dist* d, const sg_fri* f, const fe* runs, uint64_t n, con
 sg_ctx* dist_ctx(sg_dist* d) { return d->ctx; }
 int dist_world(const sg_dist* d) { return d->G; }
 int dist_rank(const sg_dist* d) { return d->g; }
+bool dist_shard_algebra(const sg_dist* d) { return d->G > 1 && d->shard_algebra; }
 void dist_count_sharded_quotient(sg_dist* d) { ++d->sharded_quotients; }
 void dist_count_sharded_interpolation(sg_dist* d, uint64_t columns) { d->sharded_interpolations += columns; }
 bool dist_can_shard(uint64_t n, int G) {
@@ -766,6 +771,7 @@ void dist_defaults(sg_dist* d) {
     if (v > 0) d->timeout_s = v;
   }
   if (const char* te = getenv("SG_DIST_FRI_TAIL")) d->fri_tail_log = atoi(te);
+  if (const char* sa = getenv("SG_DIST_SHARD_ALGEBRA")) d->shard_algebra = atoi(sa) != 0;
 }
 
 // all-gathers v over the communicator; every rank throws the same error when the values differ
@@ -799,7 +805,10 @@ extern "C" int sg_dist_create(sg_ctx* ctx, const uint8_t* id, int nranks, int ra
     SG_NCCL(ncclCommInitRank(&d->comm, nranks, u, rank));
   });
   if (rc != SG_OK) return rc;
-  rc = dist_run(d.get(), [&] { agree(d.get(), d->fri_tail_log, "SG_DIST_FRI_TAIL"); });
+  rc = dist_run(d.get(), [&] {
+    agree(d.get(), d->fri_tail_log, "SG_DIST_FRI_TAIL");
+    agree(d.get(), d->shard_algebra, "SG_DIST_SHARD_ALGEBRA");
+  });
   if (rc != SG_OK) return rc;
   *out = d.release();
   return SG_OK;
@@ -821,7 +830,10 @@ extern "C" int sg_dist_create_transport(sg_ctx* ctx, int nranks, int rank, const
     dist_defaults(d.get());
   });
   if (rc != SG_OK) return rc;
-  rc = dist_run(d.get(), [&] { agree(d.get(), d->fri_tail_log, "SG_DIST_FRI_TAIL"); });
+  rc = dist_run(d.get(), [&] {
+    agree(d.get(), d->fri_tail_log, "SG_DIST_FRI_TAIL");
+    agree(d.get(), d->shard_algebra, "SG_DIST_SHARD_ALGEBRA");
+  });
   if (rc != SG_OK) return rc;
   *out = d.release();
   return SG_OK;

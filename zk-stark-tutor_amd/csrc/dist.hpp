@@ -37,6 +37,8 @@ int dist_run(sg_dist* d, const std::function<void()>& body);
 void dist_poison(sg_dist* d, const std::string& why);
 int dist_world(const sg_dist* d);
 int dist_rank(const sg_dist* d);
+// sg_dist_stark_prove shards its trace-domain algebra (two ranks or more, SG_DIST_SHARD_ALGEBRA != 0)
+bool dist_shard_algebra(const sg_dist* d);
 void dist_count_sharded_quotient(sg_dist* d);
 void dist_count_sharded_interpolation(sg_dist* d, uint64_t columns);
 // n splits over G ranks for both the forward transform (sg_dist_plan) and the inverse

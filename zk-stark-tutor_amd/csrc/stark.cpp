@@ -712,7 +712,7 @@ bool interpolate_geometric_batch_dist(sg_dist* dd, const fe& q, uint64_t D, cons
                                       uint64_t n, std::vector<DPoly>& outs, std::vector<DevBuf>& keep) {
   sg_ctx* ctx = dist_ctx(dd);
   const int G = dist_world(dd);
-  if (G < 2 || n <= 1 || n >= D) return false;
+  if (!dist_shard_algebra(dd) || n <= 1 || n >= D) return false;
   GeoInterpCache local;
   const GeoPlan P = geo_plan(ctx, q, D, n, &local, /*env=*/false);
   const uint64_t M = P.M, f = (uint64_t)1 << P.logf, Mf = M >> P.logf;
@@ -835,7 +835,7 @@ void prove_boundary_quotients(sg_ctx* ctx, const sg_stark& st, const std::vector
     for (size_t s = 0; s < m; ++s) {
       const int64_t dz = hp_degree(bz[s]);
       // (the branch depends only on what every rank shares -- never on a per-rank environment)
-      if (dd && dist_world(dd) > 1 && dz >= 0 && dnum[s] >= dz && bz[s].size() <= 64) {
+      if (dd && dist_shard_algebra(dd) && dz >= 0 && dnum[s] >= dz && bz[s].size() <= 64) {
         const DivPlan pl = coset_divide_plan(st.omicron, D, dnum[s], dz);
         if (diffs[s].len <= pl.order && dist_can_shard(pl.order, dist_world(dd))) {
           const uint64_t nl = pl.order / (uint64_t)dist_world(dd);
@@ -991,7 +991,7 @@ void prove_transition_quotients(sg_ctx* ctx, const sg_stark& st, const std::vect
   // (one rank: its "shard" is the whole coset, which the replicated path evaluates with half the
   // transforms -- the next-row values are a rotation there)
   uint64_t Ls = 0;
-  bool sharded = dd && dist_world(dd) > 1 && !tcs.empty();
+  bool sharded = dd && dist_shard_algebra(dd) && !tcs.empty();
   for (const MPoly* tc : tcs) {
     if (!sharded) break;
     const uint64_t len = symbolic_degree_bound(*tc, Tp - 1) + 1;
