@@ -670,3 +670,54 @@ def test_dist_failure_one_rank_host_transport(stark_reference):
         assert "poisoned" in r["after"], res
         assert r["seconds"] < 60, res
     assert "injected" in res[1]["result"], res
+
+
+# ------------------------------------------- the reference's published configuration, sharded
+
+def _rpsss_worker(rank, world, port, tmp):
+    import torch.distributed as dist
+    import rpsss_case as R
+    import starkgpu as sg
+    from starkgpu import dist as D
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        c = R.Case()
+        ctx = sg.Context(0)
+        nd = D.NativeDist(ctx, transport="host")
+        rp = sg.RescuePrime(*R.RESCUE, ctx=ctx)
+        st = sg.Stark(R.EXPANSION, R.CHECKS, R.SECURITY, rp.m, R.RESCUE[3] + 1, R.TCD, ctx=ctx)
+        air = rp.transition_constraints(st.omicron, st.omicron_domain_length)
+        before = nd.counters()
+        got = st.prove(rp.trace_array(c.sk), air, rp.boundary_constraints(c.pk), sg.SignatureProofStream(R.DOCUMENT),
+                       sg.fe_array([v for row in c.trace_randomizers for v in row]),
+                       sg.fe_array(c.randomizer_coefficients), dist=nd)
+        after = nd.counters()
+        res = (got == open(os.path.join(tmp, "rpsss.bin"), "rb").read(), after[1] - before[1], after[2] - before[2])
+        flags = [None] * world
+        dist.all_gather_object(flags, res)
+        assert all(f[0] for f in flags), f"sharded RPSSS signature differs from the oracle's: {flags}"
+        # FRI domain 4096: transition quotients (coset 1024) and boundary quotients (order 512) on
+        # run shards, and the interpolation (subgroup 512) at 2 and 4 ranks
+        assert all(f[1] == 4 and f[2] == 2 for f in flags), flags
+        nd.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("world", [2, 4])
+def test_dist_rpsss_published_configuration(tmp_path, world):
+    """RPSSS::sign at rpsss.rs:103 (c = 64, FRI domain 4096, SignatureProofStream) with the prove
+    sharded over `world` ranks on this GPU (host transport over gloo), the trace-domain algebra on
+    run shards: every rank writes the oracle's 1 156 888-byte signature (rpsss.rs:89)."""
+    import torch.multiprocessing as mp
+    import rpsss_case as R
+    want = R.Case().oracle_sign()
+    assert len(want) == R.PROOF_LEN
+    (tmp_path / "rpsss.bin").write_bytes(want)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.spawn(_rpsss_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True)
