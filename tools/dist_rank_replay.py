@@ -25,7 +25,7 @@ import time
 import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, ROOT)
+sys.path[:0] = [ROOT, os.path.join(ROOT, "zk-stark-tutor_amd")]
 
 
 def _workload(dev, ctx):
