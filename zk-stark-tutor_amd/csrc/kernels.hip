@@ -1379,7 +1379,7 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
     int fuse;
     unsigned bs;
     int kind;  // 0: leaf 256, 1: leaf tail 1024, 2: node 256, 3: quad 64, 4: leaf 512, 5: quad 256, 6: node 512, 8: leaf pairs 512,
-              // 7: quad leaves 256
+              // 7: quad leaves 256, 9: pipelined nodes 256, 10: node pairs 256
     // SG_MERKLE_QUAD_LEAF_BELOW = log2 of the leaf count (all trees of the launch) under which the
     // leaf level takes a quad per leaf (k_merkle_quad_leaves); 0 disables it (A/B knob)
     static const int env_qleaf = env_int("SG_MERKLE_QUAD_LEAF_BELOW", 17);
@@ -1435,6 +1435,13 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
       // the current one hashes (k_merkle_nodes_pipe; A/B knob)
       static const int env_pipe = env_int("SG_MERKLE_NODE_PIPE", 0);
       if (env_pipe && kind == 2 && count % 256 == 0 && level + fuse - 1 < logn) kind = 9;
+      // SG_MERKLE_NODE_PAIRS=1: two nodes per lane and their parent in the lane (k_merkle_node_pairs),
+      // 256 lanes per 512 first-level nodes, the same levels fused (A/B knob)
+      static const int env_npairs = env_int("SG_MERKLE_NODE_PAIRS", 0);
+      if (env_npairs && kind == 2 && fuse >= 2 && count % 512 == 0) {
+        kind = 10;
+        if (fuse > 10) fuse = 10;  // two levels in the lane, then 256 -> 1 through LDS
+      }
       if (count < bs) {
         kind = 2;
         bs = (unsigned)count;  // a power of two (tree levels)
@@ -1466,7 +1473,7 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
     for (int k = 0; k < fuse; ++k) digests += count >> k;
     // a fused fold reads 2 source elements and writes the folded one instead of reading the leaf
     // quad kernels: 4 lanes per node; leaf pairs: 2 leaves per lane
-    const uint64_t per_block = kind == 3 || kind == 5 || kind == 7 ? bs / 4 : kind == 8 ? 2 * bs : bs;
+    const uint64_t per_block = kind == 3 || kind == 5 || kind == 7 ? bs / 4 : kind == 8 || kind == 10 ? 2 * bs : bs;
     dim3 grid((unsigned)((count + per_block - 1) / per_block), batch);
     // elems = lanes launched (the rocprofv3 Grid_Size of this dispatch), so per-wave PMC
     // instruction counts scale to any launch population

@@ -120,13 +120,12 @@ __device__ __forceinline__ void leaf_value_pair(const MerkleArgs& a, uint64_t id
     st_fe(a.fold.dst + idx, v0);
     st_fe(a.fold.dst + idx + 1, v1);
   } else {
-    const fe* l = merkle_leaves_ptr(a);
-    v0 = ld_fe(l + idx);
-    v1 = ld_fe(l + idx + 1);
+    v0 = leaf_value<false>(a, idx);
+    v1 = leaf_value<false>(a, idx + 1);
   }
 }
 
-// leaf digest: BLAKE2b-512 of the decimal string// leaf digest: BLAKE2b-512 of the decimal string (field_element.rs:46-50 bytes)
+// leaf digest: BLAKE2b-512 of the decimal string (field_element.rs:46-50 bytes)
 __device__ __forceinline__ void leaf_hash(const fe& v, uint64_t d[8]) {
   uint64_t m[16];
   uint32_t len = fe_decimal_words(v, m);

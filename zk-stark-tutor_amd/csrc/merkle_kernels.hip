@@ -102,8 +102,15 @@ __global__ __launch_bounds__(MAXB) void k_merkle_leaf_pairs(MerkleArgs a) {
     // 32-byte leaf pair and 128-byte digest pair move as whole lines (stored one compression apart,
     // the digest halves were written back to HBM as separate partial lines: 1.19x the algorithmic
     // bytes in the PMC pass)
+    // (the plain-leaf variant keeps the two-call form: the pair form's schedule takes it from 104
+    // to 132 VGPRs, 4 -> 3 waves per SIMD, and the 2^25 tree 13 % slower in the round-4 A/B)
     fe v0, v1;
-    leaf_value_pair<FOLD>(a, 2 * p, v0, v1);
+    if constexpr (FOLD) {
+      leaf_value_pair<true>(a, 2 * p, v0, v1);
+    } else {
+      v0 = leaf_value<false>(a, 2 * p);
+      v1 = leaf_value<false>(a, 2 * p + 1);
+    }
     // keep the second leaf's read beside the first: the first compression's input is tied to it
     // (the scheduler would sink the read past that compression to save 4 VGPRs, re-touching each
     // lane pair's line ~2000 instructions later)
@@ -204,6 +211,65 @@ __global__ __launch_bounds__(MAXB) void k_merkle_nodes_pipe(MerkleArgs a, uint64
   }
 }
 
+// Node level with two nodes per lane, as k_merkle_leaf_pairs for the leaves: lane p reads its four
+// children (256 contiguous bytes), hashes nodes 2p and 2p + 1 of the first level and their parent
+// itself, so the first two levels keep all waves of the block busy (the one-node kernel's fused
+// levels leave 4, 2, 1 of 4 waves busy) and each lane has two independent compressions to
+// interleave while the other's loads are in flight.  first_count is a multiple of 2 * MAXB
+// (host-checked); levels 2 .. fuse-1 follow through LDS.
+template <int MAXB>
+__global__ __launch_bounds__(MAXB) __attribute__((amdgpu_waves_per_eu(4))) void k_merkle_node_pairs(MerkleArgs a) {
+  __shared__ uint64_t sm[8][MAXB];
+  const uint32_t tid = threadIdx.x;
+  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + tid;
+  uint64_t* __restrict__ tree = merkle_tree_ptr(a);
+  uint64_t* const root_slot = merkle_root_slot(a);
+  const uint64_t* child = tree + a.off[0] * 8 + (4 * p) * 8;
+  uint64_t d[8];
+  {
+    uint64_t c0[8], c1[8], c2[8], c3[8];
+    ld_digest(child, c0);
+    ld_digest(child + 8, c1);
+    ld_digest(child + 16, c2);
+    ld_digest(child + 24, c3);
+    uint64_t l[8], r[8];
+    blake2b_node(c0, c1, l);
+    blake2b_node(c2, c3, r);
+    st_digest(tree + (a.off[1] + 2 * p) * 8, l);
+    st_digest(tree + (a.off[1] + 2 * p + 1) * 8, r);
+    blake2b_node(l, r, d);
+    st_digest(tree + (a.off[2] + p) * 8, d);
+    if (a.first_level + 1 == a.root_level && root_slot) {
+      for (int i = 0; i < 8; ++i) root_slot[i] = d[i];
+      merkle_root_publish(a, true);
+    }
+  }
+  uint32_t count = blockDim.x;
+  for (int lev = 2; lev < a.fuse; ++lev) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) sm[i][tid] = d[i];
+    __syncthreads();
+    count >>= 1;
+    if (tid < count) {
+      uint64_t l[8], r[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const ulonglong2 lr = *reinterpret_cast<const ulonglong2*>(&sm[i][2 * tid]);
+        l[i] = lr.x;
+        r[i] = lr.y;
+      }
+      blake2b_node(l, r, d);
+      const uint64_t gidx = (uint64_t)blockIdx.x * count + tid;
+      st_digest(tree + (a.off[lev + 1] + gidx) * 8, d);
+      if (a.first_level + lev == a.root_level && root_slot) {
+        for (int i = 0; i < 8; ++i) root_slot[i] = d[i];
+        merkle_root_publish(a, true);
+      }
+    }
+    __syncthreads();
+  }
+}
+
 hipError_t launch_merkle_lanes(int kind, bool fold, dim3 grid, unsigned bs, hipStream_t s, const MerkleArgs& a) {
   switch (kind) {
     case 0:
@@ -227,6 +293,7 @@ hipError_t launch_merkle_lanes(int kind, bool fold, dim3 grid, unsigned bs, hipS
       break;
     }
     case 6: hipLaunchKernelGGL((k_merkle_levels<false, 512>), grid, dim3(bs), 0, s, a); break;
+    case 10: hipLaunchKernelGGL((k_merkle_node_pairs<256>), grid, dim3(bs), 0, s, a); break;
     case 4:
       if (fold) hipLaunchKernelGGL((k_merkle_levels<true, 512, true>), grid, dim3(bs), 0, s, a);
       else hipLaunchKernelGGL((k_merkle_levels<true, 512>), grid, dim3(bs), 0, s, a);
