@@ -134,8 +134,9 @@ __device__ __forceinline__ void leaf_hash(const fe& v, uint64_t d[8]) {
   blake2b_single_block(m, len, d);
 }
 
-// Launches one of the lane-per-hash Merkle kernels (merkle_kernels.hip): kind 0/1/4 leaf levels
-// with 256/1024/512 lanes, 2/6 node levels with 256/512 lanes, 8 leaf pairs with 512 lanes.
+// Launches one of the Merkle kernels (merkle_kernels.hip): kind 0/1/4 leaf levels with 256/1024/512
+// lanes, 2/6 node levels with 256/512 lanes, 8 leaf pairs with 512 lanes, 9 pipelined nodes, 10 node
+// pairs; quad-lane kinds 3/5 node levels with 64/256 nodes, 7 leaves with 256 leaves per block.
 hipError_t launch_merkle_lanes(int kind, bool fold, dim3 grid, unsigned bs, hipStream_t s, const MerkleArgs& a);
 
 }  // namespace sg

@@ -4,8 +4,11 @@
 // This translation unit is compiled with LLVM's max-ILP machine scheduler (Makefile): it
 // interleaves the four independent G functions of each BLAKE2b half-round, trading VGPRs
 // (74 -> 104 for the leaf-pair kernel, 6 -> 4 waves per SIMD) for per-wave instruction-level
-// parallelism: 2^25 tree 2.5 % faster (profiles/r03_ab_merkle_max_ilp.log).  The NTT and quad-lane
-// kernels stay on the default scheduler (max-ILP spills them).
+// parallelism: 2^25 tree 2.5 % faster (profiles/r03_ab_merkle_max_ilp.log).  The quad-lane kernels
+// (latency-bound tree tops) live here too since round 4: under max-ILP the 2^14 / 2^16 trees, all
+// quad kernels, built 4-6 % faster on the same box (profiles/r04_ab_qilp_14.log, _16.log), although
+// the 1024-lane quad blocks (128-VGPR cap) keep 12 bytes per lane in scratch.  The NTT kernels stay
+// in kernels.hip on the default scheduler (max-ILP spills them).
 #include <cstdlib>
 
 #include "merkle_dev.hpp"
@@ -270,6 +273,223 @@ __global__ __launch_bounds__(MAXB) __attribute__((amdgpu_waves_per_eu(4))) void 
   }
 }
 
+// ---------------------------------------------------- Merkle: 4 lanes per hash
+//
+// The top of a tree is latency-bound: a level of a few thousand nodes or less
+// cannot fill the chip, and each level waits for the one below.  Here one
+// compression is split over a quad of lanes (BLAKE2b's four independent G
+// columns): lane q holds column q (v[q], v[4+q], v[8+q], v[12+q]), the
+// diagonal step rotates rows 1..3 across the quad with DPP quad_perm moves,
+// and message words are read from LDS at the round's sigma positions.
+// ~2.4x fewer dependent instructions per level than one lane per hash.
+
+// packed sigma nibbles for one lane of the quad: round r (0..9) occupies bits
+// [16r, 16r+16) as (col_x, col_y, diag_x, diag_y) = sigma[r][2q], [2q+1], [8+2q], [9+2q]
+struct SigmaPack {
+  uint32_t w[5];
+};
+__host__ __device__ constexpr uint32_t sigma_nib(int r, int q) {
+  constexpr uint8_t S[10][16] = {
+      {0, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11, 12, 13, 14, 15}, {14, 10, 4, 8, 9, 15, 13, 6, 1, 12, 0, 2, 11, 7, 5, 3},
+      {11, 8, 12, 0, 5, 2, 15, 13, 10, 14, 3, 6, 7, 1, 9, 4}, {7, 9, 3, 1, 13, 12, 11, 14, 2, 6, 5, 10, 4, 0, 15, 8},
+      {9, 0, 5, 7, 2, 4, 10, 15, 14, 1, 11, 12, 6, 8, 3, 13}, {2, 12, 6, 10, 0, 11, 8, 3, 4, 13, 7, 5, 15, 14, 1, 9},
+      {12, 5, 1, 15, 14, 13, 4, 10, 0, 7, 6, 3, 9, 2, 8, 11}, {13, 11, 7, 14, 12, 1, 3, 9, 5, 0, 15, 4, 8, 6, 2, 10},
+      {6, 15, 14, 9, 11, 3, 0, 8, 12, 2, 13, 7, 1, 4, 10, 5}, {10, 2, 8, 4, 7, 6, 1, 5, 15, 11, 9, 14, 3, 12, 13, 0}};
+  return (uint32_t)S[r][2 * q] | ((uint32_t)S[r][2 * q + 1] << 4) | ((uint32_t)S[r][8 + 2 * q] << 8) |
+         ((uint32_t)S[r][9 + 2 * q] << 12);
+}
+__device__ __forceinline__ SigmaPack sigma_pack(int q) {
+  SigmaPack p;
+#pragma unroll
+  for (int k = 0; k < 5; ++k) {
+    uint32_t v0 = q == 0 ? sigma_nib(2 * k, 0) : q == 1 ? sigma_nib(2 * k, 1) : q == 2 ? sigma_nib(2 * k, 2) : sigma_nib(2 * k, 3);
+    uint32_t v1 = q == 0 ? sigma_nib(2 * k + 1, 0) : q == 1 ? sigma_nib(2 * k + 1, 1) : q == 2 ? sigma_nib(2 * k + 1, 2)
+                                                                                              : sigma_nib(2 * k + 1, 3);
+    p.w[k] = v0 | (v1 << 16);
+  }
+  return p;
+}
+
+template <int CTRL>
+__device__ __forceinline__ uint64_t quad_perm64(uint64_t x) {
+  uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)x, CTRL, 0xF, 0xF, true);
+  uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(x >> 32), CTRL, 0xF, 0xF, true);
+  return ((uint64_t)hi << 32) | lo;
+}
+// quad_perm encodings: lane i takes lane sel[i]
+constexpr int QP_NEXT1 = 1 | (2 << 2) | (3 << 4) | (0 << 6);  // from (q+1)%4
+constexpr int QP_NEXT2 = 2 | (3 << 2) | (0 << 4) | (1 << 6);  // from (q+2)%4
+constexpr int QP_NEXT3 = 3 | (0 << 2) | (1 << 4) | (2 << 6);  // from (q+3)%4
+
+#define SG_QG(a, b, c, d, x, y)   \
+  a = a + b + (x);                \
+  d = rotr64(d ^ a, 32);          \
+  c = c + d;                      \
+  b = rotr64(b ^ c, 24);          \
+  a = a + b + (y);                \
+  d = rotr64(d ^ a, 16);          \
+  c = c + d;                      \
+  b = rotr64(b ^ c, 63);
+
+// One BLAKE2b single-block compression (final block, counter t) computed by a
+// quad.  msg: the 16 message words in LDS.  Returns h[q] and h[4+q].
+__device__ __forceinline__ void blake2b_quad(const uint64_t* msg, uint64_t t, int q, const SigmaPack& sp,
+                                             uint64_t& out_lo, uint64_t& out_hi) {
+  const uint64_t ivq = q == 0 ? SG_B2B_IV0 : q == 1 ? SG_B2B_IV1 : q == 2 ? SG_B2B_IV2 : SG_B2B_IV3;
+  const uint64_t iv4q = q == 0 ? SG_B2B_IV4 : q == 1 ? SG_B2B_IV5 : q == 2 ? SG_B2B_IV6 : SG_B2B_IV7;
+  const uint64_t hq = q == 0 ? (SG_B2B_IV0 ^ 0x01010040ull) : ivq;
+  uint64_t a = hq, b = iv4q, c = ivq;
+  uint64_t d = iv4q ^ (q == 0 ? t : 0) ^ (q == 2 ? ~0ull : 0);
+#pragma unroll
+  for (int r = 0; r < 12; ++r) {
+    const int rr = r % 10;
+    const uint32_t nib = (sp.w[rr >> 1] >> (16 * (rr & 1))) & 0xFFFFu;
+    uint64_t mx = msg[nib & 15], my = msg[(nib >> 4) & 15];
+    uint64_t dx = msg[(nib >> 8) & 15], dy = msg[nib >> 12];
+    SG_QG(a, b, c, d, mx, my)
+    b = quad_perm64<QP_NEXT1>(b);
+    c = quad_perm64<QP_NEXT2>(c);
+    d = quad_perm64<QP_NEXT3>(d);
+    SG_QG(a, b, c, d, dx, dy)
+    b = quad_perm64<QP_NEXT3>(b);
+    c = quad_perm64<QP_NEXT2>(c);
+    d = quad_perm64<QP_NEXT1>(d);
+  }
+  out_lo = hq ^ a ^ c;
+  out_hi = iv4q ^ b ^ d;
+}
+
+// The `fuse - 1` levels a quad block computes above its first digests (hlo, hhi of node `node`):
+// children through LDS, every digest written to the tree, the root published by the level reaching it.
+template <int NODES>
+__device__ __forceinline__ void quad_upper_levels(const MerkleArgs& a, uint64_t* __restrict__ tree,
+                                                  uint64_t* root_slot, uint64_t (*msg)[16], int node, int q,
+                                                  const SigmaPack& sp, uint32_t count, uint64_t hlo, uint64_t hhi) {
+  for (int lev = 1; lev < a.fuse; ++lev) {
+    __syncthreads();  // everyone finished reading msg
+    if (node < (int)count) {
+      msg[node >> 1][(node & 1) * 8 + q] = hlo;
+      msg[node >> 1][(node & 1) * 8 + 4 + q] = hhi;
+    }
+    __syncthreads();
+    count >>= 1;
+    if (node < (int)count) {
+      blake2b_quad(msg[node], 128, q, sp, hlo, hhi);
+      uint64_t gidx = (uint64_t)blockIdx.x * count + node;
+      uint64_t* dst = tree + (a.off[lev + 1] + gidx) * 8;
+      dst[q] = hlo;
+      dst[4 + q] = hhi;
+      if (a.first_level + lev == a.root_level && root_slot) {
+        root_slot[q] = hlo;
+        root_slot[4 + q] = hhi;
+        merkle_root_publish(a, q == 0);
+      }
+    }
+  }
+}
+
+// Node levels with a quad per node: 4 * NODES threads = NODES nodes at the first level,
+// `fuse` levels computed (NODES -> 1 at most).  Children of the first level are
+// read from HBM (level first_level-1), every produced digest is written to the tree.
+// NODES = 64 for wide levels; NODES = 256 takes a tree's last <= 256 nodes to the root
+// in one block (one launch fewer per tree than two 64-node steps).
+template <int NODES>
+__global__ __launch_bounds__(4 * NODES) void k_merkle_quad(MerkleArgs a) {
+  __shared__ uint64_t msg[NODES][16];
+  const int tid = threadIdx.x;
+  const int q = tid & 3;
+  const int node = tid >> 2;
+  uint64_t* __restrict__ tree = merkle_tree_ptr(a);
+  uint64_t* const root_slot = merkle_root_slot(a);
+  const SigmaPack sp = sigma_pack(q);
+  uint32_t count = blockDim.x >> 2;  // nodes of this block at the current level
+  const uint64_t gnode = (uint64_t)blockIdx.x * count + node;
+  const bool valid = gnode < a.first_count;
+  {
+    // message of node gnode = its two children, 16 consecutive words in the child level
+    const uint64_t* child = tree + (a.off[0] + 2 * gnode) * 8;
+    if (valid) {
+      uint4 v0 = reinterpret_cast<const uint4*>(child)[2 * q];
+      uint4 v1 = reinterpret_cast<const uint4*>(child)[2 * q + 1];
+      msg[node][4 * q + 0] = (uint64_t)v0.x | ((uint64_t)v0.y << 32);
+      msg[node][4 * q + 1] = (uint64_t)v0.z | ((uint64_t)v0.w << 32);
+      msg[node][4 * q + 2] = (uint64_t)v1.x | ((uint64_t)v1.y << 32);
+      msg[node][4 * q + 3] = (uint64_t)v1.z | ((uint64_t)v1.w << 32);
+    }
+  }
+  __syncthreads();
+  uint64_t hlo = 0, hhi = 0;
+  if (valid) {
+    blake2b_quad(msg[node], 128, q, sp, hlo, hhi);
+    uint64_t* dst = tree + (a.off[1] + gnode) * 8;
+    dst[q] = hlo;
+    dst[4 + q] = hhi;
+    if (a.first_level == a.root_level && root_slot) {
+      root_slot[q] = hlo;
+      root_slot[4 + q] = hhi;
+      merkle_root_publish(a, q == 0);  // the quad is one wavefront: its fence covers all 4 lanes
+    }
+  }
+  quad_upper_levels<NODES>(a, tree, root_slot, msg, node, q, sp, count, hlo, hhi);
+}
+
+// Leaf level of a latency-bound tree (a late FRI round's codeword, C4's small trees, a forest's
+// small subtrees) with a quad of lanes per leaf: each lane of the quad converts the leaf to its
+// decimal words (the quad shares a wavefront, so the redundant conversion costs no time) and
+// stores its four of the 16 message words (decimal words 0..4, zeros above); the quad then
+// compresses the single block with t = the string length (merkle_root.rs:7-32 on
+// field_element.rs:46-50 bytes), and the node levels above are fused as in k_merkle_quad.
+// FOLD: the leaf is the fold of the previous round's codeword (fri.rs:151-159), stored too.
+template <int NODES, bool FOLD>
+__global__ __launch_bounds__(4 * NODES) void k_merkle_quad_leaves(MerkleArgs a) {
+  __shared__ uint64_t msg[NODES][16];
+  const int tid = threadIdx.x;
+  const int q = tid & 3;
+  const int node = tid >> 2;
+  uint64_t* __restrict__ tree = merkle_tree_ptr(a);
+  uint64_t* const root_slot = merkle_root_slot(a);
+  const SigmaPack sp = sigma_pack(q);
+  uint32_t count = blockDim.x >> 2;  // leaves of this block
+  const uint64_t leaf = (uint64_t)blockIdx.x * count + node;
+  const bool valid = leaf < a.first_count;
+  uint32_t len = 0;
+  if (valid) {
+    fe v;
+    if constexpr (FOLD) {
+      const fe x = ld_fe(a.fold.src + leaf);
+      const fe y = ld_fe(a.fold.src + leaf + a.first_count);
+      const uint64_t e = leaf << a.fold.shift;
+      const fe K = a.fold.Kp ? ld_fe(a.fold.Kp) : a.fold.K;
+      fe t = mont_mul(K, ld_fe(a.fold.Tlo + (e & 4095)));
+      t = mont_mul(t, ld_fe(a.fold.Thi + (e >> 12)));
+      v = fe_add(fe_halve(fe_add(x, y)), mont_mul(fe_sub(x, y), t));
+      if (q == 0) st_fe(a.fold.dst + leaf, v);
+    } else {
+      v = ld_fe(merkle_leaves_ptr(a) + leaf);
+    }
+    uint64_t m[5];
+    len = fe_decimal_words(v, m);
+    msg[node][4 * q + 0] = q == 0 ? m[0] : q == 1 ? m[4] : 0;
+    msg[node][4 * q + 1] = q == 0 ? m[1] : 0;
+    msg[node][4 * q + 2] = q == 0 ? m[2] : 0;
+    msg[node][4 * q + 3] = q == 0 ? m[3] : 0;
+  }
+  __syncthreads();
+  uint64_t hlo = 0, hhi = 0;
+  if (valid) {
+    blake2b_quad(msg[node], len, q, sp, hlo, hhi);
+    uint64_t* dst = tree + (a.off[1] + leaf) * 8;
+    dst[q] = hlo;
+    dst[4 + q] = hhi;
+    if (a.first_level == a.root_level && root_slot) {
+      root_slot[q] = hlo;
+      root_slot[4 + q] = hhi;
+      merkle_root_publish(a, q == 0);
+    }
+  }
+  quad_upper_levels<NODES>(a, tree, root_slot, msg, node, q, sp, count, hlo, hhi);
+}
+
 hipError_t launch_merkle_lanes(int kind, bool fold, dim3 grid, unsigned bs, hipStream_t s, const MerkleArgs& a) {
   switch (kind) {
     case 0:
@@ -294,6 +514,12 @@ hipError_t launch_merkle_lanes(int kind, bool fold, dim3 grid, unsigned bs, hipS
     }
     case 6: hipLaunchKernelGGL((k_merkle_levels<false, 512>), grid, dim3(bs), 0, s, a); break;
     case 10: hipLaunchKernelGGL((k_merkle_node_pairs<256>), grid, dim3(bs), 0, s, a); break;
+    case 3: hipLaunchKernelGGL(k_merkle_quad<64>, grid, dim3(bs), 0, s, a); break;
+    case 5: hipLaunchKernelGGL(k_merkle_quad<256>, grid, dim3(bs), 0, s, a); break;
+    case 7:
+      if (fold) hipLaunchKernelGGL((k_merkle_quad_leaves<256, true>), grid, dim3(bs), 0, s, a);
+      else hipLaunchKernelGGL((k_merkle_quad_leaves<256, false>), grid, dim3(bs), 0, s, a);
+      break;
     case 4:
       if (fold) hipLaunchKernelGGL((k_merkle_levels<true, 512, true>), grid, dim3(bs), 0, s, a);
       else hipLaunchKernelGGL((k_merkle_levels<true, 512>), grid, dim3(bs), 0, s, a);
