@@ -39,16 +39,21 @@ def main():
 
     a, b = single(), sharded()
     assert a == b, "sharded proof bytes differ from the single-GPU proof"
+    gap = os.environ.get("SG_PROVE_GAPS") == "1"  # idle gaps between proves (tools/trace_sum.py)
     for name, fn in (("single", single), ("sharded_world1", sharded), ("single", single),
                      ("sharded_world1", sharded)):
         if only and name != only:
             continue
         torch.cuda.synchronize(dev)
-        t0 = time.perf_counter()
+        dt = 0.0
         for _ in range(steps):
+            if gap:
+                time.sleep(0.1)
+            t0 = time.perf_counter()
             fn()
-        torch.cuda.synchronize(dev)
-        print(f"{name}: {(time.perf_counter() - t0) / steps * 1e3:.3f} ms/prove", flush=True)
+            torch.cuda.synchronize(dev)
+            dt += time.perf_counter() - t0
+        print(f"{name}: {dt / steps * 1e3:.3f} ms/prove", flush=True)
     nd.close()
 
 
