@@ -45,11 +45,20 @@ def main():
     top = collections.Counter()
     for s, e, n in segs[-1]:
         top[n.split("(")[0].replace("void ", "")[:60]] += e - s
+    # per-category kernel sums of the last segment: runtime copies / fills (the host transport's
+    # staging copies land here) apart from the library's kernels
+    cats = collections.Counter()
+    for n, v in top.items():
+        c = ("runtime copy/fill" if n.startswith("__amd_rocclr") else "merkle" if "merkle" in n
+             else "ntt" if ("ntt" in n or "bitrev" in n) else "other kernels")
+        cats[c] += v
+    print("last segment by category (ms): " + ", ".join(f"{c} {v / 1e6:.3f}" for c, v in cats.most_common()))
     print("last segment, top kernels (ms):")
     for n, v in top.most_common(15):
         print(f"  {v / 1e6:8.3f}  {n}")
     if len(sys.argv) > 3:
-        json.dump({"segments": out, "top_last": {n: v / 1e6 for n, v in top.most_common(30)}},
+        json.dump({"segments": out, "top_last": {n: v / 1e6 for n, v in top.most_common(30)},
+                   "categories_last": {c: v / 1e6 for c, v in cats.items()}},
                   open(sys.argv[3], "w"), indent=1)
 
 
