@@ -50,7 +50,11 @@ def _ints(a):
 # ------------------------------------------------------------------ row-sharded ABI
 
 @pytest.mark.parametrize("n,n_in,rows", [(1, 1, 3), (2, 1, 5), (16, 16, 7), (64, 9, 4), (1 << 12, 1 << 12, 3),
-                                         (1 << 13, 1 << 10, 2), (1 << 14, 1 << 14, 5)])
+                                         (1 << 13, 1 << 10, 2), (1 << 14, 1 << 14, 5),
+                                         # 2^6..2^11 points, 2^(11 - log n) rows per tile (the whole-transform
+                                         # first pass) and row counts it does not divide (the generic path)
+                                         (64, 64, 32), (64, 33, 64), (256, 200, 16), (512, 512, 12),
+                                         (1024, 1024, 6), (1024, 77, 3), (2048, 700, 3), (2048, 2048, 1)])
 def test_ntt_rows_matches_oracle(n, n_in, rows):
     import torch
     from starkgpu import dist as D

@@ -379,9 +379,21 @@ struct FirstArgs {
   // columns are then C consecutive rows at one bit-reversed position h (64-byte runs across rows)
   // instead of C positions of one row -- the butterflies are the same (columns are independent)
   uint64_t in_il;
+  // k_ntt_first<11, WHOLE = true>: the pass runs all logn = L stages of small transforms, the
+  // tile's C columns being C whole rows (rows blockIdx.y C + k), and stores the final values:
+  // times *post (INTT n^-1), or canonical, or through the four-step epilogue (ep_out != nullptr,
+  // as pass_store) -- the bit-reversal gather and the generic all-LDS pass of a small transform
+  // in one launch
+  const fe* post;
+  fe* ep_out;
+  const fe* ep_T0;
+  const fe* ep_T1;
+  const fe* ep_T2;
+  uint64_t ep_row0, ep_j0, ep_rows;
+  int ep_logR;
 };
 
-template <int TL>
+template <int TL, bool WHOLE = false>
 __global__ __launch_bounds__(1 << (TL - 3), TL == 11 ? SG_NTT_WPE : 1) void k_ntt_first(FirstArgs a) {
   extern __shared__ fe_lds lds[];
   const int L = a.L, logC = a.logC, m = a.logn;
@@ -392,15 +404,16 @@ __global__ __launch_bounds__(1 << (TL - 3), TL == 11 ? SG_NTT_WPE : 1) void k_nt
   uint32_t bx = blockIdx.x;
   if ((gridDim.x & 7) == 0) bx = (bx & 7) * (gridDim.x >> 3) + (bx >> 3);
   const bool il = a.in_il != 0;
+  const bool rowcols = il || WHOLE;  // the tile's columns are rows (interleaved, or whole transforms)
   // column k of the tile: position h = hcol(k) of row ycol(k)
-  const uint64_t c0 = il ? (uint64_t)bx : (uint64_t)bx << logC;
-  const uint64_t y0 = il ? (uint64_t)blockIdx.y << logC : (uint64_t)blockIdx.y;
-  auto hcol = [&](uint64_t k) { return il ? c0 : c0 + k; };
-  auto ycol = [&](uint64_t k) { return il ? y0 + k : y0; };
+  const uint64_t c0 = rowcols ? (uint64_t)bx : (uint64_t)bx << logC;
+  const uint64_t y0 = rowcols ? (uint64_t)blockIdx.y << logC : (uint64_t)blockIdx.y;
+  auto hcol = [&](uint64_t k) { return rowcols ? c0 : c0 + k; };
+  auto ycol = [&](uint64_t k) { return rowcols ? y0 + k : y0; };
   // element idx of column k's row
   auto in_at = [&](uint64_t k, uint64_t idx) -> const fe* {
     if (il) return a.in[0] + idx * a.in_il + ycol(k);
-    return (a.in_ys ? a.in[0] + y0 * a.in_ys : a.in[y0]) + idx;
+    return (a.in_ys ? a.in[0] + ycol(k) * a.in_ys : a.in[ycol(k)]) + idx;
   };
   auto out_row = [&](uint64_t k) -> fe* {
     const uint64_t y = ycol(k);
@@ -465,8 +478,27 @@ __global__ __launch_bounds__(1 << (TL - 3), TL == 11 ? SG_NTT_WPE : 1) void k_nt
 #pragma unroll
     for (int mm = 0; mm < 8; ++mm) x[mm] = lds[((qq + ((uint32_t)mm << tl)) << logC) + c];
     radix_regs<3, false>(x, pa, tl, qq, 0);
-    const uint64_t h = __builtin_bitreverse64(hcol(c)) >> (64 - (m - L));
     fe* const orow = out_row(c);
+    if constexpr (WHOLE) {
+      // the transform's final values (m == L): element k = qq + mm 2^tl of row ycol(c)
+      const fe pc = a.post ? ld_fe(a.post) : fe_zero();
+#pragma unroll
+      for (int mm = 0; mm < 8; ++mm) {
+        const uint64_t k = qq + ((uint32_t)mm << tl);
+        if (a.ep_out) {
+          const uint64_t r = a.ep_row0 + ycol(c);
+          const uint64_t e = (a.ep_j0 + r) * k;  // < 2^36 (host-checked)
+          const fe w = mont_mul(mont_mul(ld_fe(a.ep_T0 + (e & 4095)), ld_fe(a.ep_T1 + ((e >> 12) & 4095))),
+                                ld_fe(a.ep_T2 + (e >> 24)));
+          const uint64_t R = (uint64_t)1 << a.ep_logR;
+          st_fe(a.ep_out + ((k >> a.ep_logR) * a.ep_rows + r) * R + (k & (R - 1)), mont_mul(x[mm], w));
+        } else {
+          st_fe(orow + k, a.post ? mont_mul(x[mm], pc) : fe_canon(x[mm]));
+        }
+      }
+      return;
+    }
+    const uint64_t h = __builtin_bitreverse64(hcol(c)) >> (64 - (m - L));
 #pragma unroll
     for (int mm = 0; mm < 8; ++mm) st_fe_stream(orow + (h << L) + qq + ((uint32_t)mm << tl), x[mm], m >= kStreamLogN);
     return;
@@ -480,7 +512,8 @@ __global__ __launch_bounds__(1 << (TL - 3), TL == 11 ? SG_NTT_WPE : 1) void k_nt
   const uint32_t tile = 1u << (L + logC);
   for (uint32_t l = threadIdx.x; l < tile; l += blockDim.x) {
     const uint32_t tt = l & ((1u << L) - 1), k = l >> L;
-    const uint64_t h = __builtin_bitreverse64(hcol(k)) >> (64 - (m - L));
+    // (whole transforms take the register path above: the host launches them with L - skip >= 3)
+    const uint64_t h = m > L ? __builtin_bitreverse64(hcol(k)) >> (64 - (m - L)) : 0;
     st_fe(out_row(k) + (h << L) + tt, lds[(tt << logC) + k]);
   }
 }
@@ -957,6 +990,7 @@ static hipError_t ntt_lds_attributes() {
     if (e == hipSuccess) e = set((const void*)k_ntt_first<11>, 65536);
     if (e == hipSuccess) e = set((const void*)k_ntt_first<12>, 65536);
     if (e == hipSuccess) e = set((const void*)k_ntt_first<13>, 131072);
+    if (e == hipSuccess) e = set((const void*)k_ntt_first<11, true>, 65536);
     return e;
   }();
   return err;
@@ -1059,13 +1093,54 @@ hipError_t launch_ntt_fused(fe* const* out, const fe* const* in, int batch, uint
   // three on 2048-element tiles (the multi-GPU interleaved gather and epilogue keep the latter)
   const int TL = (!in_il && !ep) ? ntt_first_tile(logn) : 11;
   const int LOGC1 = TL == 12 ? 1 : 2, L1 = TL - LOGC1;
+  FirstArgs a;
+  a.post = nullptr;
+  a.ep_out = nullptr;
   if (logn <= L1 + LOGC1 || logn - L1 > 63) {
+    // small transforms (2^6 .. 2^11 points) whole in one k_ntt_first<11> launch, 2^(11 - logn) rows
+    // per 256-lane tile: the gather, every stage and the final store (canonical / n^-1 / four-step
+    // epilogue) without the bit-reversal pass and the all-LDS generic pass (SG_NTT_SMALL_WHOLE=0:
+    // the latter, A/B)
+    static const bool small_whole = env_int("SG_NTT_SMALL_WHOLE", 1) != 0;
+    const int logCw = 11 - logn;
+    if (small_whole && logn >= 6 && logn <= 11 && skip <= logn - 3 && batch % (1 << logCw) == 0) {
+      for (int b = 0; b < kMaxBatch; ++b) {
+        a.out[b] = b < np ? out[b] : nullptr;
+        a.in[b] = b < np ? in[b] : nullptr;
+      }
+      a.in_ys = in_il ? 0 : in_ys;
+      a.out_ys = out_ys;
+      a.tw = tw;
+      a.sA = sA;
+      a.sB = sB;
+      a.n_in = n_in;
+      a.logn = logn;
+      a.L = logn;
+      a.logC = logCw;
+      a.skip = skip;
+      a.s_cut = ntt_tw_cut(logn);
+      a.in_il = in_il;
+      a.post = post;
+      if (ep) {
+        a.ep_out = ep->out;
+        a.ep_T0 = ep->T0;
+        a.ep_T1 = ep->T1;
+        a.ep_T2 = ep->T2;
+        a.ep_row0 = ep->row0;
+        a.ep_j0 = ep->j0;
+        a.ep_rows = ep->rows;
+        a.ep_logR = ep->logR;
+      }
+      const uint64_t n = (uint64_t)1 << logn;
+      ProfScope ps("ntt_small", batch * (16 * (n_in < n ? n_in : n) + 16 * n), s, (uint64_t)batch * n);
+      hipLaunchKernelGGL((k_ntt_first<11, true>), dim3(1, (unsigned)(batch >> logCw)), dim3(256), (size_t)16 << 11, s, a);
+      return hipGetLastError();
+    }
     hipError_t e = launch_bitrev_gather(out, in, batch, n_in, logn, sA, sB, skip, s, in_il ? 1 : in_ys, out_ys,
                                         in_il);
     if (e != hipSuccess) return e;
     return launch_ntt_dit(out, batch, tw, logn, post, skip, s, out_ys, ep);
   }
-  FirstArgs a;
   for (int b = 0; b < kMaxBatch; ++b) {
     a.out[b] = b < np ? out[b] : nullptr;
     a.in[b] = b < np ? in[b] : nullptr;
