@@ -17,7 +17,7 @@ P = o.P
 
 def plan(n, G):
     logn = n.bit_length() - 1
-    n1 = 1 << (logn // 2)
+    n1 = 1 << (logn // 2)  # dist.cpp dist_split
     return n1, n // n1
 
 

@@ -294,6 +294,32 @@ def test_c5_native_dist_2p27_one_gpu(c5_reference, world):
     mp.spawn(_c5_native_worker, args=(world, port, c5_reference), nprocs=world, join=True)
 
 
+def test_c5_native_dist_2p27_world1_rccl(c5_reference):
+    """C5 through sg_dist_ntt / sg_dist_intt on a one-rank RCCL communicator: each collective then
+    moves the whole 2 GiB shard per peer, above what one RCCL call carries (dist.cpp exchange:
+    kMaxCollBytes chunks) -- bit-identical to the single-GPU transform, and inverted."""
+    import torch
+    from starkgpu import dist as D
+    ctx = sg.Context(0)
+    nd = D.NativeDist(ctx, transport="rccl")
+    try:
+        n = 1 << C5_LOG
+        n1, n2 = nd.plan(n, 1)
+        x = np.load(os.path.join(c5_reference, "x.npy"), mmap_mode="r")
+        X = np.load(os.path.join(c5_reference, "X.npy"), mmap_mode="r")
+        cols = np.ascontiguousarray(x.reshape(n2, n1, 2).transpose(1, 0, 2))
+        dev = torch.device("cuda", 0)
+        shard = torch.from_numpy(cols.view(np.int64).reshape(-1)).to(dev)
+        del cols
+        root = o.primitive_nth_root(n)
+        runs = nd.ntt(root, shard, n2, n)
+        assert np.array_equal(runs.cpu().numpy().view(np.uint64).reshape(n, 2), X), "sg_dist_ntt at world 1"
+        back = nd.intt(root, runs, n)
+        assert torch.equal(back, shard), "sg_dist_intt at world 1"
+    finally:
+        nd.close()
+
+
 @pytest.mark.parametrize("world", [2, 8])
 def test_c5_sharded_2p27_ntt_one_gpu_gloo(c5_reference, world):
     import torch.multiprocessing as mp

@@ -8,6 +8,8 @@
 #          merkle[:LOG]         tools/bench_merkle.py  Merkle tree of 2^LOG leaves (default 25)
 #          ntt[:LOG]            tools/bench_ntt.py     NTT passes of 2^LOG (default 22)
 #          bench                bench.py --no-cpu-baseline --steps 3 --warmup 1 (prove, C2, C5, 2^24 block)
+#          dist[:STEPS[:LOG]]   tools/dist_prove_time.py  sharded prove on a one-rank RCCL communicator
+#          c5dist[:LOG]         tools/c5_dist_time.py     four-step NTT of 2^LOG on a one-rank communicator
 # VARIANT  LABEL or LABEL=K1=V1,K2=V2: environment of that variant; the key `lib` names a library
 #          build (path relative to the repo root) loaded through SG_LIB_PATH, e.g.
 #            base=lib=ab/libstarkgpu_base.so  new  fuse3=SG_MERKLE_NODE_FUSE=3
@@ -26,6 +28,8 @@ case "$KIND" in
   c2)     CMD=(python tools/c2_time.py "${A1:-22}"); LIMIT=120 ;;
   merkle) CMD=(python tools/bench_merkle.py "${A1:-25}"); LIMIT=120; PICK="ms/build" ;;
   ntt)    CMD=(python tools/bench_ntt.py "${A1:-22}"); LIMIT=120 ;;
+  dist)   CMD=(python tools/dist_prove_time.py "${A1:-5}" "${A2:-20}" sharded_world1); LIMIT=200 ;;
+  c5dist) CMD=(python tools/c5_dist_time.py "${A1:-27}"); LIMIT=200 ;;
   bench)  CMD=(python bench.py --no-cpu-baseline --steps 3 --warmup 1); LIMIT=300 ;;
   *) echo "unknown measure $KIND" >&2; exit 2 ;;
 esac

@@ -141,6 +141,7 @@ namespace {
   } while (0)
 
 constexpr uint64_t kRows = 65532;  // rows per launch: grid.y limit, a multiple of 4 (interleaved tiles)
+constexpr size_t kMaxCollBytes = (size_t)1 << 30;  // largest per-peer block of one RCCL collective call
 
 void grow_pinned(void*& p, size_t& have, size_t need) {
   if (have >= need) return;
@@ -157,10 +158,27 @@ void exchange(sg_dist* d, const void* dsend, void* drecv, size_t bytes, bool a2a
   const size_t total = bytes * d->G;
   ++d->collectives;
   if (d->comm) {  // RCCL over xGMI, stream-ordered (a 1-rank communicator runs the same calls)
-    if (a2a)
-      SG_NCCL(ncclAllToAll(dsend, drecv, bytes, ncclUint8, d->comm, ctx->stream));
-    else
-      SG_NCCL(ncclAllGather(dsend, drecv, bytes, ncclUint8, d->comm, ctx->stream));
+    if (bytes <= kMaxCollBytes) {
+      if (a2a)
+        SG_NCCL(ncclAllToAll(dsend, drecv, bytes, ncclUint8, d->comm, ctx->stream));
+      else
+        SG_NCCL(ncclAllGather(dsend, drecv, bytes, ncclUint8, d->comm, ctx->stream));
+      return;
+    }
+    // blocks above kMaxCollBytes per peer (a 2 GiB C5 shard on one rank): the same exchange as
+    // grouped point-to-point transfers of at most kMaxCollBytes each -- a single call of 2^31 bytes
+    // or more per peer returned wrong data on the box (tools/c5_dist_time.py at 2^27, world 1)
+    const uint8_t* s8 = static_cast<const uint8_t*>(dsend);
+    uint8_t* r8 = static_cast<uint8_t*>(drecv);
+    for (size_t off = 0; off < bytes; off += kMaxCollBytes) {
+      const size_t len = std::min(kMaxCollBytes, bytes - off);
+      SG_NCCL(ncclGroupStart());
+      for (int h = 0; h < d->G; ++h) {
+        SG_NCCL(ncclSend(s8 + (a2a ? (size_t)h * bytes : 0) + off, len, ncclUint8, h, d->comm, ctx->stream));
+        SG_NCCL(ncclRecv(r8 + (size_t)h * bytes + off, len, ncclUint8, h, d->comm, ctx->stream));
+      }
+      SG_NCCL(ncclGroupEnd());
+    }
     return;
   }
   if (d->G == 1) {
@@ -182,8 +200,7 @@ void exchange(sg_dist* d, const void* dsend, void* drecv, size_t bytes, bool a2a
 void plan(uint64_t n, int G, uint64_t& n1, uint64_t& n2) {
   SG_REQUIRE(n >= 2 && (n & (n - 1)) == 0, "distributed transform: n must be a power of two >= 2");
   SG_REQUIRE(G >= 1 && (G & (G - 1)) == 0, "distributed transform: the rank count must be a power of two");
-  const int logn = ilog2_exact(n);
-  n1 = (uint64_t)1 << (logn / 2);
+  n1 = dist_split(n);
   n2 = n / n1;
   SG_REQUIRE(n1 % G == 0 && n2 % (4 * (uint64_t)G) == 0,
              "distributed transform: n too small for this many ranks (needs N1 >= G and N2 >= 4 G)");
@@ -740,9 +757,15 @@ int dist_rank(const sg_dist* d) { return d->g; }
 bool dist_shard_algebra(const sg_dist* d) { return d->G > 1 && d->shard_algebra; }
 void dist_count_sharded_quotient(sg_dist* d) { ++d->sharded_quotients; }
 void dist_count_sharded_interpolation(sg_dist* d, uint64_t columns) { d->sharded_interpolations += columns; }
+uint64_t dist_split(uint64_t n) {
+  // N1 = 2^floor(log2 n / 2).  (Round 4 measured capping N1 at 2^11, so the size-N1 transforms run
+  // whole in one launch, against this split: 2^25 four-step 2.33 vs 2.27 ms, 2^27 9.25 vs 8.87 ms
+  // on one rank -- the longer size-N2 transforms cost more than the pass it saves)
+  return (uint64_t)1 << (ilog2_exact(n) / 2);
+}
 bool dist_can_shard(uint64_t n, int G) {
   if (n < 2 || (n & (n - 1)) || G < 1 || (G & (G - 1))) return false;
-  const uint64_t n1 = (uint64_t)1 << (ilog2_exact(n) / 2), n2 = n / n1;
+  const uint64_t n1 = dist_split(n), n2 = n / n1;
   // sg_dist_plan (ntt) and the inverse's interleaved first pass (intt)
   return n1 % (uint64_t)G == 0 && n2 % (4 * (uint64_t)G) == 0 && n2 % (uint64_t)G == 0 && n1 / G >= 4 &&
          (n1 / G) % 4 == 0;

@@ -42,8 +42,10 @@ bool dist_shard_algebra(const sg_dist* d);
 void dist_count_sharded_quotient(sg_dist* d);
 void dist_count_sharded_interpolation(sg_dist* d, uint64_t columns);
 // n splits over G ranks for both the forward transform (sg_dist_plan) and the inverse
+uint64_t dist_split(uint64_t n);
 bool dist_can_shard(uint64_t n, int G);
-// sg_dist_plan: n = N1 N2, N1 = 2^floor(log2 n / 2); run shards hold N1 runs of N2 / G elements
+// sg_dist_plan: n = N1 N2, N1 = dist_split(n) = 2^floor(log2 n / 2); run shards hold N1 runs of N2 / G
+// elements
 void dist_plan(uint64_t n, int G, uint64_t& n1, uint64_t& n2);
 // fft/ntt_arithmetics.rs:161-170 of a coefficient vector every rank holds (device, len <= n) into
 // this rank's run shard [N1][N2 / G] (its column shard gathered first)

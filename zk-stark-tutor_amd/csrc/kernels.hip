@@ -393,7 +393,8 @@ struct FirstArgs {
   int ep_logR;
 };
 
-template <int TL, bool WHOLE = false>
+// WHOLE variants: EP = the four-step epilogue store, POST = times *post (INTT n^-1), else canonical
+template <int TL, bool WHOLE = false, bool EP = false, bool POST = false>
 __global__ __launch_bounds__(1 << (TL - 3), TL == 11 ? SG_NTT_WPE : 1) void k_ntt_first(FirstArgs a) {
   extern __shared__ fe_lds lds[];
   const int L = a.L, logC = a.logC, m = a.logn;
@@ -411,12 +412,15 @@ __global__ __launch_bounds__(1 << (TL - 3), TL == 11 ? SG_NTT_WPE : 1) void k_nt
   auto hcol = [&](uint64_t k) { return rowcols ? c0 : c0 + k; };
   auto ycol = [&](uint64_t k) { return rowcols ? y0 + k : y0; };
   // element idx of column k's row
+  // (WHOLE: strided rows only -- a per-lane pick among the pointer array costs ~20 VGPRs)
   auto in_at = [&](uint64_t k, uint64_t idx) -> const fe* {
     if (il) return a.in[0] + idx * a.in_il + ycol(k);
+    if constexpr (WHOLE) return a.in[0] + ycol(k) * a.in_ys + idx;
     return (a.in_ys ? a.in[0] + ycol(k) * a.in_ys : a.in[ycol(k)]) + idx;
   };
   auto out_row = [&](uint64_t k) -> fe* {
     const uint64_t y = ycol(k);
+    if constexpr (WHOLE) return a.out[0] + y * a.out_ys;
     return a.out_ys ? a.out[0] + y * a.out_ys : a.out[y];
   };
   PassArgs pa;
@@ -481,11 +485,11 @@ __global__ __launch_bounds__(1 << (TL - 3), TL == 11 ? SG_NTT_WPE : 1) void k_nt
     fe* const orow = out_row(c);
     if constexpr (WHOLE) {
       // the transform's final values (m == L): element k = qq + mm 2^tl of row ycol(c)
-      const fe pc = a.post ? ld_fe(a.post) : fe_zero();
+      const fe pc = POST ? ld_fe(a.post) : fe_zero();
 #pragma unroll
       for (int mm = 0; mm < 8; ++mm) {
         const uint64_t k = qq + ((uint32_t)mm << tl);
-        if (a.ep_out) {
+        if constexpr (EP) {
           const uint64_t r = a.ep_row0 + ycol(c);
           const uint64_t e = (a.ep_j0 + r) * k;  // < 2^36 (host-checked)
           const fe w = mont_mul(mont_mul(ld_fe(a.ep_T0 + (e & 4095)), ld_fe(a.ep_T1 + ((e >> 12) & 4095))),
@@ -493,7 +497,7 @@ __global__ __launch_bounds__(1 << (TL - 3), TL == 11 ? SG_NTT_WPE : 1) void k_nt
           const uint64_t R = (uint64_t)1 << a.ep_logR;
           st_fe(a.ep_out + ((k >> a.ep_logR) * a.ep_rows + r) * R + (k & (R - 1)), mont_mul(x[mm], w));
         } else {
-          st_fe(orow + k, a.post ? mont_mul(x[mm], pc) : fe_canon(x[mm]));
+          st_fe(orow + k, POST ? mont_mul(x[mm], pc) : fe_canon(x[mm]));
         }
       }
       return;
@@ -990,7 +994,9 @@ static hipError_t ntt_lds_attributes() {
     if (e == hipSuccess) e = set((const void*)k_ntt_first<11>, 65536);
     if (e == hipSuccess) e = set((const void*)k_ntt_first<12>, 65536);
     if (e == hipSuccess) e = set((const void*)k_ntt_first<13>, 131072);
-    if (e == hipSuccess) e = set((const void*)k_ntt_first<11, true>, 65536);
+    if (e == hipSuccess) e = set((const void*)k_ntt_first<11, true, false, false>, 65536);
+    if (e == hipSuccess) e = set((const void*)k_ntt_first<11, true, false, true>, 65536);
+    if (e == hipSuccess) e = set((const void*)k_ntt_first<11, true, true>, 65536);
     return e;
   }();
   return err;
@@ -1082,6 +1088,11 @@ hipError_t launch_ntt_dit(fe* const* data, int batch, const fe* tw, int logn, co
 
 // Whole transform: fused bit-reversal first pass (when logn leaves room for a
 // later pass), then launch_ntt_dit from stage L1 + 1.  `out` must not alias `in`.
+bool ntt_small_whole(int logn, int batch, int skip, bool strided) {
+  static const bool on = env_int("SG_NTT_SMALL_WHOLE", 1) != 0;
+  return on && strided && logn >= 6 && logn <= 11 && skip <= logn - 3 && batch % (1 << (11 - logn)) == 0;
+}
+
 hipError_t launch_ntt_fused(fe* const* out, const fe* const* in, int batch, uint64_t n_in, int logn, const fe* tw,
                             const fe* sA, const fe* sB, int skip, const fe* post, hipStream_t s, uint64_t in_ys,
                             uint64_t out_ys, uint64_t in_il, const NttEpilogue* ep) {
@@ -1101,9 +1112,8 @@ hipError_t launch_ntt_fused(fe* const* out, const fe* const* in, int batch, uint
     // per 256-lane tile: the gather, every stage and the final store (canonical / n^-1 / four-step
     // epilogue) without the bit-reversal pass and the all-LDS generic pass (SG_NTT_SMALL_WHOLE=0:
     // the latter, A/B)
-    static const bool small_whole = env_int("SG_NTT_SMALL_WHOLE", 1) != 0;
     const int logCw = 11 - logn;
-    if (small_whole && logn >= 6 && logn <= 11 && skip <= logn - 3 && batch % (1 << logCw) == 0) {
+    if (ntt_small_whole(logn, batch, skip, out_ys != 0)) {
       for (int b = 0; b < kMaxBatch; ++b) {
         a.out[b] = b < np ? out[b] : nullptr;
         a.in[b] = b < np ? in[b] : nullptr;
@@ -1133,7 +1143,10 @@ hipError_t launch_ntt_fused(fe* const* out, const fe* const* in, int batch, uint
       }
       const uint64_t n = (uint64_t)1 << logn;
       ProfScope ps("ntt_small", batch * (16 * (n_in < n ? n_in : n) + 16 * n), s, (uint64_t)batch * n);
-      hipLaunchKernelGGL((k_ntt_first<11, true>), dim3(1, (unsigned)(batch >> logCw)), dim3(256), (size_t)16 << 11, s, a);
+      const dim3 grid(1, (unsigned)(batch >> logCw));
+      if (ep) hipLaunchKernelGGL((k_ntt_first<11, true, true>), grid, dim3(256), (size_t)16 << 11, s, a);
+      else if (post) hipLaunchKernelGGL((k_ntt_first<11, true, false, true>), grid, dim3(256), (size_t)16 << 11, s, a);
+      else hipLaunchKernelGGL((k_ntt_first<11, true, false, false>), grid, dim3(256), (size_t)16 << 11, s, a);
       return hipGetLastError();
     }
     hipError_t e = launch_bitrev_gather(out, in, batch, n_in, logn, sA, sB, skip, s, in_il ? 1 : in_ys, out_ys,

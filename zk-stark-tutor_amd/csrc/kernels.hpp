@@ -44,6 +44,9 @@ int ntt_first_tile(int logn);
 hipError_t launch_ntt_fused(fe* const* out, const fe* const* in, int batch, uint64_t n_in, int logn, const fe* tw,
                             const fe* sA, const fe* sB, int skip, const fe* post, hipStream_t s, uint64_t in_ys = 0,
                             uint64_t out_ys = 0, uint64_t in_il = 0, const NttEpilogue* ep = nullptr);
+// a batch of 2^logn-point transforms (2^6 .. 2^11) in strided rows runs whole in one first-pass
+// launch (2^(11 - logn) rows per tile; SG_NTT_SMALL_WHOLE=0 turns it off)
+bool ntt_small_whole(int logn, int batch, int skip, bool strided);
 uint64_t merkle_tree_digests(uint64_t n);
 // root_host (optional, per tree; pointer mode only): host-coherent 64-byte slots that receive the root.
 // start_level 1: level 0 of `tree` already holds n digests (a tree over given digests).

@@ -1317,8 +1317,7 @@ void stark_prove_dist(sg_dist* dd, const sg_stark& st, const fe* d_trace, size_t
   // a FRI domain too small to split over this many ranks (N1 >= G, N2 >= 4 G) is proved whole
   // by every rank: the same bytes, no collective
   const int G = dist_world(dd);
-  const int logNf = ilog2_exact(Nf);
-  const uint64_t p1 = (uint64_t)1 << (logNf / 2), p2 = Nf / p1;
+  const uint64_t p1 = dist_split(Nf), p2 = Nf / p1;
   if (p1 % (uint64_t)G != 0 || p2 % (4 * (uint64_t)G) != 0) {
     stark_prove(ctx, st, d_trace, rows, tcs, bnd, d_trace_rand, d_rcoef, nrc, ps);
     return;

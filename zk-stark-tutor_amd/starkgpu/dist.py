@@ -57,7 +57,8 @@ def _log2(n: int) -> int:
 
 
 def plan(n: int, world: int) -> Tuple[int, int]:
-    """(N1, N2) for an n-point transform over `world` ranks: N1 = 2^floor(log n / 2)."""
+    """(N1, N2) for an n-point transform over `world` ranks: N1 = 2^floor(log n / 2) (sg_dist_plan's
+    split, csrc/dist.cpp dist_split)."""
     logn = _log2(n)
     _log2(world)
     n1 = 1 << (logn // 2)
