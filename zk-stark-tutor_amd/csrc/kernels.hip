@@ -316,7 +316,7 @@ __global__ __launch_bounds__(256, SG_NTT_WPE) void k_ntt_pass(PassArgs a) {
 // element plus a round trip per middle step, and L/3 barriers fewer than k_ntt_pass.
 template <int TL>
 __global__ __launch_bounds__(1 << (TL - 3), TL == 11 ? SG_NTT_WPE : 1) void k_ntt_pass_rr(PassArgs a) {
-  static_assert(TL >= 11 && TL <= 13, "2^TL-element tiles, 2^(TL-3) threads");
+  static_assert(TL >= 10 && TL <= 13, "2^TL-element tiles, 2^(TL-3) threads");
   extern __shared__ fe_lds lds[];
   const int logC = a.logC, L = a.L;
   const uint32_t C = 1u << logC;
@@ -988,9 +988,11 @@ static hipError_t ntt_lds_attributes() {
     hipError_t e = set((const void*)k_ntt_pass<0>, 65536);
     if (e == hipSuccess) e = set((const void*)k_ntt_pass<12>, 65536);
     if (e == hipSuccess) e = set((const void*)k_ntt_pass<11>, 65536);
+    if (e == hipSuccess) e = set((const void*)k_ntt_pass_rr<10>, 65536);
     if (e == hipSuccess) e = set((const void*)k_ntt_pass_rr<11>, 65536);
     if (e == hipSuccess) e = set((const void*)k_ntt_pass_rr<12>, 65536);
     if (e == hipSuccess) e = set((const void*)k_ntt_pass_rr<13>, 131072);
+    if (e == hipSuccess) e = set((const void*)k_ntt_first<10>, 65536);
     if (e == hipSuccess) e = set((const void*)k_ntt_first<11>, 65536);
     if (e == hipSuccess) e = set((const void*)k_ntt_first<12>, 65536);
     if (e == hipSuccess) e = set((const void*)k_ntt_first<13>, 131072);
@@ -1012,8 +1014,8 @@ hipError_t launch_ntt_dit(fe* const* data, int batch, const fe* tw, int logn, co
   static const bool use_rr = env_int("SG_NTT_RR", 1) != 0;  // register-direct first/last steps
   const int big = big_tl;
   static const int tile_log = [] {
-    int t = env_int("SG_NTT_TILE_LOG", 11);
-    return (t == 11 || t == 12) ? t : 11;
+    int t = env_int("SG_NTT_TILE_LOG", 11);  // A/B knob: 10, 11 or 12
+    return (t >= 10 && t <= 12) ? t : 11;
   }();
   if (first_b0 >= logn) {
     for (int b = 0; post && b < np; ++b) {
@@ -1075,6 +1077,8 @@ hipError_t launch_ntt_dit(fe* const* data, int batch, const fe* tw, int logn, co
       hipLaunchKernelGGL(k_ntt_pass<12>, grid, dim3(256), lds, s, a);
     else if (tile == 2048 && threads == 256 && a.L >= 6 && use_rr)
       hipLaunchKernelGGL(k_ntt_pass_rr<11>, grid, dim3(256), lds, s, a);
+    else if (tile == 1024 && threads == 128 && a.L >= 6 && use_rr)
+      hipLaunchKernelGGL(k_ntt_pass_rr<10>, grid, dim3(128), lds, s, a);
     else if (tile == 2048 && threads == 256)
       hipLaunchKernelGGL(k_ntt_pass<11>, grid, dim3(256), lds, s, a);
     else
@@ -1175,7 +1179,9 @@ hipError_t launch_ntt_fused(fe* const* out, const fe* const* in, int batch, uint
     ProfScope ps("ntt_first", batch * (16 * (n_in < n ? n_in : n) + 16 * n), s, (uint64_t)batch * n);
     // interleaved rows: a tile is 4 rows at one position (grid: positions x row quads)
     const dim3 grid = in_il ? dim3((unsigned)(n >> L1), (unsigned)(batch >> LOGC1)) : dim3((unsigned)(n >> TL), batch);
-    if (TL == 13)
+    if (TL == 10)
+      hipLaunchKernelGGL(k_ntt_first<10>, grid, dim3(128), (size_t)16 << 10, s, a);
+    else if (TL == 13)
       hipLaunchKernelGGL(k_ntt_first<13>, grid, dim3(1024), (size_t)16 << 13, s, a);
     else if (TL == 12)
       hipLaunchKernelGGL(k_ntt_first<12>, grid, dim3(512), (size_t)16 << 12, s, a);
@@ -1195,6 +1201,8 @@ int ntt_first_tile(int logn) {
   // tiles (11 + 10: 0.202 -> 0.184 ms); at 2^22 and above the three-pass plan on 2048-element
   // tiles (4 blocks per CU) wins, and below 2^18 the launch count no longer matters
   static const bool on = env_int("SG_NTT_TILES", 1) != 0;
+  static const int forced = env_int("SG_NTT_FIRST_TILE", 0);  // A/B knob: 10 .. 13 for every size
+  if (forced >= 10 && forced <= 13) return forced;
   if (!on) return 11;
   if (logn >= 18 && logn <= 20) return 12;
   if (logn == 21) return 13;
