@@ -381,9 +381,9 @@ struct FirstArgs {
   uint64_t in_il;
   // k_ntt_first<11, WHOLE = true>: the pass runs all logn = L stages of small transforms, the
   // tile's C columns being C whole rows (rows blockIdx.y C + k), and stores the final values:
-  // times *post (INTT n^-1), or canonical, or through the four-step epilogue (ep_out != nullptr,
-  // as pass_store) -- the bit-reversal gather and the generic all-LDS pass of a small transform
-  // in one launch
+  // times *post (INTT n^-1, POST), or canonical, or through the four-step epilogue (EP, as
+  // pass_store) -- the bit-reversal gather and the generic all-LDS pass of a small transform in
+  // one launch
   const fe* post;
   fe* ep_out;
   const fe* ep_T0;
@@ -412,7 +412,7 @@ __global__ __launch_bounds__(1 << (TL - 3), TL == 11 ? SG_NTT_WPE : 1) void k_nt
   auto hcol = [&](uint64_t k) { return rowcols ? c0 : c0 + k; };
   auto ycol = [&](uint64_t k) { return rowcols ? y0 + k : y0; };
   // element idx of column k's row
-  // (WHOLE: strided rows only -- a per-lane pick among the pointer array costs ~20 VGPRs)
+  // (WHOLE launches have strided rows: ntt_small_whole requires them)
   auto in_at = [&](uint64_t k, uint64_t idx) -> const fe* {
     if (il) return a.in[0] + idx * a.in_il + ycol(k);
     if constexpr (WHOLE) return a.in[0] + ycol(k) * a.in_ys + idx;
