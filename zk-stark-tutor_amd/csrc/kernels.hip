@@ -1302,12 +1302,13 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
         }
       }
     } else if (count * (uint64_t)batch >= kQuadBelow && count >= 2) {
-      // 3 levels per launch: same-box A/Bs (profiles/r03_ab_merkle_nodes.log, r03_ab_nodes.log) put 3
-      // ahead of 4 on the 2^25 tree (4.03-4.09 vs 4.12-4.16 ms) and in the prove; coalesced child
-      // loads staged through LDS were slower (4.22-4.27 ms) and were dropped.  The level is
+      // 2 levels per launch: same-box A/Bs put 3 ahead of 4 (round 3, profiles/r03_ab_merkle_nodes.log,
+      // r03_ab_nodes.log) and 2 ahead of 3 (round 4, r04_ab_node_fuse_*.log: every fused level above
+      // the first parks half of the block's remaining waves at a barrier); coalesced child loads
+      // staged through LDS were slower (4.22-4.27 ms) and were dropped.  The level is
       // throughput-bound when all its trees together have >= kQuadBelow nodes (a forest of many
       // small subtrees included): one lane per node, blocks no larger than a tree's level.
-      static const int env_nfuse = env_int("SG_MERKLE_NODE_FUSE", 3);
+      static const int env_nfuse = env_int("SG_MERKLE_NODE_FUSE", 2);
       static const int env_nbs = env_int("SG_MERKLE_NODE_BS", 256);  // A/B knob: 256 or 512
       kind = env_nbs == 512 ? 6 : 2; bs = env_nbs == 512 ? 512u : 256u; fuse = env_nfuse;
       // SG_MERKLE_NODE_PIPE=1: blocks walk several groups, the next group's children loaded while
