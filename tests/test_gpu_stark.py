@@ -167,7 +167,9 @@ def test_stark_prove_rebuilt_constraints_keep_tables_flat(monkeypatch, generic):
         assert st.prove(trace, air, bnd, sg.IndependentProofStream(), tr, rc) == want
         counts.append(ctx.cached_tables())
         del air
-    assert counts[0][0] > 0 and all(c == counts[0] for c in counts), counts
+    # (with SG_NO_DOMAIN_CACHE=1 -- the alternate-paths suite -- nothing is cached: flat at zero)
+    cached = os.environ.get("SG_NO_DOMAIN_CACHE") != "1"
+    assert (counts[0][0] > 0 or not cached) and all(c == counts[0] for c in counts), counts
 
 
 def test_stark_prove_constraints_shared_by_two_contexts():
