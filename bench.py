@@ -545,7 +545,63 @@ def faithful_block_step(rc, o, N: int) -> float:
     return time.perf_counter() - t0
 
 
-def cpu_baseline_leg(headline_N: int, log_Ns=(12, 13, 14, 15, 16)) -> dict:
+def _other_physical_core(core: int) -> int:
+    """A CPU of this process's affinity on a different physical core than `core` (not its SMT
+    sibling), so two single-core legs can run side by side; `core` itself when there is none."""
+    def siblings(c):
+        try:
+            with open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list") as f:
+                out = set()
+                for part in f.read().strip().split(","):
+                    a, _, b = part.partition("-")
+                    out.update(range(int(a), int(b or a) + 1))
+                return out
+        except OSError:
+            return {c}
+    busy = siblings(core) | {core}
+    for c in sorted(os.sched_getaffinity(0)):
+        if c not in busy:
+            return c
+    return core
+
+
+def faithful_c2_start(core: int, log_n: int = 22):
+    """C2 on the reference's algorithms, timed directly: oracle/ref_cpu.c's ntt and
+    intt (fft/ntt.rs:7-68 over field.rs:117-131's bit-serial mul_mod) of 2^22 elements -- the
+    bench's C2 input -- on ONE pinned core.  ~30 s per transform on the box's host, so it runs in a
+    thread (ctypes drops the GIL) pinned to `core` while the one-core block leg runs on another
+    physical core.  Returns (thread, result dict filled when the thread ends)."""
+    sys.path.insert(0, os.path.join(ROOT, "oracle"))
+    import ref_cpu as rc
+    import stark_oracle as o
+    res = {}
+
+    def run():
+        try:
+            os.sched_setaffinity(threading.get_native_id(), {core})
+            n = 1 << log_n
+            x = synthetic_fe(7, b"c2", n)
+            w = o.primitive_nth_root(n)
+            t0 = time.perf_counter()
+            y = rc.ntt(w, x)
+            t1 = time.perf_counter()
+            z = rc.intt(w, y)
+            t2 = time.perf_counter()
+            res.update({"c2_faithful_ms": round((t2 - t0) * 1e3, 1), "c2_faithful_fwd_ms": round((t1 - t0) * 1e3, 1),
+                        "c2_faithful_inv_ms": round((t2 - t1) * 1e3, 1),
+                        "c2_faithful_gelem_s": round(2 * n / (t2 - t0) / 1e9, 8),
+                        "c2_faithful_roundtrip_ok": bool(np.array_equal(z, x)), "c2_faithful_cpu": core,
+                        "c2_faithful_sample": f"2^{log_n} fwd + inv NTT through oracle/ref_cpu.c (bit-serial mul_mod, "
+                                              f"the reference's radix-2 DIT), one pinned core, timed directly"})
+        except Exception as e:  # noqa: BLE001 - reported in the line, the baseline leg stands
+            res["c2_faithful_error"] = f"{type(e).__name__}: {e}"
+
+    th = threading.Thread(target=run, daemon=True)
+    th.start()
+    return th, res
+
+
+def cpu_baseline_leg(headline_N: int, log_Ns=(12, 13, 14, 15, 16), with_c2: bool = True) -> dict:
     """The reference-faithful C restatement (oracle/ref_cpu.c: bit-serial mul_mod, xgcd inverse,
     per-element pow + division in the fold, recursive Merkle with to_string leaves and O(n) opens)
     on ONE host core -- the reference is single-threaded.
@@ -555,6 +611,8 @@ def cpu_baseline_leg(headline_N: int, log_Ns=(12, 13, 14, 15, 16)) -> dict:
     t(N) = a N log2 N + b N (NTTs; hashing, folds and the O(N) opens), fitted by least squares
     (SURVEY.md 8(d)(i)).  The reference's trace interpolation and quotient algebra are O(T^2)
     and are not in this leg (cpu_baseline_e2e times them through the Python restatement).
+    Beside it (`with_c2`), C2's 2^22 fwd + inv NTT on the reference's algorithms is timed directly on
+    a second pinned core (faithful_c2_start), so the GPU's C2 line has its CPU counterpart.
     """
     sys.path.insert(0, os.path.join(ROOT, "oracle"))
     import ref_cpu as rc
@@ -563,12 +621,16 @@ def cpu_baseline_leg(headline_N: int, log_Ns=(12, 13, 14, 15, 16)) -> dict:
     # the reference is single-threaded: the leg runs pinned to one core (SURVEY.md 8(d)(i) "taskset")
     prev = os.sched_getaffinity(0)
     core = min(prev)
+    # C2 on the reference's algorithms, directly at 2^22, on another physical core meanwhile
+    c2_thread, c2 = faithful_c2_start(_other_physical_core(core)) if with_c2 else (None, {})
     os.sched_setaffinity(0, {core})
     try:
         for ln in log_Ns:
             pts.append((1 << ln, faithful_block_step(rc, o, 1 << ln)))
     finally:
         os.sched_setaffinity(0, prev)
+    if c2_thread is not None:
+        c2_thread.join()
     from scipy.optimize import nnls
     A = np.array([[n * np.log2(n), n] for n, _ in pts], dtype=np.float64)
     y = np.array([t for _, t in pts], dtype=np.float64)
@@ -590,6 +652,7 @@ def cpu_baseline_leg(headline_N: int, log_Ns=(12, 13, 14, 15, 16)) -> dict:
                                   "value": round((REGISTERS + 2) * Nh / float(t_h) / 1e9, 8),
                                   "model": f"t = {a:.3e} N log2 N + {b:.3e} N (least squares over the "
                                            f"measured points, non-negative)", "label": "extrapolated"},
+        "c2": c2 or None,
     }
 
 

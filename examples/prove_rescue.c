@@ -17,7 +17,8 @@
  * id_file, the other ranks wait for it; every rank writes the same bytes.  `nonce` (any 64-bit
  * number the launcher picks per run and passes to every rank) is written before the id, and the
  * other ranks accept only a file carrying it: an id file left over from an earlier run is never
- * read as this run's id.
+ * read as this run's id.  With nranks > 1 the nonce is required (a missing or zero nonce is a
+ * usage error).
  *
  * randomness.bin: 16-byte little-endian (lo, hi) field elements -- num_randomizers x 2 trace
  * randomizer rows (stark.rs:285-301), then max_degree + 1 randomizer coefficients
@@ -63,6 +64,11 @@ int main(int argc, char** argv) {
     } else {
       bad = 1;
     }
+  }
+  if (dist && nranks > 1 && nonce == 0) {
+    /* the nonce is what keeps a stale id file from an earlier run from being read as this run's */
+    fprintf(stderr, "--dist with nranks > 1 needs a non-zero nonce (the same on every rank)\n");
+    bad = 1;
   }
   if (bad) {
     fprintf(stderr,

@@ -54,6 +54,13 @@ int sg_ctx_trim(sg_ctx* ctx);
  * (domain / AIR coset tables, twiddle plans, interpolation kernels) -- constant across proofs
  * on one (AIR, domain), also when the constraints are rebuilt for every proof */
 int sg_ctx_cached_tables(const sg_ctx* ctx, size_t* domain_tables, size_t* twiddle_tables);
+/* Device memory (no reference counterpart): `live` = bytes of the context's buffer pool in use,
+ * `peak` = their high-water mark since creation or the last reset (the working set of the calls
+ * in between: codewords, retained trees, scratch), `pooled` = returned buffers the pool caches,
+ * device_used / device_total = hipMemGetInfo of the context's device (every process, every
+ * allocation: cached tables included).  reset_peak != 0 restarts the high-water mark at `live`. */
+int sg_ctx_memory(sg_ctx* ctx, uint64_t* live, uint64_t* peak, uint64_t* pooled, uint64_t* device_used,
+                  uint64_t* device_total, int reset_peak);
 /* HBM probe (measurement, no reference counterpart): read + write GB/s of a dwordx4 streaming
  * device copy of `bytes` (multiple of 16), best of `iters`; blocks = 0: one 16-byte element per
  * lane, else a grid-stride copy over blocks x 256 lanes */
@@ -256,10 +263,15 @@ void sg_dist_destroy(sg_dist* d);
 /* Failure containment (no reference counterpart; the reference is single-process).  Every
  * sg_dist_* call below is collective.  When one fails on a rank -- an error of its own, a failing
  * proof-stream or transport callback, an RCCL asynchronous error, or a host wait that outlasts the
- * deadline -- the communicator is POISONED on that rank: RCCL's is aborted (ncclCommAbort ends the
- * collectives in flight, so the peers' waits fail in turn), a caller transport's abort hook runs,
- * and every later call on it returns SG_ERR_INVALID.  Destroy it and create a new one.
- * Deadline: SG_DIST_TIMEOUT_S at creation (default 300 s) or sg_dist_set_timeout (per rank). */
+ * deadline -- the communicator is POISONED on that rank: RCCL's is aborted with ncclCommAbort, a
+ * caller transport's abort hook runs, and every later call on it returns SG_ERR_INVALID.  Destroy
+ * it and create a new one.  The abort is LOCAL: over RCCL the peers get no signal -- their
+ * collectives keep waiting for the failed rank until their own host-wait deadline passes, and
+ * only then do they poison their communicators and return.  Host-blocking RCCL calls
+ * (ncclCommInitRank, the connection set-up inside ncclGroupEnd) are not watched by the deadline.
+ * A caller transport can do better through its abort hook (e.g. tear its group down).
+ * Deadline: SG_DIST_TIMEOUT_S at creation (default 300 s) or sg_dist_set_timeout (per rank);
+ * callers that need fast failure set a deadline of a few times their longest collective step. */
 int sg_dist_set_timeout(sg_dist* d, double seconds);
 int sg_dist_poisoned(const sg_dist* d); /* 1 when poisoned */
 /* instrumentation: collectives this communicator issued, transition quotients and trace columns

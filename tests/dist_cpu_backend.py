@@ -1,10 +1,12 @@
 """Oracle-backed local backend for the multi-GPU driver (test infrastructure only).
 
-`starkgpu.dist.DistStark` composes local row steps with collectives; these CPU
+`dist_model.DistStark` (the test model of the sharded path) composes local row steps with
+collectives; these CPU
 versions of the row steps (built from the oracle, oracle/stark_oracle.py) let
 the distribution logic -- index maps, the all-to-all, run-root gathering,
 run-sharded folds, the FRI tail -- run over gloo on CPU with world_size > 1.
-The product backend is `starkgpu.dist.GpuRows` (HIP kernels through the C ABI).
+Its GPU backend is `dist_model.GpuRows` (HIP kernels through the C ABI's row entry points); the
+product's sharded path is the C ABI's `sg_dist_*` (`starkgpu.dist.NativeDist`).
 """
 from typing import List, Optional, Sequence
 
@@ -51,7 +53,7 @@ class CpuRows:
         b = bytes(buf.tolist())
         return [b[i:i + 64] for i in range(0, len(b), 64)]
 
-    # local steps (same contracts as starkgpu.dist.GpuRows)
+    # local steps (same contracts as dist_model.GpuRows)
     def ntt_rows(self, root, src, n_in, rows, dst, n):
         x = self.to_ints(src, rows * n_in)
         out = []

@@ -1,4 +1,4 @@
-"""Multi-rank logic of the sharded path (starkgpu/dist.py) on CPU: gloo, world 2 and 4.
+"""Multi-rank logic of the sharded path (the test model tests/dist_model.py) on CPU: gloo, world 2 and 4.
 
 The local row steps come from the oracle (tests/dist_cpu_backend.py); what is
 under test is the distribution itself -- the four-step index maps and its one
@@ -26,10 +26,11 @@ def _free_port() -> int:
 
 def _cases(world):
     from starkgpu import dist as D
+    import dist_model as M
     from dist_cpu_backend import CpuRows
 
     be = CpuRows()
-    ds = D.DistStark(be, D.Comm())
+    ds = M.DistStark(be, M.Comm())
     g = ds.g
 
     def gather(buf):

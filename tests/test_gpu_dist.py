@@ -3,7 +3,8 @@
 * the new entry points (sg_ntt_rows_dev, sg_mul_pow_dev, sg_transpose_dev,
   sg_merkle_forest_dev / sg_merkle_top_dev, sg_fri_fold_runs_dev) against the
   oracle and the single-GPU path;
-* DistStark with the HIP backend at world size 1 (in process) and world size 2
+* the test model of the sharded path (tests/dist_model.py: DistStark over the row entry points)
+  with the HIP backend at world size 1 (in process) and world size 2
   (two processes sharing this box's one GPU over gloo, device tensors staged
   through the host): four-step NTT / INTT, sharded LDE, Merkle root and FRI
   commit proof-stream bytes equal the single-GPU results (which the parity
@@ -58,8 +59,9 @@ def _ints(a):
 def test_ntt_rows_matches_oracle(n, n_in, rows):
     import torch
     from starkgpu import dist as D
+    import dist_model as M
     import ref_cpu
-    be = D.GpuRows()
+    be = M.GpuRows()
     root = o.primitive_nth_root(n)
     x = _rand(n + rows, rows * n_in)
     src = _t(x)
@@ -76,7 +78,8 @@ def test_ntt_rows_beyond_grid_limit():
     """70000 rows (> 65535 per launch) of n = 8: chunked launches, every row right."""
     import torch
     from starkgpu import dist as D
-    be = D.GpuRows()
+    import dist_model as M
+    be = M.GpuRows()
     n, rows = 8, 70000
     root = o.primitive_nth_root(n)
     pats = _rand(5, 3 * n).reshape(3, n, 2)
@@ -92,7 +95,8 @@ def test_ntt_rows_beyond_grid_limit():
 def test_mul_pow_and_transpose():
     import torch
     from starkgpu import dist as D
-    be = D.GpuRows()
+    import dist_model as M
+    be = M.GpuRows()
     rows, cols = 37, 53
     base = o.synthetic_elements(1, b"base", 1)[0]
     x = _rand(11, rows * cols)
@@ -117,7 +121,8 @@ def test_forest_top_and_fold_runs():
     import torch
     import starkgpu as sg
     from starkgpu import dist as D
-    be = D.GpuRows()
+    import dist_model as M
+    be = M.GpuRows()
     run, runs = 1 << 10, 8
     x = _rand(21, run * runs)
     buf = _t(x)
@@ -155,7 +160,8 @@ def test_dist_world1_ntt_lde_merkle(logn):
     import torch
     import starkgpu as sg
     from starkgpu import dist as D
-    ds = D.DistStark(D.GpuRows(), D.Comm())
+    import dist_model as M
+    ds = M.DistStark(M.GpuRows(), M.Comm())
     n = 1 << logn
     root = sg.primitive_nth_root(n)
     x = _rand(logn, n)
@@ -184,7 +190,8 @@ def test_dist_world1_fri_commit_stream():
     import torch
     import starkgpu as sg
     from starkgpu import dist as D
-    ds = D.DistStark(D.GpuRows(), D.Comm())
+    import dist_model as M
+    ds = M.DistStark(M.GpuRows(), M.Comm())
     n, exp, c = 1 << 14, 8, 16
     w = sg.primitive_nth_root(n)
     cw = _rand(77, n)
@@ -204,12 +211,13 @@ def _world2_worker(rank, world, port, logn):
     import torch.distributed as dist
     import starkgpu as sg
     from starkgpu import dist as D
+    import dist_model as M
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         ctx = sg.Context(0)
-        ds = D.DistStark(D.GpuRows(ctx), D.Comm())
+        ds = M.DistStark(M.GpuRows(ctx), M.Comm())
         n = 1 << logn
         root = sg.primitive_nth_root(n)
         x = _rand(logn, n)

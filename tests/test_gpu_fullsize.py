@@ -197,37 +197,6 @@ def test_trace_2p20_headline_proof_bytes_and_verified(fc):
 C5_LOG = 27
 
 
-def _c5_worker(rank, world, port, tmp):
-    import torch
-    import torch.distributed as dist
-    from starkgpu import dist as D
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(port)
-    dist.init_process_group("gloo", rank=rank, world_size=world)
-    try:
-        ctx = sg.Context(0)
-        ds = D.DistStark(D.GpuRows(ctx), D.Comm())
-        n = 1 << C5_LOG
-        n1, n2 = D.plan(n, world)
-        rows, R = n1 // world, n2 // world
-        x = np.load(os.path.join(tmp, "x.npy"), mmap_mode="r")
-        X = np.load(os.path.join(tmp, "X.npy"), mmap_mode="r")
-        # column shard: row r = x[(rank rows + r) + N1 j2], j2 < N2
-        cols = np.ascontiguousarray(x.reshape(n2, n1, 2)[:, rank * rows:(rank + 1) * rows].transpose(1, 0, 2))
-        dev = torch.device("cuda", 0)
-        shard = torch.from_numpy(cols.view(np.int64).reshape(-1)).to(dev)
-        root = o.primitive_nth_root(n)
-        out = ds.ntt(root, shard, n2, n)
-        got = out.cpu().numpy().view(np.uint64).reshape(n1, R, 2)
-        want = X.reshape(n1, n2, 2)[:, rank * R:(rank + 1) * R]
-        ok = bool(np.array_equal(got, want))
-        flags = [None] * world
-        dist.all_gather_object(flags, ok)
-        assert all(flags), f"sharded 2^{C5_LOG} NTT differs from the single-GPU transform: {flags}"
-    finally:
-        dist.destroy_process_group()
-
-
 @pytest.fixture(scope="module")
 def c5_reference(fc):
     """x (2^27 seeded elements) and X = single-GPU sg.ntt(x), checked against the CPU checker."""
@@ -318,12 +287,3 @@ def test_c5_native_dist_2p27_world1_rccl(c5_reference):
         assert torch.equal(back, shard), "sg_dist_intt at world 1"
     finally:
         nd.close()
-
-
-@pytest.mark.parametrize("world", [2, 8])
-def test_c5_sharded_2p27_ntt_one_gpu_gloo(c5_reference, world):
-    import torch.multiprocessing as mp
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-    mp.spawn(_c5_worker, args=(world, port, c5_reference), nprocs=world, join=True)

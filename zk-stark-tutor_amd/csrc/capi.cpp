@@ -33,6 +33,8 @@ void* sg_ctx::alloc(size_t bytes) {
     void* p = it->second;
     free_bufs.erase(it);
     pooled_bytes -= r;
+    live_bytes += r;
+    if (live_bytes > peak_live_bytes) peak_live_bytes = live_bytes;
     return p;
   }
   void* p = nullptr;
@@ -43,6 +45,8 @@ void* sg_ctx::alloc(size_t bytes) {
     e = hipMalloc(&p, r);
     if (e != hipSuccess) throw Error{SG_ERR_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e)};
   }
+  live_bytes += r;
+  if (live_bytes > peak_live_bytes) peak_live_bytes = live_bytes;
   return p;
 }
 
@@ -51,6 +55,7 @@ void sg_ctx::release(void* p, size_t bytes) {
   size_t r = pool_round(bytes);
   free_bufs.emplace(r, p);
   pooled_bytes += r;
+  live_bytes -= r;
 }
 
 void sg_ctx::trim() {
@@ -92,24 +97,32 @@ const fe* sg_ctx::pow_table(const fe& root, uint64_t count) {
   }
   void* table = nullptr;
   SG_HIP(hipMalloc(&table, std::max<uint64_t>(count, 1) * sizeof(fe)));
-  if (count <= 4096) {
-    SG_HIP(hipMemcpyAsync(table, A.data(), na * sizeof(fe), hipMemcpyHostToDevice, stream));
-  } else {
-    uint64_t nb = (count + 4095) / 4096;
-    std::vector<fe> B(nb);
-    fe step = acc;  // Montgomery(root^4096)
-    fe b = to_mont(fe_one());
-    for (uint64_t i = 0; i < nb; ++i) {
-      B[i] = b;
-      b = mont_mul(b, step);
+  // a wait that throws (a poisoned communicator's watch) must not leak the fresh table while the
+  // queued launch may still write it
+  try {
+    if (count <= 4096) {
+      SG_HIP(hipMemcpyAsync(table, A.data(), na * sizeof(fe), hipMemcpyHostToDevice, stream));
+    } else {
+      uint64_t nb = (count + 4095) / 4096;
+      std::vector<fe> B(nb);
+      fe step = acc;  // Montgomery(root^4096)
+      fe b = to_mont(fe_one());
+      for (uint64_t i = 0; i < nb; ++i) {
+        B[i] = b;
+        b = mont_mul(b, step);
+      }
+      DevBuf dA(this, na * sizeof(fe)), dB(this, nb * sizeof(fe));
+      SG_HIP(hipMemcpyAsync(dA.get(), A.data(), na * sizeof(fe), hipMemcpyHostToDevice, stream));
+      SG_HIP(hipMemcpyAsync(dB.get(), B.data(), nb * sizeof(fe), hipMemcpyHostToDevice, stream));
+      SG_HIP(launch_pow_table(reinterpret_cast<fe*>(table), dA.as<fe>(), dB.as<fe>(), count, stream));
+      host_wait(this, stream);  // A/B return to the pool below
     }
-    DevBuf dA(this, na * sizeof(fe)), dB(this, nb * sizeof(fe));
-    SG_HIP(hipMemcpyAsync(dA.get(), A.data(), na * sizeof(fe), hipMemcpyHostToDevice, stream));
-    SG_HIP(hipMemcpyAsync(dB.get(), B.data(), nb * sizeof(fe), hipMemcpyHostToDevice, stream));
-    SG_HIP(launch_pow_table(reinterpret_cast<fe*>(table), dA.as<fe>(), dB.as<fe>(), count, stream));
-    host_wait(this, stream);  // A/B return to the pool below
+    host_wait(this, stream);
+  } catch (...) {
+    (void)hipStreamSynchronize(stream);
+    (void)hipFree(table);
+    throw;
   }
-  host_wait(this, stream);
   pow_tables[key] = PowTable{table, count};
   return reinterpret_cast<const fe*>(table);
 }
@@ -162,14 +175,20 @@ const fe* sg_ctx::stage_twiddles(const fe& root, int logn) {
   void* t = nullptr;
   const uint64_t entries = ntt_tw_entries(logn);
   SG_HIP(hipMalloc(&t, entries * sizeof(fe)));
-  SG_HIP(launch_stage_twiddles(reinterpret_cast<fe*>(t), A, B, logn, stream));
-  const int cut = ntt_tw_cut(logn);
-  if (cut < logn) {  // stages above the cut multiply A[e & 4095] * B[e >> 12] on the fly
-    fe* tail = reinterpret_cast<fe*>(t) + (((uint64_t)1 << cut) - 1);
-    SG_HIP(hipMemcpyAsync(tail, A, 4096 * sizeof(fe), hipMemcpyDeviceToDevice, stream));
-    SG_HIP(hipMemcpyAsync(tail + 4096, B, nb * sizeof(fe), hipMemcpyDeviceToDevice, stream));
+  try {
+    SG_HIP(launch_stage_twiddles(reinterpret_cast<fe*>(t), A, B, logn, stream));
+    const int cut = ntt_tw_cut(logn);
+    if (cut < logn) {  // stages above the cut multiply A[e & 4095] * B[e >> 12] on the fly
+      fe* tail = reinterpret_cast<fe*>(t) + (((uint64_t)1 << cut) - 1);
+      SG_HIP(hipMemcpyAsync(tail, A, 4096 * sizeof(fe), hipMemcpyDeviceToDevice, stream));
+      SG_HIP(hipMemcpyAsync(tail + 4096, B, nb * sizeof(fe), hipMemcpyDeviceToDevice, stream));
+    }
+    host_wait(this, stream);
+  } catch (...) {  // as pow_table: no leak, and no free while queued work may write it
+    (void)hipStreamSynchronize(stream);
+    (void)hipFree(t);
+    throw;
   }
-  host_wait(this, stream);
   stage_tables[key] = t;
   return reinterpret_cast<const fe*>(t);
 }
@@ -352,6 +371,22 @@ extern "C" int sg_ctx_trim(sg_ctx* ctx) {
     for (auto& kv : ctx->domain_tables) (void)hipFree(kv.second);
     ctx->domain_tables.clear();
     ctx->bounded_keys.clear();
+  });
+}
+
+extern "C" int sg_ctx_memory(sg_ctx* ctx, uint64_t* live, uint64_t* peak, uint64_t* pooled, uint64_t* device_used,
+                             uint64_t* device_total, int reset_peak) {
+  return guard(ctx, [&] {
+    set_device(ctx);
+    SG_REQUIRE(live && peak && pooled && device_used && device_total, "null output");
+    *live = ctx->live_bytes;
+    *peak = ctx->peak_live_bytes;
+    *pooled = ctx->pooled_bytes;
+    size_t fr = 0, tot = 0;
+    SG_HIP(hipMemGetInfo(&fr, &tot));
+    *device_used = tot - fr;
+    *device_total = tot;
+    if (reset_peak) ctx->peak_live_bytes = ctx->live_bytes;
   });
 }
 

@@ -76,6 +76,9 @@ struct sg_ctx {
   // pool: rounded size -> free pointers
   std::multimap<size_t, void*> free_bufs;
   size_t pooled_bytes = 0;
+  // bytes of pool buffers handed out and not yet returned (rounded sizes), and their high-water
+  // mark since creation / sg_ctx_memory's reset: the working set of the calls (sg_ctx_memory)
+  size_t live_bytes = 0, peak_live_bytes = 0;
   // power tables keyed by (root limbs, count)
   std::map<std::pair<std::pair<uint64_t, uint64_t>, uint64_t>, sg::PowTable> pow_tables;
   // host-coherent pinned slots for tree roots (written by the kernel that computes them)

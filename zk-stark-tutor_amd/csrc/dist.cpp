@@ -158,20 +158,24 @@ void exchange(sg_dist* d, const void* dsend, void* drecv, size_t bytes, bool a2a
   const size_t total = bytes * d->G;
   ++d->collectives;
   if (d->comm) {  // RCCL over xGMI, stream-ordered (a 1-rank communicator runs the same calls)
-    if (bytes <= kMaxCollBytes) {
+    // one call only while the whole exchange (per-peer block x G) stays within kMaxCollBytes: the
+    // wrong data was seen at world 1, where per-peer and total bytes coincide, so which of the two
+    // RCCL mishandles is not pinned -- bound both
+    if (total <= kMaxCollBytes) {
       if (a2a)
         SG_NCCL(ncclAllToAll(dsend, drecv, bytes, ncclUint8, d->comm, ctx->stream));
       else
         SG_NCCL(ncclAllGather(dsend, drecv, bytes, ncclUint8, d->comm, ctx->stream));
       return;
     }
-    // blocks above kMaxCollBytes per peer (a 2 GiB C5 shard on one rank): the same exchange as
-    // grouped point-to-point transfers of at most kMaxCollBytes each -- a single call of 2^31 bytes
-    // or more per peer returned wrong data on the box (tools/c5_dist_time.py at 2^27, world 1)
+    // larger exchanges (a 2 GiB C5 shard on one rank, 2^27 at world 2): the same exchange as
+    // grouped point-to-point transfers, each group moving at most kMaxCollBytes in all -- a single
+    // call of 2^31 bytes returned wrong data on the box (tools/c5_dist_time.py at 2^27, world 1)
     const uint8_t* s8 = static_cast<const uint8_t*>(dsend);
     uint8_t* r8 = static_cast<uint8_t*>(drecv);
-    for (size_t off = 0; off < bytes; off += kMaxCollBytes) {
-      const size_t len = std::min(kMaxCollBytes, bytes - off);
+    const size_t chunk = std::max<size_t>((kMaxCollBytes / d->G) & ~(size_t)255, 256);
+    for (size_t off = 0; off < bytes; off += chunk) {
+      const size_t len = std::min(chunk, bytes - off);
       SG_NCCL(ncclGroupStart());
       for (int h = 0; h < d->G; ++h) {
         SG_NCCL(ncclSend(s8 + (a2a ? (size_t)h * bytes : 0) + off, len, ncclUint8, h, d->comm, ctx->stream));

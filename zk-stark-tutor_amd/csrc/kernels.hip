@@ -176,11 +176,38 @@ __device__ __forceinline__ fe twiddle_comp(const PassArgs& a, int S, uint64_t k)
 // COMP: every twiddle of the step computed from A/B (the step reaches above s_cut), else
 // every twiddle from the table -- one uniform choice per step, so the step's twiddle loads
 // stay branch-free and are issued together.
+#ifndef SG_NTT_STAGE_TW
+#define SG_NTT_STAGE_TW 0
+#endif
 template <int R, bool COMP>
 __device__ __forceinline__ void radix_regs_impl(fe* x, const PassArgs& a, int t, uint32_t g_low, uint64_t low) {
 #pragma unroll
   for (int u = 0; u < R; ++u) {
     const int S = a.b0 + t + u + 1;  // global stage, 1-based
+#if SG_NTT_STAGE_TW
+    // one stage's twiddles live at a time (2^(R-1) x 4 VGPRs instead of R 2^(R-1) x 4): the
+    // scheduling barrier keeps the compiler from hoisting the next stage's loads above this one
+    fe w[1 << (R - 1)];
+#pragma unroll
+    for (int m = 0, j = 0; m < (1 << R); ++m) {
+      if (m & (1 << u)) continue;
+      uint64_t gmod = (uint64_t)g_low + ((uint64_t)(m & ((1 << u) - 1)) << t);
+      uint64_t k = (gmod << a.b0) + low;
+      w[j++] = COMP ? twiddle_comp(a, S, k) : twiddle_tab(a, S, k);
+    }
+#pragma unroll
+    for (int m = 0, j = 0; m < (1 << R); ++m) {
+      if (m & (1 << u)) continue;
+      fe o = mont_mul(x[m + (1 << u)], w[j++]);
+      fe ev = x[m];
+      x[m] = fe_add_lazy(ev, o);
+      x[m + (1 << u)] = fe_sub_lazy(ev, o);
+#if SG_NTT_STAGE_TW == 2
+      __builtin_amdgcn_sched_barrier(0);
+#endif
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#else
 #pragma unroll
     for (int m = 0; m < (1 << R); ++m) {
       if (m & (1 << u)) continue;
@@ -192,6 +219,7 @@ __device__ __forceinline__ void radix_regs_impl(fe* x, const PassArgs& a, int t,
       x[m] = fe_add_lazy(ev, o);  // tile values stay in [0, 2^128) until the last store
       x[m + (1 << u)] = fe_sub_lazy(ev, o);
     }
+#endif
   }
 }
 

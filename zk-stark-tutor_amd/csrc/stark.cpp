@@ -474,7 +474,11 @@ const fe* rescue_xvals(sg_ctx* ctx, const RescueAirForm& f, int idx, uint64_t L,
 
 // This rank's run shard of a public table of L coset values (`full`, computed by every rank
 // locally: no collective, so ranks whose caches differ stay in step), kept under `key` + (G, g).
-const fe* shard_table(sg_dist* dd, std::vector<uint64_t> key, const fe* full, uint64_t L, std::vector<DevBuf>& keep) {
+// `bounded`: the shard of a table the replicated path keeps bounded (domain_table_put_bounded, e.g.
+// the content-keyed boundary-divisor inverses) is kept the same way, so a prover that sees varying
+// boundary zerofiers keeps a constant number of tables on the sharded path too.
+const fe* shard_table(sg_dist* dd, std::vector<uint64_t> key, const fe* full, uint64_t L, std::vector<DevBuf>& keep,
+                      bool bounded = false) {
   sg_ctx* ctx = dist_ctx(dd);
   const bool kept = ctx->domain_cache_on();
   key.insert(key.begin(), kDomainShard);
@@ -495,10 +499,16 @@ const fe* shard_table(sg_dist* dd, std::vector<uint64_t> key, const fe* full, ui
   try {
     dist_take_runs(dd, full, L, out);
   } catch (...) {
-    if (t) (void)hipFree(t);
+    if (t) {
+      (void)hipStreamSynchronize(ctx->stream);  // the queued slice may still write it
+      (void)hipFree(t);
+    }
     throw;
   }
-  if (kept) ctx->domain_table_put(key, t);
+  if (kept) {
+    if (bounded) ctx->domain_table_put_bounded(key, t);
+    else ctx->domain_table_put(key, t);
+  }
   return out;
 }
 
@@ -847,7 +857,7 @@ void prove_boundary_quotients(sg_ctx* ctx, const sg_stark& st, const std::vector
             key.push_back(fe_lo(c));
             key.push_back(fe_hi(c));
           }
-          const fe* inv_shard = shard_table(dd, key, inv, pl.order, keep);
+          const fe* inv_shard = shard_table(dd, key, inv, pl.order, keep, /*bounded=*/true);
           DevBuf vals(ctx, nl * sizeof(fe)), cols(ctx, nl * sizeof(fe));
           dist_lde_replicated(dd, pl.root, pl.order, g, diffs[s].p(), diffs[s].len, vals.as<fe>());
           dev_mul(ctx, vals.as<fe>(), vals.as<fe>(), inv_shard, nl);

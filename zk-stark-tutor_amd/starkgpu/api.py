@@ -138,6 +138,13 @@ class Context:
         self.check(self._lib.sg_ctx_cached_tables(self.handle, ctypes.byref(d), ctypes.byref(t)))
         return d.value, t.value
 
+    def memory(self, reset_peak: bool = False) -> dict:
+        """Device memory (sg_ctx_memory): the buffer pool's bytes in use, their high-water mark since
+        creation or the last reset, the pool's cached free bytes, and hipMemGetInfo's used / total."""
+        v = [ctypes.c_uint64() for _ in range(5)]
+        self.check(self._lib.sg_ctx_memory(self.handle, *[ctypes.byref(x) for x in v], int(reset_peak)))
+        return dict(zip(("live", "peak", "pooled", "device_used", "device_total"), (x.value for x in v)))
+
     def hbm_copy_gbs(self, nbytes: int = 1 << 30, iters: int = 10, blocks: int = 0) -> float:
         """Read + write GB/s of the library's dwordx4 streaming copy kernel (best of `iters`)."""
         out = ctypes.c_double()
