@@ -356,3 +356,33 @@ def test_rpsss_published_configuration_signature_roundtrip(rpsss):
                        c.randomizer_coefficients)
     assert len(other) == R.PROOF_LEN and other != want
     assert c.oracle_verify(R.FORGED, other) == (True, "")
+
+
+def test_midsize_proof_bytes_equal_oracle_digest():
+    """A mid-size Stark::prove pinned to the Python oracle itself (tests/midsize_case.py): Rescue-Prime
+    N = 1000 -> trace 1257 rows, omicron domain 4096, FRI domain 2^15, expansion 8, c = 64,
+    transition degree 3 -- between the reference's published RPSSS configuration (FRI domain 4096)
+    and the full-size cases, which only the CPU checker pins.  The GPU proof's length and SHA-256
+    equal the oracle's (tests/golden/midsize_proof.json, written by tests/golden/make_midsize.py
+    from stark_prove_oracle.Stark.prove, stark.rs:276-562); the oracle verifier accepts it and
+    rejects a false claim."""
+    import hashlib
+    import midsize_case as M
+    with open(os.path.join(os.path.dirname(__file__), "golden", "midsize_proof.json")) as f:
+        g = json.load(f)
+    rp_o, st_o, trace, bnd, tr, rc = M.light_inputs()
+    rp_g = sg.RescuePrime(*M.RESCUE)
+    st_g = sg.Stark(M.EXPANSION, M.CHECKS, M.SECURITY, rp_g.m, M.RESCUE[3] + 1, M.TCD)
+    assert (st_g.omicron_domain_length, st_g.fri_domain_length) == (g["omicron_domain"], g["fri_domain"])
+    air_g = rp_g.transition_constraints(st_g.omicron, st_g.omicron_domain_length)
+    assert st_g.num_randomizer_coefficients(air_g) == len(rc)
+    assert str(bnd[-1][2]) == g["output"]
+    got = st_g.prove(trace, air_g, bnd, sg.IndependentProofStream(), tr, rc)
+    assert len(got) == g["proof_len"]
+    assert hashlib.sha256(got).hexdigest() == g["proof_sha256"], "GPU proof != oracle proof (digest)"
+    sair = e.RescueAirAtPoint.for_rescue(rp_o, st_o.omicron)
+    ok, err = st_o.verify(sair, bnd, o.IndependentProofStream(o.deserialize(got)))
+    assert ok, err
+    false_bnd = list(bnd[:-1]) + [(bnd[-1][0], bnd[-1][1], o.add_mod(bnd[-1][2], 1))]
+    ok, _ = st_o.verify(sair, false_bnd, o.IndependentProofStream(o.deserialize(got)))
+    assert not ok

@@ -234,3 +234,19 @@ def test_fast_stark_prove_rpsss_published_configuration(fc):
     ok, err = c.oracle_verify(R.FORGED, want)
     assert not ok, "rpsss.rs:127-131"
     assert o.serialize(o.deserialize(want)) == want
+
+
+def test_fast_stark_prove_midsize_equals_oracle_digest(fc):
+    """The CPU checker on the mid-size statement pinned to the Python oracle (tests/midsize_case.py:
+    trace 1257 rows, FRI domain 2^15, c = 64): its proof bytes hash to the oracle's committed digest
+    (tests/golden/midsize_proof.json, tests/golden/make_midsize.py), the link between the
+    published-configuration pin (FRI domain 4096) and the checker's full-size use."""
+    import hashlib
+    import json
+    import midsize_case as M
+    with open(os.path.join(ROOT, "tests", "golden", "midsize_proof.json")) as f:
+        g = json.load(f)
+    rp, st, trace, bnd, tr, rc = M.light_inputs()
+    got = fc.stark_prove_rescue(rp, st, trace, bnd, tr, rc)
+    assert len(got) == g["proof_len"]
+    assert hashlib.sha256(got).hexdigest() == g["proof_sha256"]
