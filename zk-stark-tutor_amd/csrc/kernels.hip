@@ -381,206 +381,6 @@ __global__ __launch_bounds__(1 << (TL - 3), TL == 11 ? SG_NTT_WPE : 1) void k_nt
     pass_store(a, data, base + ((uint64_t)(qq + ((uint32_t)m << tl)) << a.b0) + c, x[m], post, last, pc);
 }
 
-// ---- persistent pass with the next tile prefetched into LDS (round 5)
-//
-// k_ntt_pass_rr runs "load tile, compute, store tile" once per block, and with 4 blocks per CU
-// every block of a round loads, computes and stores at the same time: the SQ passes of a 2^22 pass
-// (profiles/r05_pmc_sq_ntt_c2_and_prove.txt) have the waves parked on s_waitcnt / barriers 38 % of
-// their cycles while the SIMDs idle.  Here each block walks tiles t, t + grid, ... and overlaps the
-// memory phases with compute: the tile's elements move HBM -> LDS by LDS-DMA
-// (global_load_lds_dwordx4, no VGPRs), issued for tile k+1 as soon as tile k's last LDS read is
-// done, i.e. beside tile k's last radix-8 step; tile k's stores stay in flight while tile k+1
-// starts.  vmcnt counts loads, stores and DMA in issue order, so the order inside an iteration is
-// fixed with scheduling barriers: last-step twiddle loads, DMA(k+1), compute, first-step twiddle
-// loads of tile k+1, stores(k); the next iteration then waits for all but the 8 stores.
-// Barriers are s_barrier after lgkmcnt(0) only (no release fence: the tile's global stores must
-// not be waited for at the LDS hand-overs).
-#ifndef SG_RRP_SERIAL
-#define SG_RRP_SERIAL 0
-#endif
-template <int N>
-__device__ __forceinline__ void wait_vmcnt() {
-  static_assert(N >= 0 && N < 64, "vmcnt");
-  __builtin_amdgcn_s_waitcnt((N & 15) | (7 << 4) | (15 << 8) | ((N >> 4) << 14));
-}
-__device__ __forceinline__ void lds_barrier() {
-  __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0); vmcnt / expcnt untouched
-  __builtin_amdgcn_s_barrier();
-}
-
-template <int R>
-__device__ __forceinline__ void radix_step_nf(fe_lds* lds, const PassArgs& a, int t, uint64_t lowbase) {
-  const int logC = a.logC;
-  const uint32_t C = 1u << logC;
-  const uint32_t groups = (1u << (a.L + logC)) >> R;
-  for (uint32_t q = threadIdx.x; q < groups; q += blockDim.x) {
-    uint32_t c = q & (C - 1);
-    uint32_t qq = q >> logC;
-    uint32_t g_low = qq & ((1u << t) - 1);
-    uint32_t g_high = qq >> t;
-    uint32_t g0 = (g_high << (t + R)) | g_low;
-    fe x[1 << R];
-#pragma unroll
-    for (int m = 0; m < (1 << R); ++m) x[m] = lds[((g0 + ((uint32_t)m << t)) << logC) + c];
-    radix_regs<R>(x, a, t, g_low, lowbase + c);
-#pragma unroll
-    for (int m = 0; m < (1 << R); ++m) lds[((g0 + ((uint32_t)m << t)) << logC) + c] = x[m];
-  }
-  lds_barrier();
-}
-
-// the 7 distinct twiddles of one radix-8 register step (stages t+1..t+3 of the pass): stage u's
-// butterfly m uses gmod = g_low + (m mod 2^u) 2^t, i.e. entry (2^u - 1) + (m mod 2^u)
-template <bool COMP>
-__device__ __forceinline__ void load_tw7(fe* w, const PassArgs& a, int t, uint32_t g_low, uint64_t low) {
-#pragma unroll
-  for (int u = 0; u < 3; ++u) {
-    const int S = a.b0 + t + u + 1;
-#pragma unroll
-    for (int j = 0; j < (1 << u); ++j) {
-      const uint64_t gmod = (uint64_t)g_low + ((uint64_t)j << t);
-      const uint64_t k = (gmod << a.b0) + low;
-      w[(1 << u) - 1 + j] = COMP ? twiddle_comp(a, S, k) : twiddle_tab(a, S, k);
-    }
-  }
-}
-__device__ __forceinline__ void radix8_with(fe* x, const fe* w) {
-#pragma unroll
-  for (int u = 0; u < 3; ++u) {
-#pragma unroll
-    for (int m = 0; m < 8; ++m) {
-      if (m & (1 << u)) continue;
-      const fe o = mont_mul(x[m + (1 << u)], w[(1 << u) - 1 + (m & ((1 << u) - 1))]);
-      const fe ev = x[m];
-      x[m] = fe_add_lazy(ev, o);
-      x[m + (1 << u)] = fe_sub_lazy(ev, o);
-#if SG_RRP_SERIAL
-      __builtin_amdgcn_sched_barrier(0);  // one butterfly's temporaries live at a time
-#endif
-    }
-  }
-}
-
-// tile `tile` of the pass -> its first element index (as k_ntt_pass_rr)
-__device__ __forceinline__ void tile_pos(const PassArgs& a, uint64_t tile, uint64_t& base, uint64_t& cbC) {
-  const int lncb = a.b0 - a.logC;  // column blocks per row block: 2^lncb
-  const uint64_t h = tile >> lncb, cb = tile & (((uint64_t)1 << lncb) - 1);
-  base = (h << (a.b0 + a.L)) + (cb << a.logC);
-  cbC = cb << a.logC;
-}
-
-// the whole 2^11-element tile HBM -> LDS: wave w moves 64-element pieces w*8 .. w*8+7 (1 KiB each)
-// (thread-index values are laundered through an empty asm per use, so the compiler recomputes the
-// per-tile addresses instead of hoisting every one out of the tile loop and spilling them)
-__device__ __forceinline__ uint32_t opaque_tid() {
-  uint32_t t = threadIdx.x;
-  asm volatile("" : "+v"(t));
-  return t;
-}
-
-// ... and the 7 C twiddles of its first radix-8 step (stages b0+1 .. b0+3 for the tile's C columns,
-// 7 runs of C consecutive stage-table entries: run (2^u - 1) + j holds stage b0+u+1's
-// k = j 2^b0 + cbC + c) into lds[2048 ..), one more DMA per wave (7 C <= 256 for L >= 6): every
-// wave-instruction of the tile counts 9 in vmcnt
-__device__ __forceinline__ void dma_tile(fe_lds* lds, const fe* data, const PassArgs& a, uint64_t base, uint64_t cbC) {
-  const uint32_t tid = opaque_tid();
-  const uint32_t lane = tid & 63, w = tid >> 6;
-  const uint32_t C = 1u << a.logC;
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {
-    const uint32_t piece = w * 8 + i;
-    const uint32_t l = piece * 64 + lane;
-    const fe* src = data + base + ((uint64_t)(l >> a.logC) << a.b0) + (l & (C - 1));
-    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src), reinterpret_cast<void*>(lds + piece * 64), 16,
-                                     0, 0);
-  }
-  const uint32_t e = w * 64 + lane;  // twiddle element, < 256
-  const uint32_t r = e >> a.logC, cc = e & (C - 1);
-  if (r < 7) {
-    const int u = r == 0 ? 0 : (r < 3 ? 1 : 2);
-    const uint32_t j = r - ((1u << u) - 1);
-    const fe* src = a.tw + (((uint64_t)1 << (a.b0 + u)) - 1) + ((uint64_t)j << a.b0) + cbC + cc;
-    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src), reinterpret_cast<void*>(lds + 2048 + w * 64), 16,
-                                     0, 0);
-  }
-}
-
-template <bool COMP_FIRST, bool COMP_LAST>
-__device__ __forceinline__ void pass_rrp_body(PassArgs a, fe_lds* lds, fe* data, uint64_t ntiles) {
-  const int logC = a.logC, L = a.L;
-  const uint32_t C = 1u << logC;
-  const int tl = L - 3;
-  const bool post = a.post != nullptr;
-  const bool last = a.b0 + L == a.logn;
-  const fe pc = post ? ld_fe(a.post) : fe_zero();
-  uint64_t tile = blockIdx.x;
-  uint64_t base, cbC;
-  tile_pos(a, tile, base, cbC);
-  static_assert(!COMP_FIRST, "the first step's twiddles come from the stage table");
-  dma_tile(lds, data, a, base, cbC);
-  wait_vmcnt<0>();
-  for (;;) {
-    const uint32_t tid = opaque_tid();
-    const uint32_t c = tid & (C - 1), qq = tid >> logC;  // qq < 2^(L-3)
-    lds_barrier();  // the tile and its first-step twiddles are in LDS (every wave's DMA waited for)
-    fe x[8], w[7];
-#pragma unroll
-    for (int r = 0; r < 7; ++r) w[r] = lds[2048 + (r << logC) + c];
-#pragma unroll
-    for (int m = 0; m < 8; ++m) x[m] = lds[((8 * qq + m) << logC) + c];
-    radix8_with(x, w);
-#pragma unroll
-    for (int m = 0; m < 8; ++m) lds[((8 * qq + m) << logC) + c] = x[m];
-    lds_barrier();
-    int t = 3;
-    while (t < L - 3) {
-      int rem = L - 3 - t;
-      if (rem >= 3) { radix_step_nf<3>(lds, a, t, cbC); t += 3; }
-      else if (rem == 2) { radix_step_nf<2>(lds, a, t, cbC); t += 2; }
-      else { radix_step_nf<1>(lds, a, t, cbC); t += 1; }
-    }
-    load_tw7<COMP_LAST>(w, a, tl, qq, cbC + c);  // older than the DMA below: waiting for them
-                                                   // does not wait for the DMA
-    if constexpr (COMP_LAST) __builtin_amdgcn_sched_barrier(0);  // products before x is live
-#pragma unroll
-    for (int m = 0; m < 8; ++m) x[m] = lds[((qq + ((uint32_t)m << tl)) << logC) + c];
-    const uint64_t next = tile + gridDim.x;
-    const bool more = next < ntiles;
-    uint64_t nbase = 0, ncbC = 0;
-    if (more) tile_pos(a, next, nbase, ncbC);
-    lds_barrier();  // every wave has read the tile: the slot is free
-    __builtin_amdgcn_sched_barrier(0);
-    if (more) dma_tile(lds, data, a, nbase, ncbC);
-    __builtin_amdgcn_sched_barrier(0);
-    radix8_with(x, w);
-#pragma unroll
-    for (int m = 0; m < 8; ++m) {  // pass_store without the four-step epilogue (never launched with one)
-      fe v = x[m];
-      if (post) v = mont_mul(v, pc);
-      else if (last) v = fe_canon(v);
-      st_fe_stream(data + base + ((uint64_t)(qq + ((uint32_t)m << tl)) << a.b0) + c, v, a.logn >= kStreamLogN);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    if (!more) break;
-    wait_vmcnt<8>();  // the DMA landed; this tile's 8 stores may still be in flight
-    tile = next;
-    base = nbase;
-    cbC = ncbC;
-  }
-}
-
-// launched with min(tiles, resident blocks) blocks; 2048-element tiles + 7 C first-step twiddles,
-// 256 threads, 34 KiB LDS; COMP_LAST: the last radix-8 step reaches above s_cut (its own kernel,
-// so each variant gets its own register allocation).  The host launches it only when the first
-// step reads the stage table (b0 + 3 <= s_cut).
-template <bool COMP_LAST>
-__global__ __launch_bounds__(256, 4) void k_ntt_pass_rrp(PassArgs a, uint64_t ntiles) {
-  extern __shared__ fe_lds lds[];
-  fe* __restrict__ data = a.ys ? a.data[0] + (uint64_t)blockIdx.y * a.ys : a.data[blockIdx.y];
-  pass_rrp_body<false, COMP_LAST>(a, lds, data, ntiles);
-}
-constexpr size_t kRrpLds = (2048 + 256) * sizeof(fe);
-
 // First pass with the bit-reversal fused in (fft/ntt.rs:14 bit_reverse_copy).
 // Positions j = h*2^L + t of the bit-reversed array hold x[rev_m(j)] =
 // x[rev_{m-L}(h) + rev_L(t) * 2^(m-L)], so the C = 2^logC tiles whose
@@ -1218,8 +1018,6 @@ static hipError_t ntt_lds_attributes() {
     if (e == hipSuccess) e = set((const void*)k_ntt_pass<11>, 65536);
     if (e == hipSuccess) e = set((const void*)k_ntt_pass_rr<10>, 65536);
     if (e == hipSuccess) e = set((const void*)k_ntt_pass_rr<11>, 65536);
-    if (e == hipSuccess) e = set((const void*)k_ntt_pass_rrp<false>, 65536);
-    if (e == hipSuccess) e = set((const void*)k_ntt_pass_rrp<true>, 65536);
     if (e == hipSuccess) e = set((const void*)k_ntt_pass_rr<12>, 65536);
     if (e == hipSuccess) e = set((const void*)k_ntt_pass_rr<13>, 131072);
     if (e == hipSuccess) e = set((const void*)k_ntt_first<10>, 65536);
@@ -1232,23 +1030,6 @@ static hipError_t ntt_lds_attributes() {
     return e;
   }();
   return err;
-}
-
-// blocks of the persistent pass (k_ntt_pass_rrp) per transform row: the resident 2048-element
-// blocks (4 per CU) shared by the batch, or 0 (use k_ntt_pass_rr) when the knob is off or a block
-// would get fewer than two tiles (nothing to overlap).  SG_NTT_PERSIST: 0 off, 1 on (A/B knob).
-static unsigned persist_grid(uint64_t ntiles, int batch) {
-  static const int on = env_int("SG_NTT_PERSIST", 0);
-  if (!on) return 0;
-  static const int cus = [] {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      return 256;
-    return n > 0 ? n : 256;
-  }();
-  const uint64_t per_row = std::max<uint64_t>(1, (uint64_t)(4 * cus) / (uint64_t)batch);
-  if (ntiles < 2 * per_row) return 0;
-  return (unsigned)per_row;
 }
 
 hipError_t launch_ntt_dit(fe* const* data, int batch, const fe* tw, int logn, const fe* post, int first_b0,
@@ -1322,15 +1103,6 @@ hipError_t launch_ntt_dit(fe* const* data, int batch, const fe* tw, int logn, co
       hipLaunchKernelGGL(k_ntt_pass_rr<12>, grid, dim3(512), lds, s, a);
     else if (tile == 4096 && threads == 256)
       hipLaunchKernelGGL(k_ntt_pass<12>, grid, dim3(256), lds, s, a);
-    else if (tile == 2048 && threads == 256 && a.L >= 6 && use_rr && !a.ep_out && a.b0 + 3 <= a.s_cut &&
-             persist_grid(ntiles, batch))
-    {
-      const dim3 pg(persist_grid(ntiles, batch), batch);
-      if (a.b0 + a.L > a.s_cut)
-        hipLaunchKernelGGL(k_ntt_pass_rrp<true>, pg, dim3(256), kRrpLds, s, a, (uint64_t)ntiles);
-      else
-        hipLaunchKernelGGL(k_ntt_pass_rrp<false>, pg, dim3(256), kRrpLds, s, a, (uint64_t)ntiles);
-    }
     else if (tile == 2048 && threads == 256 && a.L >= 6 && use_rr)
       hipLaunchKernelGGL(k_ntt_pass_rr<11>, grid, dim3(256), lds, s, a);
     else if (tile == 1024 && threads == 128 && a.L >= 6 && use_rr)
