@@ -371,9 +371,11 @@ def c5_single_gpu(ctx: sg.Context, device, iters: int = 3) -> dict:
     out["c5_dist_world1_gelem_s"] = round(n / t / 1e9, 3)
     del cols, runs
     ctx.trim()
-    # the headline proof through sg_dist_stark_prove on the same one-rank communicator: the sharded
-    # prove's own cost (four-step LDEs, forests, sharded FRI rounds, batched openings) without peers;
-    # its bytes must equal the single-GPU proof's
+    # the headline proof through sg_dist_stark_prove on the same one-rank communicator: since round 5
+    # a one-rank communicator proves through the single-GPU plan (its collectives are identities);
+    # SG_DIST_WORLD1_SHARDED=1 forces the four-step path, whose own cost (four-step LDEs, forests,
+    # sharded FRI rounds, batched openings) without peers is the second line.  Bytes must equal the
+    # single-GPU proof's either way.
     try:
         wl = ProveWorkload(0, device, ctx, LOG_TRACE)
         single = wl.step().digest()
@@ -384,14 +386,20 @@ def c5_single_gpu(ctx: sg.Context, device, iters: int = 3) -> dict:
                                wl.rcoef.data_ptr(), wl.nrc, dist=nd)
             return ps.digest()
 
-        same = sharded() == single
-        torch.cuda.synchronize(device)
-        t0 = time.perf_counter()
-        for _ in range(iters):
-            sharded()
-        torch.cuda.synchronize(device)
-        out["sharded_prove_world1_ms"] = round((time.perf_counter() - t0) / iters * 1e3, 3)
-        out["sharded_prove_world1_bytes_equal_single_gpu"] = same
+        for key, forced in (("sharded_prove_world1", False), ("sharded_prove_world1_fourstep", True)):
+            if forced:
+                os.environ["SG_DIST_WORLD1_SHARDED"] = "1"
+            try:
+                same = sharded() == single
+                torch.cuda.synchronize(device)
+                t0 = time.perf_counter()
+                for _ in range(iters):
+                    sharded()
+                torch.cuda.synchronize(device)
+            finally:
+                os.environ.pop("SG_DIST_WORLD1_SHARDED", None)
+            out[key + "_ms"] = round((time.perf_counter() - t0) / iters * 1e3, 3)
+            out[key + "_bytes_equal_single_gpu"] = same
         del wl
     except Exception as e:  # noqa: BLE001
         out["sharded_prove_world1_error"] = f"{type(e).__name__}: {e}"

@@ -515,10 +515,14 @@ def _stark_checks(nd, world, rank, tmp, cases, gather, sharded_algebra=True):
                 assert sq == 0 and si == 0, f"world 1 case {k}: {sq} / {si} sharded quotients / columns"
 
 
-def test_dist_stark_prove_world1_rccl(stark_reference):
-    """sg_dist_stark_prove over a 1-rank RCCL communicator: the single-GPU / oracle proof bytes."""
+@pytest.mark.parametrize("forced", ["1", "0"])
+def test_dist_stark_prove_world1_rccl(stark_reference, monkeypatch, forced):
+    """sg_dist_stark_prove over a 1-rank RCCL communicator: the single-GPU / oracle proof bytes --
+    through the four-step path forced (SG_DIST_WORLD1_SHARDED=1: the sharded machinery over RCCL)
+    and through the default one-rank plan (the single-GPU prove)."""
     import starkgpu as sg
     from starkgpu import dist as D
+    monkeypatch.setenv("SG_DIST_WORLD1_SHARDED", forced)
     ctx = sg.Context(0)
     nd = D.NativeDist(ctx, transport="rccl")
     try:
@@ -584,12 +588,14 @@ def _load_case(tmp, k):
         np.load(os.path.join(tmp, "tr%d.npy" % k)), np.load(os.path.join(tmp, "rc%d.npy" % k))
 
 
-def test_dist_failure_world1_rccl_poisons(stark_reference):
+def test_dist_failure_world1_rccl_poisons(stark_reference, monkeypatch):
     """A call that fails after issuing collectives poisons the RCCL communicator (ncclCommAbort):
     the prove returns an error, sg_dist_poisoned reports it, and every later call fails with
-    SG_ERR_INVALID at once instead of issuing collectives out of step with the peers."""
+    SG_ERR_INVALID at once instead of issuing collectives out of step with the peers.  (The
+    four-step path is forced: a one-rank communicator otherwise proves through the single-GPU plan.)"""
     import starkgpu as sg
     from starkgpu import dist as D
+    monkeypatch.setenv("SG_DIST_WORLD1_SHARDED", "1")
     ctx = sg.Context(0)
     nd = D.NativeDist(ctx, transport="rccl")
     try:

@@ -54,6 +54,9 @@ void dist_lde_replicated(sg_dist* d, const fe& gen, uint64_t n, const fe& offset
 // fft/ntt.rs:7-68 over the ranks (a root of order exactly n): column shard [N1/G][row_len] in, run
 // shard [N1][N2/G] out; the inverse from a run shard into the column shard [N1/G][N2]
 void dist_ntt(sg_dist* d, const fe& root, const fe* cols, uint64_t row_len, uint64_t n, fe* runs);
+// fast_coset_evaluate of a coefficient column shard [N1/G][row_len] into the run shard
+void dist_coset_evaluate(sg_dist* d, const fe& gen, uint64_t n, const fe& offset, const fe* cols, uint64_t row_len,
+                         fe* runs);
 void dist_intt(sg_dist* d, const fe& root, const fe* runs, uint64_t n, fe* cols);
 // coset interpolation of a run-sharded codeword of n points on offset * <gen> into the column shard
 // [N1/G][N2] of its coefficients (distributed INTT + offset^-i)

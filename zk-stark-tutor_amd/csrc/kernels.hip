@@ -1350,6 +1350,10 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
         kind = 10;
         if (fuse > 10) fuse = 10;  // two levels in the lane, then 256 -> 1 through LDS
       }
+      // SG_MERKLE_NODE_DPP=1: levels 1 and 2 per launch with the level-2 hand-over by DPP inside each
+      // wave instead of LDS + a block barrier (k_merkle_nodes_dpp; A/B knob, round 5)
+      static const int env_ndpp = env_int("SG_MERKLE_NODE_DPP", 0);
+      if (env_ndpp && kind == 2 && fuse == 2 && count % 256 == 0 && level + 1 < logn) kind = 11;
       if (count < bs) {
         kind = 2;
         bs = (unsigned)count;  // a power of two (tree levels)

@@ -214,6 +214,44 @@ __global__ __launch_bounds__(MAXB) void k_merkle_nodes_pipe(MerkleArgs a, uint64
   }
 }
 
+// Node levels 1 and 2 without LDS or a barrier (round-5 verdict item 2): lane pairs (2i, 2i + 1)
+// hold sibling digests after level 1, the odd lane's 8 words move to the even lane by DPP
+// (__shfl_xor 1 within the wave) and the even lanes hash the parent.  Every wave proceeds on its
+// own; the price is the odd lanes idling through the level-2 compression (the LDS form idles half
+// the block's waves at a barrier instead).  fuse == 2, first_count % 256 == 0 (host-checked).
+template <int MAXB>
+__global__ __launch_bounds__(MAXB) void k_merkle_nodes_dpp(MerkleArgs a) {
+  const uint32_t tid = threadIdx.x;
+  const uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + tid;
+  uint64_t* __restrict__ tree = merkle_tree_ptr(a);
+  uint64_t* const root_slot = merkle_root_slot(a);
+  uint64_t d[8];
+  {
+    uint64_t l[8], r[8];
+    const uint64_t* child = tree + a.off[0] * 8;
+    ld_digest(child + (2 * idx) * 8, l);
+    ld_digest(child + (2 * idx + 1) * 8, r);
+    blake2b_node(l, r, d);
+    st_digest(tree + (a.off[1] + idx) * 8, d);
+  }
+  uint64_t r[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {  // quad_perm [1, 0, 3, 2]: swap with the pair partner
+    const uint32_t lo = __builtin_amdgcn_update_dpp(0u, (uint32_t)d[i], 0xB1, 0xF, 0xF, true);
+    const uint32_t hi = __builtin_amdgcn_update_dpp(0u, (uint32_t)(d[i] >> 32), 0xB1, 0xF, 0xF, true);
+    r[i] = (uint64_t)lo | ((uint64_t)hi << 32);
+  }
+  if ((tid & 1) == 0) {
+    uint64_t p[8];
+    blake2b_node(d, r, p);
+    st_digest(tree + (a.off[2] + (idx >> 1)) * 8, p);
+    if (a.first_level + 1 == a.root_level && root_slot) {
+      for (int i = 0; i < 8; ++i) root_slot[i] = p[i];
+      merkle_root_publish(a, true);
+    }
+  }
+}
+
 // Node level with two nodes per lane, as k_merkle_leaf_pairs for the leaves: lane p reads its four
 // children (256 contiguous bytes), hashes nodes 2p and 2p + 1 of the first level and their parent
 // itself, so the first two levels keep all waves of the block busy (the one-node kernel's fused
@@ -514,6 +552,7 @@ hipError_t launch_merkle_lanes(int kind, bool fold, dim3 grid, unsigned bs, hipS
     }
     case 6: hipLaunchKernelGGL((k_merkle_levels<false, 512>), grid, dim3(bs), 0, s, a); break;
     case 10: hipLaunchKernelGGL((k_merkle_node_pairs<256>), grid, dim3(bs), 0, s, a); break;
+    case 11: hipLaunchKernelGGL((k_merkle_nodes_dpp<256>), grid, dim3(bs), 0, s, a); break;
     case 3: hipLaunchKernelGGL(k_merkle_quad<64>, grid, dim3(bs), 0, s, a); break;
     case 5: hipLaunchKernelGGL(k_merkle_quad<256>, grid, dim3(bs), 0, s, a); break;
     case 7:

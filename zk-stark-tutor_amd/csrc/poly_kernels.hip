@@ -549,10 +549,15 @@ __global__ __launch_bounds__(kBlock) void k_air_rescue(AirRescueArgs a) {
 // out[k] = sum_t w_t * term_t[k - off_t] over off_t <= k < off_t + len_t (w_t Montgomery)
 __global__ __launch_bounds__(kBlock) void k_lincomb(LinCombArgs a) {
   for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < a.n; k += (uint64_t)gridDim.x * blockDim.x) {
+    uint64_t i = k;  // coefficient index
+    if (a.cols_row_len) {
+      const uint64_t r = k / a.cols_row_len;
+      i = a.cols_base + r + a.cols_n1 * (k - r * a.cols_row_len);
+    }
     fe acc = fe_zero();
     for (int t = 0; t < a.nterms; ++t) {
       uint64_t off = a.off[t];
-      if (k >= off && k - off < a.len[t]) acc = fe_add(acc, mont_mul(ld_fe(a.term[t] + (k - off)), a.w[t]));
+      if (i >= off && i - off < a.len[t]) acc = fe_add(acc, mont_mul(ld_fe(a.term[t] + (i - off)), a.w[t]));
     }
     st_fe(a.out + k, acc);
   }

@@ -37,6 +37,9 @@ struct LinCombArgs {
   uint64_t off[kLinCombMaxTerms];
   uint64_t len[kLinCombMaxTerms];
   fe w[kLinCombMaxTerms];  // Montgomery
+  // cols_row_len != 0: only a column shard of the result (the sharded prove's combination):
+  // output k = r * cols_row_len + j is coefficient cols_base + r + cols_n1 * j
+  uint64_t cols_row_len, cols_n1, cols_base;
 };
 
 hipError_t launch_ew_mul(fe* out, const fe* a, const fe* b, uint64_t n, const fe& r2, hipStream_t s);

@@ -367,16 +367,15 @@ struct DevTerm {
   fe w;
 };
 
-// device linear combination sum_t w_t * x^off_t * term_t, output length max(off + len)
-DPoly lincomb(sg_ctx* ctx, const std::vector<DevTerm>& terms) {
+uint64_t lincomb_len(const std::vector<DevTerm>& terms) {
   uint64_t n = 0;
   for (auto& t : terms) n = std::max(n, t.off + t.len);
-  DPoly out = dpoly_alloc(ctx, n);
-  if (!n) return out;
+  return n;
+}
+
+LinCombArgs lincomb_args(const std::vector<DevTerm>& terms) {
   SG_REQUIRE(terms.size() <= (size_t)kLinCombMaxTerms, "too many combination terms");
   LinCombArgs a{};
-  a.out = out.p();
-  a.n = n;
   a.nterms = (int)terms.size();
   for (size_t t = 0; t < terms.size(); ++t) {
     a.term[t] = terms[t].p;
@@ -384,8 +383,32 @@ DPoly lincomb(sg_ctx* ctx, const std::vector<DevTerm>& terms) {
     a.len[t] = terms[t].p ? terms[t].len : 0;
     a.w[t] = to_mont(terms[t].w);
   }
+  return a;
+}
+
+// device linear combination sum_t w_t * x^off_t * term_t, output length max(off + len)
+DPoly lincomb(sg_ctx* ctx, const std::vector<DevTerm>& terms) {
+  const uint64_t n = lincomb_len(terms);
+  DPoly out = dpoly_alloc(ctx, n);
+  if (!n) return out;
+  LinCombArgs a = lincomb_args(terms);
+  a.out = out.p();
+  a.n = n;
   SG_HIP(launch_lincomb(a, ctx->stream));
   return out;
+}
+
+// the same combination, only rows x row_len of its column shard: out[r][j] = coefficient
+// base + r + n1 j (zero past its length) -- what the sharded LDE gathers, computed in place of it
+void lincomb_cols(sg_ctx* ctx, const std::vector<DevTerm>& terms, uint64_t rows, uint64_t row_len, uint64_t n1,
+                  uint64_t base, fe* out) {
+  LinCombArgs a = lincomb_args(terms);
+  a.out = out;
+  a.n = rows * row_len;
+  a.cols_row_len = row_len;
+  a.cols_n1 = n1;
+  a.cols_base = base;
+  SG_HIP(launch_lincomb(a, ctx->stream));
 }
 
 // point values on the coset offset * <w_L>: P_s(y) and P_s(omicron y) (the point
@@ -1104,8 +1127,8 @@ void prove_transition_quotients(sg_ctx* ctx, const sg_stark& st, const std::vect
   }
 }
 
-// the degree check (stark.rs:451-465) and the combination polynomial (stark.rs:467-512)
-DPoly prove_combination(sg_ctx* ctx, const sg_stark& st, const std::vector<const MPoly*>& tcs, ProveAlgebra& A,
+// the degree check (stark.rs:451-465) and the combination polynomial's terms (stark.rs:467-512)
+std::vector<DevTerm> combination_terms(sg_ctx* ctx, const sg_stark& st, const std::vector<const MPoly*>& tcs, ProveAlgebra& A,
                         const std::vector<fe>& weights, const fe* d_rcoef, size_t nrc, uint64_t tcd) {
   const size_t m = st.m;
   const uint64_t D = st.D, Tp = A.Tp;
@@ -1150,7 +1173,12 @@ DPoly prove_combination(sg_ctx* ctx, const sg_stark& st, const std::vector<const
   };
   for (size_t i = 0; i < tqs.size(); ++i) add_pair(tqs[i], tcd - tqdb[i], qdeg[i]);
   for (size_t s = 0; s < m; ++s) add_pair(bqs[s], tcd - bqdb[s], qdeg[tqs.size() + s]);
-  return lincomb(ctx, terms);
+  return terms;
+}
+
+DPoly prove_combination(sg_ctx* ctx, const sg_stark& st, const std::vector<const MPoly*>& tcs, ProveAlgebra& A,
+                        const std::vector<fe>& weights, const fe* d_rcoef, size_t nrc, uint64_t tcd) {
+  return lincomb(ctx, combination_terms(ctx, st, tcs, A, weights, d_rcoef, nrc, tcd));
 }
 
 // stark.rs:276-562
@@ -1332,6 +1360,17 @@ void stark_prove_dist(sg_dist* dd, const sg_stark& st, const fe* d_trace, size_t
     stark_prove(ctx, st, d_trace, rows, tcs, bnd, d_trace_rand, d_rcoef, nrc, ps);
     return;
   }
+  // one rank: its "shard" is the whole domain and every collective an identity, so the single-GPU
+  // prove is the plan (same bytes; at the headline the four-step path costs ~6 ms more per proof).
+  // SG_DIST_WORLD1_SHARDED=1 forces the four-step path anyway (tests that exercise the sharded
+  // machinery over a one-rank RCCL communicator; one rank, so no cross-rank agreement is needed).
+  if (G == 1) {
+    const char* f = getenv("SG_DIST_WORLD1_SHARDED");
+    if (!(f && *f && *f != '0')) {
+      stark_prove(ctx, st, d_trace, rows, tcs, bnd, d_trace_rand, d_rcoef, nrc, ps);
+      return;
+    }
+  }
   uint64_t n1, n2;
   dist_plan(Nf, G, n1, n2);
   const uint64_t R = n2 / G, shard = n1 * R;
@@ -1388,10 +1427,18 @@ void stark_prove_dist(sg_dist* dd, const sg_stark& st, const fe* d_trace, size_t
   if (ps->fiat_shamir_prover(ps->user, 32, fs) != 0)
     throw Error{SG_ERR_CALLBACK, "proof stream fiat_shamir callback failed"};
   std::vector<fe> weights = sample_weights(1 + 2 * A.tqs.size() + 2 * A.bqs.size(), fs, 32);
-  DPoly comb = prove_combination(ctx, st, tcs, A, weights, d_rcoef, nrc, tcd);
-  SG_REQUIRE(comb.len <= Nf, "fast_coset_evaluate: polynomial longer than root_order");
+  // the combination (stark.rs:467-512) only as this rank's column shard of its coefficients --
+  // 1/G of the replicated elementwise sum, and the LDE's column gather with it
+  const std::vector<DevTerm> terms = combination_terms(ctx, st, tcs, A, weights, d_rcoef, nrc, tcd);
+  const uint64_t clen = lincomb_len(terms);
+  SG_REQUIRE(clen <= Nf, "fast_coset_evaluate: polynomial longer than root_order");
   DevBuf comb_runs(ctx, shard * sizeof(fe));
-  dist_lde_replicated(dd, st.omega, Nf, g, comb.p(), comb.len, comb_runs.as<fe>());
+  {
+    const uint64_t rows = n1 / (uint64_t)G, row_len = std::max<uint64_t>((clen + n1 - 1) / n1, 1);
+    DevBuf cols(ctx, rows * row_len * sizeof(fe));
+    lincomb_cols(ctx, terms, rows, row_len, n1, (uint64_t)dist_rank(dd) * rows, cols.as<fe>());
+    dist_coset_evaluate(dd, st.omega, Nf, g, cols.as<fe>(), row_len, comb_runs.as<fe>());
+  }
   mark("dist_combination_lde");
   // FRI (stark.rs:514-522), then the openings (stark.rs:524-560) of the boundary-quotient and
   // randomizer codewords at the quadrupled indices, each value + path from the leaf's owner
