@@ -739,3 +739,52 @@ def test_dist_rpsss_published_configuration(tmp_path, world):
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     mp.spawn(_rpsss_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True)
+
+
+# ----------------------------------------------------------------- mid-size statement pinned to the oracle
+
+def _midsize_worker(rank, world, port, results):
+    import hashlib
+    import torch.distributed as dist
+    import starkgpu as sg
+    from starkgpu import dist as D
+    import midsize_case as M
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        nd = D.NativeDist(sg.Context(0), transport="host")
+        rp_o, st_o, trace, bnd, tr, rc = M.light_inputs()
+        rp_g = sg.RescuePrime(*M.RESCUE, ctx=nd.ctx)
+        st_g = sg.Stark(M.EXPANSION, M.CHECKS, M.SECURITY, rp_g.m, M.RESCUE[3] + 1, M.TCD, ctx=nd.ctx)
+        air = rp_g.transition_constraints(st_g.omicron, st_g.omicron_domain_length)
+        nd.set_fri_tail(0)  # every FRI round sharded at this size
+        got = st_g.prove(trace, air, bnd, sg.IndependentProofStream(), tr, rc, dist=nd)
+        out = [None] * world
+        dist.all_gather_object(out, (len(got), hashlib.sha256(got).hexdigest(), nd.counters()[1]))
+        if rank == 0:
+            with open(results, "w") as f:
+                json.dump(out, f)
+        nd.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+@pytest.mark.parametrize("world", [2, 4])
+def test_dist_stark_prove_midsize_equals_oracle_digest(world, tmp_path):
+    """sg_dist_stark_prove of the mid-size statement (tests/midsize_case.py: trace 1257 rows, FRI
+    domain 2^15, c = 64) over `world` ranks on this GPU (host transport): every rank's proof hashes
+    to the Python oracle's committed digest (tests/golden/midsize_proof.json) -- the sharded path
+    pinned to the oracle itself above the toy sizes, every FRI round sharded."""
+    import torch.multiprocessing as mp
+    with open(os.path.join(os.path.dirname(__file__), "golden", "midsize_proof.json")) as f:
+        g = json.load(f)
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    res = str(tmp_path / "midsize.json")
+    mp.spawn(_midsize_worker, args=(world, port, res), nprocs=world, join=True)
+    out = json.load(open(res))
+    assert all(n == g["proof_len"] and h == g["proof_sha256"] for n, h, _ in out), out
+    assert all(sq > 0 for _, _, sq in out), "the quotients' coset work should run on run shards"

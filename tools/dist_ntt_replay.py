@@ -159,6 +159,7 @@ def replay(world, logn, out, steps):
         _run(lib, ctx, h, root, cols_t, row, n, runs_t, back_t)
         torch.cuda.synchronize()
         dt += time.perf_counter() - t0
+    time.sleep(0.5)  # the check's own single-GPU transform must not join the last step's trace segment
     got = runs_t.cpu().numpy()
     rec = np.fromfile(os.path.join(out, "runs.bin"), dtype=np.int64)
     # rank 0's run shard [k1][c] = X[k1 N2 + c], c < R, of the single-GPU transform
