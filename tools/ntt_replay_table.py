@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Per-step device time of the sharded NTT replays (tools/dist_ntt_replay.py) from their rocprofv3
 kernel traces: the trace is cut into steps at idle gaps >= 300 ms; the steps are the segments made
-of library kernels (sg::...); the first one (plan building) is dropped and the rest averaged.
+of library kernels (sg::...); the first one (plan building) is dropped -- and in a replay the last segment, the check's own single-GPU
+transform -- and the rest averaged.
 Prints a markdown table per transform size: single GPU vs rank 0 at world G -- library kernels by
 class (NTT passes, four-step transposes, other library kernels), runtime copies / fills (the host
 transport's staging), and the library total's ratio to the single-GPU transform.
@@ -17,7 +18,7 @@ import sys
 GAP_NS = 300e6
 
 
-def steps(path):
+def steps(path, replay):
     rows = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in csv.DictReader(open(path)))
     segs, cur, end = [], [], 0
     for k in rows:
@@ -29,7 +30,9 @@ def steps(path):
     if cur:
         segs.append(cur)
     lib = [s for s in segs if any(n.startswith(("sg::", "void sg::")) for _, _, n in s)]
-    return lib[1:] if len(lib) > 1 else lib
+    # drop the first step (plan building) and, in a replay, the last segment: the check's single-GPU
+    # transform (tools/dist_ntt_replay.py sleeps before it)
+    return lib[1:-1] if replay else lib[1:]
 
 
 def classify(name):
@@ -45,8 +48,8 @@ def classify(name):
     return "other"
 
 
-def summarize(path):
-    sts = steps(path)
+def summarize(path, replay):
+    sts = steps(path, replay)
     acc = {"ntt": 0.0, "transpose": 0.0, "other": 0.0, "copies": 0.0}
     for s in sts:
         for a, b, n in s:
@@ -64,7 +67,8 @@ def main():
     d = sys.argv[1]
     res = {}
     for p in sorted(glob.glob(os.path.join(d, "*", "*kernel_trace.csv"))):
-        res[os.path.basename(os.path.dirname(p))] = summarize(p)
+        name = os.path.basename(os.path.dirname(p))
+        res[name] = summarize(p, name.startswith("replay"))
     for L in sorted({int(k.split("_")[1]) for k in res}):
         cols = [("single GPU", res.get(f"single_{L}"))] + [(f"world {G}, rank 0", res.get(f"replay_{L}_{G}"))
                                                             for G in (2, 4, 8)]
