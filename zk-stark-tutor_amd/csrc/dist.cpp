@@ -224,11 +224,17 @@ void tables3(sg_ctx* ctx, const fe& base, const fe** T) {
 // X = DFT_root over (n1, n2): input rows (row_len entries per row, zero beyond; or, with in_il,
 // R' interleaved rows of n2 entries: row r's element j at in[j * in_il + r]); output
 // [R][n1] rows (row c = k2 - g R, element k1); post: Montgomery constant on every output
+//
+// nv > 1: nv vectors at once, row r of vector v being row v rows + r of the input (at
+// in + (v rows + r) row_len, or interleaved: in_il >= nv rows) and its output row c at
+// out + (v R + c) n1 -- one exchange and one launch per step for all of them (the epilogue packs
+// [h][r][v][c], so the received block is nv R interleaved columns)
 void four_step(sg_dist* d, const fe& root, const fe* in, uint64_t row_len, uint64_t in_il, uint64_t n1, uint64_t n2,
-               fe* out, const fe* post_host) {
+               fe* out, const fe* post_host, uint64_t nv = 1) {
   sg_ctx* ctx = d->ctx;
   const int G = d->G;
   const uint64_t rows = n1 / G, R = n2 / G;
+  SG_REQUIRE(nv >= 1 && (!in_il || in_il >= nv * rows), "distributed transform: bad batched layout");
   SG_REQUIRE(row_len >= 1 && row_len <= n2, "distributed transform: row length must be in [1, N2]");
   SG_REQUIRE((uint64_t)n1 * n2 <= ((uint64_t)1 << 36), "distributed transform: n above 2^36");
   const int log1 = ilog2_exact(n1), log2 = ilog2_exact(n2);
@@ -238,21 +244,26 @@ void four_step(sg_dist* d, const fe& root, const fe* in, uint64_t row_len, uint6
   const fe* tw1 = ctx->stage_twiddles(w1, log1);
   const fe* T[3];
   tables3(ctx, root, T);
-  DevBuf z(ctx, rows * n2 * sizeof(fe)), send(ctx, rows * n2 * sizeof(fe)), recv(ctx, n1 * R * sizeof(fe));
-  // 1. size-N2 NTTs; the last pass applies w^(j1 k2) and packs [h][r][c] for the all-to-all
+  const uint64_t vrows = nv * rows, C = nv * R;  // rows of all vectors; received columns
+  DevBuf z(ctx, vrows * n2 * sizeof(fe)), send(ctx, vrows * n2 * sizeof(fe)), recv(ctx, n1 * C * sizeof(fe));
+  // 1. size-N2 NTTs; the last pass applies w^(j1 k2) and packs [h][r][v][c] for the all-to-all
   int skip = 0;
   if (!in_il)
     while (skip < log2 && (row_len << (skip + 1)) <= n2) ++skip;
-  for (uint64_t r0 = 0; r0 < rows; r0 += kRows) {
-    const uint64_t cnt = std::min<uint64_t>(kRows, rows - r0);
+  for (uint64_t r0 = 0; r0 < vrows; r0 += kRows) {
+    const uint64_t cnt = std::min<uint64_t>(kRows, vrows - r0);
     NttEpilogue ep{send.as<fe>(), T[0], T[1], T[2], r0, (uint64_t)d->g * rows, rows, ilog2_exact(R)};
+    if (nv > 1) {
+      ep.vlog = ilog2_exact(rows);
+      ep.k = nv;
+    }
     fe* zo = z.as<fe>() + r0 * n2;
     const fe* ii = in_il ? in + r0 : in + r0 * row_len;
     SG_HIP(launch_ntt_fused(&zo, &ii, (int)cnt, row_len, log2, tw2, nullptr, nullptr, skip, nullptr, ctx->stream,
                             in_il ? 1 : row_len, n2, in_il, &ep));
   }
-  // 2. the one exchange: rank h receives block h of every rank -> recv = [j1][c]
-  exchange(d, send.get(), recv.get(), rows * R * sizeof(fe), /*a2a=*/true);
+  // 2. the one exchange: rank h receives block h of every rank -> recv = [j1][v][c]
+  exchange(d, send.get(), recv.get(), vrows * R * sizeof(fe), /*a2a=*/true);
   // 3. size-N1 NTTs over the R interleaved columns of recv
   DevBuf dpost;
   const fe* post = nullptr;
@@ -261,11 +272,11 @@ void four_step(sg_dist* d, const fe& root, const fe* in, uint64_t row_len, uint6
     SG_HIP(hipMemcpyAsync(dpost.get(), post_host, sizeof(fe), hipMemcpyHostToDevice, ctx->stream));
     post = dpost.as<fe>();
   }
-  for (uint64_t c0 = 0; c0 < R; c0 += kRows) {
-    const uint64_t cnt = std::min<uint64_t>(kRows, R - c0);
+  for (uint64_t c0 = 0; c0 < C; c0 += kRows) {
+    const uint64_t cnt = std::min<uint64_t>(kRows, C - c0);
     fe* oo = out + c0 * n1;
     const fe* rr = recv.as<fe>() + c0;
-    SG_HIP(launch_ntt_fused(&oo, &rr, (int)cnt, n1, log1, tw1, nullptr, nullptr, 0, post, ctx->stream, 1, n1, R,
+    SG_HIP(launch_ntt_fused(&oo, &rr, (int)cnt, n1, log1, tw1, nullptr, nullptr, 0, post, ctx->stream, 1, n1, C,
                             nullptr));
   }
 }
@@ -273,42 +284,72 @@ void four_step(sg_dist* d, const fe& root, const fe* in, uint64_t row_len, uint6
 }  // namespace
 
 void dist_ntt(sg_dist* d, const fe& root, const fe* cols, uint64_t row_len, uint64_t n, fe* runs) {
+  dist_ntt_batch(d, root, cols, row_len, n, runs, 1);
+}
+
+void dist_ntt_batch(sg_dist* d, const fe& root, const fe* cols, uint64_t row_len, uint64_t n, fe* runs, uint64_t nv) {
+  if (nv == 0) return;
   uint64_t n1, n2;
   plan(n, d->G, n1, n2);
   check_order_n(root, n);
   const uint64_t R = n2 / d->G;
-  DevBuf t(d->ctx, R * n1 * sizeof(fe));
-  four_step(d, root, cols, row_len, 0, n1, n2, t.as<fe>(), nullptr);
-  SG_HIP(launch_swap01(t.as<fe>(), runs, R, n1, 1, d->ctx->stream));  // [c][k1] -> [k1][c]
+  DevBuf t(d->ctx, nv * R * n1 * sizeof(fe));
+  four_step(d, root, cols, row_len, 0, n1, n2, t.as<fe>(), nullptr, nv);
+  SG_HIP(launch_swap01(t.as<fe>(), runs, R, n1, 1, d->ctx->stream, nv));  // [v][c][k1] -> [v][k1][c]
 }
 
 void dist_intt(sg_dist* d, const fe& root, const fe* runs, uint64_t n, fe* cols) {
+  dist_intt_batch(d, root, runs, n, cols, 1);
+}
+
+void dist_intt_batch(sg_dist* d, const fe& root, const fe* runs, uint64_t n, fe* cols, uint64_t nv) {
+  if (nv == 0) return;
   uint64_t n1, n2;
   plan(n, d->G, n1, n2);
   check_order_n(root, n);
   // the run shard [n1][R] is the interleaved column shard of (N1', N2') = (n2, n1): row c of
-  // length n1 at runs[k1 R + c]; the inverse four-step's output rows [n1/G][n2] are the column shard
+  // length n1 at runs[k1 R + c]; the inverse four-step's output rows [n1/G][n2] are the column shard.
+  // Batched: the run shards [v][n1][R] transposed to [n1][v][R] first, i.e. nv R interleaved rows
   const fe inv = fe_inv(root);
   const fe ninv = to_mont(fe_inv(fe_from_u64(n)));
   SG_REQUIRE(n2 % d->G == 0 && (n1 / d->G) % 4 == 0 && n1 / d->G >= 4,
              "distributed intt: n too small for this many ranks (needs N1 >= 4 G)");
-  four_step(d, inv, runs, n1, n2 / d->G, n2, n1, cols, &ninv);
+  const uint64_t R = n2 / d->G;
+  if (nv == 1) {
+    four_step(d, inv, runs, n1, R, n2, n1, cols, &ninv);
+    return;
+  }
+  DevBuf t(d->ctx, nv * n1 * R * sizeof(fe));
+  SG_HIP(launch_swap01(runs, t.as<fe>(), nv, n1, R, d->ctx->stream));
+  four_step(d, inv, t.as<fe>(), n1, nv * R, n2, n1, cols, &ninv, nv);
 }
 
 void dist_coset_evaluate(sg_dist* d, const fe& gen, uint64_t n, const fe& offset, const fe* cols, uint64_t row_len,
                          fe* runs) {
+  dist_coset_evaluate_batch(d, gen, n, &offset, cols, row_len, runs, 1);
+}
+
+void dist_coset_evaluate_batch(sg_dist* d, const fe& gen, uint64_t n, const fe* offsets, const fe* cols,
+                               uint64_t row_len, fe* runs, uint64_t nv) {
+  if (nv == 0) return;
   uint64_t n1, n2;
   plan(n, d->G, n1, n2);
-  const uint64_t rows = n1 / d->G;
+  const uint64_t rows = n1 / d->G, one = rows * row_len;
   SG_REQUIRE(row_len >= 1 && row_len <= n2, "distributed LDE: row length must be in [1, N2]");
-  // Polynomial::scale (polynomial.rs:109-121): coefficient j = (g rows + r) + N1 c times offset^j
-  DevBuf sc(d->ctx, rows * row_len * sizeof(fe));
-  SG_HIP(hipMemcpyAsync(sc.get(), cols, rows * row_len * sizeof(fe), hipMemcpyDeviceToDevice, d->ctx->stream));
-  const fe* T[3];
-  tables3(d->ctx, offset, T);
-  SG_HIP(launch_mul_pow(sc.as<fe>(), rows, row_len, n1, 0, (uint64_t)d->g * rows, 1, T[0], T[1], T[2],
-                        d->ctx->stream));
-  dist_ntt(d, gen, sc.as<fe>(), row_len, n, runs);
+  // Polynomial::scale (polynomial.rs:109-121): coefficient j = (g rows + r) + N1 c times offset^j,
+  // one launch per run of equal offsets
+  DevBuf sc(d->ctx, nv * one * sizeof(fe));
+  SG_HIP(hipMemcpyAsync(sc.get(), cols, nv * one * sizeof(fe), hipMemcpyDeviceToDevice, d->ctx->stream));
+  for (uint64_t v0 = 0; v0 < nv;) {
+    uint64_t v1 = v0 + 1;
+    while (v1 < nv && fe_eq(offsets[v1], offsets[v0])) ++v1;
+    const fe* T[3];
+    tables3(d->ctx, offsets[v0], T);
+    SG_HIP(launch_mul_pow(sc.as<fe>() + v0 * one, rows, row_len, n1, 0, (uint64_t)d->g * rows, 1, T[0], T[1], T[2],
+                          d->ctx->stream, v1 - v0));
+    v0 = v1;
+  }
+  dist_ntt_batch(d, gen, sc.as<fe>(), row_len, n, runs, nv);
 }
 
 // root of the natural-order codeword held as runs [k1s][R] on every rank (merkle_root.rs:21-32):
@@ -381,48 +422,94 @@ void dist_merkle_root(sg_dist* d, const fe* runs, uint64_t k1s, uint64_t R, uint
 
 void dist_lde_replicated(sg_dist* d, const fe& gen, uint64_t n, const fe& offset, const fe* coeffs, uint64_t len,
                          fe* runs) {
+  dist_lde_replicated_batch(d, gen, n, &offset, &coeffs, &len, runs, 1);
+}
+
+void dist_lde_replicated_batch(sg_dist* d, const fe& gen, uint64_t n, const fe* offsets, const fe* const* coeffs,
+                               const uint64_t* lens, fe* runs, uint64_t nv) {
+  if (nv == 0) return;
   uint64_t n1, n2;
   plan(n, d->G, n1, n2);
-  SG_REQUIRE(len <= n, "fast_coset_evaluate: polynomial longer than root_order");
+  uint64_t len = 0;
+  for (uint64_t v = 0; v < nv; ++v) {
+    SG_REQUIRE(lens[v] <= n, "fast_coset_evaluate: polynomial longer than root_order");
+    len = std::max(len, lens[v]);
+  }
   const uint64_t rows = n1 / d->G;
-  const uint64_t row_len = std::max<uint64_t>((len + n1 - 1) / n1, 1);
-  // column shard: row r = coefficients (g rows + r) + N1 j, zero past len
-  DevBuf cols(d->ctx, rows * row_len * sizeof(fe));
-  SG_HIP(launch_gather_cols(cols.as<fe>(), coeffs, len, rows, row_len, n1, (uint64_t)d->g * rows, d->ctx->stream));
-  dist_coset_evaluate(d, gen, n, offset, cols.as<fe>(), row_len, runs);
+  const uint64_t row_len = std::max<uint64_t>((len + n1 - 1) / n1, 1);  // the longest vector's
+  // column shards: row r = coefficients (g rows + r) + N1 j, zero past each vector's length
+  DevBuf cols(d->ctx, nv * rows * row_len * sizeof(fe));
+  for (uint64_t v = 0; v < nv; ++v)
+    SG_HIP(launch_gather_cols(cols.as<fe>() + v * rows * row_len, coeffs[v], lens[v], rows, row_len, n1,
+                              (uint64_t)d->g * rows, d->ctx->stream));
+  dist_coset_evaluate_batch(d, gen, n, offsets, cols.as<fe>(), row_len, runs, nv);
 }
 
 // Coset interpolation of a run-sharded codeword (the values of a polynomial of degree < n on
 // offset * <gen>, ntt_arithmetics.rs:172-181): its coefficients as this rank's column shard
 // [N1/G][N2] -- the distributed INTT, then coefficient i = (g rows + r) + N1 j times offset^-i.
 void dist_coset_interpolate(sg_dist* d, const fe& gen, uint64_t n, const fe& offset, const fe* runs, fe* cols) {
+  dist_coset_interpolate_batch(d, gen, n, offset, runs, cols, 1);
+}
+
+void dist_coset_interpolate_batch(sg_dist* d, const fe& gen, uint64_t n, const fe& offset, const fe* runs, fe* cols,
+                                  uint64_t nv) {
+  if (nv == 0) return;
   uint64_t n1, n2;
   plan(n, d->G, n1, n2);
-  dist_intt(d, gen, runs, n, cols);
+  dist_intt_batch(d, gen, runs, n, cols, nv);
   const uint64_t rows = n1 / d->G;
   const fe* T[3];
   tables3(d->ctx, fe_inv(offset), T);
-  SG_HIP(launch_mul_pow(cols, rows, n2, n1, 0, (uint64_t)d->g * rows, 1, T[0], T[1], T[2], d->ctx->stream));
+  SG_HIP(launch_mul_pow(cols, rows, n2, n1, 0, (uint64_t)d->g * rows, 1, T[0], T[1], T[2], d->ctx->stream, nv));
 }
 
 // every rank's column shard [N1/G][N2] -> the whole vector in natural order on every rank: one
 // all-gather ([g][r][j] = [j1][j]) and one transpose to [j][j1] (index j1 + N1 j)
 void dist_gather_columns(sg_dist* d, const fe* cols, uint64_t n, fe* out) {
+  dist_gather_columns_batch(d, cols, n, &out, 1);
+}
+
+// (nv column shards [v][N1/G][N2] at once: one all-gather, [g][v] -> [v][g], then per vector)
+void dist_gather_columns_batch(sg_dist* d, const fe* cols, uint64_t n, fe* const* outs, uint64_t nv) {
+  if (nv == 0) return;
   uint64_t n1, n2;
   plan(n, d->G, n1, n2);
-  DevBuf all(d->ctx, n * sizeof(fe));
-  exchange(d, cols, all.get(), (n1 / d->G) * n2 * sizeof(fe), /*a2a=*/false);
-  SG_HIP(launch_swap01(all.as<fe>(), out, n1, n2, 1, d->ctx->stream));
+  const uint64_t one = (n1 / d->G) * n2;
+  DevBuf all(d->ctx, nv * n * sizeof(fe));
+  exchange(d, cols, all.get(), nv * one * sizeof(fe), /*a2a=*/false);  // [g][v][r][j]
+  const fe* src = all.as<fe>();
+  DevBuf byv;
+  if (nv > 1) {
+    byv = DevBuf(d->ctx, nv * n * sizeof(fe));
+    SG_HIP(launch_swap01(all.as<fe>(), byv.as<fe>(), d->G, nv, one, d->ctx->stream));  // [v][g][r][j]
+    src = byv.as<fe>();
+  }
+  for (uint64_t v = 0; v < nv; ++v) SG_HIP(launch_swap01(src + v * n, outs[v], n1, n2, 1, d->ctx->stream));
 }
 
 // every rank's run shard [N1][N2/G] -> the whole codeword in natural order on every rank
 void dist_gather_runs(sg_dist* d, const fe* runs, uint64_t n, fe* out) {
+  dist_gather_runs_batch(d, runs, n, &out, 1);
+}
+
+// (nv run shards [v][N1][R] at once: one all-gather, [g][v] -> [v][g], then per vector)
+void dist_gather_runs_batch(sg_dist* d, const fe* runs, uint64_t n, fe* const* outs, uint64_t nv) {
+  if (nv == 0) return;
   uint64_t n1, n2;
   plan(n, d->G, n1, n2);
-  const uint64_t R = n2 / d->G;
-  DevBuf all(d->ctx, n * sizeof(fe));
-  exchange(d, runs, all.get(), n1 * R * sizeof(fe), /*a2a=*/false);                  // [g][k1][c]
-  SG_HIP(launch_swap01(all.as<fe>(), out, d->G, n1, R, d->ctx->stream));              // [k1][g][c]
+  const uint64_t R = n2 / d->G, one = n1 * R;
+  DevBuf all(d->ctx, nv * n * sizeof(fe));
+  exchange(d, runs, all.get(), nv * one * sizeof(fe), /*a2a=*/false);  // [g][v][k1][c]
+  const fe* src = all.as<fe>();
+  DevBuf byv;
+  if (nv > 1) {
+    byv = DevBuf(d->ctx, nv * n * sizeof(fe));
+    SG_HIP(launch_swap01(all.as<fe>(), byv.as<fe>(), d->G, nv, one, d->ctx->stream));  // [v][g][k1][c]
+    src = byv.as<fe>();
+  }
+  for (uint64_t v = 0; v < nv; ++v)
+    SG_HIP(launch_swap01(src + v * n, outs[v], d->G, n1, R, d->ctx->stream));  // [k1][g][c]
 }
 
 // this rank's run shard of a natural-order vector every rank holds (no exchange)
@@ -608,21 +695,21 @@ void dist_open_batch(sg_dist* d, uint64_t R, uint64_t n2, std::vector<OpenReq>& 
     if (pl.lm) pl.top_dig = add_job(sr.top.get(), true, tidx);
     qtot += q.I.size();
   }
-  // every gather at once, one round trip
+  // every gather at once, one round trip: the absolute address of every entry (values first, then
+  // digests, each in output order), two launches whatever the number of rounds and buffers
   std::vector<fe> vals(nvals);
   std::vector<uint8_t> dig(ndig * 64);
   if (!jobs.empty()) {
-    DevBuf dI(ctx, idx.size() * 8), dV(ctx, std::max<size_t>(nvals, 1) * sizeof(fe)), dD(ctx, std::max<size_t>(ndig, 1) * 64);
-    SG_HIP(hipMemcpyAsync(dI.get(), idx.data(), idx.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+    std::vector<uint64_t> addr(nvals + ndig);
     for (const Job& jb : jobs) {
-      const uint64_t* ix = dI.as<uint64_t>() + jb.idx0;
-      if (jb.digest)
-        SG_HIP(launch_gather_digests(static_cast<const uint64_t*>(jb.src), ix, dD.as<uint64_t>() + jb.out0 * 8,
-                                     (uint32_t)jb.count, ctx->stream));
-      else
-        SG_HIP(launch_gather_fe(static_cast<const fe*>(jb.src), ix, dV.as<fe>() + jb.out0, (uint32_t)jb.count,
-                                ctx->stream));
+      const uint64_t base = reinterpret_cast<uint64_t>(jb.src);
+      uint64_t* a = addr.data() + (jb.digest ? nvals : 0) + jb.out0;
+      for (size_t k = 0; k < jb.count; ++k) a[k] = base + (jb.digest ? 64 : sizeof(fe)) * idx[jb.idx0 + k];
     }
+    DevBuf dA(ctx, addr.size() * 8), dV(ctx, std::max<size_t>(nvals, 1) * sizeof(fe)), dD(ctx, std::max<size_t>(ndig, 1) * 64);
+    SG_HIP(hipMemcpyAsync(dA.get(), addr.data(), addr.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+    SG_HIP(launch_gather_abs(dA.as<uint64_t>(), dV.get(), (uint32_t)nvals, false, ctx->stream));
+    SG_HIP(launch_gather_abs(dA.as<uint64_t>() + nvals, dD.get(), (uint32_t)ndig, true, ctx->stream));
     if (nvals) SG_HIP(hipMemcpyAsync(vals.data(), dV.get(), nvals * sizeof(fe), hipMemcpyDeviceToHost, ctx->stream));
     if (ndig) SG_HIP(hipMemcpyAsync(dig.data(), dD.get(), ndig * 64, hipMemcpyDeviceToHost, ctx->stream));
     host_wait(ctx, ctx->stream);

@@ -51,19 +51,37 @@ void dist_plan(uint64_t n, int G, uint64_t& n1, uint64_t& n2);
 // this rank's run shard [N1][N2 / G] (its column shard gathered first)
 void dist_lde_replicated(sg_dist* d, const fe& gen, uint64_t n, const fe& offset, const fe* coeffs, uint64_t len,
                          fe* runs);
+// nv polynomials at once (offsets[v], coeffs[v] of lens[v]) into run shards runs + v n / G
+void dist_lde_replicated_batch(sg_dist* d, const fe& gen, uint64_t n, const fe* offsets, const fe* const* coeffs,
+                               const uint64_t* lens, fe* runs, uint64_t nv);
 // fft/ntt.rs:7-68 over the ranks (a root of order exactly n): column shard [N1/G][row_len] in, run
 // shard [N1][N2/G] out; the inverse from a run shard into the column shard [N1/G][N2]
 void dist_ntt(sg_dist* d, const fe& root, const fe* cols, uint64_t row_len, uint64_t n, fe* runs);
+// nv transforms at once (one exchange, one launch per step): column shard v at cols + v N1/G row_len,
+// run shard v at runs + v n / G
+void dist_ntt_batch(sg_dist* d, const fe& root, const fe* cols, uint64_t row_len, uint64_t n, fe* runs, uint64_t nv);
 // fast_coset_evaluate of a coefficient column shard [N1/G][row_len] into the run shard
 void dist_coset_evaluate(sg_dist* d, const fe& gen, uint64_t n, const fe& offset, const fe* cols, uint64_t row_len,
                          fe* runs);
+// nv column shards at once (v at cols + v N1/G row_len, offsets[v]) into runs + v n / G
+void dist_coset_evaluate_batch(sg_dist* d, const fe& gen, uint64_t n, const fe* offsets, const fe* cols,
+                               uint64_t row_len, fe* runs, uint64_t nv);
 void dist_intt(sg_dist* d, const fe& root, const fe* runs, uint64_t n, fe* cols);
+// nv inverses at once: run shard v at runs + v n / G, column shard v at cols + v n / G
+void dist_intt_batch(sg_dist* d, const fe& root, const fe* runs, uint64_t n, fe* cols, uint64_t nv);
 // coset interpolation of a run-sharded codeword of n points on offset * <gen> into the column shard
 // [N1/G][N2] of its coefficients (distributed INTT + offset^-i)
 void dist_coset_interpolate(sg_dist* d, const fe& gen, uint64_t n, const fe& offset, const fe* runs, fe* cols);
+// nv codewords at once (run shard v at runs + v n / G, column shard v at cols + v n / G)
+void dist_coset_interpolate_batch(sg_dist* d, const fe& gen, uint64_t n, const fe& offset, const fe* runs, fe* cols,
+                                  uint64_t nv);
 // all-gathers: column shards / run shards of an n-vector -> the whole vector, natural order, every rank
 void dist_gather_columns(sg_dist* d, const fe* cols, uint64_t n, fe* out);
+// nv column shards (v at cols + v n / G) into outs[v], one all-gather
+void dist_gather_columns_batch(sg_dist* d, const fe* cols, uint64_t n, fe* const* outs, uint64_t nv);
 void dist_gather_runs(sg_dist* d, const fe* runs, uint64_t n, fe* out);
+// nv run shards (v at runs + v n / G) into outs[v], one all-gather
+void dist_gather_runs_batch(sg_dist* d, const fe* runs, uint64_t n, fe* const* outs, uint64_t nv);
 // this rank's run shard [N1][N2/G] of a natural-order n-vector (a strided copy, no exchange)
 void dist_take_runs(sg_dist* d, const fe* full, uint64_t n, fe* runs);
 // merkle_root.rs:21-32 of a run-sharded codeword; with `keep`, the forest and top tree are retained

@@ -140,18 +140,30 @@ struct PassArgs {
   const fe* ep_T2;
   uint64_t ep_row0, ep_j0, ep_rows;
   int ep_logR;
+  // batched four-step (ep_k vectors, 2^ep_vlog rows each, one exchange): row r is row r & (2^ep_vlog
+  // - 1) of vector r >> ep_vlog, stored at [k >> ep_logR][row][vector][k & (2^ep_logR - 1)];
+  // ep_k = 1, ep_vlog = 63 for one vector
+  int ep_vlog;
+  uint64_t ep_k;
 };
+
+// the four-step epilogue's store of output k of (batched) row r: times w^((ep_j0 + row) k), to the
+// all-to-all send buffer (PassArgs / FirstArgs)
+template <class Args>
+__device__ __forceinline__ void ep_store(const Args& a, uint64_t r, uint64_t k, const fe& v) {
+  const uint64_t rl = r & ((1ull << a.ep_vlog) - 1), vv = r >> a.ep_vlog;
+  const uint64_t e = (a.ep_j0 + rl) * k;  // < 2^36 (host-checked)
+  const fe w = mont_mul(mont_mul(ld_fe(a.ep_T0 + (e & 4095)), ld_fe(a.ep_T1 + ((e >> 12) & 4095))),
+                        ld_fe(a.ep_T2 + (e >> 24)));
+  const uint64_t R = (uint64_t)1 << a.ep_logR;
+  st_fe(a.ep_out + (((k >> a.ep_logR) * a.ep_rows + rl) * a.ep_k + vv) * R + (k & (R - 1)), mont_mul(v, w));
+}
 
 // store of a transform's element k (row pointer `row`) at the end of a pass
 __device__ __forceinline__ void pass_store(const PassArgs& a, fe* row, uint64_t k, fe v, bool post, bool last,
                                            const fe& pc) {
   if (last && a.ep_out) {
-    const uint64_t r = a.ep_row0 + blockIdx.y;
-    const uint64_t e = (a.ep_j0 + r) * k;  // < 2^36 (host-checked)
-    const fe w = mont_mul(mont_mul(ld_fe(a.ep_T0 + (e & 4095)), ld_fe(a.ep_T1 + ((e >> 12) & 4095))),
-                          ld_fe(a.ep_T2 + (e >> 24)));
-    const uint64_t R = (uint64_t)1 << a.ep_logR;
-    st_fe(a.ep_out + ((k >> a.ep_logR) * a.ep_rows + r) * R + (k & (R - 1)), mont_mul(v, w));
+    ep_store(a, a.ep_row0 + blockIdx.y, k, v);
     return;
   }
   if (post) v = mont_mul(v, pc);
@@ -419,6 +431,8 @@ struct FirstArgs {
   const fe* ep_T2;
   uint64_t ep_row0, ep_j0, ep_rows;
   int ep_logR;
+  int ep_vlog;  // as PassArgs
+  uint64_t ep_k;
 };
 
 // WHOLE variants: EP = the four-step epilogue store, POST = times *post (INTT n^-1), else canonical
@@ -518,12 +532,7 @@ __global__ __launch_bounds__(1 << (TL - 3), TL == 11 ? SG_NTT_WPE : 1) void k_nt
       for (int mm = 0; mm < 8; ++mm) {
         const uint64_t k = qq + ((uint32_t)mm << tl);
         if constexpr (EP) {
-          const uint64_t r = a.ep_row0 + ycol(c);
-          const uint64_t e = (a.ep_j0 + r) * k;  // < 2^36 (host-checked)
-          const fe w = mont_mul(mont_mul(ld_fe(a.ep_T0 + (e & 4095)), ld_fe(a.ep_T1 + ((e >> 12) & 4095))),
-                                ld_fe(a.ep_T2 + (e >> 24)));
-          const uint64_t R = (uint64_t)1 << a.ep_logR;
-          st_fe(a.ep_out + ((k >> a.ep_logR) * a.ep_rows + r) * R + (k & (R - 1)), mont_mul(x[mm], w));
+          ep_store(a, a.ep_row0 + ycol(c), k, x[mm]);
         } else {
           st_fe(orow + k, POST ? mont_mul(x[mm], pc) : fe_canon(x[mm]));
         }
@@ -568,6 +577,7 @@ __global__ void k_scale_const(fe* __restrict__ data, uint64_t n, const fe* __res
 // Montgomery power tables (T0: base^i, T1: base^(i<<12), T2: base^(i<<24)).
 // Twiddles of the four-step (omega^(j1*k2)) and the coset scale (offset^j) are
 // both of this form.
+// (nb arrays of rows x cols back to back, each scaled alike)
 struct MulPowArgs {
   fe* data;
   uint64_t rows, cols;
@@ -575,13 +585,14 @@ struct MulPowArgs {
   const fe* T0;
   const fe* T1;
   const fe* T2;
+  uint64_t nb;
 };
 
 __global__ __launch_bounds__(256) void k_mul_pow(MulPowArgs a) {
-  const uint64_t total = a.rows * a.cols;
+  const uint64_t total = a.rows * a.cols * a.nb;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t l = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; l < total; l += stride) {
-    const uint64_t r = l / a.cols, c = l - r * a.cols;
+    const uint64_t rr = l / a.cols, c = l - rr * a.cols, r = rr % a.rows;
     const uint64_t e = (a.a0 + a.a1 * r) * c + a.b0 + a.b1 * r;
     fe w = mont_mul(ld_fe(a.T0 + (e & 4095)), ld_fe(a.T1 + ((e >> 12) & 4095)));
     w = mont_mul(w, ld_fe(a.T2 + (e >> 24)));
@@ -592,22 +603,26 @@ __global__ __launch_bounds__(256) void k_mul_pow(MulPowArgs a) {
 // out[b][a][c] = in[a][b][c] for an A x B x C array (swap the two outer axes).
 // C >= 16: every (a, b) run of C elements is a coalesced copy.  C < 16: 32 x 32
 // tiles of (a, b) through LDS so both the reads and the writes are coalesced.
+// nb arrays back to back (array v at v A B C in both)
 __global__ __launch_bounds__(256) void k_swap01_runs(const fe* __restrict__ in, fe* __restrict__ out, uint64_t A,
-                                                     uint64_t B, uint64_t C) {
-  const uint64_t total = A * B * C;
+                                                     uint64_t B, uint64_t C, uint64_t nb) {
+  const uint64_t one = A * B * C, total = one * nb;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t l = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; l < total; l += stride) {
     const uint64_t c = l % C, ab = l / C;
-    const uint64_t b = ab % B, aa = ab / B;  // l = ((aa * B) + b) * C + c (input order)
-    st_fe(out + (b * A + aa) * C + c, ld_fe(in + l));
+    const uint64_t b = ab % B, aa = (ab / B) % A, v = l / one;  // l = (((v A + aa) B) + b) C + c
+    st_fe(out + v * one + (b * A + aa) * C + c, ld_fe(in + l));
   }
 }
 
 __global__ __launch_bounds__(256) void k_swap01_tiled(const fe* __restrict__ in, fe* __restrict__ out, uint64_t A,
                                                       uint64_t B, uint64_t C) {
   __shared__ fe tile[32][33];
-  // blockIdx.x: tile over b (32 wide), blockIdx.y: tile over a, blockIdx.z: c
-  const uint64_t b0 = (uint64_t)blockIdx.x * 32, a0 = (uint64_t)blockIdx.y * 32, c = blockIdx.z;
+  // blockIdx.x: tile over b (32 wide), blockIdx.y: tile over a, blockIdx.z: c + C v (array v)
+  const uint64_t b0 = (uint64_t)blockIdx.x * 32, a0 = (uint64_t)blockIdx.y * 32, c = blockIdx.z % C;
+  const uint64_t vo = (blockIdx.z / C) * A * B * C;
+  in += vo;
+  out += vo;
   const uint32_t tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
   for (uint32_t k = ty; k < 32; k += 8) {
     const uint64_t aa = a0 + k, b = b0 + tx;
@@ -670,12 +685,15 @@ __global__ void k_gather_digests(const uint64_t* __restrict__ tree, const uint64
 }
 
 // column shard of a replicated coefficient vector: out[r][j] = in[base + r + n1 j] (0 past len)
+// (nb vectors: vector v from in + v in_stride into out + v rows row_len)
 __global__ void k_gather_cols(fe* __restrict__ out, const fe* __restrict__ in, uint64_t len, uint64_t rows,
-                              uint64_t row_len, uint64_t n1, uint64_t base) {
+                              uint64_t row_len, uint64_t n1, uint64_t base, uint64_t nb, uint64_t in_stride) {
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= rows * row_len) return;
-  const uint64_t r = t / row_len, j = t % row_len, src = base + r + n1 * j;
-  st_fe(out + t, src < len ? ld_fe(in + src) : fe_zero());
+  const uint64_t one = rows * row_len;
+  if (t >= one * nb) return;
+  const uint64_t v = t / one, tl = t % one;
+  const uint64_t r = tl / row_len, j = tl % row_len, src = base + r + n1 * j;
+  st_fe(out + t, src < len ? ld_fe(in + v * in_stride + src) : fe_zero());
 }
 
 __global__ void k_gather_fe(const fe* __restrict__ src, const uint64_t* __restrict__ idx, fe* __restrict__ out,
@@ -683,6 +701,19 @@ __global__ void k_gather_fe(const fe* __restrict__ src, const uint64_t* __restri
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= count) return;
   st_fe(out + i, ld_fe(src + idx[i]));
+}
+
+template <bool DIGEST>
+__global__ void k_gather_abs(const uint64_t* __restrict__ addr, void* __restrict__ out, uint32_t count) {
+  uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= count) return;
+  if constexpr (DIGEST) {
+    uint64_t d[8];
+    ld_digest(reinterpret_cast<const uint64_t*>(addr[i]), d);
+    st_digest(static_cast<uint64_t*>(out) + (uint64_t)i * 8, d);
+  } else {
+    st_fe(static_cast<fe*>(out) + i, ld_fe(reinterpret_cast<const fe*>(addr[i])));
+  }
 }
 
 // ---------------------------------------------- FRI Fiat-Shamir on the device
@@ -897,14 +928,24 @@ hipError_t launch_serialize_tail(const TailItem* items, uint32_t count, uint8_t*
   return hipGetLastError();
 }
 
+hipError_t launch_gather_abs(const uint64_t* addr, void* out, uint32_t count, bool digest, hipStream_t s) {
+  if (!count) return hipSuccess;
+  ProfScope ps(digest ? "gather_digests" : "gather_fe", (digest ? 72ull : 24ull) * count, s);
+  if (digest)
+    hipLaunchKernelGGL(k_gather_abs<true>, dim3((count + 255) / 256), dim3(256), 0, s, addr, out, count);
+  else
+    hipLaunchKernelGGL(k_gather_abs<false>, dim3((count + 255) / 256), dim3(256), 0, s, addr, out, count);
+  return hipGetLastError();
+}
+
 hipError_t launch_gather_cols(fe* out, const fe* in, uint64_t len, uint64_t rows, uint64_t row_len, uint64_t n1,
-                              uint64_t base, hipStream_t s) {
-  const uint64_t total = rows * row_len;
+                              uint64_t base, hipStream_t s, uint64_t nb, uint64_t in_stride) {
+  const uint64_t total = rows * row_len * nb;
   if (!total) return hipSuccess;
   if ((total + 255) / 256 > 0x7FFFFFFFull) return hipErrorInvalidValue;
   ProfScope ps("gather_cols", 32 * total, s);
   hipLaunchKernelGGL(k_gather_cols, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, s, out, in, len, rows, row_len,
-                     n1, base);
+                     n1, base, nb, in_stride);
   return hipGetLastError();
 }
 
@@ -1088,6 +1129,8 @@ hipError_t launch_ntt_dit(fe* const* data, int batch, const fe* tw, int logn, co
       a.ep_j0 = ep->j0;
       a.ep_rows = ep->rows;
       a.ep_logR = ep->logR;
+      a.ep_vlog = ep->vlog;
+      a.ep_k = ep->k;
     }
     uint64_t tile = (uint64_t)1 << (a.L + a.logC);
     uint64_t ntiles = ((uint64_t)1 << logn) / tile;
@@ -1172,6 +1215,8 @@ hipError_t launch_ntt_fused(fe* const* out, const fe* const* in, int batch, uint
         a.ep_j0 = ep->j0;
         a.ep_rows = ep->rows;
         a.ep_logR = ep->logR;
+        a.ep_vlog = ep->vlog;
+        a.ep_k = ep->k;
       }
       const uint64_t n = (uint64_t)1 << logn;
       ProfScope ps("ntt_small", batch * (16 * (n_in < n ? n_in : n) + 16 * n), s, (uint64_t)batch * n);
@@ -1257,6 +1302,12 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
   //  * smaller levels (latency-bound): a quad of lanes per node, up to 7 levels fused.
   // SG_MERKLE_QUAD_BELOW = log2 of the threshold (A/B only)
   static const uint64_t kQuadBelow = (uint64_t)1 << env_int("SG_MERKLE_QUAD_BELOW", 16);
+  // forests (the sharded prove's run subtrees: thousands of trees of ~2^10 leaves per launch):
+  // a node level with <= 2^SG_MERKLE_FOREST_QUAD digests per tree goes to the quad-lane kernel,
+  // every level to each tree's root in one launch, however many trees the launch holds -- the
+  // one-lane-per-node kernel would run blocks of count (< 64) lanes, i.e. partial waves, and
+  // need two more launches per forest.  0 disables it (A/B knob).
+  static const int kForestQuad = env_int("SG_MERKLE_FOREST_QUAD", 6);
   int logn = 0;
   while (((uint64_t)1 << logn) < n) ++logn;
   int level = start_level;
@@ -1329,7 +1380,8 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
           if (fuse > 11) fuse = 11;  // leaf + level 1 in the lane, then 512 -> 1 through LDS
         }
       }
-    } else if (count * (uint64_t)batch >= kQuadBelow && count >= 2) {
+    } else if (count * (uint64_t)batch >= kQuadBelow && count >= 2 &&
+               !(kForestQuad > 0 && batch > 1 && count <= ((uint64_t)1 << kForestQuad))) {
       // 2 levels per launch: same-box A/Bs put 3 ahead of 4 (round 3, profiles/r03_ab_merkle_nodes.log,
       // r03_ab_nodes.log) and 2 ahead of 3 (round 4, r04_ab_node_fuse_*.log: every fused level above
       // the first parks half of the block's remaining waves at a barrier); coalesced child loads
@@ -1412,24 +1464,25 @@ static unsigned grid_stride_blocks(uint64_t n) {
 }
 
 hipError_t launch_mul_pow(fe* data, uint64_t rows, uint64_t cols, uint64_t a0, uint64_t a1, uint64_t b0,
-                          uint64_t b1, const fe* T0, const fe* T1, const fe* T2, hipStream_t s) {
-  if (rows * cols == 0) return hipSuccess;
-  MulPowArgs a{data, rows, cols, a0, a1, b0, b1, T0, T1, T2};
-  ProfScope ps("mul_pow", 32 * rows * cols, s);
-  hipLaunchKernelGGL(k_mul_pow, dim3(grid_stride_blocks(rows * cols)), dim3(256), 0, s, a);
+                          uint64_t b1, const fe* T0, const fe* T1, const fe* T2, hipStream_t s, uint64_t nb) {
+  if (rows * cols * nb == 0) return hipSuccess;
+  MulPowArgs a{data, rows, cols, a0, a1, b0, b1, T0, T1, T2, nb};
+  ProfScope ps("mul_pow", 32 * rows * cols * nb, s);
+  hipLaunchKernelGGL(k_mul_pow, dim3(grid_stride_blocks(rows * cols * nb)), dim3(256), 0, s, a);
   return hipGetLastError();
 }
 
-hipError_t launch_swap01(const fe* in, fe* out, uint64_t A, uint64_t B, uint64_t C, hipStream_t s) {
-  if (A * B * C == 0) return hipSuccess;
-  ProfScope ps("transpose", 32 * A * B * C, s);
+hipError_t launch_swap01(const fe* in, fe* out, uint64_t A, uint64_t B, uint64_t C, hipStream_t s, uint64_t nb) {
+  if (A * B * C * nb == 0) return hipSuccess;
+  ProfScope ps("transpose", 32 * A * B * C * nb, s);
   if (C >= 16 || A == 1 || B == 1) {
-    hipLaunchKernelGGL(k_swap01_runs, dim3(grid_stride_blocks(A * B * C)), dim3(256), 0, s, in, out, A, B, C);
+    hipLaunchKernelGGL(k_swap01_runs, dim3(grid_stride_blocks(A * B * C * nb)), dim3(256), 0, s, in, out, A, B, C,
+                       nb);
   } else {
     uint64_t gx = (B + 31) / 32, gy = (A + 31) / 32;
-    if (gx > 0x7FFFFFFFull || gy > 65535 || C > 65535) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_swap01_tiled, dim3((unsigned)gx, (unsigned)gy, (unsigned)C), dim3(256), 0, s, in, out, A,
-                       B, C);
+    if (gx > 0x7FFFFFFFull || gy > 65535 || C * nb > 65535) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_swap01_tiled, dim3((unsigned)gx, (unsigned)gy, (unsigned)(C * nb)), dim3(256), 0, s, in,
+                       out, A, B, C);
   }
   return hipGetLastError();
 }

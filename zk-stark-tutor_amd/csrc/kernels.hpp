@@ -30,6 +30,10 @@ struct NttEpilogue {
   const fe* T2;
   uint64_t row0, j0, rows;
   int logR;
+  // batched: k vectors of 2^vlog rows each (row r of the launch = row r mod 2^vlog of vector
+  // r >> vlog), send buffer [peer][row][vector][R]
+  int vlog = 63;
+  uint64_t k = 1;
 };
 // big_tl (12 / 13): the stages after first_b0 run as ONE pass on 2^big_tl-element tiles when they fit
 // (the plan launch_ntt_fused picks for mid-size transforms); 0: passes on 2048-element tiles
@@ -82,9 +86,13 @@ hipError_t launch_gather_digests(const uint64_t* tree, const uint64_t* idx, uint
 // lane, else `blocks` x 256 lanes grid-stride
 hipError_t launch_copy16(const void* src, void* dst, uint64_t bytes, unsigned blocks, hipStream_t s);
 hipError_t launch_gather_fe(const fe* src, const uint64_t* idx, fe* out, uint32_t count, hipStream_t s);
-// out[r][j] = in[base + r + n1 j] for r < rows, j < row_len (0 past len): a column shard
+// gathers from absolute device addresses (one launch for openings spread over many buffers):
+// out[i] = the 64-byte digest (digest = true) or 16-byte element at addr[i]
+hipError_t launch_gather_abs(const uint64_t* addr, void* out, uint32_t count, bool digest, hipStream_t s);
+// out[r][j] = in[base + r + n1 j] for r < rows, j < row_len (0 past len): a column shard; nb such
+// gathers at once, vector v from in + v in_stride into out + v rows row_len
 hipError_t launch_gather_cols(fe* out, const fe* in, uint64_t len, uint64_t rows, uint64_t row_len, uint64_t n1,
-                              uint64_t base, hipStream_t s);
+                              uint64_t base, hipStream_t s, uint64_t nb = 1, uint64_t in_stride = 0);
 
 // Proof-stream objects serialized on the device (the tail of a proof: FRI query phase and the
 // Stark openings): [code u8][len u64 BE][payload] at byte offset `dst` of the output, with
@@ -102,9 +110,11 @@ struct TailItem {
 hipError_t launch_serialize_tail(const TailItem* items, uint32_t count, uint8_t* out, uint64_t bytes, hipStream_t s);
 
 // row-sharded helpers (four-step NTT, sharded Merkle / FRI)
+// (nb: that many rows x cols arrays back to back, each scaled alike)
 hipError_t launch_mul_pow(fe* data, uint64_t rows, uint64_t cols, uint64_t a0, uint64_t a1, uint64_t b0,
-                          uint64_t b1, const fe* T0, const fe* T1, const fe* T2, hipStream_t s);
-hipError_t launch_swap01(const fe* in, fe* out, uint64_t A, uint64_t B, uint64_t C, hipStream_t s);
+                          uint64_t b1, const fe* T0, const fe* T1, const fe* T2, hipStream_t s, uint64_t nb = 1);
+// out[b][a][c] = in[a][b][c] for nb A x B x C arrays back to back
+hipError_t launch_swap01(const fe* in, fe* out, uint64_t A, uint64_t B, uint64_t C, hipStream_t s, uint64_t nb = 1);
 hipError_t launch_fri_fold_runs(fe* out, const fe* in, uint64_t half, uint64_t run, uint64_t run_stride,
                                 uint64_t run_off, const fe* T0, const fe* T1, const fe* T2, const fe& K,
                                 hipStream_t s);

@@ -757,11 +757,11 @@ bool interpolate_geometric_batch_dist(sg_dist* dd, const fe& q, uint64_t D, cons
   // residue-class rows of a_i = y_i / Z'(q^i) (replicated: cols * M elements), then their transforms
   DevBuf rowsbuf(ctx, cols * M * sizeof(fe));
   SG_HIP(launch_geo_rows(rowsbuf.as<fe>(), y, ys, P.Zdi, n, P.logf, M, cols, fe_r2(), ctx->stream));
-  DevBuf A(ctx, cols * f * Ml * sizeof(fe)), colsbuf(ctx, rows * row_len * sizeof(fe));
-  for (uint64_t t = 0; t < cols * f; ++t) {
-    SG_HIP(launch_gather_cols(colsbuf.as<fe>(), rowsbuf.as<fe>() + t * Mf, Mf, rows, row_len, n1, row0, ctx->stream));
-    dist_ntt(dd, P.qf, colsbuf.as<fe>(), row_len, M, A.as<fe>() + t * Ml);
-  }
+  // all cols * f rows' column shards in one gather, their transforms as one batch (one exchange)
+  const uint64_t nt = cols * f;
+  DevBuf A(ctx, nt * Ml * sizeof(fe)), colsbuf(ctx, nt * rows * row_len * sizeof(fe));
+  SG_HIP(launch_gather_cols(colsbuf.as<fe>(), rowsbuf.as<fe>(), Mf, rows, row_len, n1, row0, ctx->stream, nt, Mf));
+  dist_ntt_batch(dd, P.qf, colsbuf.as<fe>(), row_len, M, A.as<fe>(), nt);
   // the kernel rows on this rank's run shards ([r][Ml], kept with the domain tables)
   std::vector<uint64_t> kkey = {kDomainGeoInterp, fe_lo(q), fe_hi(q), D, (uint64_t)P.logf, 0xB0B};
   const fe* K = nullptr;
@@ -794,23 +794,25 @@ bool interpolate_geometric_batch_dist(sg_dist* dd, const fe& q, uint64_t D, cons
   }
   DevBuf Shat(ctx, cols * Ml * sizeof(fe)), Scol(ctx, cols * Ml * sizeof(fe));
   SG_HIP(launch_geo_dot(Shat.as<fe>(), A.as<fe>(), K, P.logf, Ml, cols, fe_r2(), ctx->stream));
-  for (size_t c = 0; c < cols; ++c) dist_intt(dd, P.qf, Shat.as<fe>() + c * Ml, M, Scol.as<fe>() + c * Ml);
+  dist_intt_batch(dd, P.qf, Shat.as<fe>(), M, Scol.as<fe>(), cols);
   // P(q^(f k)) / M on the column shards, then the coefficients (run shards) and every rank's copy
   const fe *iA, *iB;
   pow_tables2(ctx, fe_inv(q), D, &iA, &iB);
   const fe minv_m = to_mont(fe_inv(fe_from_u64(M)));
-  DevBuf V(ctx, cols * Ml * sizeof(fe)), runs(ctx, Ml * sizeof(fe));
+  DevBuf V(ctx, cols * Ml * sizeof(fe)), runs(ctx, cols * Ml * sizeof(fe));
   SG_HIP(launch_interp_assemble_cols(V.as<fe>(), y, ys, P.Zv, Scol.as<fe>(), n, P.logf, cols, rows, n2, n1, row0, iA, iB,
                                      minv_m, to_mont(minv_m), ctx->stream));
   const fe qfi = fe_inv(P.qf);
+  dist_ntt_batch(dd, qfi, V.as<fe>(), n2, M, runs.as<fe>(), cols);
+  std::vector<fe*> ptrs;
   for (size_t c = 0; c < cols; ++c) {
-    dist_ntt(dd, qfi, V.as<fe>() + c * Ml, n2, M, runs.as<fe>());
     DPoly out = dpoly_alloc(ctx, D);
-    dist_gather_runs(dd, runs.as<fe>(), M, out.p());
     if (M < D) SG_HIP(hipMemsetAsync(out.p() + M, 0, (D - M) * sizeof(fe), ctx->stream));
     out.len = n;
+    ptrs.push_back(out.p());
     outs.push_back(std::move(out));
   }
+  dist_gather_runs_batch(dd, runs.as<fe>(), M, ptrs.data(), cols);
   dist_count_sharded_interpolation(dd, cols);
   return true;
 }
@@ -865,14 +867,23 @@ void prove_boundary_quotients(sg_ctx* ctx, const sg_stark& st, const std::vector
       nums.emplace_back(diffs.back().p(), diffs.back().len);
     }
     const std::vector<int64_t> dnum = dev_degrees(ctx, nums);
+    // the sharded quotients of one coset size go through the distributed LDE, interpolation and
+    // all-gather as one batch each; the others through the replicated division
+    struct Sharded {
+      size_t s;
+      DivPlan pl;
+      const fe* inv_shard;
+    };
+    std::vector<Sharded> sh;
+    std::vector<DevBuf> keep;  // divisor tables (and their shards) until the batches are enqueued
+    const size_t b0 = bqs.size();
+    bqs.resize(b0 + m);
     for (size_t s = 0; s < m; ++s) {
       const int64_t dz = hp_degree(bz[s]);
       // (the branch depends only on what every rank shares -- never on a per-rank environment)
       if (dd && dist_shard_algebra(dd) && dz >= 0 && dnum[s] >= dz && bz[s].size() <= 64) {
         const DivPlan pl = coset_divide_plan(st.omicron, D, dnum[s], dz);
         if (diffs[s].len <= pl.order && dist_can_shard(pl.order, dist_world(dd))) {
-          const uint64_t nl = pl.order / (uint64_t)dist_world(dd);
-          std::vector<DevBuf> keep;
           const fe* inv = divisor_inverse_values(ctx, pl, g, Zs[s].p(), Zs[s].len, bz[s].data(), &keep);
           std::vector<uint64_t> key = {kDomainDivisorInverse, pl.order, fe_lo(pl.root), fe_hi(pl.root), fe_lo(g),
                                        fe_hi(g), bz[s].size()};
@@ -880,21 +891,40 @@ void prove_boundary_quotients(sg_ctx* ctx, const sg_stark& st, const std::vector
             key.push_back(fe_lo(c));
             key.push_back(fe_hi(c));
           }
-          const fe* inv_shard = shard_table(dd, key, inv, pl.order, keep, /*bounded=*/true);
-          DevBuf vals(ctx, nl * sizeof(fe)), cols(ctx, nl * sizeof(fe));
-          dist_lde_replicated(dd, pl.root, pl.order, g, diffs[s].p(), diffs[s].len, vals.as<fe>());
-          dev_mul(ctx, vals.as<fe>(), vals.as<fe>(), inv_shard, nl);
-          dist_coset_interpolate(dd, pl.root, pl.order, g, vals.as<fe>(), cols.as<fe>());
-          DPoly full = dpoly_alloc(ctx, pl.order);
-          dist_gather_columns(dd, cols.as<fe>(), pl.order, full.p());
-          full.len = std::min(pl.result_len, pl.order);  // the reference's truncation (coset_divide_finish)
-          bqs.push_back(std::move(full));
-          dist_count_sharded_quotient(dd);
+          sh.push_back(Sharded{s, pl, shard_table(dd, key, inv, pl.order, keep, /*bounded=*/true)});
           continue;
         }
       }
-      bqs.push_back(fast_coset_divide_dev(ctx, st.omicron, D, g, diffs[s].p(), diffs[s].len, Zs[s].p(), Zs[s].len,
-                                          dz, bz[s].data(), dnum[s]));
+      bqs[b0 + s] = fast_coset_divide_dev(ctx, st.omicron, D, g, diffs[s].p(), diffs[s].len, Zs[s].p(), Zs[s].len,
+                                          dz, bz[s].data(), dnum[s]);
+    }
+    for (size_t i0 = 0; i0 < sh.size();) {
+      size_t i1 = i0 + 1;
+      while (i1 < sh.size() && sh[i1].pl.order == sh[i0].pl.order) ++i1;
+      const DivPlan& pl = sh[i0].pl;
+      const uint64_t nv = i1 - i0, nl = pl.order / (uint64_t)dist_world(dd);
+      std::vector<fe> offs(nv, g);
+      std::vector<const fe*> srcs;
+      std::vector<uint64_t> lens;
+      std::vector<fe*> outs;
+      for (size_t i = i0; i < i1; ++i) {
+        srcs.push_back(diffs[sh[i].s].p());
+        lens.push_back(diffs[sh[i].s].len);
+      }
+      DevBuf vals(ctx, nv * nl * sizeof(fe)), cols(ctx, nv * nl * sizeof(fe));
+      dist_lde_replicated_batch(dd, pl.root, pl.order, offs.data(), srcs.data(), lens.data(), vals.as<fe>(), nv);
+      for (size_t i = i0; i < i1; ++i) {
+        fe* v = vals.as<fe>() + (i - i0) * nl;
+        dev_mul(ctx, v, v, sh[i].inv_shard, nl);
+        DPoly full = dpoly_alloc(ctx, pl.order);
+        full.len = std::min(sh[i].pl.result_len, pl.order);  // the reference's truncation (coset_divide_finish)
+        outs.push_back(full.p());
+        bqs[b0 + sh[i].s] = std::move(full);
+        dist_count_sharded_quotient(dd);
+      }
+      dist_coset_interpolate_batch(dd, pl.root, pl.order, g, vals.as<fe>(), cols.as<fe>(), nv);
+      dist_gather_columns_batch(dd, cols.as<fe>(), pl.order, outs.data(), nv);
+      i0 = i1;
     }
   }
 }
@@ -1042,14 +1072,25 @@ void prove_transition_quotients(sg_ctx* ctx, const sg_stark& st, const std::vect
     const int G = dist_world(dd);
     const fe wL = root_of_order(Ls);
     sco.L = Ls / (uint64_t)G;
+    // the 2m distributed LDEs as one batch (one exchange), then each run shard into its array
+    std::vector<fe> offs;
+    std::vector<const fe*> srcs;
+    std::vector<uint64_t> lens;
     for (int pass = 0; pass < 2; ++pass)
       for (size_t s = 0; s < trace_polys.size(); ++s) {
-        sco.V.push_back(dpoly_alloc(ctx, sco.L));
-        dist_lde_replicated(dd, wL, Ls, pass ? fe_mul(g, st.omicron) : g, trace_polys[s].p(), trace_polys[s].len,
-                            sco.V.back().p());
-        sco.var.push_back((int)sco.V.size() - 1);
-        sco.shift.push_back(0);
+        offs.push_back(pass ? fe_mul(g, st.omicron) : g);
+        srcs.push_back(trace_polys[s].p());
+        lens.push_back(trace_polys[s].len);
       }
+    DevBuf lde(ctx, offs.size() * sco.L * sizeof(fe));
+    dist_lde_replicated_batch(dd, wL, Ls, offs.data(), srcs.data(), lens.data(), lde.as<fe>(), offs.size());
+    for (size_t v = 0; v < offs.size(); ++v) {
+      sco.V.push_back(dpoly_alloc(ctx, sco.L));
+      SG_HIP(hipMemcpyAsync(sco.V.back().p(), lde.as<fe>() + v * sco.L, sco.L * sizeof(fe), hipMemcpyDeviceToDevice,
+                            ctx->stream));
+      sco.var.push_back((int)sco.V.size() - 1);
+      sco.shift.push_back(0);
+    }
     DivPlan pl;
     pl.root = wL;
     pl.order = Ls;
@@ -1057,23 +1098,30 @@ void prove_transition_quotients(sg_ctx* ctx, const sg_stark& st, const std::vect
     tz_shard = dcache ? shard_table(dd, tz_key_at(kDomainTzInverse, pl), tz_inverse(pl), Ls, air_keep)
                       : shard_table(dd, tz_key_at(kDomainTzValues, pl), tz_values(pl), Ls, air_keep);
   }
-  for (const MPoly* tc : tcs) {
-    const uint64_t len = symbolic_degree_bound(*tc, Tp - 1) + 1;
-    const uint64_t L = next_pow2(len);
-    if (sharded) {
-      const uint64_t nl = sco.L;
-      DPoly vals = transition_values_rescue(ctx, *tc->rescue, sco, g, air_keep, dd, Ls);
-      DevBuf qv(ctx, nl * sizeof(fe)), cols(ctx, nl * sizeof(fe));
-      if (tz_shard_inverse) dev_mul(ctx, qv.as<fe>(), vals.p(), tz_shard, nl);
-      else dev_div(ctx, qv.as<fe>(), vals.p(), tz_shard, nl);
-      dist_coset_interpolate(dd, root_of_order(Ls), Ls, g, qv.as<fe>(), cols.as<fe>());
+  if (sharded) {
+    // every constraint's quotient values on the rank's run shard, then their coset interpolations
+    // and all-gathers as one batch each (one exchange apiece for all constraints)
+    const uint64_t nl = sco.L, nq = tcs.size();
+    DevBuf qv(ctx, nq * nl * sizeof(fe)), cols(ctx, nq * nl * sizeof(fe));
+    std::vector<fe*> outs;
+    for (size_t q = 0; q < nq; ++q) {
+      const uint64_t len = symbolic_degree_bound(*tcs[q], Tp - 1) + 1;
+      DPoly vals = transition_values_rescue(ctx, *tcs[q]->rescue, sco, g, air_keep, dd, Ls);
+      if (tz_shard_inverse) dev_mul(ctx, qv.as<fe>() + q * nl, vals.p(), tz_shard, nl);
+      else dev_div(ctx, qv.as<fe>() + q * nl, vals.p(), tz_shard, nl);
       DPoly out = dpoly_alloc(ctx, Ls);  // all Ls coefficients, on every rank
-      dist_gather_columns(dd, cols.as<fe>(), Ls, out.p());
+      outs.push_back(out.p());
       pending.push_back(Pending{tqs.size(), std::move(vals), len, Ls, true});
       dist_count_sharded_quotient(dd);
       tqs.push_back(std::move(out));
-      continue;
     }
+    dist_coset_interpolate_batch(dd, root_of_order(Ls), Ls, g, qv.as<fe>(), cols.as<fe>(), nq);
+    dist_gather_columns_batch(dd, cols.as<fe>(), Ls, outs.data(), nq);
+  }
+  for (const MPoly* tc : tcs) {
+    if (sharded) break;
+    const uint64_t len = symbolic_degree_bound(*tc, Tp - 1) + 1;
+    const uint64_t L = next_pow2(len);
     auto cit = cosets.find(L);
     if (cit == cosets.end()) cit = cosets.emplace(L, air_coset(ctx, trace_polys, L, st.omicron, g, st.D)).first;
     DPoly vals = transition_values(ctx, *tc, cit->second, g, air_keep);
