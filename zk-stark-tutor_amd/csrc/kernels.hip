@@ -592,7 +592,7 @@ __global__ __launch_bounds__(256) void k_mul_pow(MulPowArgs a) {
   const uint64_t total = a.rows * a.cols * a.nb;
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t l = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; l < total; l += stride) {
-    const uint64_t rr = l / a.cols, c = l - rr * a.cols, r = rr % a.rows;
+    const uint64_t rr = l / a.cols, c = l - rr * a.cols, r = a.nb > 1 ? rr % a.rows : rr;
     const uint64_t e = (a.a0 + a.a1 * r) * c + a.b0 + a.b1 * r;
     fe w = mont_mul(ld_fe(a.T0 + (e & 4095)), ld_fe(a.T1 + ((e >> 12) & 4095)));
     w = mont_mul(w, ld_fe(a.T2 + (e >> 24)));
@@ -610,7 +610,8 @@ __global__ __launch_bounds__(256) void k_swap01_runs(const fe* __restrict__ in, 
   const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
   for (uint64_t l = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; l < total; l += stride) {
     const uint64_t c = l % C, ab = l / C;
-    const uint64_t b = ab % B, aa = (ab / B) % A, v = l / one;  // l = (((v A + aa) B) + b) C + c
+    const uint64_t b = ab % B, vaa = ab / B;  // l = (((v A + aa) B) + b) C + c
+    const uint64_t v = nb > 1 ? vaa / A : 0, aa = vaa - v * A;
     st_fe(out + v * one + (b * A + aa) * C + c, ld_fe(in + l));
   }
 }
@@ -691,7 +692,7 @@ __global__ void k_gather_cols(fe* __restrict__ out, const fe* __restrict__ in, u
   const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint64_t one = rows * row_len;
   if (t >= one * nb) return;
-  const uint64_t v = t / one, tl = t % one;
+  const uint64_t v = nb > 1 ? t / one : 0, tl = t - v * one;
   const uint64_t r = tl / row_len, j = tl % row_len, src = base + r + n1 * j;
   st_fe(out + t, src < len ? ld_fe(in + v * in_stride + src) : fe_zero());
 }
