@@ -630,12 +630,18 @@ void wait_roots(sg_ctx* ctx, int batch, uint64_t seq, int slot0, hipStream_t s) 
   std::atomic_thread_fence(std::memory_order_acquire);
 }
 
-std::unique_ptr<sg_tree> new_tree(sg_ctx* ctx, uint64_t n) {
+std::unique_ptr<sg_tree> new_tree(sg_ctx* ctx, uint64_t n, const fe* lean_leaves) {
   SG_REQUIRE(n > 0 && (n & (n - 1)) == 0, "Leafs len must be power of two");
   std::unique_ptr<sg_tree> t(new sg_tree());
   t->n = n;
   t->logn = ilog2_exact(n);
-  t->buf = DevBuf(ctx, merkle_tree_digests(n) * 64);
+  // SG_LEAN_TREES=0: every tree keeps its leaf digests (A/B knob, alternate path)
+  static const bool lean_on = [] {
+    const char* v = getenv("SG_LEAN_TREES");
+    return !(v && *v == '0');
+  }();
+  t->leaves = (lean_on && n >= 2) ? lean_leaves : nullptr;
+  t->buf = DevBuf(ctx, (merkle_tree_digests(n) - (t->leaves ? n : 0)) * 64);
   return t;
 }
 
@@ -655,12 +661,14 @@ uint64_t launch_trees(sg_ctx* ctx, const fe* const* d_leaves, int batch, sg_tree
   uint64_t* flags_dev[4] = {nullptr, nullptr, nullptr, nullptr};
   for (int b = 0; b < batch; ++b) {
     SG_REQUIRE(trees[b]->n == trees[0]->n, "trees of one launch must have equal sizes");
-    bufs[b] = trees[b]->buf.as<uint64_t>();
+    SG_REQUIRE(!trees[b]->leaves == !trees[0]->leaves, "trees of one launch must be alike lean");
+    bufs[b] = tree_vptr(trees[b]);
     roots_dev[b] = ctx->pinned_roots_dev + 8 * (slot0 + b);
     flags_dev[b] = ctx->pinned_roots_dev + sg_ctx::kFlagIndex + slot0 + b;
   }
   const uint64_t seq = ++ctx->root_seq;
-  SG_HIP(launch_merkle_tree(d_leaves, bufs, batch, trees[0]->n, roots_dev, s, 0, 0, 0, flags_dev, seq));
+  SG_HIP(launch_merkle_tree(d_leaves, bufs, batch, trees[0]->n, roots_dev, s, 0, 0, 0, flags_dev, seq, nullptr,
+                            trees[0]->leaves != nullptr));
   return seq;
 }
 
@@ -688,11 +696,12 @@ void fill_tree(sg_ctx* ctx, const fe* d_leaves, sg_tree* t, const FoldLeaves* fo
 
 // fill_tree in two halves, so work can be queued behind the tree before the host waits for its root
 uint64_t fill_tree_launch(sg_ctx* ctx, const fe* d_leaves, sg_tree* t, const FoldLeaves* fold) {
-  uint64_t* buf = t->buf.as<uint64_t>();
+  uint64_t* buf = tree_vptr(t);
   uint64_t* root_dev = ctx->pinned_roots_dev;
   uint64_t* flag_dev = ctx->pinned_roots_dev + sg_ctx::kFlagIndex;
   const uint64_t seq = ++ctx->root_seq;
-  SG_HIP(launch_merkle_tree(&d_leaves, &buf, 1, t->n, &root_dev, ctx->stream, 0, 0, 0, &flag_dev, seq, fold));
+  SG_HIP(launch_merkle_tree(&d_leaves, &buf, 1, t->n, &root_dev, ctx->stream, 0, 0, 0, &flag_dev, seq, fold,
+                            t->leaves != nullptr));
   return seq;
 }
 
@@ -712,12 +721,20 @@ void path_indices(const sg_tree* t, uint64_t index, std::vector<uint64_t>& idx) 
   for (int lv = 0; lv < t->logn; ++lv) idx.push_back(level_offset(t->n, lv) + ((index >> lv) ^ 1));
 }
 
+// the gather address of digest `i` of tree t (launch_gather_abs): a lean tree's leaf digest is
+// tagged (bit 0) as the address of the leaf value to rehash
+uint64_t digest_addr(const sg_tree* t, uint64_t i) {
+  if (t->leaves && i < t->n) return ((uint64_t)(uintptr_t)(t->leaves + i)) | 1;
+  return tree_vbase(t) + 64 * i;
+}
+
 void gather_digests(sg_ctx* ctx, const sg_tree* t, const std::vector<uint64_t>& idx, uint8_t* out) {
   if (idx.empty()) return;
+  std::vector<uint64_t> addr(idx.size());
+  for (size_t k = 0; k < idx.size(); ++k) addr[k] = digest_addr(t, idx[k]);
   DevBuf di(ctx, idx.size() * 8), dout(ctx, idx.size() * 64);
-  SG_HIP(hipMemcpyAsync(di.get(), idx.data(), idx.size() * 8, hipMemcpyHostToDevice, ctx->stream));
-  SG_HIP(launch_gather_digests(t->buf.as<uint64_t>(), di.as<uint64_t>(), dout.as<uint64_t>(), (uint32_t)idx.size(),
-                               ctx->stream));
+  SG_HIP(hipMemcpyAsync(di.get(), addr.data(), addr.size() * 8, hipMemcpyHostToDevice, ctx->stream));
+  SG_HIP(launch_gather_abs(di.as<uint64_t>(), dout.get(), (uint32_t)idx.size(), true, ctx->stream));
   SG_HIP(hipMemcpyAsync(out, dout.get(), idx.size() * 64, hipMemcpyDeviceToHost, ctx->stream));
   host_wait(ctx, ctx->stream);
 }
@@ -977,7 +994,8 @@ void TailWriter::leafs(const fe* a, const fe* b, const fe* c) {
 void TailWriter::path(const sg_tree* t, uint64_t index) {
   SG_REQUIRE(t->logn <= 64, "tree too deep");
   TailItem it{};
-  it.src[0] = (uint64_t)(uintptr_t)t->buf.get();
+  it.src[0] = tree_vbase(t);
+  it.src[1] = (uint64_t)(uintptr_t)t->leaves;  // lean: the level-0 sibling is rehashed from these
   it.dst = bytes;
   it.n = t->n;
   it.index = index;
@@ -1083,17 +1101,15 @@ void fri_commit_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, co
       len /= 2;
     }
   }
+  // lean trees over the round codewords the state keeps (the query phase rehashes a leaf sibling)
   std::vector<std::unique_ptr<sg_tree>> trees(rounds);
   for (size_t r = 0; r < rounds; ++r) {
-    trees[r].reset(new sg_tree());
-    trees[r]->n = plan[r].len;
-    trees[r]->logn = ilog2_exact(plan[r].len);
-    trees[r]->buf = DevBuf(ctx, merkle_tree_digests(plan[r].len) * 64);
     if (r + 1 < rounds) {
       st.codewords.emplace_back(ctx, (plan[r].len / 2) * sizeof(fe));
       st.cw.push_back(st.codewords.back().as<fe>());
       st.lengths.push_back(plan[r].len / 2);
     }
+    trees[r] = new_tree(ctx, plan[r].len, st.cw[r]);
   }
   // Round r >= 1 hashes the fold of round r-1 in the same launch that computes it
   // (the fold is written out too: later rounds and the query phase read it).
@@ -1122,8 +1138,9 @@ void fri_commit_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, co
       SG_REQUIRE(fe_eq(fe_pow(plan[r].omega, len - 1), plan[r].winv),
                  "error in commit: omega does not have the right order!");  // fri.rs:133
       const fe* lv = st.cw[r];
-      uint64_t* buf = trees[r]->buf.as<uint64_t>();
-      SG_HIP(launch_merkle_tree(&lv, &buf, 1, len, nullptr, ctx->stream, 0, 0, 0, nullptr, 0, r ? &fold : nullptr));
+      uint64_t* buf = tree_vptr(trees[r].get());
+      SG_HIP(launch_merkle_tree(&lv, &buf, 1, len, nullptr, ctx->stream, 0, 0, 0, nullptr, 0, r ? &fold : nullptr,
+                                trees[r]->leaves != nullptr));
       const uint64_t* rootp = buf + level_offset(len, trees[r]->logn) * 8;
       uint64_t* rout = droots.as<uint64_t>() + 8 * r;
       if (r == rounds - 1) {

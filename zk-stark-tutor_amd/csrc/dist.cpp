@@ -647,14 +647,16 @@ void dist_open_batch(sg_dist* d, uint64_t R, uint64_t n2, std::vector<OpenReq>& 
     bool digest;         // 64-byte digests (else 16-byte elements)
     size_t idx0, count;  // index range in `idx`
     size_t out0;         // output offset in values (elements) or digests (64-byte units)
+    const sg_tree* tree = nullptr;  // digests of a local tree (a lean one rehashes its leaf level)
   };
   std::vector<uint64_t> idx;
   std::vector<Job> jobs;
   size_t nvals = 0, ndig = 0;
-  auto add_job = [&](const void* src, bool digest, const std::vector<uint64_t>& ix) -> size_t {
+  auto add_job = [&](const void* src, bool digest, const std::vector<uint64_t>& ix,
+                     const sg_tree* tree = nullptr) -> size_t {
     const size_t out0 = digest ? ndig : nvals;
     if (ix.empty()) return out0;
-    jobs.push_back({src, digest, idx.size(), ix.size(), out0});
+    jobs.push_back({src, digest, idx.size(), ix.size(), out0, tree});
     idx.insert(idx.end(), ix.begin(), ix.end());
     (digest ? ndig : nvals) += ix.size();
     return out0;
@@ -674,7 +676,7 @@ void dist_open_batch(sg_dist* d, uint64_t R, uint64_t n2, std::vector<OpenReq>& 
       for (uint64_t i : q.I) path_indices(q.tree, i, pidx);
       q.depth = q.tree->logn;
       pl.vals_at = add_job(q.cw, false, q.I);
-      pl.path_dig = add_job(q.tree->buf.get(), true, pidx);
+      pl.path_dig = add_job(nullptr, true, pidx, q.tree);
       continue;
     }
     const ShardedRound& sr = *q.sr;
@@ -704,7 +706,8 @@ void dist_open_batch(sg_dist* d, uint64_t R, uint64_t n2, std::vector<OpenReq>& 
     for (const Job& jb : jobs) {
       const uint64_t base = reinterpret_cast<uint64_t>(jb.src);
       uint64_t* a = addr.data() + (jb.digest ? nvals : 0) + jb.out0;
-      for (size_t k = 0; k < jb.count; ++k) a[k] = base + (jb.digest ? 64 : sizeof(fe)) * idx[jb.idx0 + k];
+      for (size_t k = 0; k < jb.count; ++k)
+        a[k] = jb.tree ? digest_addr(jb.tree, idx[jb.idx0 + k]) : base + (jb.digest ? 64 : sizeof(fe)) * idx[jb.idx0 + k];
     }
     DevBuf dA(ctx, addr.size() * 8), dV(ctx, std::max<size_t>(nvals, 1) * sizeof(fe)), dD(ctx, std::max<size_t>(ndig, 1) * 64);
     SG_HIP(hipMemcpyAsync(dA.get(), addr.data(), addr.size() * 8, hipMemcpyHostToDevice, ctx->stream));

@@ -21,9 +21,22 @@
 struct sg_tree {
   uint64_t n = 0;
   int logn = 0;
-  sg::DevBuf buf;  // (2n - 1) digests x 8 u64
+  sg::DevBuf buf;  // (2n - 1) digests x 8 u64; a lean tree: levels 1.. only (n - 1 digests)
   uint8_t root[64];
+  // lean trees (the prove's retained commitments): the leaf digests are not kept -- an opening
+  // rehashes the sibling leaf from these values, which the tree's owner keeps alive -- so the
+  // tree holds 64 B per leaf instead of 128 B
+  const sg::fe* leaves = nullptr;
 };
+
+namespace sg {
+// the address level-offset arithmetic starts from: the buffer, or for a lean tree n digests before
+// it (level 0 is never stored or read there)
+inline uint64_t tree_vbase(const sg_tree* t) {
+  return (uint64_t)(uintptr_t)t->buf.get() - (t->leaves ? 64 * t->n : 0);
+}
+inline uint64_t* tree_vptr(const sg_tree* t) { return reinterpret_cast<uint64_t*>((uintptr_t)tree_vbase(t)); }
+}  // namespace sg
 
 struct sg_fri_state {
   std::vector<sg::DevBuf> codewords;  // round r codeword (device); [0] empty when borrowed
@@ -107,7 +120,8 @@ void coset_evaluate_batch(sg_ctx* ctx, const fe& generator, uint64_t root_order,
 void build_trees(sg_ctx* ctx, const fe* const* d_leaves, int batch, uint64_t n, std::unique_ptr<sg_tree>* out);
 // split form for trees built on another stream: allocate, launch (roots into pinned slots
 // slot0..slot0+batch-1), then wait for the published roots
-std::unique_ptr<sg_tree> new_tree(sg_ctx* ctx, uint64_t n);
+// lean_leaves != nullptr (n >= 2): a lean tree over those values (they must outlive the tree)
+std::unique_ptr<sg_tree> new_tree(sg_ctx* ctx, uint64_t n, const fe* lean_leaves = nullptr);
 uint64_t launch_trees(sg_ctx* ctx, const fe* const* d_leaves, int batch, sg_tree* const* trees, int slot0,
                       hipStream_t s);
 void finish_trees(sg_ctx* ctx, sg_tree* const* trees, int batch, uint64_t seq, int slot0, hipStream_t s);
@@ -116,6 +130,8 @@ void fill_tree(sg_ctx* ctx, const fe* d_leaves, sg_tree* t, const FoldLeaves* fo
 uint64_t fill_tree_launch(sg_ctx* ctx, const fe* d_leaves, sg_tree* t, const FoldLeaves* fold = nullptr);
 void fill_tree_finish(sg_ctx* ctx, sg_tree* t, uint64_t seq);
 void path_indices(const sg_tree* t, uint64_t index, std::vector<uint64_t>& idx);
+// launch_gather_abs address of digest i of t (a lean tree's leaf digests: the tagged leaf address)
+uint64_t digest_addr(const sg_tree* t, uint64_t i);
 void gather_digests(sg_ctx* ctx, const sg_tree* t, const std::vector<uint64_t>& idx, uint8_t* out);
 
 size_t fri_num_rounds(const sg_fri* f);

@@ -704,13 +704,16 @@ __global__ void k_gather_fe(const fe* __restrict__ src, const uint64_t* __restri
   st_fe(out + i, ld_fe(src + idx[i]));
 }
 
+// DIGEST: an address with bit 0 set is a lean tree's leaf value, rehashed (merkle_root.rs:25-30)
 template <bool DIGEST>
 __global__ void k_gather_abs(const uint64_t* __restrict__ addr, void* __restrict__ out, uint32_t count) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= count) return;
   if constexpr (DIGEST) {
     uint64_t d[8];
-    ld_digest(reinterpret_cast<const uint64_t*>(addr[i]), d);
+    const uint64_t ad = addr[i];
+    if (ad & 1) leaf_hash(ld_fe(reinterpret_cast<const fe*>(ad & ~1ull)), d);
+    else ld_digest(reinterpret_cast<const uint64_t*>(ad), d);
     st_digest(static_cast<uint64_t*>(out) + (uint64_t)i * 8, d);
   } else {
     st_fe(static_cast<fe*>(out) + i, ld_fe(reinterpret_cast<const fe*>(addr[i])));
@@ -890,14 +893,16 @@ __global__ __launch_bounds__(64) void k_serialize_tail(const TailItem* __restric
     uint8_t* e = o + 9 + 72 * (uint64_t)l;
     put_be64_dev(e, 64);
     const uint64_t d = 2 * it.n - 2 * (it.n >> l) + ((it.index >> l) ^ 1);  // level l sibling
-    const uint4* q = reinterpret_cast<const uint4*>(it.src[0] + 64 * d);
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const uint4 v = q[k];
-      const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int j = 0; j < 16; ++j) e[8 + 16 * k + j] = (uint8_t)(w[j >> 2] >> (8 * (j & 3)));
+    uint64_t h[8];
+    if (l == 0 && it.src[1]) {  // a lean tree: the sibling leaf rehashed from its value
+      leaf_hash(ld_fe(reinterpret_cast<const fe*>(it.src[1]) + d), h);
+    } else {
+      ld_digest(reinterpret_cast<const uint64_t*>(it.src[0] + 64 * d), h);
     }
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) e[8 + 8 * k + j] = (uint8_t)(h[k] >> (8 * j));
   } else {
     const fe v = ld_fe(reinterpret_cast<const fe*>(it.src[l]));
     uint8_t* e = o + 9 + 16 * (uint64_t)l;
@@ -1289,7 +1294,7 @@ uint64_t merkle_tree_digests(uint64_t n) { return 2 * n - 1; }
 hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, int batch, uint64_t n,
                               uint64_t* const* root_host, hipStream_t s, uint64_t leaves_ys, uint64_t tree_ys,
                               int start_level, uint64_t* const* root_flag, uint64_t root_seq,
-                              const FoldLeaves* fold) {
+                              const FoldLeaves* fold, bool skip_l0) {
   if (!batch_ok(batch, tree_ys) || (start_level == 0 && (leaves_ys != 0) != (tree_ys != 0))) return hipErrorInvalidValue;
   const int np = tree_ys ? 1 : batch;
   // Launch plan.  Levels 0..logn; level k has n >> k digests at offset 2n - 2(n >> k).
@@ -1322,6 +1327,7 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
       a.root_flag[b] = (a.root_host[b] && root_flag) ? root_flag[b] : nullptr;
     }
     a.root_seq = root_seq;
+    a.skip_l0 = (skip_l0 && level == 0) ? 1u : 0u;
     const bool fold_here = fold && level == 0;
     a.fold.src = fold_here ? fold->src : nullptr;
     a.fold.dst = fold_here ? fold->dst : nullptr;
@@ -1364,6 +1370,7 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
         // forest's subtrees included) fuse node levels (A/B knob)
         static const int env_fmin = env_int("SG_MERKLE_LEAF_FUSE_MIN", 18);
         fuse = count * (uint64_t)batch >= ((uint64_t)1 << env_fmin) ? env_fuse : 1;
+        if (skip_l0 && fuse < 2) fuse = 2;  // a lean tree's leaf launch computes level 1 too
         if (bs < lbs) kind = 0;
         {
           int lg = 0;  // a block's fused levels end at its single digest
@@ -1426,6 +1433,8 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
       while (((uint64_t)1 << lg) < nodes) ++lg;
       fuse = lg + 1;
     }
+    // a lean tree's leaf launch computes level 1 too: no later launch reads the leaf digests
+    if (a.skip_l0 && (fuse < 2 || logn < 1)) return hipErrorInvalidValue;
     if (level + fuse - 1 > logn) fuse = logn - level + 1;
     if (fuse < 1 || fuse > kMaxFuse) return hipErrorInvalidValue;
     a.fuse = fuse;
@@ -1433,9 +1442,10 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
       int lv = level - 1 + k;
       a.off[k] = (lv < 0 || lv > logn) ? 0 : (2 * n - 2 * (n >> lv));
     }
-    // algorithmic bytes: leaves read once (16 B) + every digest of these levels written once (64 B)
+    // algorithmic bytes: leaves read once (16 B) + every digest of these levels written once (64 B;
+    // a lean tree's leaf digests are not written)
     uint64_t digests = 0;
-    for (int k = 0; k < fuse; ++k) digests += count >> k;
+    for (int k = a.skip_l0 ? 1 : 0; k < fuse; ++k) digests += count >> k;
     // a fused fold reads 2 source elements and writes the folded one instead of reading the leaf
     // quad kernels: 4 lanes per node; leaf pairs: 2 leaves per lane
     const uint64_t per_block = kind == 3 || kind == 5 || kind == 7 ? bs / 4 : kind == 8 || kind == 10 ? 2 * bs : bs;

@@ -54,7 +54,7 @@ __global__ __launch_bounds__(MAXB) void k_merkle_levels(MerkleArgs a) {
       ld_digest(child + (2 * idx + 1) * 8, r);
       blake2b_node(l, r, d);
     }
-    st_digest(tree + (a.off[1] + idx) * 8, d);
+    if (!(LEAF && a.skip_l0)) st_digest(tree + (a.off[1] + idx) * 8, d);  // lean: no leaf digests
     if (a.first_level == a.root_level && root_slot) {
       for (int i = 0; i < 8; ++i) root_slot[i] = d[i];
       merkle_root_publish(a, true);
@@ -122,8 +122,10 @@ __global__ __launch_bounds__(MAXB) void k_merkle_leaf_pairs(MerkleArgs a) {
     uint64_t l[8], r[8];
     leaf_hash(v0, l);
     leaf_hash(v1, r);
-    st_digest(tree + (a.off[1] + 2 * p) * 8, l);
-    st_digest(tree + (a.off[1] + 2 * p + 1) * 8, r);
+    if (!a.skip_l0) {  // lean trees keep no leaf digests
+      st_digest(tree + (a.off[1] + 2 * p) * 8, l);
+      st_digest(tree + (a.off[1] + 2 * p + 1) * 8, r);
+    }
     blake2b_node(l, r, d);
     st_digest(tree + (a.off[2] + p) * 8, d);
     if (a.first_level + 1 == a.root_level && root_slot) {
@@ -516,9 +518,11 @@ __global__ __launch_bounds__(4 * NODES) void k_merkle_quad_leaves(MerkleArgs a) 
   uint64_t hlo = 0, hhi = 0;
   if (valid) {
     blake2b_quad(msg[node], len, q, sp, hlo, hhi);
-    uint64_t* dst = tree + (a.off[1] + leaf) * 8;
-    dst[q] = hlo;
-    dst[4 + q] = hhi;
+    if (!a.skip_l0) {  // lean trees keep no leaf digests
+      uint64_t* dst = tree + (a.off[1] + leaf) * 8;
+      dst[q] = hlo;
+      dst[4 + q] = hhi;
+    }
     if (a.first_level == a.root_level && root_slot) {
       root_slot[q] = hlo;
       root_slot[4 + q] = hhi;
