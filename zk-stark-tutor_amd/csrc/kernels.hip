@@ -1442,10 +1442,11 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
       int lv = level - 1 + k;
       a.off[k] = (lv < 0 || lv > logn) ? 0 : (2 * n - 2 * (n >> lv));
     }
-    // algorithmic bytes: leaves read once (16 B) + every digest of these levels written once (64 B;
-    // a lean tree's leaf digests are not written)
+    // algorithmic bytes (Merkle(n) = 16 n + 64 (2n - 1)): leaves read once (16 B) +
+    // 64 B per digest of these levels -- a lean tree's leaf digests count although they are not
+    // stored (the figure prices the algorithm; its PMC traffic is then below it)
     uint64_t digests = 0;
-    for (int k = a.skip_l0 ? 1 : 0; k < fuse; ++k) digests += count >> k;
+    for (int k = 0; k < fuse; ++k) digests += count >> k;
     // a fused fold reads 2 source elements and writes the folded one instead of reading the leaf
     // quad kernels: 4 lanes per node; leaf pairs: 2 leaves per lane
     const uint64_t per_block = kind == 3 || kind == 5 || kind == 7 ? bs / 4 : kind == 8 || kind == 10 ? 2 * bs : bs;
