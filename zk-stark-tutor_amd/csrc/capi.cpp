@@ -630,7 +630,7 @@ void wait_roots(sg_ctx* ctx, int batch, uint64_t seq, int slot0, hipStream_t s) 
   std::atomic_thread_fence(std::memory_order_acquire);
 }
 
-std::unique_ptr<sg_tree> new_tree(sg_ctx* ctx, uint64_t n, const fe* lean_leaves) {
+std::unique_ptr<sg_tree> new_tree(sg_ctx* ctx, uint64_t n, const fe* lean_leaves, int drop) {
   SG_REQUIRE(n > 0 && (n & (n - 1)) == 0, "Leafs len must be power of two");
   std::unique_ptr<sg_tree> t(new sg_tree());
   t->n = n;
@@ -640,8 +640,15 @@ std::unique_ptr<sg_tree> new_tree(sg_ctx* ctx, uint64_t n, const fe* lean_leaves
     const char* v = getenv("SG_LEAN_TREES");
     return !(v && *v == '0');
   }();
-  t->leaves = (lean_on && n >= 2) ? lean_leaves : nullptr;
-  t->buf = DevBuf(ctx, (merkle_tree_digests(n) - (t->leaves ? n : 0)) * 64);
+  // SG_LEAN_DROP=k: at most k levels dropped (A/B knob; the default is what the caller asks)
+  static const int drop_cap = [] {
+    const char* v = getenv("SG_LEAN_DROP");
+    return v && *v ? atoi(v) : 64;
+  }();
+  drop = std::min(drop, drop_cap);
+  t->drop = (lean_on && lean_leaves && n >= 2) ? std::min(std::max(drop, 0), t->logn) : 0;
+  t->leaves = t->drop ? lean_leaves : nullptr;
+  t->buf = DevBuf(ctx, (2 * (n >> t->drop) - 1) * 64);  // levels drop .. log2 n
   return t;
 }
 
@@ -661,14 +668,14 @@ uint64_t launch_trees(sg_ctx* ctx, const fe* const* d_leaves, int batch, sg_tree
   uint64_t* flags_dev[4] = {nullptr, nullptr, nullptr, nullptr};
   for (int b = 0; b < batch; ++b) {
     SG_REQUIRE(trees[b]->n == trees[0]->n, "trees of one launch must have equal sizes");
-    SG_REQUIRE(!trees[b]->leaves == !trees[0]->leaves, "trees of one launch must be alike lean");
+    SG_REQUIRE(trees[b]->drop == trees[0]->drop, "trees of one launch must be alike lean");
     bufs[b] = tree_vptr(trees[b]);
     roots_dev[b] = ctx->pinned_roots_dev + 8 * (slot0 + b);
     flags_dev[b] = ctx->pinned_roots_dev + sg_ctx::kFlagIndex + slot0 + b;
   }
   const uint64_t seq = ++ctx->root_seq;
   SG_HIP(launch_merkle_tree(d_leaves, bufs, batch, trees[0]->n, roots_dev, s, 0, 0, 0, flags_dev, seq, nullptr,
-                            trees[0]->leaves != nullptr));
+                            trees[0]->drop));
   return seq;
 }
 
@@ -701,7 +708,7 @@ uint64_t fill_tree_launch(sg_ctx* ctx, const fe* d_leaves, sg_tree* t, const Fol
   uint64_t* flag_dev = ctx->pinned_roots_dev + sg_ctx::kFlagIndex;
   const uint64_t seq = ++ctx->root_seq;
   SG_HIP(launch_merkle_tree(&d_leaves, &buf, 1, t->n, &root_dev, ctx->stream, 0, 0, 0, &flag_dev, seq, fold,
-                            t->leaves != nullptr));
+                            t->drop));
   return seq;
 }
 
@@ -724,7 +731,8 @@ void path_indices(const sg_tree* t, uint64_t index, std::vector<uint64_t>& idx) 
 // the gather address of digest `i` of tree t (launch_gather_abs): a lean tree's leaf digest is
 // tagged (bit 0) as the address of the leaf value to rehash
 uint64_t digest_addr(const sg_tree* t, uint64_t i) {
-  if (t->leaves && i < t->n) return ((uint64_t)(uintptr_t)(t->leaves + i)) | 1;
+  SG_REQUIRE(t->drop <= 1, "gathers rehash the leaf level only");
+  if (t->drop && i < t->n) return ((uint64_t)(uintptr_t)(t->leaves + i)) | 1;
   return tree_vbase(t) + 64 * i;
 }
 
@@ -995,7 +1003,8 @@ void TailWriter::path(const sg_tree* t, uint64_t index) {
   SG_REQUIRE(t->logn <= 64, "tree too deep");
   TailItem it{};
   it.src[0] = tree_vbase(t);
-  it.src[1] = (uint64_t)(uintptr_t)t->leaves;  // lean: the level-0 sibling is rehashed from these
+  it.src[1] = (uint64_t)(uintptr_t)t->leaves;  // lean: the low siblings are rehashed from these
+  it.src[2] = (uint64_t)t->drop;
   it.dst = bytes;
   it.n = t->n;
   it.index = index;
@@ -1057,7 +1066,7 @@ void put_u128_be(std::vector<uint8_t>& out, const fe& a) {
 
 // fri.rs:115-172.  Retains every round's codeword and tree in `st`.
 void fri_commit_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, const sg_proof_stream* ps,
-                    sg_fri_state& st, bool borrow_input) {
+                    sg_fri_state& st, bool borrow_input, int drop) {
   SG_REQUIRE(ps && ps->push && ps->fiat_shamir_prover, "proof stream callbacks required");
   size_t rounds = fri_num_rounds(f);
   SG_REQUIRE(rounds >= 1, "FRI: zero rounds for this domain");
@@ -1109,7 +1118,7 @@ void fri_commit_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, co
       st.cw.push_back(st.codewords.back().as<fe>());
       st.lengths.push_back(plan[r].len / 2);
     }
-    trees[r] = new_tree(ctx, plan[r].len, st.cw[r]);
+    trees[r] = new_tree(ctx, plan[r].len, st.cw[r], drop);
   }
   // Round r >= 1 hashes the fold of round r-1 in the same launch that computes it
   // (the fold is written out too: later rounds and the query phase read it).
@@ -1140,7 +1149,7 @@ void fri_commit_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, co
       const fe* lv = st.cw[r];
       uint64_t* buf = tree_vptr(trees[r].get());
       SG_HIP(launch_merkle_tree(&lv, &buf, 1, len, nullptr, ctx->stream, 0, 0, 0, nullptr, 0, r ? &fold : nullptr,
-                                trees[r]->leaves != nullptr));
+                                trees[r]->drop));
       const uint64_t* rootp = buf + level_offset(len, trees[r]->logn) * 8;
       uint64_t* rout = droots.as<uint64_t>() + 8 * r;
       if (r == rounds - 1) {

@@ -624,7 +624,7 @@ void dist_fri_commit(sg_dist* d, const sg_fri* f, const fe* runs, uint64_t n, co
   sub.domain_length = length;
   SG_REQUIRE(fri_num_rounds(&sub) == rounds - r, "FRI tail round count mismatch");
   if (keep) {
-    fri_commit_dev(ctx, &sub, full.as<fe>(), length, ps, keep->tail, /*borrow_input=*/false);
+    fri_commit_dev(ctx, &sub, full.as<fe>(), length, ps, keep->tail, /*borrow_input=*/false, /*drop=*/1);
     for (uint64_t l : keep->tail.lengths) keep->lengths.push_back(l);
     return;
   }

@@ -23,17 +23,18 @@ struct sg_tree {
   int logn = 0;
   sg::DevBuf buf;  // (2n - 1) digests x 8 u64; a lean tree: levels 1.. only (n - 1 digests)
   uint8_t root[64];
-  // lean trees (the prove's retained commitments): the leaf digests are not kept -- an opening
-  // rehashes the sibling leaf from these values, which the tree's owner keeps alive -- so the
-  // tree holds 64 B per leaf instead of 128 B
+  // lean trees (the prove's retained commitments): the levels below `drop` are not kept -- an
+  // opening rehashes the 2^drop-leaf block around its leaf from these values, which the tree's
+  // owner keeps alive -- so the tree holds 128 / 2^drop B per leaf instead of 128 B
   const sg::fe* leaves = nullptr;
+  int drop = 0;
 };
 
 namespace sg {
-// the address level-offset arithmetic starts from: the buffer, or for a lean tree n digests before
-// it (level 0 is never stored or read there)
+// the address level-offset arithmetic starts from: the buffer, or for a lean tree the offset of
+// level `drop` before it (the levels below are never stored or read there)
 inline uint64_t tree_vbase(const sg_tree* t) {
-  return (uint64_t)(uintptr_t)t->buf.get() - (t->leaves ? 64 * t->n : 0);
+  return (uint64_t)(uintptr_t)t->buf.get() - 64 * (2 * t->n - 2 * (t->n >> t->drop));
 }
 inline uint64_t* tree_vptr(const sg_tree* t) { return reinterpret_cast<uint64_t*>((uintptr_t)tree_vbase(t)); }
 }  // namespace sg
@@ -120,8 +121,9 @@ void coset_evaluate_batch(sg_ctx* ctx, const fe& generator, uint64_t root_order,
 void build_trees(sg_ctx* ctx, const fe* const* d_leaves, int batch, uint64_t n, std::unique_ptr<sg_tree>* out);
 // split form for trees built on another stream: allocate, launch (roots into pinned slots
 // slot0..slot0+batch-1), then wait for the published roots
-// lean_leaves != nullptr (n >= 2): a lean tree over those values (they must outlive the tree)
-std::unique_ptr<sg_tree> new_tree(sg_ctx* ctx, uint64_t n, const fe* lean_leaves = nullptr);
+// lean_leaves != nullptr (n >= 2): a lean tree over those values (they must outlive the tree) that
+// keeps no digests below level min(drop, log2 n)
+std::unique_ptr<sg_tree> new_tree(sg_ctx* ctx, uint64_t n, const fe* lean_leaves = nullptr, int drop = 1);
 uint64_t launch_trees(sg_ctx* ctx, const fe* const* d_leaves, int batch, sg_tree* const* trees, int slot0,
                       hipStream_t s);
 void finish_trees(sg_ctx* ctx, sg_tree* const* trees, int batch, uint64_t seq, int slot0, hipStream_t s);
@@ -166,8 +168,10 @@ struct ObjWriter {
 };
 void put_u128_be_at(uint8_t* out, const fe& a);
 void put_u128_be(std::vector<uint8_t>& out, const fe& a);
+// drop: the round trees' levels not kept (lean trees; the sharded prove's tail keeps drop <= 1, which
+// its absolute-address openings rehash)
 void fri_commit_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, const sg_proof_stream* ps,
-                    sg_fri_state& st, bool borrow_input = false);
+                    sg_fri_state& st, bool borrow_input = false, int drop = 3);
 // Objects pushed after a proof's last Fiat-Shamir draw (the FRI query phase, fri.rs:174-208, and
 // the Stark openings, stark.rs:524-560): collected as TailItems, serialized by one device launch
 // (k_serialize_tail) and appended with one copy -- straight into a native stream's page-locked

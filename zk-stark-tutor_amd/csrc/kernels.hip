@@ -870,47 +870,6 @@ __global__ void __launch_bounds__(256) k_copy16_stride(const sg_u32x4* __restric
 }
 
 // gather from a list of absolute device addresses (one launch for every round's openings)
-// --------------------------------------------- proof-stream tail serialization
-
-__device__ __forceinline__ void put_be64_dev(uint8_t* o, uint64_t v) {
-#pragma unroll
-  for (int i = 0; i < 8; ++i) o[i] = (uint8_t)(v >> (56 - 8 * i));
-}
-
-// one 64-lane block per object (TailItem in kernels.hpp); lane 0 writes the 9-byte header,
-// lane k the k-th element / path entry (a path has log2(n) <= 64 entries)
-__global__ __launch_bounds__(64) void k_serialize_tail(const TailItem* __restrict__ items, uint8_t* __restrict__ out) {
-  const TailItem it = items[blockIdx.x];
-  const uint32_t l = threadIdx.x;
-  uint8_t* o = out + it.dst;
-  const bool path = it.code == 2;  // SG_OBJ_PATH
-  if (l == 0) {
-    o[0] = (uint8_t)it.code;
-    put_be64_dev(o + 1, (path ? 72ull : 16ull) * it.count);
-  }
-  if (l >= it.count) return;
-  if (path) {
-    uint8_t* e = o + 9 + 72 * (uint64_t)l;
-    put_be64_dev(e, 64);
-    const uint64_t d = 2 * it.n - 2 * (it.n >> l) + ((it.index >> l) ^ 1);  // level l sibling
-    uint64_t h[8];
-    if (l == 0 && it.src[1]) {  // a lean tree: the sibling leaf rehashed from its value
-      leaf_hash(ld_fe(reinterpret_cast<const fe*>(it.src[1]) + d), h);
-    } else {
-      ld_digest(reinterpret_cast<const uint64_t*>(it.src[0] + 64 * d), h);
-    }
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) e[8 + 8 * k + j] = (uint8_t)(h[k] >> (8 * j));
-  } else {
-    const fe v = ld_fe(reinterpret_cast<const fe*>(it.src[l]));
-    uint8_t* e = o + 9 + 16 * (uint64_t)l;
-    put_be64_dev(e, fe_hi(v));
-    put_be64_dev(e + 8, fe_lo(v));
-  }
-}
-
 // ------------------------------------------------------------- launchers
 
 // tuning knob from the environment (plan experiments); `def` when unset
@@ -927,12 +886,6 @@ hipError_t launch_gather_digests(const uint64_t* tree, const uint64_t* idx, uint
   return hipGetLastError();
 }
 
-hipError_t launch_serialize_tail(const TailItem* items, uint32_t count, uint8_t* out, uint64_t bytes, hipStream_t s) {
-  if (!count) return hipSuccess;
-  ProfScope ps("serialize_tail", bytes, s);
-  hipLaunchKernelGGL(k_serialize_tail, dim3(count), dim3(64), 0, s, items, out);
-  return hipGetLastError();
-}
 
 hipError_t launch_gather_abs(const uint64_t* addr, void* out, uint32_t count, bool digest, hipStream_t s) {
   if (!count) return hipSuccess;
@@ -1294,7 +1247,7 @@ uint64_t merkle_tree_digests(uint64_t n) { return 2 * n - 1; }
 hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, int batch, uint64_t n,
                               uint64_t* const* root_host, hipStream_t s, uint64_t leaves_ys, uint64_t tree_ys,
                               int start_level, uint64_t* const* root_flag, uint64_t root_seq,
-                              const FoldLeaves* fold, bool skip_l0) {
+                              const FoldLeaves* fold, int drop) {
   if (!batch_ok(batch, tree_ys) || (start_level == 0 && (leaves_ys != 0) != (tree_ys != 0))) return hipErrorInvalidValue;
   const int np = tree_ys ? 1 : batch;
   // Launch plan.  Levels 0..logn; level k has n >> k digests at offset 2n - 2(n >> k).
@@ -1327,7 +1280,7 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
       a.root_flag[b] = (a.root_host[b] && root_flag) ? root_flag[b] : nullptr;
     }
     a.root_seq = root_seq;
-    a.skip_l0 = (skip_l0 && level == 0) ? 1u : 0u;
+    a.drop = (uint32_t)(drop > 0 ? drop : 0);
     const bool fold_here = fold && level == 0;
     a.fold.src = fold_here ? fold->src : nullptr;
     a.fold.dst = fold_here ? fold->dst : nullptr;
@@ -1370,7 +1323,7 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
         // forest's subtrees included) fuse node levels (A/B knob)
         static const int env_fmin = env_int("SG_MERKLE_LEAF_FUSE_MIN", 18);
         fuse = count * (uint64_t)batch >= ((uint64_t)1 << env_fmin) ? env_fuse : 1;
-        if (skip_l0 && fuse < 2) fuse = 2;  // a lean tree's leaf launch computes level 1 too
+        if (fuse < drop + 1) fuse = drop + 1;  // a lean tree's leaf launch reaches a stored level
         if (bs < lbs) kind = 0;
         {
           int lg = 0;  // a block's fused levels end at its single digest
@@ -1433,8 +1386,8 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
       while (((uint64_t)1 << lg) < nodes) ++lg;
       fuse = lg + 1;
     }
-    // a lean tree's leaf launch computes level 1 too: no later launch reads the leaf digests
-    if (a.skip_l0 && (fuse < 2 || logn < 1)) return hipErrorInvalidValue;
+    // a lean tree's leaf launch reaches level `drop` (or the root): no later launch reads a dropped level
+    if (level == 0 && drop > 0 && fuse < drop + 1 && fuse < logn + 1) return hipErrorInvalidValue;
     if (level + fuse - 1 > logn) fuse = logn - level + 1;
     if (fuse < 1 || fuse > kMaxFuse) return hipErrorInvalidValue;
     a.fuse = fuse;

@@ -50,9 +50,10 @@ struct MerkleArgs {
   uint64_t leaves_ys, tree_ys;     // != 0: strided rows of trees (leaves[0] + y * leaves_ys, tree[0] + y * tree_ys)
   uint64_t* root_flag[kMaxBatch];  // with root_host: set to root_seq (system scope) once the root is visible
   uint64_t root_seq;
-  // lean trees (the prove's retained trees): the leaf digests (level 0) are not stored -- the
-  // openings rehash a sibling leaf from the codeword -- so a tree keeps n - 1 digests, not 2n - 1
-  uint32_t skip_l0;
+  // lean trees (the prove's retained trees): the levels below `drop` are not stored -- the
+  // openings rehash the 2^drop-leaf block around a leaf from the codeword -- so a tree keeps
+  // 2 n / 2^drop - 1 digests, not 2n - 1
+  uint32_t drop;
   // FRI: the leaves are the fold of the previous round's codeword (fri.rs:151-159),
   // computed here and also stored (dst) -- one launch instead of fold + leaf hash
   struct {

@@ -11,7 +11,9 @@
 // in kernels.hip on the default scheduler (max-ILP spills them).
 #include <cstdlib>
 
+#include "kernels.hpp"
 #include "merkle_dev.hpp"
+#include "profiler.hpp"
 
 namespace sg {
 
@@ -54,7 +56,7 @@ __global__ __launch_bounds__(MAXB) void k_merkle_levels(MerkleArgs a) {
       ld_digest(child + (2 * idx + 1) * 8, r);
       blake2b_node(l, r, d);
     }
-    if (!(LEAF && a.skip_l0)) st_digest(tree + (a.off[1] + idx) * 8, d);  // lean: no leaf digests
+    if (a.first_level >= a.drop) st_digest(tree + (a.off[1] + idx) * 8, d);  // lean: dropped levels unstored
     if (a.first_level == a.root_level && root_slot) {
       for (int i = 0; i < 8; ++i) root_slot[i] = d[i];
       merkle_root_publish(a, true);
@@ -76,7 +78,7 @@ __global__ __launch_bounds__(MAXB) void k_merkle_levels(MerkleArgs a) {
       }
       blake2b_node(l, r, d);
       uint64_t gidx = (uint64_t)blockIdx.x * count + tid;
-      st_digest(tree + (a.off[lev + 1] + gidx) * 8, d);
+      if (a.first_level + lev >= a.drop) st_digest(tree + (a.off[lev + 1] + gidx) * 8, d);
       if (a.first_level + lev == a.root_level && root_slot) {
         for (int i = 0; i < 8; ++i) root_slot[i] = d[i];
         merkle_root_publish(a, true);
@@ -122,12 +124,12 @@ __global__ __launch_bounds__(MAXB) void k_merkle_leaf_pairs(MerkleArgs a) {
     uint64_t l[8], r[8];
     leaf_hash(v0, l);
     leaf_hash(v1, r);
-    if (!a.skip_l0) {  // lean trees keep no leaf digests
+    if (a.drop == 0) {  // lean trees keep no leaf digests
       st_digest(tree + (a.off[1] + 2 * p) * 8, l);
       st_digest(tree + (a.off[1] + 2 * p + 1) * 8, r);
     }
     blake2b_node(l, r, d);
-    st_digest(tree + (a.off[2] + p) * 8, d);
+    if (a.drop <= 1) st_digest(tree + (a.off[2] + p) * 8, d);
     if (a.first_level + 1 == a.root_level && root_slot) {
       for (int i = 0; i < 8; ++i) root_slot[i] = d[i];
       merkle_root_publish(a, true);
@@ -149,7 +151,7 @@ __global__ __launch_bounds__(MAXB) void k_merkle_leaf_pairs(MerkleArgs a) {
       }
       blake2b_node(l, r, d);
       uint64_t gidx = (uint64_t)blockIdx.x * count + tid;
-      st_digest(tree + (a.off[lev + 1] + gidx) * 8, d);
+      if (a.first_level + lev >= a.drop) st_digest(tree + (a.off[lev + 1] + gidx) * 8, d);
       if (a.first_level + lev == a.root_level && root_slot) {
         for (int i = 0; i < 8; ++i) root_slot[i] = d[i];
         merkle_root_publish(a, true);
@@ -415,10 +417,12 @@ __device__ __forceinline__ void quad_upper_levels(const MerkleArgs& a, uint64_t*
     count >>= 1;
     if (node < (int)count) {
       blake2b_quad(msg[node], 128, q, sp, hlo, hhi);
-      uint64_t gidx = (uint64_t)blockIdx.x * count + node;
-      uint64_t* dst = tree + (a.off[lev + 1] + gidx) * 8;
-      dst[q] = hlo;
-      dst[4 + q] = hhi;
+      if (a.first_level + lev >= a.drop) {  // lean trees: dropped levels unstored
+        uint64_t gidx = (uint64_t)blockIdx.x * count + node;
+        uint64_t* dst = tree + (a.off[lev + 1] + gidx) * 8;
+        dst[q] = hlo;
+        dst[4 + q] = hhi;
+      }
       if (a.first_level + lev == a.root_level && root_slot) {
         root_slot[q] = hlo;
         root_slot[4 + q] = hhi;
@@ -518,7 +522,7 @@ __global__ __launch_bounds__(4 * NODES) void k_merkle_quad_leaves(MerkleArgs a) 
   uint64_t hlo = 0, hhi = 0;
   if (valid) {
     blake2b_quad(msg[node], len, q, sp, hlo, hhi);
-    if (!a.skip_l0) {  // lean trees keep no leaf digests
+    if (a.drop == 0) {  // lean trees keep no leaf digests
       uint64_t* dst = tree + (a.off[1] + leaf) * 8;
       dst[q] = hlo;
       dst[4 + q] = hhi;
@@ -530,6 +534,98 @@ __global__ __launch_bounds__(4 * NODES) void k_merkle_quad_leaves(MerkleArgs a) 
     }
   }
   quad_upper_levels<NODES>(a, tree, root_slot, msg, node, q, sp, count, hlo, hhi);
+}
+
+// --------------------------------------------- proof-stream tail serialization
+
+__device__ __forceinline__ void put_be64_dev(uint8_t* o, uint64_t v) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o[i] = (uint8_t)(v >> (56 - 8 * i));
+}
+
+// one 64-lane block per object (TailItem in kernels.hpp); lane 0 writes the 9-byte header, lane k
+// the k-th element / path entry (a path has log2(n) <= 64 entries).  A lean tree's path (src[2] = K
+// <= 3 levels not stored): the aligned 2^K-leaf block holding the opened leaf is rehashed from the
+// leaf values (src[1]) into LDS, a quad of lanes per compression (the decimal leaf words as in
+// k_merkle_quad_leaves, then the node levels), so its K - 1 dependent steps take quad-lane
+// latency; the block's nodes are the path's first K siblings (merkle_root.rs:25-53).
+__global__ __launch_bounds__(64) void k_serialize_tail(const TailItem* __restrict__ items, uint8_t* __restrict__ out) {
+  const TailItem it = items[blockIdx.x];
+  const uint32_t l = threadIdx.x;
+  uint8_t* o = out + it.dst;
+  const bool path = it.code == 2;  // SG_OBJ_PATH
+  if (l == 0) {
+    o[0] = (uint8_t)it.code;
+    put_be64_dev(o + 1, (path ? 72ull : 16ull) * it.count);
+  }
+  __shared__ uint64_t msg[8][16];  // level-0 messages (decimal leaf words)
+  __shared__ uint64_t mt[16][8];   // the block's levels 0 .. K-1: 2^K + 2^(K-1) + ... digests
+  const uint32_t K = path ? (uint32_t)it.src[2] : 0u;  // uniform over the block
+  if (K) {
+    const fe* lv = reinterpret_cast<const fe*>(it.src[1]);
+    const uint64_t base = it.index & ~((1ull << K) - 1);
+    const int q = (int)(l & 3), node = (int)(l >> 2);
+    const SigmaPack sp = sigma_pack(q);
+    const bool on0 = node < (1 << K);
+    uint32_t len = 0;
+    if (on0) {
+      uint64_t m[5];
+      len = fe_decimal_words(ld_fe(lv + base + node), m);
+      msg[node][4 * q + 0] = q == 0 ? m[0] : q == 1 ? m[4] : 0;
+      msg[node][4 * q + 1] = q == 0 ? m[1] : 0;
+      msg[node][4 * q + 2] = q == 0 ? m[2] : 0;
+      msg[node][4 * q + 3] = q == 0 ? m[3] : 0;
+    }
+    __syncthreads();
+    uint64_t hlo = 0, hhi = 0;
+    if (on0) {
+      blake2b_quad(msg[node], len, q, sp, hlo, hhi);
+      mt[node][q] = hlo;
+      mt[node][4 + q] = hhi;
+    }
+    __syncthreads();
+    for (uint32_t lev = 1, off = 0, cnt = 1u << K; lev < K; ++lev) {
+      if (node < (int)(cnt >> 1)) {
+        blake2b_quad(&mt[off + 2 * node][0], 128, q, sp, hlo, hhi);  // children adjacent: 16 words
+        mt[off + cnt + node][q] = hlo;
+        mt[off + cnt + node][4 + q] = hhi;
+      }
+      __syncthreads();
+      off += cnt;
+      cnt >>= 1;
+    }
+  }
+  if (l >= it.count) return;
+  if (path) {
+    uint8_t* e = o + 9 + 72 * (uint64_t)l;
+    put_be64_dev(e, 64);
+    uint64_t h[8];
+    if (l < K) {  // sibling at level l inside the rehashed block
+      const uint32_t off = (1u << (K + 1)) - (1u << (K + 1 - l));  // 2^K + 2^(K-1) + ... (l terms)
+      const uint32_t sib = (uint32_t)(((it.index >> l) ^ 1) & ((1ull << (K - l)) - 1));
+#pragma unroll
+      for (int k = 0; k < 8; ++k) h[k] = mt[off + sib][k];
+    } else {
+      const uint64_t d = 2 * it.n - 2 * (it.n >> l) + ((it.index >> l) ^ 1);  // level l sibling
+      ld_digest(reinterpret_cast<const uint64_t*>(it.src[0] + 64 * d), h);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) e[8 + 8 * k + j] = (uint8_t)(h[k] >> (8 * j));
+  } else {
+    const fe v = ld_fe(reinterpret_cast<const fe*>(it.src[l]));
+    uint8_t* e = o + 9 + 16 * (uint64_t)l;
+    put_be64_dev(e, fe_hi(v));
+    put_be64_dev(e + 8, fe_lo(v));
+  }
+}
+
+hipError_t launch_serialize_tail(const TailItem* items, uint32_t count, uint8_t* out, uint64_t bytes, hipStream_t s) {
+  if (!count) return hipSuccess;
+  ProfScope ps("serialize_tail", bytes, s);
+  hipLaunchKernelGGL(k_serialize_tail, dim3(count), dim3(64), 0, s, items, out);
+  return hipGetLastError();
 }
 
 hipError_t launch_merkle_lanes(int kind, bool fold, dim3 grid, unsigned bs, hipStream_t s, const MerkleArgs& a) {

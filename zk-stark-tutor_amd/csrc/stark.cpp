@@ -1258,8 +1258,8 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
   for (size_t s = 0; s < m; ++s) bq_cw.push_back(dpoly_alloc(ctx, Nf));
   DPoly r_cw = dpoly_alloc(ctx, Nf);
   // lean trees: the openings rehash a leaf sibling from these codewords, which live to the end
-  for (size_t s = 0; s < m; ++s) bq_trees[s] = new_tree(ctx, Nf, bq_cw[s].p());
-  std::unique_ptr<sg_tree> r_tree = new_tree(ctx, Nf, r_cw.p());
+  for (size_t s = 0; s < m; ++s) bq_trees[s] = new_tree(ctx, Nf, bq_cw[s].p(), 3);
+  std::unique_ptr<sg_tree> r_tree = new_tree(ctx, Nf, r_cw.p(), 3);
   SideDrain side_drain{ctx};
   // randomizer codeword (stark.rs:424-445) first: it depends on nothing else, so its LDE and
   // its tree run on the side stream while the main stream interpolates the trace.  The tables
