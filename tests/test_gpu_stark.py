@@ -227,6 +227,33 @@ def test_stark_prove_c4_factored_air_equals_expanded(monkeypatch):
     assert st_g.prove(trace, air_g, bnd, sg.IndependentProofStream(), tr, rc) == factored
 
 
+@pytest.mark.parametrize("env", [{"SG_LEAN_DROP": "1"}, {"SG_LEAN_DROP": "2"}, {"SG_LEAN_TREES": "0"}])
+def test_lean_tree_layouts_keep_proof_bytes(monkeypatch, env):
+    """The prove's retained trees drop their low levels (three by default; an opening rehashes the
+    8-leaf block around its leaf from the codeword): every layout -- one or two levels dropped, or
+    every level kept -- writes the same proof bytes, equal to the oracle's at a small size and to
+    each other at C4 (trace 2^16, FRI domain 2^21, c = 64: 13 FRI rounds, their paths rehashed)."""
+    rp, st_o, st_g, air_o, air_g, trace, bnd, tr, rc, out = _case(40, 4, 3, 4, 2, b"lean-trees")
+    want = st_o.prove(trace, air_o, bnd, o.IndependentProofStream(), tr, rc)
+    N = 65278
+    rp_g = sg.RescuePrime(2, 1, 128, N)
+    st_c4 = sg.Stark(8, 64, 128, 2, N + 1, 3)
+    air_c4 = rp_g.transition_constraints(st_c4.omicron, st_c4.omicron_domain_length)
+    inp = o.sample(b"lean-trees-c4")
+    trace_c4 = rp_g.trace_array(inp)
+    r = e.randomness_from_seed(b"lean-trees-c4", 2 * st_c4.num_randomizers + st_c4.num_randomizer_coefficients(air_c4))
+    tr_c4 = sg.fe_array(r[:2 * st_c4.num_randomizers])
+    rc_c4 = sg.fe_array(r[2 * st_c4.num_randomizers:])
+    rp_o = e.RescuePrime(2, 1, 128, N)
+    bnd_c4 = rp_o.boundary_constraints(rp_o.hash(inp))
+    default_small = st_g.prove(trace, air_g, bnd, sg.IndependentProofStream(), tr, rc)
+    default_c4 = st_c4.prove(trace_c4, air_c4, bnd_c4, sg.IndependentProofStream(), tr_c4, rc_c4)
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    assert st_g.prove(trace, air_g, bnd, sg.IndependentProofStream(), tr, rc) == want == default_small
+    assert st_c4.prove(trace_c4, air_c4, bnd_c4, sg.IndependentProofStream(), tr_c4, rc_c4) == default_c4
+
+
 def test_stark_prove_negated_constraints():
     """A negated native Rescue-Prime constraint (-tc, and the empty MPolynomial minus tc: the
     reference's Add returns the other operand) is evaluated as -tc, not through the factored form of

@@ -635,16 +635,13 @@ std::unique_ptr<sg_tree> new_tree(sg_ctx* ctx, uint64_t n, const fe* lean_leaves
   std::unique_ptr<sg_tree> t(new sg_tree());
   t->n = n;
   t->logn = ilog2_exact(n);
-  // SG_LEAN_TREES=0: every tree keeps its leaf digests (A/B knob, alternate path)
-  static const bool lean_on = [] {
-    const char* v = getenv("SG_LEAN_TREES");
-    return !(v && *v == '0');
-  }();
+  // SG_LEAN_TREES=0: every tree keeps all its levels (A/B knob, alternate path; read per tree, so
+  // a test can compare the layouts in one process)
+  const char* lv = getenv("SG_LEAN_TREES");
+  const bool lean_on = !(lv && *lv == '0');
   // SG_LEAN_DROP=k: at most k levels dropped (A/B knob; the default is what the caller asks)
-  static const int drop_cap = [] {
-    const char* v = getenv("SG_LEAN_DROP");
-    return v && *v ? atoi(v) : 64;
-  }();
+  const char* dv = getenv("SG_LEAN_DROP");
+  const int drop_cap = dv && *dv ? atoi(dv) : 64;
   drop = std::min(drop, drop_cap);
   t->drop = (lean_on && lean_leaves && n >= 2) ? std::min(std::max(drop, 0), t->logn) : 0;
   t->leaves = t->drop ? lean_leaves : nullptr;
