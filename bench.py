@@ -54,8 +54,8 @@ REGISTERS = 2       # Rescue-Prime m = 2
 HBM_PEAK_GBS = 8000.0
 # PMC HBM bytes of this workload's kernels (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes on
 # `bench.py --steps 3 --warmup 1 --no-side`, tools/pmc_passes.sh + tools/pmc_traffic.py)
-PMC_TRAFFIC_FILE = "r05_pmc_traffic_e2e_lean.json"
-PMC_VALU_FILE = "r05_pmc_valu_e2e_lean.json"  # SQ_INSTS_VALU pass (tools/pmc_passes.sh + tools/pmc_valu.py)
+PMC_TRAFFIC_FILE = "r05_pmc_traffic_e2e_final.json"
+PMC_VALU_FILE = "r05_pmc_valu_e2e_final.json"  # SQ_INSTS_VALU pass (tools/pmc_passes.sh + tools/pmc_valu.py)
 
 
 def synthetic_fe(seed: int, tag: bytes, n: int) -> np.ndarray:
