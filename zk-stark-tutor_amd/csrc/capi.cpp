@@ -666,7 +666,7 @@ uint64_t launch_trees(sg_ctx* ctx, const fe* const* d_leaves, int batch, sg_tree
   for (int b = 0; b < batch; ++b) {
     SG_REQUIRE(trees[b]->n == trees[0]->n, "trees of one launch must have equal sizes");
     SG_REQUIRE(trees[b]->drop == trees[0]->drop, "trees of one launch must be alike lean");
-    bufs[b] = tree_vptr(trees[b]);
+    bufs[b] = trees[b]->buf.as<uint64_t>();
     roots_dev[b] = ctx->pinned_roots_dev + 8 * (slot0 + b);
     flags_dev[b] = ctx->pinned_roots_dev + sg_ctx::kFlagIndex + slot0 + b;
   }
@@ -700,7 +700,7 @@ void fill_tree(sg_ctx* ctx, const fe* d_leaves, sg_tree* t, const FoldLeaves* fo
 
 // fill_tree in two halves, so work can be queued behind the tree before the host waits for its root
 uint64_t fill_tree_launch(sg_ctx* ctx, const fe* d_leaves, sg_tree* t, const FoldLeaves* fold) {
-  uint64_t* buf = tree_vptr(t);
+  uint64_t* buf = t->buf.as<uint64_t>();
   uint64_t* root_dev = ctx->pinned_roots_dev;
   uint64_t* flag_dev = ctx->pinned_roots_dev + sg_ctx::kFlagIndex;
   const uint64_t seq = ++ctx->root_seq;
@@ -730,7 +730,7 @@ void path_indices(const sg_tree* t, uint64_t index, std::vector<uint64_t>& idx) 
 uint64_t digest_addr(const sg_tree* t, uint64_t i) {
   SG_REQUIRE(t->drop <= 1, "gathers rehash the leaf level only");
   if (t->drop && i < t->n) return ((uint64_t)(uintptr_t)(t->leaves + i)) | 1;
-  return tree_vbase(t) + 64 * i;
+  return (uint64_t)(uintptr_t)t->buf.get() + 64 * (i - (2 * t->n - 2 * (t->n >> t->drop)));  // levels >= drop
 }
 
 void gather_digests(sg_ctx* ctx, const sg_tree* t, const std::vector<uint64_t>& idx, uint8_t* out) {
@@ -999,7 +999,7 @@ void TailWriter::leafs(const fe* a, const fe* b, const fe* c) {
 void TailWriter::path(const sg_tree* t, uint64_t index) {
   SG_REQUIRE(t->logn <= 64, "tree too deep");
   TailItem it{};
-  it.src[0] = tree_vbase(t);
+  it.src[0] = (uint64_t)(uintptr_t)t->buf.get();
   it.src[1] = (uint64_t)(uintptr_t)t->leaves;  // lean: the low siblings are rehashed from these
   it.src[2] = (uint64_t)t->drop;
   it.dst = bytes;
@@ -1144,10 +1144,10 @@ void fri_commit_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, co
       SG_REQUIRE(fe_eq(fe_pow(plan[r].omega, len - 1), plan[r].winv),
                  "error in commit: omega does not have the right order!");  // fri.rs:133
       const fe* lv = st.cw[r];
-      uint64_t* buf = tree_vptr(trees[r].get());
+      uint64_t* buf = trees[r]->buf.as<uint64_t>();
       SG_HIP(launch_merkle_tree(&lv, &buf, 1, len, nullptr, ctx->stream, 0, 0, 0, nullptr, 0, r ? &fold : nullptr,
                                 trees[r]->drop));
-      const uint64_t* rootp = buf + level_offset(len, trees[r]->logn) * 8;
+      const uint64_t* rootp = buf + tree_level_offset(trees[r].get(), trees[r]->logn) * 8;
       uint64_t* rout = droots.as<uint64_t>() + 8 * r;
       if (r == rounds - 1) {
         SG_HIP(hipMemcpyAsync(rout, rootp, 64, hipMemcpyDeviceToDevice, ctx->stream));

@@ -31,12 +31,11 @@ struct sg_tree {
 };
 
 namespace sg {
-// the address level-offset arithmetic starts from: the buffer, or for a lean tree the offset of
-// level `drop` before it (the levels below are never stored or read there)
-inline uint64_t tree_vbase(const sg_tree* t) {
-  return (uint64_t)(uintptr_t)t->buf.get() - 64 * (2 * t->n - 2 * (t->n >> t->drop));
+// digest offset of level `level` (>= t->drop) in the tree's buffer: a lean tree's buffer starts at
+// level `drop`
+inline uint64_t tree_level_offset(const sg_tree* t, int level) {
+  return (2 * t->n - 2 * (t->n >> level)) - (2 * t->n - 2 * (t->n >> t->drop));
 }
-inline uint64_t* tree_vptr(const sg_tree* t) { return reinterpret_cast<uint64_t*>((uintptr_t)tree_vbase(t)); }
 }  // namespace sg
 
 struct sg_fri_state {

@@ -1391,9 +1391,12 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
     if (level + fuse - 1 > logn) fuse = logn - level + 1;
     if (fuse < 1 || fuse > kMaxFuse) return hipErrorInvalidValue;
     a.fuse = fuse;
+    // digest offsets in the buffer: a lean tree's buffer starts at level `drop` (the dropped levels
+    // are never stored or read)
+    const uint64_t dropped = drop > 0 ? 2 * n - 2 * (n >> drop) : 0;
     for (int k = 0; k <= kMaxFuse; ++k) {
       int lv = level - 1 + k;
-      a.off[k] = (lv < 0 || lv > logn) ? 0 : (2 * n - 2 * (n >> lv));
+      a.off[k] = (lv < 0 || lv > logn || lv < drop) ? 0 : (2 * n - 2 * (n >> lv)) - dropped;
     }
     // algorithmic bytes (Merkle(n) = 16 n + 64 (2n - 1)): leaves read once (16 B) +
     // 64 B per digest of these levels -- a lean tree's leaf digests count although they are not

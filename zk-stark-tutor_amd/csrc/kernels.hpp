@@ -76,8 +76,8 @@ struct DevTranscript {
 hipError_t launch_fri_fs(DevTranscript* fs, const uint64_t* root, uint64_t* root_out, fe* k_out, const fe& C,
                          const fe& r2, hipStream_t s);
 // root_flag (optional, with root_host): set to root_seq after the root is visible to the host.
-// drop: a lean tree (n >= 2) -- the levels below `drop` are not stored (`tree` is the tree's
-// virtual base: levels >= drop at their usual offsets, the dropped ones before the allocation).
+// drop: a lean tree (n >= 2) -- the levels below `drop` are not stored: `tree` holds levels drop ..
+// log2 n, level l at digest offset (2n - 2(n >> l)) - (2n - 2(n >> drop)).
 hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, int batch, uint64_t n,
                               uint64_t* const* root_host, hipStream_t s, uint64_t leaves_ys = 0,
                               uint64_t tree_ys = 0, int start_level = 0, uint64_t* const* root_flag = nullptr,
@@ -101,8 +101,8 @@ hipError_t launch_gather_cols(fe* out, const fe* in, uint64_t len, uint64_t rows
 // Value / Leafs payloads as `count` big-endian u128 elements read from src[0..count) and a Path
 // payload as `count` = log2(n) entries [64 u64 BE][digest] of leaf `index` in the tree whose
 // digests start at src[0] (merkle_root.rs:34-53 order, proof_stream_enum.rs:95-126); for a lean
-// tree src[2] = K > 0 levels are not stored and its first K siblings are rehashed from the leaf
-// values at src[1].
+// tree src[2] = K > 0 levels are not stored (the digests at src[0] start at level K) and its first
+// K siblings are rehashed from the leaf values at src[1].
 struct TailItem {
   uint64_t src[3];
   uint64_t dst;

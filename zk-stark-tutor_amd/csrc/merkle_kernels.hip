@@ -606,7 +606,8 @@ __global__ __launch_bounds__(64) void k_serialize_tail(const TailItem* __restric
 #pragma unroll
       for (int k = 0; k < 8; ++k) h[k] = mt[off + sib][k];
     } else {
-      const uint64_t d = 2 * it.n - 2 * (it.n >> l) + ((it.index >> l) ^ 1);  // level l sibling
+      // level l sibling; a lean tree's buffer starts at level K
+      const uint64_t d = (2 * it.n - 2 * (it.n >> l)) - (2 * it.n - 2 * (it.n >> K)) + ((it.index >> l) ^ 1);
       ld_digest(reinterpret_cast<const uint64_t*>(it.src[0] + 64 * d), h);
     }
 #pragma unroll
