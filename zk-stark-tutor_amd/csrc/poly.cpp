@@ -348,6 +348,76 @@ DPoly fast_coset_divide_dev(sg_ctx* ctx, fe root, uint64_t root_order, const fe&
   return coset_divide_finish(ctx, pl, offset, vl.as<fe>(), vr.as<fe>());
 }
 
+constexpr int kNttBatch = 4;  // transforms per pointer-mode launch (the kernels' kMaxBatch)
+// batched only while the transforms are latency-bound (C4: 2^16-2^17 points, 0.09 ms per proof);
+// at the headline's 2^20-2^21 the per-column launches on the main stream leave the side stream's
+// trees more of the chip (batched: +0.1 ms per proof, profiles/r05_ab_bqbatch_*.log)
+constexpr uint64_t kNttBatchMaxOrder = (uint64_t)1 << 18;
+
+std::vector<DPoly> fast_coset_divide_batch_dev(sg_ctx* ctx, fe root, uint64_t root_order, const fe& offset,
+                                               const std::vector<DivItem>& items) {
+  check_root(root, root_order);
+  std::vector<DPoly> out(items.size());
+  std::vector<DivPlan> plans(items.size());
+  std::vector<size_t> batch;  // items taking the batched path (one coset size, equal dividend lengths)
+  for (size_t i = 0; i < items.size(); ++i) {
+    const DivItem& it = items[i];
+    plans[i] = coset_divide_plan(root, root_order, it.dl, it.dr);
+    const DivPlan& pl = plans[i];
+    const bool ok = !pl.zero_lhs && it.rhs_host && it.lr <= 64 && ctx->domain_cache_on() && pl.order <= kNttBatchMaxOrder &&
+                    it.ll > (uint64_t)kSmallPolyMax && it.ll <= pl.order && pl.order >= 2 &&
+                    (batch.empty() || (pl.order == plans[batch[0]].order && it.ll == items[batch[0]].ll));
+    if (ok) batch.push_back(i);
+  }
+  if (batch.size() < 2) batch.clear();
+  for (size_t i = 0; i < items.size(); ++i) {
+    if (std::find(batch.begin(), batch.end(), i) != batch.end()) continue;
+    const DivItem& it = items[i];
+    out[i] = fast_coset_divide_dev(ctx, root, root_order, offset, it.lhs, it.ll, it.rhs, it.lr, it.dr, it.rhs_host,
+                                   it.dl);
+  }
+  if (batch.empty()) return out;
+  // the reference's inner() on the coset (ref_inner_ntt: len <= order, so no padding beyond order),
+  // the product with 1 / the divisor's values, the inverse transform and the offset^-i scale
+  const DivPlan& pl = plans[batch[0]];
+  const uint64_t ll = items[batch[0]].ll;
+  const int logo = ilog2_exact(pl.order);
+  const fe *sA, *sB;
+  pow_tables2(ctx, offset, std::max<uint64_t>(ll, 1), &sA, &sB);
+  const fe ninv_m = to_mont(fe_inv(fe_from_u64(pl.order)));
+  for (size_t b0 = 0; b0 < batch.size(); b0 += kNttBatch) {
+    const int nb = (int)std::min<size_t>(kNttBatch, batch.size() - b0);
+    std::vector<DevBuf> vals, coefs;
+    fe* vo[kNttBatch] = {};
+    const fe* vi[kNttBatch] = {};
+    fe* co[kNttBatch] = {};
+    const fe* ci[kNttBatch] = {};
+    for (int k = 0; k < nb; ++k) {
+      vals.emplace_back(ctx, pl.order * sizeof(fe));
+      coefs.emplace_back(ctx, pl.order * sizeof(fe));
+      vo[k] = vals.back().as<fe>();
+      vi[k] = items[batch[b0 + k]].lhs;
+      co[k] = coefs.back().as<fe>();
+      ci[k] = vo[k];
+    }
+    ntt_run(ctx, vo, vi, nb, ll, logo, pl.root, sA, sB, 0, nullptr);
+    for (int k = 0; k < nb; ++k) {
+      const DivItem& it = items[batch[b0 + k]];
+      dev_mul(ctx, vo[k], vo[k], divisor_inverse_values(ctx, plans[batch[b0 + k]], offset, it.rhs, it.lr, it.rhs_host),
+              pl.order);  // a / b = a * b^-1 (field_element.rs:82-90)
+    }
+    ntt_run(ctx, co, ci, nb, pl.order, logo, fe_inv(pl.root), nullptr, nullptr, 0, &ninv_m);
+    for (int k = 0; k < nb; ++k) {
+      const DivPlan& p = plans[batch[b0 + k]];
+      const uint64_t keep = std::min(p.result_len, p.order);
+      DPoly q = dpoly_alloc(ctx, keep);
+      dev_scale_pow(ctx, q.p(), co[k], keep, fe_inv(offset));
+      out[batch[b0 + k]] = std::move(q);
+    }
+  }
+  return out;
+}
+
 // ------------------------------------------------------------------ geometric domains
 
 DPoly zerofier_geometric_dev(sg_ctx* ctx, const fe& q, uint64_t D, uint64_t n) {
@@ -543,13 +613,26 @@ std::vector<DPoly> interpolate_geometric_batch_dev(sg_ctx* ctx, const fe& q, uin
   pow_tables2(ctx, fe_inv(q), D, &iA, &iB);
   SG_HIP(launch_interp_assemble(S.as<fe>(), y, ys, Zv, va.as<fe>(), n, M, logf, cols, iA, iB, fe_r2(),
                                 ctx->stream));
-  // the coefficients land in each result's own buffer (D >= n slots, zero above M: degree < n <= M)
-  for (size_t c = 0; c < cols; ++c) {
-    DPoly out = dpoly_alloc(ctx, D);
-    intt_sized(ctx, qf, S.as<fe>() + c * M, logM, out.p());
-    if (M < D) SG_HIP(hipMemsetAsync(out.p() + M, 0, (D - M) * sizeof(fe), ctx->stream));
-    out.len = n;
-    outs.push_back(std::move(out));
+  // the coefficients land in each result's own buffer (D >= n slots, zero above M: degree < n <= M),
+  // up to kNttBatch columns' inverse transforms per launch
+  const fe ninv_m = to_mont(fe_inv(fe_from_u64(M)));
+  for (size_t c0 = 0; c0 < cols; c0 += kNttBatch) {
+    const int nb = (int)std::min<size_t>(kNttBatch, cols - c0);
+    fe* o[kNttBatch] = {};
+    const fe* in[kNttBatch] = {};
+    for (int k = 0; k < nb; ++k) {
+      DPoly out = dpoly_alloc(ctx, D);
+      if (M < D) SG_HIP(hipMemsetAsync(out.p() + M, 0, (D - M) * sizeof(fe), ctx->stream));
+      out.len = n;
+      o[k] = out.p();
+      in[k] = S.as<fe>() + (c0 + k) * M;
+      outs.push_back(std::move(out));
+    }
+    if (M < 2 || M > kNttBatchMaxOrder) {
+      for (int k = 0; k < nb; ++k) intt_sized(ctx, qf, in[k], logM, o[k]);
+    } else {
+      ntt_run(ctx, o, in, nb, M, logM, fe_inv(qf), nullptr, nullptr, 0, &ninv_m);
+    }
   }
   return outs;
 }

@@ -86,6 +86,21 @@ const fe* divisor_inverse_values(sg_ctx* ctx, const DivPlan& pl, const fe& offse
 DPoly fast_coset_divide_dev(sg_ctx* ctx, fe root, uint64_t root_order, const fe& offset, const fe* lhs, uint64_t ll,
                             const fe* rhs, uint64_t lr, int64_t rhs_degree = -2, const fe* rhs_host = nullptr,
                             int64_t lhs_degree = -2);
+// fast_coset_divide_dev for several quotients on one coset at once (the boundary quotients): items
+// whose plans share one coset size, with equal dividend lengths and small host-known divisors, run
+// their dividends' coset transforms and their inverse transforms as batched launches (up to
+// kMaxBatch per launch); any other item goes through fast_coset_divide_dev.  Same results.
+struct DivItem {
+  const fe* lhs;
+  uint64_t ll;
+  const fe* rhs;
+  uint64_t lr;
+  int64_t dr;           // divisor degree (>= 0)
+  const fe* rhs_host;   // its coefficients on the host
+  int64_t dl;           // dividend degree (-1: zero polynomial)
+};
+std::vector<DPoly> fast_coset_divide_batch_dev(sg_ctx* ctx, fe root, uint64_t root_order, const fe& offset,
+                                               const std::vector<DivItem>& items);
 // prod_{i<n} (x - q^i) for q of order D (ntt_arithmetics.rs:66-113 on the domain q^0..q^(n-1)), length n + 1;
 // n == D reproduces the reference's wrapped result (D zeros)
 DPoly zerofier_geometric_dev(sg_ctx* ctx, const fe& q, uint64_t D, uint64_t n);

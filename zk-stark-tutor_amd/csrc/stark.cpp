@@ -878,6 +878,8 @@ void prove_boundary_quotients(sg_ctx* ctx, const sg_stark& st, const std::vector
     std::vector<DevBuf> keep;  // divisor tables (and their shards) until the batches are enqueued
     const size_t b0 = bqs.size();
     bqs.resize(b0 + m);
+    std::vector<DivItem> rep_items;
+    std::vector<size_t> rep_slots;
     for (size_t s = 0; s < m; ++s) {
       const int64_t dz = hp_degree(bz[s]);
       // (the branch depends only on what every rank shares -- never on a per-rank environment)
@@ -895,8 +897,13 @@ void prove_boundary_quotients(sg_ctx* ctx, const sg_stark& st, const std::vector
           continue;
         }
       }
-      bqs[b0 + s] = fast_coset_divide_dev(ctx, st.omicron, D, g, diffs[s].p(), diffs[s].len, Zs[s].p(), Zs[s].len,
-                                          dz, bz[s].data(), dnum[s]);
+      rep_items.push_back(DivItem{diffs[s].p(), diffs[s].len, Zs[s].p(), Zs[s].len, dz, bz[s].data(), dnum[s]});
+      rep_slots.push_back(b0 + s);
+    }
+    // the replicated quotients' coset divisions, their transforms batched (one coset size)
+    {
+      std::vector<DPoly> q = fast_coset_divide_batch_dev(ctx, st.omicron, D, g, rep_items);
+      for (size_t k = 0; k < q.size(); ++k) bqs[rep_slots[k]] = std::move(q[k]);
     }
     for (size_t i0 = 0; i0 < sh.size();) {
       size_t i1 = i0 + 1;
