@@ -56,6 +56,8 @@ HBM_PEAK_GBS = 8000.0
 # `bench.py --steps 3 --warmup 1 --no-side`, tools/pmc_passes.sh + tools/pmc_traffic.py)
 PMC_TRAFFIC_FILE = "r05_pmc_traffic_e2e_final.json"
 PMC_VALU_FILE = "r05_pmc_valu_e2e_final.json"  # SQ_INSTS_VALU pass (tools/pmc_passes.sh + tools/pmc_valu.py)
+VALU_MIX_FILE = "r05_valu_mix_final.json"  # static full/half-rate mix of the same build (tools/valu_mix.py)
+MAX_CLOCK_GHZ = 2.4  # MI355X_MICROARCH.md:34
 
 
 def synthetic_fe(seed: int, tag: bytes, n: int) -> np.ndarray:
@@ -781,6 +783,72 @@ def standalone_launch(ctx, device, name: str, n: int):
             "frac": round(gbs / HBM_PEAK_GBS, 4)}
 
 
+def prove_valu_budget(breakdown, ms_per_step):
+    """Whole-prove VALU issue: every timed launch of one prove (the last warmup step) priced at its
+    kernel's SQ_INSTS_VALU per wave (PMC pass of this build) times the waves it ran, summed and set
+    against the prove's wall time -- the chip-wide counterpart of roofline.valu, for a job whose two
+    streams overlap kernels (a kernel's own live rate then says little about the chip).
+
+    waves: Merkle scopes record the lanes they launch; the NTT passes hold 8 elements per lane
+    (2048 / 4096 / 8192-element tiles on 256 / 512 / 1024 lanes), so lanes = elements / 8.
+    peak = 1 wave64 instruction / SIMD / 2 clk x 1024 SIMDs at the 2.4 GHz maximum clock (the clock the
+    chip holds under this load is lower, so the fractions are lower bounds); mix roof = each kernel's
+    full/half-rate mix (clk per instruction per SIMD, tools/valu_mix.py) summed over its instructions."""
+    vf = os.path.join(ROOT, "profiles", PMC_VALU_FILE)
+    mf = os.path.join(ROOT, "profiles", VALU_MIX_FILE)
+    if not (os.path.exists(vf) and os.path.exists(mf)):
+        return None
+    per_wave = json.load(open(vf))["kernels"]
+    mix = json.load(open(mf))["kernels"]
+    blake_clk = mix.get("merkle_nodes", {}).get("clk_per_wave_instr_per_simd")
+    instr = simd_clk = covered_ms = total_ms = 0.0
+    kinds = {}
+    for k, v in breakdown.items():
+        total_ms += v["ms"]
+        key = "ntt_pass" if k.startswith("ntt_pass") else k
+        if key not in per_wave:
+            continue
+        if key == "ntt_pass":
+            lanes = v["bytes"] / 32.0 / 8.0
+        elif key == "ntt_first":
+            lanes = v.get("elems", 0) / 8.0
+        else:
+            lanes = v.get("elems", 0)
+        if lanes <= 0:
+            continue
+        n = per_wave[key]["valu_instr_per_wave"] * lanes / 64.0
+        # the quad-lane tree kernels run the same BLAKE2b body as the node kernel
+        clk = mix.get(key, {}).get("clk_per_wave_instr_per_simd") or blake_clk
+        instr += n
+        simd_clk += n * clk
+        covered_ms += v["ms"]
+        kinds[k] = int(n)
+    if instr <= 0 or ms_per_step <= 0:
+        return None
+    t = ms_per_step * 1e-3
+    hz = MAX_CLOCK_GHZ * 1e9
+    peak = 1024 * hz / 2.0
+    rate = instr / t
+    # SIMD-clk the instructions need at their mix / SIMD-clk the prove's wall time holds
+    mix_frac = simd_clk / (1024 * hz * t)
+    # the clock the chip held in the PMC pass of the dominant (leaf) kernel, under the same load
+    load_ghz = per_wave.get("merkle_leaves", {}).get("clock_ghz")
+    return {"wave_instr_per_prove": int(instr), "per_kernel": kinds,
+            "mix_frac_at_load_clock": round(simd_clk / (1024 * load_ghz * 1e9 * t), 4) if load_ghz else None,
+            "load_clock_ghz": round(load_ghz, 3) if load_ghz else None,
+            "achieved": round(rate, -6), "peak": round(peak, -6), "frac": round(rate / peak, 4),
+            "mix_frac": round(mix_frac, 4), "clock_ghz": MAX_CLOCK_GHZ,
+            "mix_floor_ms": round(simd_clk / (1024 * hz) * 1e3, 3),
+            "covered_device_ms_frac": round(covered_ms / total_ms, 4) if total_ms > 0 else None,
+            "unit": "wave64 VALU instr/s",
+            "source": f"profiles/{PMC_VALU_FILE} (instructions per wave) x the waves of every launch of the last "
+                      f"warmup prove; profiles/{VALU_MIX_FILE} (full/half-rate mix); peak and mix_floor_ms at the "
+                      f"{MAX_CLOCK_GHZ} GHz maximum clock (MI355X_MICROARCH.md:34), so frac / mix_frac are lower bounds",
+            "definition": "the whole prove's VALU instructions (kernels covering covered_device_ms_frac of its device "
+                          "time) over its wall time; mix_frac = the SIMD cycles those instructions need at their "
+                          "measured full/half-rate costs / the SIMD cycles of the wall time"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -916,6 +984,7 @@ def main():
         "data": "synthetic: Rescue-Prime execution trace of a seeded input; randomizers from a seeded "
                 "SHAKE256 stream (SURVEY.md 8(d))",
         "ntt": ntt_stats,
+        "prove_valu": prove_valu_budget(breakdown, ms_per_step) if args.log_trace == LOG_TRACE else None,
         "config": {"workload": f"Stark::prove, Rescue-Prime m={REGISTERS} trace {wl.rows} rows "
                                f"(+{wl.stark.num_randomizers} randomizers = 2^{args.log_trace} - 1), "
                                f"expansion {EXPANSION}, c={COLINEARITY}, security 128, transition degree 3 "
