@@ -188,6 +188,57 @@ def test_stark_prove_constraints_shared_by_two_contexts():
     assert s1.prove(trace, air, bnd, sg.IndependentProofStream(), tr, rc) == want
 
 
+def test_stark_prove_contexts_in_concurrent_threads():
+    """One context per host thread (the C ABI's rule), several proofs in flight on one GPU: three
+    threads, each with its own context, prove C4-sized traces (trace 2^16, FRI domain 2^21) twice
+    at the same time; every proof equals the same trace's proof run alone, and the small case equals
+    the oracle's (tools/concurrent_provers.py times the headline this way)."""
+    import threading
+    rp, st_o, st_g, air_o, air_g, trace, bnd, tr, rc, out = _case(40, 4, 3, 4, 2, b"threads")
+    want_small = st_o.prove(trace, air_o, bnd, o.IndependentProofStream(), tr, rc)
+    N = 65278
+    rp_o = e.RescuePrime(2, 1, 128, N)
+    jobs = []
+    for i in range(3):
+        ctx = sg.Context(0)
+        st = sg.Stark(8, 64, 128, 2, N + 1, 3, ctx=ctx)
+        air = sg.RescuePrime(2, 1, 128, N, ctx=ctx).transition_constraints(st.omicron, st.omicron_domain_length)
+        inp = o.sample(b"threads-%d" % i)
+        r = e.randomness_from_seed(b"threads-%d" % i, 2 * st.num_randomizers + st.num_randomizer_coefficients(air))
+        args = (sg.RescuePrime(2, 1, 128, N, ctx=ctx).trace_array(inp), air,
+                rp_o.boundary_constraints(rp_o.hash(inp)))
+        tr_i, rc_i = sg.fe_array(r[:2 * st.num_randomizers]), sg.fe_array(r[2 * st.num_randomizers:])
+        alone = st.prove(*args, sg.IndependentProofStream(), tr_i, rc_i)
+        jobs.append((st, args, tr_i, rc_i, alone))
+    small_ctx = sg.Context(0)
+    st_small = sg.Stark(4, 3, 4, 2, 41, 2, ctx=small_ctx)
+    air_small = sg.RescuePrime(2, 1, 4, 40, ctx=small_ctx).transition_constraints(st_small.omicron,
+                                                                                   st_small.omicron_domain_length)
+    got, errs = {}, []
+    start = threading.Barrier(len(jobs) + 1)
+
+    def run(i):
+        try:
+            start.wait()
+            if i == len(jobs):
+                got[i] = [st_small.prove(trace, air_small, bnd, sg.IndependentProofStream(), tr, rc) for _ in range(4)]
+                return
+            st, args, tr_i, rc_i, _ = jobs[i]
+            got[i] = [st.prove(*args, sg.IndependentProofStream(), tr_i, rc_i) for _ in range(2)]
+        except Exception as ex:
+            errs.append(repr(ex))
+
+    th = [threading.Thread(target=run, args=(i,)) for i in range(len(jobs) + 1)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    for i, (_, _, _, _, alone) in enumerate(jobs):
+        assert all(p == alone for p in got[i]), i
+    assert all(p == want_small for p in got[len(jobs)])
+
+
 def test_stark_prove_rescue_factored_air_equals_expanded(monkeypatch):
     """The native Rescue-Prime AIR is evaluated in its factored form (rescue_prime.rs:246-283:
     sum MDS prev^alpha + first(x) - (sum MDSinv (next - second(x)))^alpha); SG_AIR_GENERIC=1
