@@ -1297,15 +1297,19 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
     int fuse;
     unsigned bs;
     int kind;  // 0: leaf 256, 1: leaf tail 1024, 2: node 256, 3: quad 64, 4: leaf 512, 5: quad 256, 6: node 512, 8: leaf pairs 512,
-              // 7: quad leaves 256, 9: pipelined nodes 256, 10: node pairs 256
+              // 7: quad leaves 256, 9: pipelined nodes 256, 10: node pairs 256, 11: nodes DPP 256, 12: quad leaves 64
     // SG_MERKLE_QUAD_LEAF_BELOW = log2 of the leaf count (all trees of the launch) under which the
     // leaf level takes a quad per leaf (k_merkle_quad_leaves); 0 disables it (A/B knob)
     static const int env_qleaf = env_int("SG_MERKLE_QUAD_LEAF_BELOW", 17);
     if (level == 0 && env_qleaf > 0 && count * (uint64_t)batch < ((uint64_t)1 << env_qleaf)) {
       // latency-bound leaf level: up to 256 leaves per 1024-lane block, every level fused up to
       // the block's single digest (the whole tree when it has <= 256 leaves)
-      kind = 7;
-      const uint64_t nodes = count < 256 ? count : 256;
+      // SG_MERKLE_QUAD_LEAF_NODES = leaves per block (256 or 64; A/B knob): a 256-leaf block puts
+      // 16 waves on one CU, whose first levels then run at that CU's issue rate
+      static const int env_qln = env_int("SG_MERKLE_QUAD_LEAF_NODES", 256);
+      const uint64_t qcap = env_qln == 64 ? 64 : 256;
+      kind = qcap == 64 ? 12 : 7;
+      const uint64_t nodes = count < qcap ? count : qcap;
       bs = (unsigned)(4 * nodes);
       int lg = 0;
       while (((uint64_t)1 << lg) < nodes) ++lg;
@@ -1378,7 +1382,9 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
       // the last <= 256 nodes of a tree go to the root in one 1024-lane block
       // (SG_MERKLE_QUAD_TOP=0: 64-node blocks only)
       static const int env_top = env_int("SG_MERKLE_QUAD_TOP", 1);
-      const uint64_t cap = (env_top && count <= 256) ? 256 : 64;
+      // SG_MERKLE_QUAD_TOP_MAX = the largest level that one block takes to the root (A/B knob)
+      static const uint64_t top_max = (uint64_t)env_int("SG_MERKLE_QUAD_TOP_MAX", 256);
+      const uint64_t cap = (env_top && count <= top_max && count <= 256) ? 256 : 64;
       kind = cap == 256 ? 5 : 3;
       uint64_t nodes = count < cap ? count : cap;
       bs = (unsigned)(4 * nodes);
@@ -1405,11 +1411,11 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
     for (int k = 0; k < fuse; ++k) digests += count >> k;
     // a fused fold reads 2 source elements and writes the folded one instead of reading the leaf
     // quad kernels: 4 lanes per node; leaf pairs: 2 leaves per lane
-    const uint64_t per_block = kind == 3 || kind == 5 || kind == 7 ? bs / 4 : kind == 8 || kind == 10 ? 2 * bs : bs;
+    const uint64_t per_block = kind == 3 || kind == 5 || kind == 7 || kind == 12 ? bs / 4 : kind == 8 || kind == 10 ? 2 * bs : bs;
     dim3 grid((unsigned)((count + per_block - 1) / per_block), batch);
     // elems = lanes launched (the rocprofv3 Grid_Size of this dispatch), so per-wave PMC
     // instruction counts scale to any launch population
-    ProfScope ps(kind == 7  ? "merkle_leaves_quad"
+    ProfScope ps(kind == 7 || kind == 12 ? "merkle_leaves_quad"
                  : level == 0 ? (fold_here ? "merkle_fold_leaves" : "merkle_leaves")
                             : (kind == 3 || kind == 5 ? "merkle_nodes_quad" : "merkle_nodes"),
                  batch * ((level == 0 ? (fold_here ? 48 : 16) * count : 0) + 64 * digests), s,

@@ -660,6 +660,10 @@ hipError_t launch_merkle_lanes(int kind, bool fold, dim3 grid, unsigned bs, hipS
       if (fold) hipLaunchKernelGGL((k_merkle_quad_leaves<256, true>), grid, dim3(bs), 0, s, a);
       else hipLaunchKernelGGL((k_merkle_quad_leaves<256, false>), grid, dim3(bs), 0, s, a);
       break;
+    case 12:
+      if (fold) hipLaunchKernelGGL((k_merkle_quad_leaves<64, true>), grid, dim3(bs), 0, s, a);
+      else hipLaunchKernelGGL((k_merkle_quad_leaves<64, false>), grid, dim3(bs), 0, s, a);
+      break;
     case 4:
       if (fold) hipLaunchKernelGGL((k_merkle_levels<true, 512, true>), grid, dim3(bs), 0, s, a);
       else hipLaunchKernelGGL((k_merkle_levels<true, 512>), grid, dim3(bs), 0, s, a);
