@@ -34,7 +34,9 @@ extern "C" {
 #define SG_ERR_HIP (-2)          /* HIP runtime error */
 #define SG_ERR_NONCANONICAL (-3) /* field element >= p */
 #define SG_ERR_CALLBACK (-4)     /* a proof-stream callback returned non-zero */
-#define SG_ERR_NOMEM (-5)
+#define SG_ERR_NOMEM (-5)        /* device (or host) memory exhausted; the context stays usable */
+/* A failed call leaves no HIP error behind on the calling thread (its hipGetLastError is cleared), so
+ * the caller's own HIP work (e.g. torch's) is unaffected; sg_last_error(ctx) holds the message. */
 
 typedef struct {
   uint64_t lo, hi;

@@ -181,6 +181,30 @@ def test_merkle_rejects_non_pow2():
         sg.MerkleRoot.commit([1, 2, 3])
 
 
+def test_merkle_tree_beyond_device_memory_is_nomem():
+    """A tree that cannot fit: 2^32 device-resident leaves (a 64 GiB codeword) whose digests would
+    take 512 GiB, above the GPU's 288 GB.  sg_merkle_build_dev returns SG_ERR_NOMEM (the ABI never
+    aborts), holds nothing afterwards, and the same context then builds a tree whose root and
+    path equal the oracle's (merkle_root.rs:21-32, 55-66)."""
+    import torch
+    ctx = sg.Context(0)
+    n = 1 << 32
+    big = torch.empty((n, 2), dtype=torch.int64, device=torch.device("cuda", 0))  # in bounds, never hashed
+    live = ctx.memory()["live"]
+    with pytest.raises(sg.StarkGpuError) as err:
+        sg.DeviceTree(big.data_ptr(), n, ctx=ctx)
+    from starkgpu._lib import SG_ERR_NOMEM
+    assert err.value.code == SG_ERR_NOMEM, err.value
+    assert ctx.memory()["live"] == live
+    del big
+    vals = rnd(7, 1 << 10, b"after-nomem")
+    small = torch.from_numpy(sg.fe_array(vals).view(np.int64)).to(torch.device("cuda", 0))
+    t = sg.DeviceTree(small.data_ptr(), len(vals), ctx=ctx)
+    assert t.root() == o.merkle_commit(vals)
+    assert t.open(333) == o.merkle_open(333, vals)
+    t.free()
+
+
 # ------------------------------------------------------------------ proof stream
 
 def test_stream_serialization_matches_oracle():

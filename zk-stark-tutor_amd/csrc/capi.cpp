@@ -40,10 +40,16 @@ void* sg_ctx::alloc(size_t bytes) {
   void* p = nullptr;
   hipError_t e = hipMalloc(&p, r);
   if (e != hipSuccess) {
+    // a failed hipMalloc also sets the thread's HIP last error: clear it, so the failure does not
+    // surface later in the caller's own HIP calls (torch checks hipGetLastError after its launches)
+    (void)hipGetLastError();
     // drop the cache and retry once
     trim();
     e = hipMalloc(&p, r);
-    if (e != hipSuccess) throw Error{SG_ERR_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e)};
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      throw Error{SG_ERR_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e)};
+    }
   }
   live_bytes += r;
   if (live_bytes > peak_live_bytes) peak_live_bytes = live_bytes;

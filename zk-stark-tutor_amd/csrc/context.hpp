@@ -24,8 +24,8 @@ struct Error {
 #define SG_HIP(call)                                                                              \
   do {                                                                                            \
     hipError_t _e = (call);                                                                       \
-    if (_e != hipSuccess)                                                                         \
-      throw ::sg::Error{-2, std::string(#call) + ": " + hipGetErrorString(_e)};                   \
+    if (_e != hipSuccess) /* out of device memory is SG_ERR_NOMEM, anything else SG_ERR_HIP */    \
+      throw ::sg::Error{_e == hipErrorOutOfMemory ? -5 : -2, std::string(#call) + ": " + hipGetErrorString(_e)}; \
   } while (0)
 #define SG_REQUIRE(cond, msg)                    \
   do {                                           \

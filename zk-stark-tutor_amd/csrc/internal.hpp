@@ -78,6 +78,9 @@ int guard(sg_ctx* ctx, F&& f) {
       // a failed call may leave divisions in flight: drain and clear the zero-divisor flag
       (void)hipStreamSynchronize(ctx->stream);
       if (ctx->div_zero_flag) *reinterpret_cast<volatile uint32_t*>(ctx->div_zero_flag) = 0;
+      // the error is reported through the return code and sg_last_error: clear the thread's HIP
+      // last error (a failed hipMalloc sets it), so it does not surface in the caller's own HIP calls
+      (void)hipGetLastError();
     } else {
       host_last_error() = e.msg;
     }
