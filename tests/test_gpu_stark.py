@@ -239,6 +239,60 @@ def test_stark_prove_contexts_in_concurrent_threads():
     assert all(p == want_small for p in got[len(jobs)])
 
 
+@pytest.fixture(scope="module")
+def c4_case():
+    """C4 inputs (trace 2^16, FRI domain 2^21, c = 64) and the working-set peak of one proof."""
+    N = 65278
+    rp_o = e.RescuePrime(2, 1, 128, N)
+    inp = o.sample(b"oom-c4")
+    ctx = sg.Context(0)
+    st = sg.Stark(8, 64, 128, 2, N + 1, 3, ctx=ctx)
+    rp = sg.RescuePrime(2, 1, 128, N, ctx=ctx)
+    air = rp.transition_constraints(st.omicron, st.omicron_domain_length)
+    r = e.randomness_from_seed(b"oom-c4", 2 * st.num_randomizers + st.num_randomizer_coefficients(air))
+    case = {"N": N, "trace": rp.trace_array(inp), "bnd": rp_o.boundary_constraints(rp_o.hash(inp)),
+            "tr": sg.fe_array(r[:2 * st.num_randomizers]), "rc": sg.fe_array(r[2 * st.num_randomizers:])}
+    ctx.memory(reset_peak=True)
+    case["proof"] = st.prove(case["trace"], air, case["bnd"], sg.IndependentProofStream(), case["tr"], case["rc"])
+    case["peak"] = ctx.memory()["peak"]
+    case["air"], case["ctx"] = air, ctx  # constraints built uncapped, proved on any context
+    return case
+
+
+@pytest.mark.parametrize("frac", [0.02, 0.15, 0.35, 0.55, 0.75, 0.95])
+def test_stark_prove_out_of_memory_at_every_stage(monkeypatch, c4_case, frac):
+    """A C4 prove whose buffer pool is capped below its working set (SG_POOL_LIMIT_BYTES, a test
+    knob read at context creation) fails with SG_ERR_NOMEM wherever the cap bites -- early in the
+    trace interpolation, amid the quotients and the side stream's trees, or in FRI -- hands every
+    pool buffer back (live bytes as before the call), and leaves the context usable: a proof that
+    fits under the cap then equals the oracle's, and the C4 proof equals the uncapped one once a
+    context without the cap proves it.  (The constraints are built on an uncapped context.)"""
+    from starkgpu._lib import SG_ERR_NOMEM
+    limit = int(frac * c4_case["peak"])
+    monkeypatch.setenv("SG_POOL_LIMIT_BYTES", str(limit))
+    ctx = sg.Context(0)
+    monkeypatch.delenv("SG_POOL_LIMIT_BYTES")
+    N = c4_case["N"]
+    st = sg.Stark(8, 64, 128, 2, N + 1, 3, ctx=ctx)
+    live = ctx.memory()["live"]
+    with pytest.raises(sg.StarkGpuError) as err:
+        st.prove(c4_case["trace"], c4_case["air"], c4_case["bnd"], sg.IndependentProofStream(), c4_case["tr"],
+                 c4_case["rc"])
+    assert err.value.code == SG_ERR_NOMEM, err.value
+    assert ctx.memory()["live"] == live
+    # a small proof under the same cap, on the same context
+    rp, st_o, st_g, air_o, air_g, trace, bnd, tr, rc, out = _case(40, 4, 3, 4, 2, b"after-oom")
+    want = st_o.prove(trace, air_o, bnd, o.IndependentProofStream(), tr, rc)
+    st_s = sg.Stark(4, 3, 4, 2, 41, 2, ctx=ctx)
+    ctx.memory(reset_peak=True)
+    assert st_s.prove(trace, air_g, bnd, sg.IndependentProofStream(), tr, rc) == want
+    assert ctx.memory()["peak"] <= limit
+    # the same C4 inputs on an uncapped context
+    st2 = sg.Stark(8, 64, 128, 2, N + 1, 3, ctx=sg.Context(0))
+    assert st2.prove(c4_case["trace"], c4_case["air"], c4_case["bnd"], sg.IndependentProofStream(), c4_case["tr"],
+                     c4_case["rc"]) == c4_case["proof"]
+
+
 def test_stark_prove_rescue_factored_air_equals_expanded(monkeypatch):
     """The native Rescue-Prime AIR is evaluated in its factored form (rescue_prime.rs:246-283:
     sum MDS prev^alpha + first(x) - (sum MDSinv (next - second(x)))^alpha); SG_AIR_GENERIC=1

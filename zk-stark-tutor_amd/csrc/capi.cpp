@@ -28,6 +28,9 @@ using namespace sg;
 
 void* sg_ctx::alloc(size_t bytes) {
   size_t r = pool_round(bytes);
+  // test knob: a working-set cap below the device's (SG_POOL_LIMIT_BYTES at context creation)
+  if (pool_limit && live_bytes + r > pool_limit)
+    throw Error{SG_ERR_NOMEM, "device buffer pool limit (SG_POOL_LIMIT_BYTES) reached"};
   auto it = free_bufs.find(r);
   if (it != free_bufs.end()) {
     void* p = it->second;
@@ -255,6 +258,7 @@ extern "C" int sg_ctx_create(int device, sg_ctx** out) {
   auto* ctx = new (std::nothrow) sg_ctx();
   if (!ctx) return SG_ERR_NOMEM;
   ctx->device = device;
+  if (const char* pl = getenv("SG_POOL_LIMIT_BYTES")) ctx->pool_limit = (size_t)strtoull(pl, nullptr, 0);
   // the main stream (the prove's critical path) at the highest priority, the side stream (its
   // Merkle trees, which otherwise hold every CU while a small main-stream kernel waits) at the
   // lowest: C4 prove 3.05-3.19 -> 2.98-3.03 ms, headline unchanged (profiles/r03_ab_stream_priority*.log).

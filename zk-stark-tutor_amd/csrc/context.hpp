@@ -79,6 +79,9 @@ struct sg_ctx {
   // bytes of pool buffers handed out and not yet returned (rounded sizes), and their high-water
   // mark since creation / sg_ctx_memory's reset: the working set of the calls (sg_ctx_memory)
   size_t live_bytes = 0, peak_live_bytes = 0;
+  // SG_POOL_LIMIT_BYTES (read at creation; 0 = none): alloc fails with SG_ERR_NOMEM past this many
+  // live bytes -- the tests drive every allocation point of a prove into the out-of-memory path
+  size_t pool_limit = 0;
   // power tables keyed by (root limbs, count)
   std::map<std::pair<std::pair<uint64_t, uint64_t>, uint64_t>, sg::PowTable> pow_tables;
   // host-coherent pinned slots for tree roots (written by the kernel that computes them)
