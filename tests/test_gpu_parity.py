@@ -181,6 +181,44 @@ def test_merkle_rejects_non_pow2():
         sg.MerkleRoot.commit([1, 2, 3])
 
 
+def test_entry_points_under_a_pool_cap(monkeypatch):
+    """Every hot-path entry point on a context whose buffer pool is capped at 256 KiB
+    (SG_POOL_LIMIT_BYTES, a test knob): inputs past the cap fail with SG_ERR_NOMEM -- ntt / intt /
+    fast_coset_evaluate at 2^16, a 2^14-leaf Merkle commit, FRI::prove on a 2^14 codeword -- each
+    leaves no pool buffer behind, and the same calls at sizes under the cap then equal the oracle's."""
+    from starkgpu._lib import SG_ERR_NOMEM
+    monkeypatch.setenv("SG_POOL_LIMIT_BYTES", str(256 << 10))
+    ctx = sg.Context(0)
+    monkeypatch.delenv("SG_POOL_LIMIT_BYTES")
+    big = rnd(11, 1 << 16, b"cap")
+    r16 = o.primitive_nth_root(1 << 16)
+    omega, cw = _fri_case(1 << 14, 8, 16, 1 << 14)
+    calls = [lambda: sg.ntt(r16, big, ctx=ctx), lambda: sg.intt(r16, big, ctx=ctx),
+             lambda: sg.fast_coset_evaluate(r16, 1 << 16, o.GENERATOR, big[:1 << 12], ctx=ctx),
+             lambda: sg.MerkleRoot.commit(big[:1 << 14], ctx=ctx),
+             lambda: sg.FRI(o.GENERATOR, omega, 1 << 14, 8, 16, ctx=ctx).prove(cw, sg.IndependentProofStream())]
+    for call in calls:
+        live = ctx.memory()["live"]
+        with pytest.raises(sg.StarkGpuError) as err:
+            call()
+        assert err.value.code == SG_ERR_NOMEM, err.value
+        assert ctx.memory()["live"] == live
+    small = big[:256]
+    r8 = o.primitive_nth_root(256)
+    assert sg.to_ints(sg.ntt(r8, small, ctx=ctx)) == o.ntt(r8, small)
+    assert sg.to_ints(sg.intt(r8, small, ctx=ctx)) == o.intt(r8, small)
+    w10 = o.primitive_nth_root(1 << 10)
+    assert sg.to_ints(sg.fast_coset_evaluate(w10, 1 << 10, o.GENERATOR, small[:100], ctx=ctx)) == \
+        o.fast_coset_evaluate(w10, 1 << 10, o.GENERATOR, small[:100])
+    assert sg.MerkleRoot.commit(small, ctx=ctx) == o.merkle_commit(small)
+    omega, cw = _fri_case(1024, 8, 2, 1024)
+    ops = o.IndependentProofStream()
+    otop = o.FRI(o.GENERATOR, omega, 1024, 8, 2).prove(cw, ops)
+    gps = sg.IndependentProofStream()
+    assert sg.FRI(o.GENERATOR, omega, 1024, 8, 2, ctx=ctx).prove(cw, gps) == otop
+    assert gps.digest() == ops.digest()
+
+
 def test_merkle_tree_beyond_device_memory_is_nomem():
     """A tree that cannot fit: 2^32 device-resident leaves (a 64 GiB codeword) whose digests would
     take 512 GiB, above the GPU's 288 GB.  sg_merkle_build_dev returns SG_ERR_NOMEM (the ABI never
