@@ -182,12 +182,13 @@ def test_merkle_rejects_non_pow2():
 
 
 def test_entry_points_under_a_pool_cap(monkeypatch):
-    """Every hot-path entry point on a context whose buffer pool is capped at 256 KiB
+    """Every hot-path entry point on a context whose buffer pool is capped at 512 KiB
     (SG_POOL_LIMIT_BYTES, a test knob): inputs past the cap fail with SG_ERR_NOMEM -- ntt / intt /
     fast_coset_evaluate at 2^16, a 2^14-leaf Merkle commit, FRI::prove on a 2^14 codeword -- each
-    leaves no pool buffer behind, and the same calls at sizes under the cap then equal the oracle's."""
+    leaves no pool buffer behind, and the same calls at sizes under the cap (with any tree layout,
+    SG_LEAN_TREES=0 included) then equal the oracle's."""
     from starkgpu._lib import SG_ERR_NOMEM
-    monkeypatch.setenv("SG_POOL_LIMIT_BYTES", str(256 << 10))
+    monkeypatch.setenv("SG_POOL_LIMIT_BYTES", str(512 << 10))
     ctx = sg.Context(0)
     monkeypatch.delenv("SG_POOL_LIMIT_BYTES")
     big = rnd(11, 1 << 16, b"cap")
@@ -211,11 +212,11 @@ def test_entry_points_under_a_pool_cap(monkeypatch):
     assert sg.to_ints(sg.fast_coset_evaluate(w10, 1 << 10, o.GENERATOR, small[:100], ctx=ctx)) == \
         o.fast_coset_evaluate(w10, 1 << 10, o.GENERATOR, small[:100])
     assert sg.MerkleRoot.commit(small, ctx=ctx) == o.merkle_commit(small)
-    omega, cw = _fri_case(1024, 8, 2, 1024)
+    omega, cw = _fri_case(256, 4, 2, 256)
     ops = o.IndependentProofStream()
-    otop = o.FRI(o.GENERATOR, omega, 1024, 8, 2).prove(cw, ops)
+    otop = o.FRI(o.GENERATOR, omega, 256, 4, 2).prove(cw, ops)
     gps = sg.IndependentProofStream()
-    assert sg.FRI(o.GENERATOR, omega, 1024, 8, 2, ctx=ctx).prove(cw, gps) == otop
+    assert sg.FRI(o.GENERATOR, omega, 256, 4, 2, ctx=ctx).prove(cw, gps) == otop
     assert gps.digest() == ops.digest()
 
 
