@@ -570,6 +570,66 @@ def test_dist_stark_prove_one_gpu_host_transport(stark_reference, world, cases, 
     mp.spawn(_stark_worker, args=(world, port, stark_reference, cases, shard), nprocs=world, join=True)
 
 
+def _bounded_cache_worker(rank, world, port, tmp, nfill):
+    """Rank body of test_dist_prove_with_bounded_cache_full: see there."""
+    import torch.distributed as dist
+    import starkgpu as sg
+    from starkgpu import dist as D
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        N, exp, c, sec, tcd = STARK_CASES[2]
+        trace = np.load(os.path.join(tmp, "trace2.npy"))
+        tr, rc = np.load(os.path.join(tmp, "tr2.npy")), np.load(os.path.join(tmp, "rc2.npy"))
+        rows = sg.to_ints(trace)
+
+        def bnd(cyc):  # register 0 pinned at cycle 0 (one zerofier for every statement), register 1 at `cyc`
+            return [(0, 0, rows[0]), (cyc, 1, rows[2 * cyc + 1])]
+
+        # expected bytes of the last statement: the single-GPU prove on a context of its own
+        ref_ctx = sg.Context(0)
+        st_r = sg.Stark(exp, c, sec, 2, N + 1, tcd, ctx=ref_ctx)
+        air_r = sg.RescuePrime(2, 1, sec, N, ctx=ref_ctx).transition_constraints(st_r.omicron, st_r.omicron_domain_length)
+        last = nfill + 2
+        want = st_r.prove(trace, air_r, bnd(last), sg.IndependentProofStream(), tr, rc)
+        want_first = st_r.prove(trace, air_r, bnd(1), sg.IndependentProofStream(), tr, rc)
+        nd = D.NativeDist(sg.Context(0), transport="host")
+        nd.set_fri_tail(0)
+        st = sg.Stark(exp, c, sec, 2, N + 1, tcd, ctx=nd.ctx)
+        air = sg.RescuePrime(2, 1, sec, N, ctx=nd.ctx).transition_constraints(st.omicron, st.omicron_domain_length)
+        before = nd.counters()
+        ok_first = st.prove(trace, air, bnd(1), sg.IndependentProofStream(), tr, rc, dist=nd) == want_first
+        sharded = nd.counters()[1] - before[1]
+        for cyc in range(2, last):  # two new bounded tables per statement (register 1's inverse + shard)
+            st.prove(trace, air, bnd(cyc), sg.IndependentProofStream(), tr, rc, dist=nd)
+        ok_last = st.prove(trace, air, bnd(last), sg.IndependentProofStream(), tr, rc, dist=nd) == want
+        tables = nd.ctx.cached_tables()[0]
+        flags = [None] * world
+        dist.all_gather_object(flags, (ok_first, ok_last, sharded, tables))
+        assert all(f[0] and f[1] for f in flags), f"proof bytes differ with the bounded cache full: {flags}"
+        assert all(f[2] >= 2 for f in flags), f"the boundary quotients did not run sharded: {flags}"
+        nd.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(600)
+def test_dist_prove_with_bounded_cache_full(stark_reference):
+    """the sharded boundary quotients hold every register's divisor-inverse
+    shard (a bounded, content-keyed table) until their batch is enqueued, while later registers
+    insert new tables.  Register 0's zerofier (cycle 0) is the same in every statement, so its
+    tables sit at the front of the FIFO once the cache is full; the last statement then hits them
+    and inserts register 1's, which would evict (hipFree) the shard still to be read.  The cache is
+    pinned for the call (sg::BoundedPin): world 2 on this box's GPU (host transport), the statement
+    proved after 32 distinct ones writes the single-GPU prove's bytes, as does the first."""
+    import torch.multiprocessing as mp
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.spawn(_bounded_cache_worker, args=(2, port, stark_reference, 31), nprocs=2, join=True)
+
+
 # ----------------------------------------------------------------- failure containment
 
 class _FailingStream(o.IndependentProofStream):

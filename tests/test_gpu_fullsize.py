@@ -14,6 +14,11 @@ tests/test_oracle_fast.py) and against the oracle's own verifiers:
   structure) accepts the proof and rejects a false claim;
 * C5: the 2^27-point NTT sharded over 2 and 8 ranks (one process per rank on this box's one GPU,
   gloo host-staged exchange) bit-identical to the single-GPU transform and to the checker.
+
+C2 and C3 are also pinned to the Python oracle itself (VERDICT r05 "Next round" 2): the GPU's
+outputs hash to the SHA-256 digests tests/golden/make_fullsize.py computed with
+oracle/stark_oracle.py (ntt / intt / fast_coset_evaluate / FRI.prove at these exact inputs, 24 min of
+Python), stored in tests/golden/fullsize_digests.json.
 """
 import hashlib
 import os
@@ -25,12 +30,20 @@ import time
 import numpy as np
 import pytest
 
+import json
+
 import stark_oracle as o
 import stark_prove_oracle as e
 import starkgpu as sg
 
 pytestmark = pytest.mark.gpu
 P = o.P
+ORACLE = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "fullsize_digests.json")))
+
+
+def elem_digest(a: np.ndarray) -> str:
+    """SHA-256 of an (n, 2) u64 element array as 16 LE bytes per element (make_fullsize.py's encoding)."""
+    return hashlib.sha256(np.ascontiguousarray(a, dtype="<u8").tobytes()).hexdigest()
 
 
 @pytest.fixture(scope="module")
@@ -65,7 +78,9 @@ def test_c2_dense_2p22_ntt_intt_elementwise(fc):
     n = 1 << 22
     root = o.primitive_nth_root(n)
     x = synthetic(0, b"c2", n)
+    assert elem_digest(x) == ORACLE["c2"]["input"]["sha256"]
     X = sg.ntt(root, x)
+    assert elem_digest(X) == ORACLE["c2"]["ntt"]["sha256"], "ntt 2^22 != the Python oracle's (digest)"
     assert np.array_equal(X, fc.ntt(root, x)), "ntt 2^22 != checker"
     Y = sg.intt(root, X)
     assert np.array_equal(Y, fc.intt(root, X)), "intt 2^22 != checker"
@@ -77,7 +92,9 @@ def test_c2_dense_2p22_ntt_intt_elementwise(fc):
     imp[n - 1, 0] = 1
     assert np.array_equal(sg.ntt(root, imp), fc.ntt(root, imp))
     ragged = x[: n - 5]
-    assert np.array_equal(sg.ntt(root, ragged), fc.ntt(root, ragged))
+    R = sg.ntt(root, ragged)
+    assert elem_digest(R) == ORACLE["c2"]["ragged_ntt_n_minus_5"]["sha256"], "ragged ntt != oracle digest"
+    assert np.array_equal(R, fc.ntt(root, ragged))
 
 
 @pytest.mark.parametrize("logn", [16, 17, 18, 19, 20, 21, 23])
@@ -106,12 +123,19 @@ def test_c3_fri_prove_2p24_exp8_c64(fc):
     d = N // exp
     w = o.primitive_nth_root(N)
     coeffs = synthetic(0, b"c3", d)
+    assert elem_digest(coeffs) == ORACLE["c3"]["coeffs"]["sha256"]
     cw = sg.fast_coset_evaluate(w, N, o.GENERATOR, coeffs)
+    assert elem_digest(cw) == ORACLE["c3"]["lde"]["sha256"], "LDE 2^21 -> 2^24 != the Python oracle's (digest)"
     assert np.array_equal(cw, fc.fast_coset_evaluate(w, N, o.GENERATOR, coeffs)), "LDE 2^21 -> 2^24 != checker"
     gps = sg.IndependentProofStream()
     top = sg.FRI(o.GENERATOR, w, N, exp, c).prove(cw, gps)
+    proof = gps.digest()
+    assert len(proof) == ORACLE["c3"]["proof_len"] and hashlib.sha256(proof).hexdigest() == ORACLE["c3"]["proof_sha256"], \
+        "FRI::prove bytes != the Python oracle's (digest)"
+    assert list(top) == ORACLE["c3"]["top_indices"]
     ref, ref_top = fc.fri_prove(o.GENERATOR, w, cw, exp, c)
     objs = gps.objects()
+    assert [ob[1].hex() for ob in objs if ob[0] == o.ROOT] == ORACLE["c3"]["roots"]
     assert objs[0] == (o.ROOT, fc.merkle_commit(cw)), "round-0 root != checker"
     assert top == ref_top
     assert gps.digest() == ref, "FRI::prove proof bytes != checker"

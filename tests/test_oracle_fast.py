@@ -5,6 +5,7 @@ FRI proofs, trace-2^20 verification)."""
 import os
 import subprocess
 
+import numpy as np
 import pytest
 
 import stark_oracle as o
@@ -250,3 +251,48 @@ def test_fast_stark_prove_midsize_equals_oracle_digest(fc):
     got = fc.stark_prove_rescue(rp, st, trace, bnd, tr, rc)
     assert len(got) == g["proof_len"]
     assert hashlib.sha256(got).hexdigest() == g["proof_sha256"]
+
+
+def test_fast_cpu_fullsize_equals_python_oracle_digests(fc):
+    """The CPU checker at BASELINE's full sizes against the Python oracle itself: C2 (2^22 NTT and a
+    ragged input, fft/ntt.rs:7-68) and C3 (LDE 2^21 -> 2^24 + FRI::prove, fri.rs:210-248) hash to the
+    digests tests/golden/make_fullsize.py computed with oracle/stark_oracle.py (~16 s here)."""
+    import hashlib
+    import json
+    import os
+    G = json.load(open(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "fullsize_digests.json")))
+
+    def d(a):
+        return hashlib.sha256(np.ascontiguousarray(a, dtype="<u8").tobytes()).hexdigest()
+
+    n = 1 << 22
+    root = o.primitive_nth_root(n)
+    x = _synth_np(b"c2", n)
+    assert d(x) == G["c2"]["input"]["sha256"]
+    assert d(fc.ntt(root, x)) == G["c2"]["ntt"]["sha256"]
+    assert d(fc.ntt(root, x[: n - 5])) == G["c2"]["ragged_ntt_n_minus_5"]["sha256"]
+    N = 1 << 24
+    w = o.primitive_nth_root(N)
+    coeffs = _synth_np(b"c3", N // 8)
+    assert d(coeffs) == G["c3"]["coeffs"]["sha256"]
+    cw = fc.fast_coset_evaluate(w, N, o.GENERATOR, coeffs)
+    assert d(cw) == G["c3"]["lde"]["sha256"]
+    proof, top = fc.fri_prove(o.GENERATOR, w, cw, 8, 64)
+    assert len(proof) == G["c3"]["proof_len"] and hashlib.sha256(proof).hexdigest() == G["c3"]["proof_sha256"]
+    assert list(top) == G["c3"]["top_indices"]
+
+
+def _synth_np(tag: bytes, n: int) -> np.ndarray:
+    """o.synthetic_elements(0, tag, n) as an (n, 2) u64 array, vectorized (one conditional subtraction
+    of p: a 128-bit value is < 2p)."""
+    import hashlib
+    P = o.P
+    raw = hashlib.shake_256(b"sg-bench" + (0).to_bytes(8, "big") + tag).digest(16 * n)
+    be = np.frombuffer(raw, dtype=">u8").reshape(n, 2)
+    hi, lo = be[:, 0].astype(np.uint64), be[:, 1].astype(np.uint64)
+    p_hi, p_lo = np.uint64(P >> 64), np.uint64(P & (2**64 - 1))
+    ge = (hi > p_hi) | ((hi == p_hi) & (lo >= p_lo))
+    borrow = (lo < p_lo) & ge
+    lo = np.where(ge, lo - p_lo, lo)
+    hi = np.where(ge, hi - p_hi - borrow.astype(np.uint64), hi)
+    return np.ascontiguousarray(np.stack([lo, hi], axis=1))

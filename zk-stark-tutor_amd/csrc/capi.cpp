@@ -157,15 +157,21 @@ bool sg_ctx::domain_cache_on() const {
 void sg_ctx::domain_table_put_bounded(const std::vector<uint64_t>& key, void* p) {
   domain_table_put(key, p);
   bounded_keys.push_back(key);
+  if (bounded_pins == 0) bounded_evict();
+}
+
+void sg_ctx::bounded_evict() {
   if (bounded_keys.size() <= kBoundedTables) return;
-  host_wait(this, stream);  // queued work may still read the oldest table
+  host_wait(this, stream);  // queued work may still read the oldest tables
   host_wait(this, side);
-  auto it = domain_tables.find(bounded_keys.front());
-  if (it != domain_tables.end()) {
-    (void)hipFree(it->second);
-    domain_tables.erase(it);
+  while (bounded_keys.size() > kBoundedTables) {
+    auto it = domain_tables.find(bounded_keys.front());
+    if (it != domain_tables.end()) {
+      (void)hipFree(it->second);
+      domain_tables.erase(it);
+    }
+    bounded_keys.erase(bounded_keys.begin());
   }
-  bounded_keys.erase(bounded_keys.begin());
 }
 
 void* sg_ctx::domain_table(const std::vector<uint64_t>& key) const {
@@ -652,7 +658,9 @@ std::unique_ptr<sg_tree> new_tree(sg_ctx* ctx, uint64_t n, const fe* lean_leaves
   // SG_LEAN_DROP=k: at most k levels dropped (A/B knob; the default is what the caller asks)
   const char* dv = getenv("SG_LEAN_DROP");
   const int drop_cap = dv && *dv ? atoi(dv) : 64;
-  drop = std::min(drop, drop_cap);
+  // at most 3: an opening rehashes the 2^drop-leaf block around its leaf, and k_serialize_tail's
+  // LDS rehash buffers (msg[8][16], mt[16][8]) hold 8-leaf blocks
+  drop = std::min(std::min(drop, drop_cap), 3);
   t->drop = (lean_on && lean_leaves && n >= 2) ? std::min(std::max(drop, 0), t->logn) : 0;
   t->leaves = t->drop ? lean_leaves : nullptr;
   t->buf = DevBuf(ctx, (2 * (n >> t->drop) - 1) * 64);  // levels drop .. log2 n

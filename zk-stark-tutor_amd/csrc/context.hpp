@@ -123,6 +123,11 @@ struct sg_ctx {
   static constexpr size_t kBoundedTables = 64;
   std::vector<std::vector<uint64_t>> bounded_keys;  // insertion order
   void domain_table_put_bounded(const std::vector<uint64_t>& key, void* p);
+  // while > 0 (sg::BoundedPin), bounded tables are not evicted: a caller that holds pointers to
+  // several of them across further inserts (the sharded boundary quotients keep every divisor
+  // shard until their batch is enqueued) pins the cache; the last unpin evicts down to the bound
+  int bounded_pins = 0;
+  void bounded_evict();
   // pinned host staging buffers (grown on demand): slot 0 uploads gather addresses,
   // slot 1 receives gathered openings -- pageable copies of MBs cost ~10x more
   void* staging_ptr[2] = {nullptr, nullptr};
@@ -131,6 +136,25 @@ struct sg_ctx {
 };
 
 namespace sg {
+// RAII pin of the context's bounded table cache (sg_ctx::bounded_pins)
+class BoundedPin {
+ public:
+  explicit BoundedPin(sg_ctx* c) : c_(c) { ++c_->bounded_pins; }
+  ~BoundedPin() {
+    if (--c_->bounded_pins == 0) {
+      try {
+        c_->bounded_evict();
+      } catch (...) {  // a failed wait leaves the surplus for the next insert
+      }
+    }
+  }
+  BoundedPin(const BoundedPin&) = delete;
+  BoundedPin& operator=(const BoundedPin&) = delete;
+
+ private:
+  sg_ctx* c_;
+};
+
 inline size_t pool_round(size_t bytes) {
   size_t r = 256;
   while (r < bytes) r <<= 1;

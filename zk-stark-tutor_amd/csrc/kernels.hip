@@ -22,12 +22,38 @@
 #include <cstdint>
 #include <cstdlib>
 #include "fe128.hpp"
+#include "fe128_asm.inc"
 #include "dev_util.hpp"
 #include "blake2b.hpp"
 #include "leaf_decimal.hpp"
 #include "kernels.hpp"
 #include "profiler.hpp"
 #include "merkle_dev.hpp"
+
+// SG_NTT_ASM (default 1): the NTT kernels' field products and butterflies are the generated inline
+// asm of fe128_asm.inc, whose carry chains are interleaved so that no carry read waits on its writer
+// (tools/gen_fe_asm.py); 0: the C++ forms of fe128.hpp, same results.  The asm's fixed VGPR window
+// pushes k_ntt_pass_rr<11> past 128 VGPRs unless the launch bound asks for 4 waves per SIMD (no
+// spill at 128), so that bound is the default with it.
+#ifndef SG_NTT_ASM
+#define SG_NTT_ASM 0
+#endif
+#ifndef SG_NTT_WPE
+#define SG_NTT_WPE (SG_NTT_ASM ? 4 : 1)
+#endif
+namespace sg {
+// a * b * 2^-128 mod p, canonical, for a < 2^128 and b < p (fe128.hpp mont_mul)
+#ifndef SG_NTT_ASM_MUL
+#define SG_NTT_ASM_MUL SG_NTT_ASM
+#endif
+__device__ __forceinline__ fe ntt_mul(const fe& a, const fe& b) {
+#if SG_NTT_ASM_MUL && defined(__HIP_DEVICE_COMPILE__)
+  return mont_mul_asm(a, b);
+#else
+  return mont_mul(a, b);
+#endif
+}
+}  // namespace sg
 
 namespace sg {
 
@@ -153,10 +179,10 @@ template <class Args>
 __device__ __forceinline__ void ep_store(const Args& a, uint64_t r, uint64_t k, const fe& v) {
   const uint64_t rl = r & ((1ull << a.ep_vlog) - 1), vv = r >> a.ep_vlog;
   const uint64_t e = (a.ep_j0 + rl) * k;  // < 2^36 (host-checked)
-  const fe w = mont_mul(mont_mul(ld_fe(a.ep_T0 + (e & 4095)), ld_fe(a.ep_T1 + ((e >> 12) & 4095))),
+  const fe w = ntt_mul(ntt_mul(ld_fe(a.ep_T0 + (e & 4095)), ld_fe(a.ep_T1 + ((e >> 12) & 4095))),
                         ld_fe(a.ep_T2 + (e >> 24)));
   const uint64_t R = (uint64_t)1 << a.ep_logR;
-  st_fe(a.ep_out + (((k >> a.ep_logR) * a.ep_rows + rl) * a.ep_k + vv) * R + (k & (R - 1)), mont_mul(v, w));
+  st_fe(a.ep_out + (((k >> a.ep_logR) * a.ep_rows + rl) * a.ep_k + vv) * R + (k & (R - 1)), ntt_mul(v, w));
 }
 
 // store of a transform's element k (row pointer `row`) at the end of a pass
@@ -166,7 +192,7 @@ __device__ __forceinline__ void pass_store(const PassArgs& a, fe* row, uint64_t 
     ep_store(a, a.ep_row0 + blockIdx.y, k, v);
     return;
   }
-  if (post) v = mont_mul(v, pc);
+  if (post) v = ntt_mul(v, pc);
   else if (last) v = fe_canon(v);
   st_fe_stream(row + k, v, a.logn >= kStreamLogN);
 }
@@ -180,6 +206,29 @@ __device__ __forceinline__ fe twiddle_comp(const PassArgs& a, int S, uint64_t k)
   const fe* tA = a.tw + (((uint64_t)1 << a.s_cut) - 1);
   const uint64_t e = k << (a.logn - S);
   return mont_mul(ld_fe(tA + (e & 4095)), ld_fe(tA + 4096 + (e >> 12)));
+}
+
+// One radix-2 butterfly of the reference's DIT graph (fft/ntt.rs:26-46): o = x * w (Montgomery,
+// w a Montgomery twiddle), e <- e + o, x <- e - o, lazily reduced (fe128.hpp).
+__device__ __forceinline__ void butterfly(fe& e, fe& x, const fe& w) {
+#if SG_NTT_ASM && defined(__HIP_DEVICE_COMPILE__)
+  bfly_asm(e, x, w);
+#else
+  fe o = mont_mul(x, w);
+  fe ev = e;
+  e = fe_add_lazy(ev, o);
+  x = fe_sub_lazy(ev, o);
+#endif
+}
+// twiddle 1: o = x (canonical), e <- e + x, x <- e - x
+__device__ __forceinline__ void butterfly_unit(fe& e, fe& x) {
+#if SG_NTT_ASM && defined(__HIP_DEVICE_COMPILE__)
+  addsub_asm(e, x);
+#else
+  fe ev = e;
+  e = fe_add_lazy(ev, x);
+  x = fe_sub_lazy(ev, x);
+#endif
 }
 
 // R radix-2 stages (tile-local stages t+1 .. t+R) on the 2^R elements of one group held
@@ -226,10 +275,7 @@ __device__ __forceinline__ void radix_regs_impl(fe* x, const PassArgs& a, int t,
       uint64_t gmod = (uint64_t)g_low + ((uint64_t)(m & ((1 << u) - 1)) << t);
       uint64_t k = (gmod << a.b0) + low;
       fe w = COMP ? twiddle_comp(a, S, k) : twiddle_tab(a, S, k);
-      fe o = mont_mul(x[m + (1 << u)], w);
-      fe ev = x[m];
-      x[m] = fe_add_lazy(ev, o);  // tile values stay in [0, 2^128) until the last store
-      x[m + (1 << u)] = fe_sub_lazy(ev, o);
+      butterfly(x[m], x[m + (1 << u)], w);  // tile values stay in [0, 2^128) until the last store
     }
 #endif
   }
@@ -246,12 +292,12 @@ __device__ __forceinline__ void radix8_first(fe* x, const PassArgs& a) {
     for (int m = 0; m < 8; ++m) {
       if (m & (1 << u)) continue;
       const int k = m & ((1 << u) - 1);
-      fe o;
-      if (k == 0) o = u == 0 ? x[m + (1 << u)] : fe_canon(x[m + (1 << u)]);
-      else o = mont_mul(x[m + (1 << u)], twiddle_tab(a, u + 1, (uint64_t)k));
-      fe ev = x[m];
-      x[m] = fe_add_lazy(ev, o);
-      x[m + (1 << u)] = fe_sub_lazy(ev, o);
+      if (k == 0) {
+        if (u != 0) x[m + (1 << u)] = fe_canon(x[m + (1 << u)]);
+        butterfly_unit(x[m], x[m + (1 << u)]);
+      } else {
+        butterfly(x[m], x[m + (1 << u)], twiddle_tab(a, u + 1, (uint64_t)k));
+      }
     }
   }
 }
@@ -290,11 +336,8 @@ __device__ __forceinline__ void radix_step(fe_lds* lds, const PassArgs& a, int t
 // register steps, store.  TL > 0: the tile is exactly 2^TL elements handled
 // by 256 threads, so the loads/stores are unrolled (all 2^TL/256 global loads
 // of a thread in flight at once); TL == 0: generic loop for small transforms.
-#ifndef SG_NTT_WPE
-#define SG_NTT_WPE 1
-#endif
 template <int TL>
-__global__ __launch_bounds__(256, SG_NTT_WPE) void k_ntt_pass(PassArgs a) {
+__global__ __launch_bounds__(256) void k_ntt_pass(PassArgs a) {
   extern __shared__ fe_lds lds[];
   const int logC = a.logC;
   const uint32_t C = 1u << logC;
@@ -355,7 +398,7 @@ __global__ __launch_bounds__(256, SG_NTT_WPE) void k_ntt_pass(PassArgs a) {
 // qq + m 2^(L-3)).  Only the middle stages go through LDS: one LDS write + one read per
 // element plus a round trip per middle step, and L/3 barriers fewer than k_ntt_pass.
 template <int TL>
-__global__ __launch_bounds__(1 << (TL - 3), TL == 11 ? SG_NTT_WPE : 1) void k_ntt_pass_rr(PassArgs a) {
+__global__ __launch_bounds__(1 << (TL - 3), SG_NTT_WPE) void k_ntt_pass_rr(PassArgs a) {
   static_assert(TL >= 10 && TL <= 13, "2^TL-element tiles, 2^(TL-3) threads");
   extern __shared__ fe_lds lds[];
   const int logC = a.logC, L = a.L;
@@ -488,7 +531,7 @@ __global__ __launch_bounds__(1 << (TL - 3), TL == 11 ? SG_NTT_WPE : 1) void k_nt
       x[j] = fe_zero();
       if (idx < a.n_in) {
         x[j] = ld_fe_stream(in_at(c, idx), m >= kStreamLogN);
-        if (a.sA) x[j] = mont_mul(x[j], mont_mul(ld_fe(a.sA + (idx & 4095)), ld_fe(a.sB + (idx >> 12))));
+        if (a.sA) x[j] = ntt_mul(x[j], ntt_mul(ld_fe(a.sA + (idx & 4095)), ld_fe(a.sB + (idx >> 12))));
       }
     }
     radix8_first(x, pa);
@@ -504,7 +547,7 @@ __global__ __launch_bounds__(1 << (TL - 3), TL == 11 ? SG_NTT_WPE : 1) void k_nt
       fe v = fe_zero();
       if (idx < a.n_in) {
         v = ld_fe(in_at(k, idx));
-        if (a.sA) v = mont_mul(v, mont_mul(ld_fe(a.sA + (idx & 4095)), ld_fe(a.sB + (idx >> 12))));
+        if (a.sA) v = ntt_mul(v, ntt_mul(ld_fe(a.sA + (idx & 4095)), ld_fe(a.sB + (idx >> 12))));
       }
       const uint32_t tr = __builtin_bitreverse32(u) >> (32 - L);
       for (uint32_t r = 0; r < rep; ++r) lds[((tr + r) << logC) + k] = v;
@@ -534,7 +577,7 @@ __global__ __launch_bounds__(1 << (TL - 3), TL == 11 ? SG_NTT_WPE : 1) void k_nt
         if constexpr (EP) {
           ep_store(a, a.ep_row0 + ycol(c), k, x[mm]);
         } else {
-          st_fe(orow + k, POST ? mont_mul(x[mm], pc) : fe_canon(x[mm]));
+          st_fe(orow + k, POST ? ntt_mul(x[mm], pc) : fe_canon(x[mm]));
         }
       }
       return;

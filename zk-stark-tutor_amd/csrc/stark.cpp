@@ -876,6 +876,9 @@ void prove_boundary_quotients(sg_ctx* ctx, const sg_stark& st, const std::vector
     };
     std::vector<Sharded> sh;
     std::vector<DevBuf> keep;  // divisor tables (and their shards) until the batches are enqueued
+    // the bounded divisor-shard tables sh[i].inv_shard stay allocated until the batches below are
+    // enqueued: no eviction while later inserts (more shards, the replicated divisions) happen
+    BoundedPin pin(ctx);
     const size_t b0 = bqs.size();
     bqs.resize(b0 + m);
     std::vector<DivItem> rep_items;
