@@ -267,13 +267,17 @@ void sg_dist_destroy(sg_dist* d);
  * proof-stream or transport callback, an RCCL asynchronous error, or a host wait that outlasts the
  * deadline -- the communicator is POISONED on that rank: RCCL's is aborted with ncclCommAbort, a
  * caller transport's abort hook runs, and every later call on it returns SG_ERR_INVALID.  Destroy
- * it and create a new one.  The abort is LOCAL: over RCCL the peers get no signal -- their
- * collectives keep waiting for the failed rank until their own host-wait deadline passes, and
- * only then do they poison their communicators and return.  Host-blocking RCCL calls
- * (ncclCommInitRank, the connection set-up inside ncclGroupEnd) are not watched by the deadline.
- * A caller transport can do better through its abort hook (e.g. tear its group down).
- * Deadline: SG_DIST_TIMEOUT_S at creation (default 300 s) or sg_dist_set_timeout (per rank);
- * callers that need fast failure set a deadline of a few times their longest collective step. */
+ * it and create a new one.  ncclCommAbort is local; so that the peers of an RCCL communicator
+ * learn of it, the failing rank also raises an out-of-band flag -- a node-local file named from
+ * the unique id, /dev/shm/sg_dist_abort_<FNV-1a of the id> -- that every rank's host waits poll
+ * about every 10 ms: a peer waiting inside a call then poisons its own communicator (aborting its
+ * collectives) and returns SG_ERR_HIP ("a peer rank failed (rank r of G: reason)") within
+ * milliseconds.  Ranks on other nodes (no shared /dev/shm) fail at their deadline instead.
+ * Host-blocking RCCL calls (ncclCommInitRank, the connection set-up inside ncclGroupEnd) are not
+ * watched.  A caller transport gets the abort hook instead of the flag (e.g. tear its group down).
+ * Deadline: SG_DIST_TIMEOUT_S at creation (default 30 s) or sg_dist_set_timeout (per rank): the
+ * longest one host wait inside a communicator call may last (the prove's longest is well under a
+ * second at the headline size, a few seconds at 2^27 rows over 8 ranks). */
 int sg_dist_set_timeout(sg_dist* d, double seconds);
 int sg_dist_poisoned(const sg_dist* d); /* 1 when poisoned */
 /* instrumentation: collectives this communicator issued, transition quotients and trace columns

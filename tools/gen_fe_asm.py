@@ -217,6 +217,12 @@ def addsub(g, e, o, sum_out, diff_out):
 # ----------------------------------------------------------------------------- scheduler
 
 HAZ = 2  # wait states between a VALU write of an SGPR and a VALU read of it
+# wait states between a VALU write of an SGPR and a scalar (SALU / SMEM / VMEM-address) access that
+# may write or read it: the VALU's SGPR write-back can land after a scalar write issued too soon
+# (a late carry overwrote a kernel-argument pointer that hipcc's s_load put in the same SGPR
+# right after a block: an illegal address).  Inside a block this orders the s_or; at the end of a
+# block the generator pads the last VALU-written SGPR to this distance, since hipcc cannot see it.
+VALU_SGPR_SCALAR = 5
 
 
 def deps(ops):
@@ -234,7 +240,10 @@ def deps(ops):
                 preds[i].append((w, dist))
         for r in op.vdst + [s for s in op.sdst if s != "junk"]:
             if r in last_w:
-                preds[i].append((last_w[r], 1))  # WAW
+                w = last_w[r]
+                # WAW: a scalar write after a VALU write of the same SGPR waits for its write-back
+                dist = 1 + VALU_SGPR_SCALAR if r in op.sdst and op.salu and not ops[w].salu else 1
+                preds[i].append((w, dist))
             for rd in reads_since.get(r, []):
                 if rd != i:
                     preds[i].append((rd, 1))  # WAR
@@ -335,12 +344,17 @@ def allocate(ops, order, fixed_v, nsgpr_max=12):
                 vmap[b] = [reg, reg + 1]
                 vbusy[b] = [reg, reg + 1]
             elif b.startswith("c"):
-                if free_s:
+                if op.salu:
+                    # a scalar write never lands on a pair a VALU of this block wrote (its late
+                    # write-back could overwrite it): SALU-written carries get pairs of their own
+                    s = "salu%d" % len([k for k in smap.values() if str(k).startswith("salu")])
+                elif free_s:
                     s = free_s.pop()
                 else:
                     s, nsg = nsg, nsg + 1
                 smap[b] = s
-                sbusy[b] = s
+                if not op.salu:
+                    sbusy[b] = s
         # a register read but never written (cannot happen for temps)
     assert nsg <= nsgpr_max, nsg
     return vmap, smap, nwin, nsg
@@ -368,7 +382,7 @@ def render(ops, order, vmap, smap, win_base, opnames):
         if r == "junk":
             return "%[sj]"
         if r in smap:
-            return "%%[s%d]" % smap[r]
+            return "%%[s%s]" % smap[r]
         return "%%[%s]" % opnames.get(r, r)
 
     lines, nops = [], 0
@@ -385,6 +399,16 @@ def render(ops, order, vmap, smap, win_base, opnames):
                 return sname(r)
             return vname(r)
         lines.append(re.sub(r"\{([^}]+)\}", sub, op.fmt))
+    # the block's end: pad so that its last VALU-written SGPR is VALU_SGPR_SCALAR wait states old
+    # (hipcc's next instruction may be a scalar write or read of that register)
+    since = 0
+    for l, i in zip(reversed(lines), reversed(order)):
+        if l is None or ops[i].salu or not ops[i].sdst:
+            since += 1
+            continue
+        break
+    lines = lines + [None] * max(0, VALU_SGPR_SCALAR - since)
+    nops += max(0, VALU_SGPR_SCALAR - since)
     # merge consecutive nops into s_nop N
     out, run = [], 0
     for l in lines + ["END"]:
@@ -603,12 +627,19 @@ def check(blk, name, trials=3000, seed=1):
 WIN_BASE = int(os.environ.get("SG_ASM_WIN_BASE", "2"))
 
 
+def snames(blk):
+    """The block's SGPR-pair operands: VALU carries s0.., SALU-only pairs ssalu0.., the junk pair."""
+    text = "\n".join(blk["lines"])
+    salu = sorted(set(re.findall(r"%\[(ssalu\d+)\]", text)))
+    return ["s%d" % k for k in range(blk["nsg"])] + salu + ["sj"]
+
+
 def cxx(name, blk, win_base):
     io = blk["io"]
     nwin = blk["nwin"]
     outs = ['[%s] "=v"(%s)' % (o, o) for o in io["outs"]]
     inouts = ['[%s] "+v"(%s)' % (o, o) for o in io["inout"]]
-    souts = ['[s%d] "=&s"(s%d)' % (k, k) for k in range(blk["nsg"])] + ['[sj] "=&s"(sj)']
+    souts = ['[%s] "=&s"(%s)' % (k, k) for k in snames(blk)]
     ins = ['[%s] "v"(%s)' % (i, i) for i in io["ins"]]
     used_consts = set(re.findall(r"%\[(P3s|NEGP3v|P3v)\]", "\n".join(blk["lines"])))
     cins = []
@@ -665,7 +696,7 @@ def gen(win_base=WIN_BASE):
   fe r = {{o0, o1, o2, o3}};
   return r;
 }
-""" % (", ".join(["s%d" % k for k in range(b["nsg"])] + ["sj"]), body, outs, ins, clob))
+""" % (", ".join(snames(b)), body, outs, ins, clob))
     for name, sig, pre, post in (
         ("bfly", "fe& e, fe& x, const fe& w",
          "uint32_t e0 = e.w[0], e1 = e.w[1], e2 = e.w[2], e3 = e.w[3], x0 = x.w[0], x1 = x.w[1], x2 = x.w[2], x3 = x.w[3];\n"
@@ -700,7 +731,7 @@ def gen(win_base=WIN_BASE):
       : %s);
   %s
 }
-""" % (fname, sig, pre, ", ".join(["s%d" % k for k in range(b["nsg"])] + ["sj"]), body, outs,
+""" % (fname, sig, pre, ", ".join(snames(b)), body, outs,
        ins if ins else "", clob if clob else "", post))
     src.append("}  // namespace sg\n#endif\n")
     return "".join(src), built

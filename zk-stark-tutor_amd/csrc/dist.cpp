@@ -28,6 +28,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <memory>
@@ -52,10 +53,16 @@ struct sg_dist {
   // way into) a collective this rank never joins.  The communicator is then poisoned: RCCL's is
   // aborted (ncclCommAbort ends the collectives in flight), a caller transport gets its abort hook,
   // and every later call returns SG_ERR_INVALID.  A host wait that outlasts timeout_s
-  // (SG_DIST_TIMEOUT_S, default 300 s) or an RCCL asynchronous error poisons it the same way.
+  // (SG_DIST_TIMEOUT_S, default 30 s) or an RCCL asynchronous error poisons it the same way.
+  // RCCL communicators also share an out-of-band abort flag: a node-local file named from the
+  // unique id (/dev/shm/sg_dist_abort_<hash>) that a poisoned rank creates and every rank's host
+  // waits poll (every ~10 ms), so the peers of a failed rank fail within milliseconds instead of
+  // waiting out the deadline (one process per GPU of one node; across nodes the deadline applies).
   bool dead = false;
   std::string dead_reason;
-  double timeout_s = 300.0;
+  double timeout_s = 30.0;
+  std::string abort_path;  // empty: no flag (host transport: the caller's abort hook does this)
+  double abort_polled = -1.0;
   // codeword size (log2 elements) at which a sharded FRI commit hands over to the single-GPU
   // rounds: part of the collective schedule, so it is agreed by all ranks (sg_dist_set_fri_tail)
   int fri_tail_log = 20;
@@ -74,10 +81,31 @@ struct sg_dist {
 
 namespace sg {
 
+// the out-of-band abort flag: created by a rank that poisons its communicator (first writer wins)
+void raise_abort_flag(sg_dist* d, const std::string& why) {
+  if (d->abort_path.empty()) return;
+  FILE* f = fopen(d->abort_path.c_str(), "wx");  // exclusive: an existing flag keeps the first reason
+  if (!f) return;
+  fprintf(f, "rank %d of %d: %s", d->g, d->G, why.c_str());
+  fclose(f);
+}
+
+// "" when no peer has raised the flag, else its text
+std::string read_abort_flag(const sg_dist* d) {
+  if (d->abort_path.empty()) return "";
+  FILE* f = fopen(d->abort_path.c_str(), "r");
+  if (!f) return "";
+  char buf[512] = {0};
+  const size_t n = fread(buf, 1, sizeof(buf) - 1, f);
+  fclose(f);
+  return std::string(buf, n).empty() ? std::string("a peer rank failed") : std::string(buf, n);
+}
+
 void dist_poison(sg_dist* d, const std::string& why) {
   if (d->dead) return;
   d->dead = true;
   d->dead_reason = why;
+  raise_abort_flag(d, why);
   if (d->comm) {
     (void)ncclCommAbort(d->comm);  // ends the collectives in flight on this rank
     d->comm = nullptr;
@@ -100,6 +128,16 @@ int dist_run(sg_dist* d, const std::function<void()>& body) {
           ncclResult_t e = ncclSuccess;
           if (ncclCommGetAsyncError(dd->comm, &e) == ncclSuccess && e != ncclSuccess && e != ncclInProgress) {
             const std::string m = std::string("RCCL asynchronous error: ") + ncclGetErrorString(e);
+            dist_poison(dd, m);
+            throw Error{SG_ERR_HIP, m};
+          }
+        }
+        // the out-of-band flag, polled about every 10 ms of a wait (a stat-sized file read)
+        if (!dd->abort_path.empty() && (waited_s - dd->abort_polled >= 0.01 || waited_s < dd->abort_polled)) {
+          dd->abort_polled = waited_s;
+          const std::string peer = read_abort_flag(dd);
+          if (!peer.empty()) {
+            const std::string m = "a peer rank failed (" + peer + ")";
             dist_poison(dd, m);
             throw Error{SG_ERR_HIP, m};
           }
@@ -919,6 +957,12 @@ extern "C" int sg_dist_create(sg_ctx* ctx, const uint8_t* id, int nranks, int ra
     dist_defaults(d.get());
     ncclUniqueId u;
     memcpy(u.internal, id, SG_DIST_ID_BYTES);
+    // the abort flag's name: FNV-1a of the unique id (the same on every rank of this communicator)
+    uint64_t h = 1469598103934665603ull;
+    for (int i = 0; i < SG_DIST_ID_BYTES; ++i) h = (h ^ id[i]) * 1099511628211ull;
+    char path[64];
+    snprintf(path, sizeof(path), "/dev/shm/sg_dist_abort_%016llx", (unsigned long long)h);
+    d->abort_path = path;
     SG_NCCL(ncclCommInitRank(&d->comm, nranks, u, rank));
   });
   if (rc != SG_OK) return rc;
@@ -956,7 +1000,12 @@ extern "C" int sg_dist_create_transport(sg_ctx* ctx, int nranks, int rank, const
   return SG_OK;
 }
 
-extern "C" void sg_dist_destroy(sg_dist* d) { delete d; }
+extern "C" void sg_dist_destroy(sg_dist* d) {
+  // a communicator that ended cleanly removes its (never raised) flag name; a raised flag stays
+  // for peers that have not yet polled it (a few bytes in /dev/shm per failed communicator)
+  if (d && !d->dead && !d->abort_path.empty()) (void)remove(d->abort_path.c_str());
+  delete d;
+}
 
 extern "C" int sg_dist_set_fri_tail(sg_dist* d, int log2_elements) {
   return dist_run(d, [&] {
