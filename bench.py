@@ -375,7 +375,7 @@ def c5_single_gpu(ctx: sg.Context, device, iters: int = 3) -> dict:
     ctx.trim()
     # the headline proof through sg_dist_stark_prove on the same one-rank communicator: since round 5
     # a one-rank communicator proves through the single-GPU plan (its collectives are identities);
-    # SG_DIST_WORLD1_SHARDED=1 forces the four-step path, whose own cost (four-step LDEs, forests,
+    # the context option world1_sharded forces the four-step path, whose own cost (four-step LDEs, forests,
     # sharded FRI rounds, batched openings) without peers is the second line.  Bytes must equal the
     # single-GPU proof's either way.
     try:
@@ -389,8 +389,7 @@ def c5_single_gpu(ctx: sg.Context, device, iters: int = 3) -> dict:
             return ps.digest()
 
         for key, forced in (("sharded_prove_world1", False), ("sharded_prove_world1_fourstep", True)):
-            if forced:
-                os.environ["SG_DIST_WORLD1_SHARDED"] = "1"
+            ctx.set_option("world1_sharded", int(forced))
             try:
                 same = sharded() == single
                 torch.cuda.synchronize(device)
@@ -399,7 +398,7 @@ def c5_single_gpu(ctx: sg.Context, device, iters: int = 3) -> dict:
                     sharded()
                 torch.cuda.synchronize(device)
             finally:
-                os.environ.pop("SG_DIST_WORLD1_SHARDED", None)
+                ctx.set_option("world1_sharded", 0)
             out[key + "_ms"] = round((time.perf_counter() - t0) / iters * 1e3, 3)
             out[key + "_bytes_equal_single_gpu"] = same
         del wl

@@ -56,6 +56,19 @@ int sg_ctx_trim(sg_ctx* ctx);
  * (domain / AIR coset tables, twiddle plans, interpolation kernels) -- constant across proofs
  * on one (AIR, domain), also when the constraints are rebuilt for every proof */
 int sg_ctx_cached_tables(const sg_ctx* ctx, size_t* domain_tables, size_t* twiddle_tables);
+/* Options of a context (no reference counterpart; every setting writes the same proof bytes --
+ * tests compare the equivalent paths this way, and no environment variable switches them):
+ *   "domain_cache"   1 (default; 0 also by SG_NO_DOMAIN_CACHE=1 at creation): public domain /
+ *                    AIR tables kept across calls, else recomputed in every call
+ *   "air_generic"    0 (default): the Rescue-Prime AIR in its factored form; 1: its expanded groups
+ *   "geo_decimate"   1 (default): decimated geometric interpolation; 0: the full group
+ *   "lean_trees"     1 (default): the retained prove / FRI trees drop their lowest levels
+ *   "stream_pin"     1 (default): a native proof stream's buffer is page-locked for device copies
+ *   "world1_sharded" 0 (default): a one-rank communicator proves through the single-GPU plan; 1:
+ *                    through the four-step path (tests of the sharded machinery over RCCL)
+ *   "lean_drop"      3 (default): the most levels a lean tree drops (0..3; 0 = keep every level)
+ * SG_ERR_INVALID for an unknown name. */
+int sg_ctx_set_option(sg_ctx* ctx, const char* name, int64_t value);
 /* Device memory (no reference counterpart): `live` = bytes of the context's buffer pool in use,
  * `peak` = their high-water mark since creation or the last reset (the working set of the calls
  * in between: codewords, retained trees, scratch), `pooled` = returned buffers the pool caches,

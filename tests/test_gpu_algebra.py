@@ -135,7 +135,7 @@ def test_interpolate_geometric_large(logD, n):
 def test_interpolate_geometric_decimated_vs_checker(logD, monkeypatch):
     """n <= D / f: the interpolant comes from its values on the subgroup of order D / f (f residue-class
     convolutions sharing one inverse transform) -- equal to the CPU checker (fast_cpu, pinned to the
-    oracle) and to the full-group form (SG_GEO_DECIMATE=0), for f = 16, 4, 2 and none."""
+    oracle) and to the full-group form (context option geo_decimate = 0), for f = 16, 4, 2 and none."""
     import torch
     import fast_cpu as fc
     D = 1 << logD
@@ -145,11 +145,10 @@ def test_interpolate_geometric_decimated_vs_checker(logD, monkeypatch):
         vals = o.synthetic_elements(n, b"decimated", n)
         y = torch.from_numpy(sg.fe_array(vals).view(np.int64)).to(dev)
         want = fc.ints(fc.geo_interpolate(q, D, vals))
-        monkeypatch.delenv("SG_GEO_DECIMATE", raising=False)
         got = sg.fast_interpolate_geometric_dev(q, D, y.data_ptr(), n)
         assert got.coefficients == want, n
-        monkeypatch.setenv("SG_GEO_DECIMATE", "0")
-        assert sg.fast_interpolate_geometric_dev(q, D, y.data_ptr(), n).coefficients == want, n
+        with sg.Context.default().option("geo_decimate", 0, 1):
+            assert sg.fast_interpolate_geometric_dev(q, D, y.data_ptr(), n).coefficients == want, n
 
 
 # ---- arbitrary (non-geometric) domains of any size (ntt_arithmetics.rs:66-113, 172-237) ----

@@ -518,12 +518,12 @@ def _stark_checks(nd, world, rank, tmp, cases, gather, sharded_algebra=True):
 @pytest.mark.parametrize("forced", ["1", "0"])
 def test_dist_stark_prove_world1_rccl(stark_reference, monkeypatch, forced):
     """sg_dist_stark_prove over a 1-rank RCCL communicator: the single-GPU / oracle proof bytes --
-    through the four-step path forced (SG_DIST_WORLD1_SHARDED=1: the sharded machinery over RCCL)
+    through the four-step path forced (context option world1_sharded: the sharded machinery over RCCL)
     and through the default one-rank plan (the single-GPU prove)."""
     import starkgpu as sg
     from starkgpu import dist as D
-    monkeypatch.setenv("SG_DIST_WORLD1_SHARDED", forced)
     ctx = sg.Context(0)
+    ctx.set_option("world1_sharded", int(forced))
     nd = D.NativeDist(ctx, transport="rccl")
     try:
         _stark_checks(nd, 1, 0, stark_reference, range(len(STARK_CASES)), lambda a: [a])
@@ -655,8 +655,8 @@ def test_dist_failure_world1_rccl_poisons(stark_reference, monkeypatch):
     four-step path is forced: a one-rank communicator otherwise proves through the single-GPU plan.)"""
     import starkgpu as sg
     from starkgpu import dist as D
-    monkeypatch.setenv("SG_DIST_WORLD1_SHARDED", "1")
     ctx = sg.Context(0)
+    ctx.set_option("world1_sharded", 1)
     nd = D.NativeDist(ctx, transport="rccl")
     try:
         (N, exp, c, sec, tcd), bnd, trace, tr, rc = _load_case(stark_reference, 1)

@@ -137,7 +137,8 @@ def test_stark_prove_domain_tables_cached_and_recomputed(monkeypatch):
     """The public domain tables the context keeps (trace-domain zerofier transforms, the transition
     zerofier's coset values and inverse, the AIR x-polynomials' coset values, boundary-divisor
     inverses) give the same proof bytes as recomputing them: first proof (tables built), second
-    proof (tables reused), and a proof with SG_NO_DOMAIN_CACHE=1 -- all equal to the oracle's."""
+    proof (tables reused), and a proof with the tables recomputed (context option domain_cache = 0,
+    what SG_NO_DOMAIN_CACHE=1 sets at creation) -- all equal to the oracle's."""
     rp, st_o, st_g, air_o, air_g, trace, bnd, tr, rc, out = _case(40, 4, 3, 4, 2, b"domain-cache")
     want = st_o.prove(trace, air_o, bnd, o.IndependentProofStream(), tr, rc)
     ctx = sg.Context(0)  # a fresh context: nothing cached yet
@@ -145,7 +146,7 @@ def test_stark_prove_domain_tables_cached_and_recomputed(monkeypatch):
     air = sg.RescuePrime(2, 1, 4, 40, ctx=ctx).transition_constraints(st.omicron, st.omicron_domain_length)
     assert st.prove(trace, air, bnd, sg.IndependentProofStream(), tr, rc) == want
     assert st.prove(trace, air, bnd, sg.IndependentProofStream(), tr, rc) == want
-    monkeypatch.setenv("SG_NO_DOMAIN_CACHE", "1")
+    ctx.set_option("domain_cache", 0)
     assert st.prove(trace, air, bnd, sg.IndependentProofStream(), tr, rc) == want
 
 
@@ -155,10 +156,10 @@ def test_stark_prove_rebuilt_constraints_keep_tables_flat(monkeypatch, generic):
     The AIR's coset tables are keyed by content (the Rescue parameters and domain, or a digest of
     each x-polynomial for the expanded groups), so rebuilding the constraints for each of 5 proofs
     leaves the context's table count where the first proof put it; every proof equals the oracle's."""
-    monkeypatch.setenv("SG_AIR_GENERIC", generic)
     rp, st_o, st_g, air_o, air_g, trace, bnd, tr, rc, out = _case(40, 4, 3, 4, 2, b"rebuilt-air")
     want = st_o.prove(trace, air_o, bnd, o.IndependentProofStream(), tr, rc)
     ctx = sg.Context(0)
+    ctx.set_option("air_generic", int(generic))
     st = sg.Stark(4, 3, 4, 2, 41, 2, ctx=ctx)
     rpg = sg.RescuePrime(2, 1, 4, 40, ctx=ctx)
     counts = []
@@ -295,8 +296,8 @@ def test_stark_prove_out_of_memory_at_every_stage(monkeypatch, c4_case, frac):
 
 def test_stark_prove_rescue_factored_air_equals_expanded(monkeypatch):
     """The native Rescue-Prime AIR is evaluated in its factored form (rescue_prime.rs:246-283:
-    sum MDS prev^alpha + first(x) - (sum MDSinv (next - second(x)))^alpha); SG_AIR_GENERIC=1
-    evaluates its expanded monomial groups instead.  Same proof bytes either way, equal to the
+    sum MDS prev^alpha + first(x) - (sum MDSinv (next - second(x)))^alpha); the context option
+    air_generic = 1 evaluates its expanded monomial groups instead.  Same proof bytes either way, equal to the
     oracle's, for an honest and a false witness (the transition values differ from zero there)."""
     rp, st_o, st_g, air_o, air_g, trace, bnd, tr, rc, out = _case(40, 4, 3, 4, 2, b"factored-air")
     want = st_o.prove(trace, air_o, bnd, o.IndependentProofStream(), tr, rc)
@@ -305,9 +306,9 @@ def test_stark_prove_rescue_factored_air_equals_expanded(monkeypatch):
     want_bad = st_o.prove(bad, air_o, bnd, o.IndependentProofStream(), tr, rc)
     got = st_g.prove(trace, air_g, bnd, sg.IndependentProofStream(), tr, rc)
     got_bad = st_g.prove(bad, air_g, bnd, sg.IndependentProofStream(), tr, rc)
-    monkeypatch.setenv("SG_AIR_GENERIC", "1")
-    assert st_g.prove(trace, air_g, bnd, sg.IndependentProofStream(), tr, rc) == want
-    assert st_g.prove(bad, air_g, bnd, sg.IndependentProofStream(), tr, rc) == want_bad
+    with st_g.ctx.option("air_generic", 1, 0):
+        assert st_g.prove(trace, air_g, bnd, sg.IndependentProofStream(), tr, rc) == want
+        assert st_g.prove(bad, air_g, bnd, sg.IndependentProofStream(), tr, rc) == want_bad
     assert got == want and got_bad == want_bad
 
 
@@ -328,12 +329,12 @@ def test_stark_prove_c4_factored_air_equals_expanded(monkeypatch):
     rc = sg.fe_array(r[2 * st_g.num_randomizers:])
     bnd = rp_o.boundary_constraints(rp_o.hash(inp))
     factored = st_g.prove(trace, air_g, bnd, sg.IndependentProofStream(), tr, rc)
-    monkeypatch.setenv("SG_AIR_GENERIC", "1")
-    assert st_g.prove(trace, air_g, bnd, sg.IndependentProofStream(), tr, rc) == factored
+    with st_g.ctx.option("air_generic", 1, 0):
+        assert st_g.prove(trace, air_g, bnd, sg.IndependentProofStream(), tr, rc) == factored
 
 
-@pytest.mark.parametrize("env", [{"SG_LEAN_DROP": "1"}, {"SG_LEAN_DROP": "2"}, {"SG_LEAN_TREES": "0"}])
-def test_lean_tree_layouts_keep_proof_bytes(monkeypatch, env):
+@pytest.mark.parametrize("opts", [{"lean_drop": 1}, {"lean_drop": 2}, {"lean_trees": 0}])
+def test_lean_tree_layouts_keep_proof_bytes(opts):
     """The prove's retained trees drop their low levels (three by default; an opening rehashes the
     8-leaf block around its leaf from the codeword): every layout -- one or two levels dropped, or
     every level kept -- writes the same proof bytes, equal to the oracle's at a small size and to
@@ -353,10 +354,16 @@ def test_lean_tree_layouts_keep_proof_bytes(monkeypatch, env):
     bnd_c4 = rp_o.boundary_constraints(rp_o.hash(inp))
     default_small = st_g.prove(trace, air_g, bnd, sg.IndependentProofStream(), tr, rc)
     default_c4 = st_c4.prove(trace_c4, air_c4, bnd_c4, sg.IndependentProofStream(), tr_c4, rc_c4)
-    for k, v in env.items():
-        monkeypatch.setenv(k, v)
-    assert st_g.prove(trace, air_g, bnd, sg.IndependentProofStream(), tr, rc) == want == default_small
-    assert st_c4.prove(trace_c4, air_c4, bnd_c4, sg.IndependentProofStream(), tr_c4, rc_c4) == default_c4
+    ctx = sg.Context.default()
+    assert st_g.ctx is ctx and st_c4.ctx is ctx
+    try:
+        for k, v in opts.items():
+            ctx.set_option(k, v)
+        assert st_g.prove(trace, air_g, bnd, sg.IndependentProofStream(), tr, rc) == want == default_small
+        assert st_c4.prove(trace_c4, air_c4, bnd_c4, sg.IndependentProofStream(), tr_c4, rc_c4) == default_c4
+    finally:
+        ctx.set_option("lean_drop", 3)
+        ctx.set_option("lean_trees", 1)
 
 
 def test_stark_prove_negated_constraints():

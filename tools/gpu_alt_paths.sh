@@ -1,5 +1,7 @@
 # The GPU suite with every alternate path forced at once (each is a default's A/B knob; the proofs
-# and roots must not depend on any of them):
+# and roots must not depend on any of them).  Since round 6 the product library reads none of these
+# (csrc/knobs.hpp): the suite loads the A/B build (make -C zk-stark-tutor_amd ab) via SG_LIB_PATH,
+# which reads them at context creation / first use:
 #   SG_NO_DOMAIN_CACHE=1          public domain/AIR tables recomputed per proof
 #   SG_AIR_GENERIC=1              the Rescue AIR through its expanded groups
 #   SG_NTT_TILES=0                three-pass NTTs on 2048-element tiles at every size
@@ -21,6 +23,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 TAG=${1:-alt}
 cd "$R"
 mkdir -p gpurun_out
+SG_LIB_PATH=$R/zk-stark-tutor_amd/starkgpu/libstarkgpu_ab.so \
 SG_NO_DOMAIN_CACHE=1 SG_AIR_GENERIC=1 SG_NTT_TILES=0 SG_GEO_DECIMATE=0 SG_STREAM_PRIORITY=0 SG_DIST_FRI_TAIL=0 \
 SG_MERKLE_QUAD_LEAF_BELOW=0 SG_MERKLE_QUAD_TOP=0 SG_MERKLE_LEAF_PAIRS=0 SG_MERKLE_NODE_FUSE=3 SG_NTT_SMALL_WHOLE=0 \
 SG_MERKLE_FOREST_QUAD=0 SG_LEAN_TREES=0 SG_MERKLE_QUAD_LEAF_NODES=64 SG_MERKLE_QUAD_TOP_MAX=64 \

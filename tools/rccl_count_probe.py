@@ -7,6 +7,7 @@ boundary (2^31 - 256 bytes as uint8).  Each line: dtype, count, bytes, and wheth
 buffer equals the sent one (world 1: all-to-all and all-gather are copies).
 
 usage: rccl_count_probe.py [log2_bytes]   (default 31)
+       rccl_count_probe.py sweep           all-to-all (int64) at sizes between 1 GiB and 2 GiB
 """
 import os
 import sys
@@ -16,7 +17,34 @@ import torch
 import torch.distributed as dist
 
 
+def sweep():
+    """all_to_all_single, int64 elements, world 1: the largest per-call size that stays exact."""
+    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+    os.environ.setdefault("MASTER_PORT", "29534")
+    dist.init_process_group("nccl", rank=0, world_size=1)
+    dev = torch.device("cuda", 0)
+    top = 1 << 31
+    src = torch.randint(0, 256, (top,), dtype=torch.uint8, device=dev)
+    dst = torch.empty_like(src)
+    gib = 1 << 30
+    for nb in (gib - 256, gib, gib + 256, gib + (1 << 20), gib + (1 << 23), gib + (1 << 24), gib + (1 << 28),
+               gib + (1 << 29), top - (1 << 28), top - 256, top):
+        s, d = src[:nb].view(torch.int64), dst[:nb].view(torch.int64)
+        d.fill_(0)
+        torch.cuda.synchronize()
+        dist.all_to_all_single(d, s)
+        torch.cuda.synchronize()
+        eq = d.view(torch.uint8) == s.view(torch.uint8)
+        ok = bool(eq.all().item())
+        first_bad = -1 if ok else int(torch.argmin(eq.to(torch.uint8)).item())
+        print("all_to_all int64 bytes %11d (%.6f GiB)  equal %s  first wrong byte %d" % (nb, nb / gib, ok, first_bad),
+              flush=True)
+    dist.destroy_process_group()
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "sweep":
+        return sweep()
     logb = int(sys.argv[1]) if len(sys.argv) > 1 else 31
     os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
     os.environ.setdefault("MASTER_PORT", "29533")

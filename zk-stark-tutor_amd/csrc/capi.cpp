@@ -149,10 +149,12 @@ void* sg_ctx::staging(int slot, size_t bytes) {
   return staging_ptr[slot];
 }
 
-bool sg_ctx::domain_cache_on() const {
-  const char* v = getenv("SG_NO_DOMAIN_CACHE");  // read per call: tests toggle it between proofs
-  return !(v && *v && *v != '0');
+namespace sg {
+int ab_knob(const char* name, int def) {
+  const char* v = getenv(name);
+  return v && *v ? atoi(v) : def;
 }
+}  // namespace sg
 
 void sg_ctx::domain_table_put_bounded(const std::vector<uint64_t>& key, void* p) {
   domain_table_put(key, p);
@@ -264,13 +266,23 @@ extern "C" int sg_ctx_create(int device, sg_ctx** out) {
   auto* ctx = new (std::nothrow) sg_ctx();
   if (!ctx) return SG_ERR_NOMEM;
   ctx->device = device;
+  // the library's runtime environment, read here once: the pool cap (a test
+  // knob) and the domain-table cache
   if (const char* pl = getenv("SG_POOL_LIMIT_BYTES")) ctx->pool_limit = (size_t)strtoull(pl, nullptr, 0);
+  if (const char* dc = getenv("SG_NO_DOMAIN_CACHE")) ctx->opt.domain_cache = !(*dc && *dc != '0');
+#if SG_AB_KNOBS
+  ctx->opt.air_generic = ab_knob("SG_AIR_GENERIC", 0) != 0;
+  ctx->opt.geo_decimate = ab_knob("SG_GEO_DECIMATE", 1) != 0;
+  ctx->opt.lean_trees = ab_knob("SG_LEAN_TREES", 1) != 0;
+  ctx->opt.stream_pin = getenv("SG_STREAM_NO_PIN") == nullptr;
+  ctx->opt.world1_sharded = ab_knob("SG_DIST_WORLD1_SHARDED", 0) != 0;
+  ctx->opt.lean_drop = std::min(std::max(ab_knob("SG_LEAN_DROP", 3), 0), 3);
+#endif
   // the main stream (the prove's critical path) at the highest priority, the side stream (its
   // Merkle trees, which otherwise hold every CU while a small main-stream kernel waits) at the
   // lowest: C4 prove 3.05-3.19 -> 2.98-3.03 ms, headline unchanged (profiles/r03_ab_stream_priority*.log).
-  // SG_STREAM_PRIORITY=0 creates both at the default priority.
-  const char* pe = getenv("SG_STREAM_PRIORITY");
-  const bool prio = !(pe && pe[0] == '0');
+  // SG_STREAM_PRIORITY=0 (A/B builds) creates both at the default priority.
+  const bool prio = SG_KNOB(STREAM_PRIORITY, 1) != 0;
   int prio_low = 0, prio_high = 0;
   if (hipSetDevice(device) != hipSuccess ||
       (prio && hipDeviceGetStreamPriorityRange(&prio_low, &prio_high) != hipSuccess) ||
@@ -410,6 +422,24 @@ extern "C" int sg_ctx_cached_tables(const sg_ctx* ctx, size_t* domain_tables, si
   if (!ctx || !domain_tables || !twiddle_tables) return SG_ERR_INVALID;
   *domain_tables = ctx->domain_tables.size();
   *twiddle_tables = ctx->pow_tables.size() + ctx->stage_tables.size() + ctx->interp_tables.size();
+  return SG_OK;
+}
+
+extern "C" int sg_ctx_set_option(sg_ctx* ctx, const char* name, int64_t value) {
+  if (!ctx || !name) return SG_ERR_INVALID;
+  const std::string n(name);
+  const bool v = value != 0;
+  if (n == "domain_cache") ctx->opt.domain_cache = v;
+  else if (n == "air_generic") ctx->opt.air_generic = v;
+  else if (n == "geo_decimate") ctx->opt.geo_decimate = v;
+  else if (n == "lean_trees") ctx->opt.lean_trees = v;
+  else if (n == "stream_pin") ctx->opt.stream_pin = v;
+  else if (n == "world1_sharded") ctx->opt.world1_sharded = v;
+  else if (n == "lean_drop" && value >= 0 && value <= 3) ctx->opt.lean_drop = (int)value;
+  else {
+    ctx->last_error = "unknown context option: " + n;
+    return SG_ERR_INVALID;
+  }
   return SG_OK;
 }
 
@@ -651,16 +681,13 @@ std::unique_ptr<sg_tree> new_tree(sg_ctx* ctx, uint64_t n, const fe* lean_leaves
   std::unique_ptr<sg_tree> t(new sg_tree());
   t->n = n;
   t->logn = ilog2_exact(n);
-  // SG_LEAN_TREES=0: every tree keeps all its levels (A/B knob, alternate path; read per tree, so
-  // a test can compare the layouts in one process)
-  const char* lv = getenv("SG_LEAN_TREES");
-  const bool lean_on = !(lv && *lv == '0');
-  // SG_LEAN_DROP=k: at most k levels dropped (A/B knob; the default is what the caller asks)
-  const char* dv = getenv("SG_LEAN_DROP");
-  const int drop_cap = dv && *dv ? atoi(dv) : 64;
-  // at most 3: an opening rehashes the 2^drop-leaf block around its leaf, and k_serialize_tail's
-  // LDS rehash buffers (msg[8][16], mt[16][8]) hold 8-leaf blocks
-  drop = std::min(std::min(drop, drop_cap), 3);
+  // option lean_trees = 0: every tree keeps all its levels (sg_ctx_set_option; a test compares the
+  // layouts in one process)
+  const bool lean_on = ctx->opt.lean_trees;
+  // option lean_drop = k: at most k levels dropped; never more than 3: an opening rehashes the
+  // 2^drop-leaf block around its leaf, and k_serialize_tail's LDS rehash buffers (msg[8][16],
+  // mt[16][8]) hold 8-leaf blocks
+  drop = std::min(std::min(drop, ctx->opt.lean_drop), 3);
   t->drop = (lean_on && lean_leaves && n >= 2) ? std::min(std::max(drop, 0), t->logn) : 0;
   t->leaves = t->drop ? lean_leaves : nullptr;
   t->buf = DevBuf(ctx, (2 * (n >> t->drop) - 1) * 64);  // levels drop .. log2 n
@@ -1043,7 +1070,7 @@ void TailWriter::flush(sg_ctx* ctx, const sg_proof_stream* ps) {
     // runtime refuses to page-lock the body)
     Stream& st = reinterpret_cast<sg_stream*>(ps->user)->s;
     st.body.reserve(st.body.size() + bytes);  // grow first: the registration covers the block
-    const bool pinned = st.body.pin();
+    const bool pinned = ctx->opt.stream_pin && st.body.pin();
     uint8_t* dst = st.append_block(bytes, offs, field);
     if (pinned) {
       SG_HIP(hipMemcpyAsync(dst, dout.get(), bytes, hipMemcpyDeviceToHost, ctx->stream));
@@ -1138,66 +1165,8 @@ void fri_commit_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, co
   // Round r >= 1 hashes the fold of round r-1 in the same launch that computes it
   // (the fold is written out too: later rounds and the query phase read it).
   FoldLeaves fold{};
-  // SG_FRI_DEVICE_FS=1 (opt-in, read per call): a native stream's Fiat-Shamir continues on the
-  // device (k_fri_fs after each round's tree), every round is enqueued at once with no host round
-  // trip between a root and the next fold, and the roots are pushed afterwards (the host sponge
-  // absorbs them on its next draw).  Byte-identical, but slower on MI355X: a one-wave Keccak
-  // (two permutations per round) costs more than the host round trip it replaces
-  // (profiles/r03_ab_devfs.log: prove 27.4-27.8 vs 26.5-26.9 ms), so the host loop below stays the
-  // default.  Callback streams (any ProofStream implementation) always take the host loop.
-  const char* dev_fs_env = getenv("SG_FRI_DEVICE_FS");
-  if (dev_fs_env && *dev_fs_env == '1' && ps->push == stream_push_cb && rounds >= 2) {
-    Stream& S = reinterpret_cast<sg_stream*>(ps->user)->s;
-    DevTranscript h{};
-    uint8_t pend[136];
-    size_t plen = 0;
-    S.fs_snapshot(h.st, pend, &plen);
-    for (size_t i = 0; i < plen; ++i) h.st[i / 8] ^= (uint64_t)pend[i] << (8 * (i % 8));  // the partial block
-    h.plen = (uint32_t)plen;
-    DevBuf dfs(ctx, sizeof(DevTranscript)), dK(ctx, rounds * sizeof(fe)), droots(ctx, rounds * 64);
-    SG_HIP(hipMemcpyAsync(dfs.get(), &h, sizeof(h), hipMemcpyHostToDevice, ctx->stream));
-    const fe r2 = fe_r2();
-    for (size_t r = 0; r < rounds; ++r) {
-      const uint64_t len = plan[r].len;
-      SG_REQUIRE(fe_eq(fe_pow(plan[r].omega, len - 1), plan[r].winv),
-                 "error in commit: omega does not have the right order!");  // fri.rs:133
-      const fe* lv = st.cw[r];
-      uint64_t* buf = trees[r]->buf.as<uint64_t>();
-      SG_HIP(launch_merkle_tree(&lv, &buf, 1, len, nullptr, ctx->stream, 0, 0, 0, nullptr, 0, r ? &fold : nullptr,
-                                trees[r]->drop));
-      const uint64_t* rootp = buf + tree_level_offset(trees[r].get(), trees[r]->logn) * 8;
-      uint64_t* rout = droots.as<uint64_t>() + 8 * r;
-      if (r == rounds - 1) {
-        SG_HIP(hipMemcpyAsync(rout, rootp, 64, hipMemcpyDeviceToDevice, ctx->stream));
-        break;
-      }
-      const fe C = to_mont(fe_mul(plan[r].oinv, inv2));
-      SG_HIP(launch_fri_fs(dfs.as<DevTranscript>(), rootp, rout, dK.as<fe>() + r, C, r2, ctx->stream));
-      fold.src = st.cw[r];
-      fold.dst = const_cast<fe*>(st.cw[r + 1]);
-      fold.Tlo = Tlo;
-      fold.Thi = Thi;
-      fold.shift = (int)r;
-      fold.K = fe_zero();
-      fold.Kp = dK.as<fe>() + r;
-    }
-    std::vector<uint8_t> roots(rounds * 64);
-    const uint64_t last_len = st.lengths.back();
-    std::vector<fe> last(last_len);
-    SG_HIP(hipMemcpyAsync(roots.data(), droots.get(), roots.size(), hipMemcpyDeviceToHost, ctx->stream));
-    SG_HIP(hipMemcpyAsync(last.data(), st.cw.back(), last_len * sizeof(fe), hipMemcpyDeviceToHost, ctx->stream));
-    host_wait(ctx, ctx->stream);
-    for (size_t r = 0; r < rounds; ++r) {
-      memcpy(trees[r]->root, roots.data() + 64 * r, 64);
-      st.trees.push_back(std::move(trees[r]));
-      push_obj(ps, SG_OBJ_ROOT, st.trees.back()->root, 64);
-    }
-    std::vector<uint8_t> payload;
-    payload.reserve(last_len * 16);
-    for (auto& v : last) put_u128_be(payload, v);
-    push_obj(ps, SG_OBJ_CODEWORD, payload.data(), payload.size());  // fri.rs:166
-    return;
-  }
+  // (round 3's device-side Fiat-Shamir -- a one-wave Keccak per round instead of the host round
+  // trip -- was byte-identical but slower, profiles/r03_ab_devfs*.log, and was removed in round 6)
   const uint64_t last_len = st.lengths.back();
   fe* last = nullptr;  // the last codeword on the host (pinned staging)
   for (size_t r = 0; r < rounds; ++r) {

@@ -114,7 +114,21 @@ struct sg_ctx {
   // twiddle plans: key = a tag and the parameters, value = a device buffer owned by the context.
   // SG_NO_DOMAIN_CACHE=1 recomputes them in every call instead.
   std::map<std::vector<uint64_t>, void*> domain_tables;
-  bool domain_cache_on() const;
+  // Options of this context (sg_ctx_set_option; every setting writes the same bytes -- tests use
+  // them to compare equivalent paths).  The environment sets only domain_cache, at creation
+  // (SG_NO_DOMAIN_CACHE=1: public domain / AIR tables recomputed in every call); A/B builds
+  // (knobs.hpp) also read SG_AIR_GENERIC, SG_GEO_DECIMATE, SG_LEAN_TREES, SG_STREAM_NO_PIN and
+  // SG_DIST_WORLD1_SHARDED here.
+  struct Options {
+    bool domain_cache = true;    // keep public domain / AIR tables across calls
+    bool air_generic = false;    // Rescue AIR through its expanded monomial groups (else factored)
+    bool geo_decimate = true;    // decimated geometric interpolation (else the full group)
+    bool lean_trees = true;      // retained prove / FRI trees drop their lowest levels
+    bool stream_pin = true;      // native proof streams page-lock their buffer for device copies
+    bool world1_sharded = false; // a one-rank communicator proves through the four-step path
+    int lean_drop = 3;           // the most levels a lean tree drops (0..3)
+  } opt;
+  bool domain_cache_on() const { return opt.domain_cache; }
   void* domain_table(const std::vector<uint64_t>& key) const;
   void domain_table_put(const std::vector<uint64_t>& key, void* p) { domain_tables[key] = p; }
   // content-keyed tables (1 / a small divisor's coset values, poly.cpp) are bounded: beyond

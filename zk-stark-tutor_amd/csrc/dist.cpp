@@ -401,7 +401,11 @@ void dist_forest_alloc(sg_dist* d, uint64_t k1s, uint64_t R, PendingForest& pf) 
   SG_REQUIRE(R >= 1 && (R & (R - 1)) == 0 && k1s >= 1 && (k1s & (k1s - 1)) == 0, "Leafs len must be power of two");
   pf.k1s = k1s;
   pf.R = R;
-  pf.per = merkle_tree_digests(R) * 8;  // u64 per subtree
+  // lean subtrees (R >= 2): levels 1 .. log2 R stored, R - 1 digests instead of 2R - 1 -- the leaf
+  // digests are half a forest's bytes (64 B per codeword element per rank), and an opening rehashes
+  // its sibling leaf from the run (k_gather_abs) instead of reading it
+  pf.drop = R >= 2 ? 1 : 0;
+  pf.per = (merkle_tree_digests(R) - (pf.drop ? R : 0)) * 8;  // u64 per subtree
   pf.forest = DevBuf(d->ctx, k1s * pf.per * 8);
   pf.roots = DevBuf(d->ctx, k1s * 64);
 }
@@ -412,10 +416,11 @@ void dist_forest_launch(sg_dist* d, const fe* runs, PendingForest& pf, hipStream
     const int cnt = (int)std::min<uint64_t>(kRows, pf.k1s - t0);
     const fe* lv = runs + t0 * pf.R;
     uint64_t* tr = pf.forest.as<uint64_t>() + t0 * pf.per;
-    SG_HIP(launch_merkle_tree(&lv, &tr, cnt, pf.R, nullptr, s, pf.R, pf.per, 0));
+    SG_HIP(launch_merkle_tree(&lv, &tr, cnt, pf.R, nullptr, s, pf.R, pf.per, 0, nullptr, 0, nullptr, pf.drop));
   }
-  SG_HIP(launch_gather_roots(pf.forest.as<uint64_t>(), pf.per, (2 * pf.R - 2) * 8, pf.roots.as<uint64_t>(), pf.k1s,
-                             s));
+  // the subtree roots: digest 2R - 2 of a full subtree, R - 2 of a lean one
+  const uint64_t root_digest = 2 * pf.R - 2 - (pf.drop ? pf.R : 0);
+  SG_HIP(launch_gather_roots(pf.forest.as<uint64_t>(), pf.per, root_digest * 8, pf.roots.as<uint64_t>(), pf.k1s, s));
 }
 
 void dist_forest_finish(sg_dist* d, PendingForest& pf, uint8_t root[64], ShardedRound* keep) {
@@ -430,6 +435,7 @@ void dist_forest_finish(sg_dist* d, PendingForest& pf, uint8_t root[64], Sharded
     keep->k1s = k1s;
     keep->m = m;
     keep->per = pf.per;
+    keep->drop = pf.drop;
   }
   if (m == 1) {
     SG_HIP(hipMemcpyAsync(root, ordered.get(), 64, hipMemcpyDeviceToHost, ctx->stream));
@@ -686,15 +692,16 @@ void dist_open_batch(sg_dist* d, uint64_t R, uint64_t n2, std::vector<OpenReq>& 
     size_t idx0, count;  // index range in `idx`
     size_t out0;         // output offset in values (elements) or digests (64-byte units)
     const sg_tree* tree = nullptr;  // digests of a local tree (a lean one rehashes its leaf level)
+    bool abs = false;    // `idx` holds absolute addresses (bit 0 set: a leaf value to rehash)
   };
   std::vector<uint64_t> idx;
   std::vector<Job> jobs;
   size_t nvals = 0, ndig = 0;
   auto add_job = [&](const void* src, bool digest, const std::vector<uint64_t>& ix,
-                     const sg_tree* tree = nullptr) -> size_t {
+                     const sg_tree* tree = nullptr, bool abs = false) -> size_t {
     const size_t out0 = digest ? ndig : nvals;
     if (ix.empty()) return out0;
-    jobs.push_back({src, digest, idx.size(), ix.size(), out0, tree});
+    jobs.push_back({src, digest, idx.size(), ix.size(), out0, tree, abs});
     idx.insert(idx.end(), ix.begin(), ix.end());
     (digest ? ndig : nvals) += ix.size();
     return out0;
@@ -728,10 +735,18 @@ void dist_open_batch(sg_dist* d, uint64_t R, uint64_t n2, std::vector<OpenReq>& 
       const uint64_t k1 = i / n2, c = i % R;
       pl.own.push_back(k);
       eidx.push_back(k1 * R + c);
-      for (int lv = 0; lv < lr; ++lv) didx.push_back(k1 * (sr.per / 8) + level_offset(R, lv) + ((c >> lv) ^ 1));
+      // absolute addresses of the subtree path: a lean subtree's leaf-level sibling is its value in
+      // the run (bit 0 set: k_gather_abs rehashes it), the levels above sit R digests earlier
+      const uint64_t fbase = reinterpret_cast<uint64_t>(sr.forest.get()) + 64 * k1 * (sr.per / 8);
+      for (int lv = 0; lv < lr; ++lv) {
+        if (lv < sr.drop)
+          didx.push_back(reinterpret_cast<uint64_t>(sr.cw + k1 * R + (c ^ 1)) | 1);
+        else
+          didx.push_back(fbase + 64 * (level_offset(R, lv) - (sr.drop ? R : 0) + ((c >> lv) ^ 1)));
+      }
     }
     pl.own_vals = add_job(sr.cw, false, eidx);
-    pl.own_dig = add_job(sr.forest.get(), true, didx);
+    pl.own_dig = add_job(nullptr, true, didx, nullptr, /*abs=*/true);
     if (pl.lm) pl.top_dig = add_job(sr.top.get(), true, tidx);
     qtot += q.I.size();
   }
@@ -745,7 +760,9 @@ void dist_open_batch(sg_dist* d, uint64_t R, uint64_t n2, std::vector<OpenReq>& 
       const uint64_t base = reinterpret_cast<uint64_t>(jb.src);
       uint64_t* a = addr.data() + (jb.digest ? nvals : 0) + jb.out0;
       for (size_t k = 0; k < jb.count; ++k)
-        a[k] = jb.tree ? digest_addr(jb.tree, idx[jb.idx0 + k]) : base + (jb.digest ? 64 : sizeof(fe)) * idx[jb.idx0 + k];
+        a[k] = jb.abs    ? idx[jb.idx0 + k]
+               : jb.tree ? digest_addr(jb.tree, idx[jb.idx0 + k])
+                         : base + (jb.digest ? 64 : sizeof(fe)) * idx[jb.idx0 + k];
     }
     DevBuf dA(ctx, addr.size() * 8), dV(ctx, std::max<size_t>(nvals, 1) * sizeof(fe)), dD(ctx, std::max<size_t>(ndig, 1) * 64);
     SG_HIP(hipMemcpyAsync(dA.get(), addr.data(), addr.size() * 8, hipMemcpyHostToDevice, ctx->stream));

@@ -13,6 +13,7 @@ namespace sg {
 // leaves per run) and the top tree over the G k1s run roots in global run order (every rank).
 struct ShardedRound {
   uint64_t k1s = 0, m = 0, per = 0;  // runs per rank, run roots overall, u64 per subtree
+  int drop = 0;                      // 1: the subtrees are lean (leaf digests not stored; rehashed)
   const fe* cw = nullptr;            // [k1s][R]
   DevBuf cw_own;
   DevBuf forest;
@@ -91,6 +92,7 @@ void dist_merkle_root(sg_dist* d, const fe* runs, uint64_t k1s, uint64_t R, uint
 // beforehand), then the all-gather of the run roots and the top tree on the context's stream
 struct PendingForest {
   uint64_t k1s = 0, R = 0, per = 0;
+  int drop = 0;  // lean subtrees: the leaf level is not stored (an opening rehashes the sibling leaf)
   DevBuf forest, roots;
 };
 void dist_forest_alloc(sg_dist* d, uint64_t k1s, uint64_t R, PendingForest& pf);

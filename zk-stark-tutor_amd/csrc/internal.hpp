@@ -14,6 +14,7 @@
 
 #include "../../include/stark_gpu.h"
 #include "context.hpp"
+#include "knobs.hpp"
 #include "fe128.hpp"
 #include "kernels.hpp"
 
@@ -142,11 +143,11 @@ size_t fri_num_rounds(const sg_fri* f);
 // fri.rs:88-113 (the reduced-index rejection included)
 void sample_indices(const uint8_t* seed, size_t seed_len, size_t size, size_t reduced_size, size_t number,
                     size_t* out);
-// SG_PROVE_TIMING=1: host-clock phase marks of the prover on stderr (diagnostics only)
+// SG_PROVE_TIMING=1 (A/B builds, knobs.hpp): host-clock phase marks of the prover on stderr
 struct PhaseMarks {
   bool on;
   std::chrono::steady_clock::time_point t0, last;
-  PhaseMarks() : on(getenv("SG_PROVE_TIMING") != nullptr), t0(std::chrono::steady_clock::now()), last(t0) {}
+  PhaseMarks() : on(SG_KNOB(PROVE_TIMING, 0) != 0), t0(std::chrono::steady_clock::now()), last(t0) {}
   void operator()(const char* name) {
     if (!on) return;
     auto now = std::chrono::steady_clock::now();

@@ -28,6 +28,7 @@
 #include "leaf_decimal.hpp"
 #include "kernels.hpp"
 #include "profiler.hpp"
+#include "knobs.hpp"
 #include "merkle_dev.hpp"
 
 // SG_NTT_ASM (default 1): the NTT kernels' field products and butterflies are the generated inline
@@ -763,137 +764,6 @@ __global__ void k_gather_abs(const uint64_t* __restrict__ addr, void* __restrict
   }
 }
 
-// ---------------------------------------------- FRI Fiat-Shamir on the device
-//
-// FRI::commit's per-round draw (fri.rs:136-146): push(Root) then alpha = Field::sample(
-// fiat_shamir_prover(32)), i.e. SHAKE256 over the serialized stream (proof_stream.rs:36-41,
-// proof_stream_enum.rs:161-190) -- continued on the device from the host sponge's state, so the
-// rounds of a native stream's commit are enqueued back to back with no host round trip.  One
-// lane: the sponge absorbs the 73-byte Root object [0][64 as u64 BE][digest], squeezes 32 bytes
-// from a padded copy, and the fold constant K = Montgomery(alpha offset_r^-1 2^-1) goes to memory
-// for the next round's fold (FoldLeaves::Kp).
-
-__device__ __forceinline__ uint64_t rotl64(uint64_t x, int n) { return n == 0 ? x : rotr64(x, 64 - n); }
-
-// Keccak-f[1600] on 25 lanes held in registers (constant indices only; rounds unrolled so the
-// round constants are immediates: no scratch, no constant-memory loads)
-__device__ __forceinline__ void keccak_round_dev(uint64_t (&a)[25], uint64_t rc) {
-  const uint64_t c0 = a[0] ^ a[5] ^ a[10] ^ a[15] ^ a[20], c1 = a[1] ^ a[6] ^ a[11] ^ a[16] ^ a[21];
-  const uint64_t c2 = a[2] ^ a[7] ^ a[12] ^ a[17] ^ a[22], c3 = a[3] ^ a[8] ^ a[13] ^ a[18] ^ a[23];
-  const uint64_t c4 = a[4] ^ a[9] ^ a[14] ^ a[19] ^ a[24];
-  const uint64_t d0 = c4 ^ rotl64(c1, 1), d1 = c0 ^ rotl64(c2, 1), d2 = c1 ^ rotl64(c3, 1);
-  const uint64_t d3 = c2 ^ rotl64(c4, 1), d4 = c3 ^ rotl64(c0, 1);
-  // theta + rho + pi: b[y, 2x + 3y] = rotl(a[x, y] ^ d[x], r[x, y])
-  const uint64_t b00 = a[0] ^ d0, b10 = rotl64(a[6] ^ d1, 44), b20 = rotl64(a[12] ^ d2, 43);
-  const uint64_t b30 = rotl64(a[18] ^ d3, 21), b40 = rotl64(a[24] ^ d4, 14);
-  const uint64_t b01 = rotl64(a[3] ^ d3, 28), b11 = rotl64(a[9] ^ d4, 20), b21 = rotl64(a[10] ^ d0, 3);
-  const uint64_t b31 = rotl64(a[16] ^ d1, 45), b41 = rotl64(a[22] ^ d2, 61);
-  const uint64_t b02 = rotl64(a[1] ^ d1, 1), b12 = rotl64(a[7] ^ d2, 6), b22 = rotl64(a[13] ^ d3, 25);
-  const uint64_t b32 = rotl64(a[19] ^ d4, 8), b42 = rotl64(a[20] ^ d0, 18);
-  const uint64_t b03 = rotl64(a[4] ^ d4, 27), b13 = rotl64(a[5] ^ d0, 36), b23 = rotl64(a[11] ^ d1, 10);
-  const uint64_t b33 = rotl64(a[17] ^ d2, 15), b43 = rotl64(a[23] ^ d3, 56);
-  const uint64_t b04 = rotl64(a[2] ^ d2, 62), b14 = rotl64(a[8] ^ d3, 55), b24 = rotl64(a[14] ^ d4, 39);
-  const uint64_t b34 = rotl64(a[15] ^ d0, 41), b44 = rotl64(a[21] ^ d1, 2);
-  // chi (+ iota on lane 0); row y holds b[0..4][y]
-  a[0] = b00 ^ (~b10 & b20) ^ rc;
-  a[1] = b10 ^ (~b20 & b30);
-  a[2] = b20 ^ (~b30 & b40);
-  a[3] = b30 ^ (~b40 & b00);
-  a[4] = b40 ^ (~b00 & b10);
-  a[5] = b01 ^ (~b11 & b21);
-  a[6] = b11 ^ (~b21 & b31);
-  a[7] = b21 ^ (~b31 & b41);
-  a[8] = b31 ^ (~b41 & b01);
-  a[9] = b41 ^ (~b01 & b11);
-  a[10] = b02 ^ (~b12 & b22);
-  a[11] = b12 ^ (~b22 & b32);
-  a[12] = b22 ^ (~b32 & b42);
-  a[13] = b32 ^ (~b42 & b02);
-  a[14] = b42 ^ (~b02 & b12);
-  a[15] = b03 ^ (~b13 & b23);
-  a[16] = b13 ^ (~b23 & b33);
-  a[17] = b23 ^ (~b33 & b43);
-  a[18] = b33 ^ (~b43 & b03);
-  a[19] = b43 ^ (~b03 & b13);
-  a[20] = b04 ^ (~b14 & b24);
-  a[21] = b14 ^ (~b24 & b34);
-  a[22] = b24 ^ (~b34 & b44);
-  a[23] = b34 ^ (~b44 & b04);
-  a[24] = b44 ^ (~b04 & b14);
-}
-
-__device__ __forceinline__ void keccak_f1600_dev(uint64_t (&a)[25]) {
-  keccak_round_dev(a, 0x0000000000000001ull); keccak_round_dev(a, 0x0000000000008082ull);
-  keccak_round_dev(a, 0x800000000000808aull); keccak_round_dev(a, 0x8000000080008000ull);
-  keccak_round_dev(a, 0x000000000000808bull); keccak_round_dev(a, 0x0000000080000001ull);
-  keccak_round_dev(a, 0x8000000080008081ull); keccak_round_dev(a, 0x8000000000008009ull);
-  keccak_round_dev(a, 0x000000000000008aull); keccak_round_dev(a, 0x0000000000000088ull);
-  keccak_round_dev(a, 0x0000000080008009ull); keccak_round_dev(a, 0x000000008000000aull);
-  keccak_round_dev(a, 0x000000008000808bull); keccak_round_dev(a, 0x800000000000008bull);
-  keccak_round_dev(a, 0x8000000000008089ull); keccak_round_dev(a, 0x8000000000008003ull);
-  keccak_round_dev(a, 0x8000000000008002ull); keccak_round_dev(a, 0x8000000000000080ull);
-  keccak_round_dev(a, 0x000000000000800aull); keccak_round_dev(a, 0x800000008000000aull);
-  keccak_round_dev(a, 0x8000000080008081ull); keccak_round_dev(a, 0x8000000000008080ull);
-  keccak_round_dev(a, 0x0000000080000001ull); keccak_round_dev(a, 0x8000000080008008ull);
-}
-
-// Two waves.  The sponge lanes live in LDS while the 73 object bytes are XORed in at their
-// (run-time) byte positions -- thread k handles byte k -- so no register array is indexed at run
-// time; thread 0 runs the permutations on the lanes loaded into registers by constant index.
-__global__ __launch_bounds__(128) void k_fri_fs(DevTranscript* __restrict__ fs, const uint64_t* __restrict__ root,
-                                               uint64_t* __restrict__ root_out, fe* __restrict__ k_out, fe C, fe r2) {
-  __shared__ uint64_t S[25];
-  __shared__ uint64_t S2[17];  // bytes past the current block (absorbed after its permutation)
-  const uint32_t k = threadIdx.x;
-  if (k < 25) S[k] = fs->st[k];
-  if (k < 17) S2[k] = 0;
-  if (k < 8) root_out[k] = root[k];
-  const uint32_t pos = fs->plen;  // bytes already in the current block (< 136)
-  __syncthreads();
-  // the Root object (proof_stream_enum.rs:67-127): code 0, payload length 64 (u64 BE), digest
-  constexpr uint32_t kObj = 73;  // <= blockDim.x
-  uint32_t byte = 0;
-  if (k == 8) byte = 64;
-  if (k >= 9 && k < kObj) byte = (uint32_t)(root[(k - 9) >> 3] >> (8 * ((k - 9) & 7))) & 0xFF;
-  uint8_t* Sb = reinterpret_cast<uint8_t*>(S);
-  uint8_t* S2b = reinterpret_cast<uint8_t*>(S2);
-  const uint32_t p = pos + k;
-  if (k < kObj && byte) {
-    if (p < 136) Sb[p] ^= (uint8_t)byte;  // distinct bytes per lane: no two lanes touch one byte
-    else S2b[p - 136] = (uint8_t)byte;
-  }
-  __syncthreads();
-  uint32_t npos = pos + kObj;
-  if (npos >= 136) {  // the block is complete: permute, then the spill bytes start the next one
-    if (k == 0) {
-      uint64_t a[25];
-#pragma unroll
-      for (int i = 0; i < 25; ++i) a[i] = S[i];
-      keccak_f1600_dev(a);
-#pragma unroll
-      for (int i = 0; i < 25; ++i) S[i] = a[i] ^ (i < 17 ? S2[i] : 0);
-    }
-    npos -= 136;
-    __syncthreads();
-  }
-  if (k < 25) fs->st[k] = S[k];
-  if (k == 0) fs->plen = npos;
-  __syncthreads();
-  // fiat_shamir_prover(32): pad (SHAKE256 suffix 0x1F at npos, final bit 0x80 at byte 135), squeeze
-  if (k == 0) {
-    Sb[npos] ^= 0x1F;
-    Sb[135] ^= 0x80;
-    uint64_t a[25];
-#pragma unroll
-    for (int i = 0; i < 25; ++i) a[i] = S[i];
-    keccak_f1600_dev(a);
-    // Field::sample (field.rs:87-99): the last 16 of the 32 bytes, big-endian, mod p (< 2p)
-    const uint64_t hi = __builtin_bswap64(a[2]), lo = __builtin_bswap64(a[3]);
-    fe alpha = fe_make(lo, hi);
-    if (!fe_is_canonical(alpha)) alpha = fe_sub_lazy(alpha, fe_make(1, 0xCB8ull << 52));
-    st_fe(k_out, mont_mul(mont_mul(alpha, r2), C));
-  }
-}
 
 // HBM copy probe (measurement only): one 16-byte element per lane, non-temporal loads and stores
 // (streamed data: no cache keeps it).  tools/microbench_copy.hip measured this flat form fastest
@@ -915,11 +785,6 @@ __global__ void __launch_bounds__(256) k_copy16_stride(const sg_u32x4* __restric
 // gather from a list of absolute device addresses (one launch for every round's openings)
 // ------------------------------------------------------------- launchers
 
-// tuning knob from the environment (plan experiments); `def` when unset
-static int env_int(const char* name, int def) {
-  const char* v = getenv(name);
-  return v && *v ? atoi(v) : def;
-}
 
 hipError_t launch_gather_digests(const uint64_t* tree, const uint64_t* idx, uint64_t* out, uint32_t count,
                                  hipStream_t s) {
@@ -960,12 +825,6 @@ hipError_t launch_gather_fe(const fe* src, const uint64_t* idx, fe* out, uint32_
 
 static inline unsigned nblocks(uint64_t n, unsigned bs) { return (unsigned)((n + bs - 1) / bs); }
 
-hipError_t launch_fri_fs(DevTranscript* fs, const uint64_t* root, uint64_t* root_out, fe* k_out, const fe& C,
-                         const fe& r2, hipStream_t s) {
-  ProfScope ps("fri_fs", 0, s);
-  hipLaunchKernelGGL(k_fri_fs, dim3(1), dim3(128), 0, s, fs, root, root_out, k_out, C, r2);
-  return hipGetLastError();
-}
 
 hipError_t launch_copy16(const void* src, void* dst, uint64_t bytes, unsigned blocks, hipStream_t s) {
   if (bytes < 16) return hipSuccess;
@@ -994,8 +853,8 @@ int ntt_tw_cut(int logn) {
   // twiddles: A/B on MI355X (tools/ab_ntt_tw.sh) -- at 2^22 and 2^25 the top three stages'
   // n/2 + n/4 + n/8 table entries cost more HBM time than one Montgomery product per twiddle,
   // deeper cuts trade too much VALU.  SG_NTT_TWCUT forces an absolute cut (experiments).
-  static const int top = env_int("SG_NTT_TWTOP", 3);
-  static const int forced = env_int("SG_NTT_TWCUT", 0);
+  static const int top = SG_KNOB(NTT_TWTOP, 3);
+  static const int forced = SG_KNOB(NTT_TWCUT, 0);
   int c = forced > 0 ? forced : (logn >= 15 ? logn - top : logn);
   if (c < 12) c = 12;
   return logn < c ? logn : c;
@@ -1082,10 +941,10 @@ hipError_t launch_ntt_dit(fe* const* data, int batch, const fe* tw, int logn, co
   if (ys && ys != ((uint64_t)1 << logn)) return hipErrorInvalidValue;  // rows are contiguous transforms
   const int np = ys ? 1 : batch;
   if (const hipError_t e = ntt_lds_attributes(); e != hipSuccess) return e;
-  static const bool use_rr = env_int("SG_NTT_RR", 1) != 0;  // register-direct first/last steps
+  static const bool use_rr = SG_KNOB(NTT_RR, 1) != 0;  // register-direct first/last steps
   const int big = big_tl;
   static const int tile_log = [] {
-    int t = env_int("SG_NTT_TILE_LOG", 11);  // A/B knob: 10, 11 or 12
+    int t = SG_KNOB(NTT_TILE_LOG, 11);  // A/B knob: 10, 11 or 12
     return (t >= 10 && t <= 12) ? t : 11;
   }();
   if (first_b0 >= logn) {
@@ -1166,7 +1025,7 @@ hipError_t launch_ntt_dit(fe* const* data, int batch, const fe* tw, int logn, co
 // Whole transform: fused bit-reversal first pass (when logn leaves room for a
 // later pass), then launch_ntt_dit from stage L1 + 1.  `out` must not alias `in`.
 bool ntt_small_whole(int logn, int batch, int skip, bool strided) {
-  static const bool on = env_int("SG_NTT_SMALL_WHOLE", 1) != 0;
+  static const bool on = SG_KNOB(NTT_SMALL_WHOLE, 1) != 0;
   return on && strided && logn >= 6 && logn <= 11 && skip <= logn - 3 && batch % (1 << (11 - logn)) == 0;
 }
 
@@ -1275,8 +1134,8 @@ int ntt_first_tile(int logn) {
   // 2^18-2^20 fastest with 2^12 tiles (11 + 7..9 stages: 2^20 0.148 -> 0.115 ms), 2^21 with 2^13
   // tiles (11 + 10: 0.202 -> 0.184 ms); at 2^22 and above the three-pass plan on 2048-element
   // tiles (4 blocks per CU) wins, and below 2^18 the launch count no longer matters
-  static const bool on = env_int("SG_NTT_TILES", 1) != 0;
-  static const int forced = env_int("SG_NTT_FIRST_TILE", 0);  // A/B knob: 10 .. 13 for every size
+  static const bool on = SG_KNOB(NTT_TILES, 1) != 0;
+  static const int forced = SG_KNOB(NTT_FIRST_TILE, 0);  // A/B knob: 10 .. 13 for every size
   if (forced >= 10 && forced <= 13) return forced;
   if (!on) return 11;
   if (logn >= 18 && logn <= 20) return 12;
@@ -1303,13 +1162,13 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
   //  * node levels with >= kQuadBelow digests: one lane per node, 3 levels fused;
   //  * smaller levels (latency-bound): a quad of lanes per node, up to 7 levels fused.
   // SG_MERKLE_QUAD_BELOW = log2 of the threshold (A/B only)
-  static const uint64_t kQuadBelow = (uint64_t)1 << env_int("SG_MERKLE_QUAD_BELOW", 16);
+  static const uint64_t kQuadBelow = (uint64_t)1 << SG_KNOB(MERKLE_QUAD_BELOW, 16);
   // forests (the sharded prove's run subtrees: thousands of trees of ~2^10 leaves per launch):
   // a node level with <= 2^SG_MERKLE_FOREST_QUAD digests per tree goes to the quad-lane kernel,
   // every level to each tree's root in one launch, however many trees the launch holds -- the
   // one-lane-per-node kernel would run blocks of count (< 64) lanes, i.e. partial waves, and
   // need two more launches per forest.  0 disables it (A/B knob).
-  static const int kForestQuad = env_int("SG_MERKLE_FOREST_QUAD", 6);
+  static const int kForestQuad = SG_KNOB(MERKLE_FOREST_QUAD, 6);
   int logn = 0;
   while (((uint64_t)1 << logn) < n) ++logn;
   int level = start_level;
@@ -1331,7 +1190,6 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
     a.fold.Thi = fold_here ? fold->Thi : nullptr;
     a.fold.shift = fold_here ? fold->shift : 0;
     a.fold.K = fold_here ? fold->K : fe_zero();
-    a.fold.Kp = fold_here ? fold->Kp : nullptr;
     a.leaves_ys = leaves_ys;
     a.tree_ys = tree_ys;
     a.root_level = (uint64_t)logn;
@@ -1340,16 +1198,16 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
     int fuse;
     unsigned bs;
     int kind;  // 0: leaf 256, 1: leaf tail 1024, 2: node 256, 3: quad 64, 4: leaf 512, 5: quad 256, 6: node 512, 8: leaf pairs 512,
-              // 7: quad leaves 256, 9: pipelined nodes 256, 10: node pairs 256, 11: nodes DPP 256, 12: quad leaves 64
+              // 7: quad leaves 256, 12: quad leaves 64
     // SG_MERKLE_QUAD_LEAF_BELOW = log2 of the leaf count (all trees of the launch) under which the
     // leaf level takes a quad per leaf (k_merkle_quad_leaves); 0 disables it (A/B knob)
-    static const int env_qleaf = env_int("SG_MERKLE_QUAD_LEAF_BELOW", 17);
+    static const int env_qleaf = SG_KNOB(MERKLE_QUAD_LEAF_BELOW, 17);
     if (level == 0 && env_qleaf > 0 && count * (uint64_t)batch < ((uint64_t)1 << env_qleaf)) {
       // latency-bound leaf level: up to 256 leaves per 1024-lane block, every level fused up to
       // the block's single digest (the whole tree when it has <= 256 leaves)
       // SG_MERKLE_QUAD_LEAF_NODES = leaves per block (256 or 64; A/B knob): a 256-leaf block puts
       // 16 waves on one CU, whose first levels then run at that CU's issue rate
-      static const int env_qln = env_int("SG_MERKLE_QUAD_LEAF_NODES", 256);
+      static const int env_qln = SG_KNOB(MERKLE_QUAD_LEAF_NODES, 256);
       const uint64_t qcap = env_qln == 64 ? 64 : 256;
       kind = qcap == 64 ? 12 : 7;
       const uint64_t nodes = count < qcap ? count : qcap;
@@ -1361,14 +1219,14 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
       if (count <= 64) {
         kind = 1; bs = (unsigned)count; fuse = logn + 1;
       } else {
-        static const int env_bs = env_int("SG_MERKLE_LEAF_BS", 512);
-        static const int env_fuse = env_int("SG_MERKLE_LEAF_FUSE", 4);
+        static const int env_bs = SG_KNOB(MERKLE_LEAF_BS, 512);
+        static const int env_fuse = SG_KNOB(MERKLE_LEAF_FUSE, 4);
         unsigned lbs = env_bs == 512 ? 512u : 256u;
         kind = lbs == 512 ? 4 : 0;
         bs = count < lbs ? (unsigned)count : lbs;
         // leaf levels of >= 2^SG_MERKLE_LEAF_FUSE_MIN leaves (all trees of the launch together, a
         // forest's subtrees included) fuse node levels (A/B knob)
-        static const int env_fmin = env_int("SG_MERKLE_LEAF_FUSE_MIN", 18);
+        static const int env_fmin = SG_KNOB(MERKLE_LEAF_FUSE_MIN, 18);
         fuse = count * (uint64_t)batch >= ((uint64_t)1 << env_fmin) ? env_fuse : 1;
         if (fuse < drop + 1) fuse = drop + 1;  // a lean tree's leaf launch reaches a stored level
         if (bs < lbs) kind = 0;
@@ -1380,7 +1238,7 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
         // two leaves per lane (k_merkle_leaf_pairs), 512 lanes per 1024 leaves, the same levels fused:
         // 2^25 tree 4.13 -> 4.08 ms, prove -0.15 ms (profiles/r03_ab_leaf_pairs.log).
         // SG_MERKLE_LEAF_PAIRS = 0 restores one leaf per lane; k > 1 fuses k - 1 levels more (A/B knob)
-        static const int env_pairs = env_int("SG_MERKLE_LEAF_PAIRS", 1);
+        static const int env_pairs = SG_KNOB(MERKLE_LEAF_PAIRS, 1);
         if (env_pairs > 0 && fuse >= 2 && count % 1024 == 0) {
           kind = 8;
           bs = 512;
@@ -1396,24 +1254,12 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
       // staged through LDS were slower (4.22-4.27 ms) and were dropped.  The level is
       // throughput-bound when all its trees together have >= kQuadBelow nodes (a forest of many
       // small subtrees included): one lane per node, blocks no larger than a tree's level.
-      static const int env_nfuse = env_int("SG_MERKLE_NODE_FUSE", 2);
-      static const int env_nbs = env_int("SG_MERKLE_NODE_BS", 256);  // A/B knob: 256 or 512
+      // (rejected and removed in round 6, their A/B logs kept: a grid-stride kernel prefetching the
+      // next group's children, r04_ab_node_pipe*; two nodes per lane, r04_ab_node_pairs*; the
+      // level-2 hand-over by DPP, r05_ab_node_dpp_* -- none beat this plan on the same box)
+      static const int env_nfuse = SG_KNOB(MERKLE_NODE_FUSE, 2);
+      static const int env_nbs = SG_KNOB(MERKLE_NODE_BS, 256);  // A/B knob: 256 or 512
       kind = env_nbs == 512 ? 6 : 2; bs = env_nbs == 512 ? 512u : 256u; fuse = env_nfuse;
-      // SG_MERKLE_NODE_PIPE=1: blocks walk several groups, the next group's children loaded while
-      // the current one hashes (k_merkle_nodes_pipe; A/B knob)
-      static const int env_pipe = env_int("SG_MERKLE_NODE_PIPE", 0);
-      if (env_pipe && kind == 2 && count % 256 == 0 && level + fuse - 1 < logn) kind = 9;
-      // SG_MERKLE_NODE_PAIRS=1: two nodes per lane and their parent in the lane (k_merkle_node_pairs),
-      // 256 lanes per 512 first-level nodes, the same levels fused (A/B knob)
-      static const int env_npairs = env_int("SG_MERKLE_NODE_PAIRS", 0);
-      if (env_npairs && kind == 2 && fuse >= 2 && count % 512 == 0) {
-        kind = 10;
-        if (fuse > 10) fuse = 10;  // two levels in the lane, then 256 -> 1 through LDS
-      }
-      // SG_MERKLE_NODE_DPP=1: levels 1 and 2 per launch with the level-2 hand-over by DPP inside each
-      // wave instead of LDS + a block barrier (k_merkle_nodes_dpp; A/B knob, round 5)
-      static const int env_ndpp = env_int("SG_MERKLE_NODE_DPP", 0);
-      if (env_ndpp && kind == 2 && fuse == 2 && count % 256 == 0 && level + 1 < logn) kind = 11;
       if (count < bs) {
         kind = 2;
         bs = (unsigned)count;  // a power of two (tree levels)
@@ -1424,9 +1270,9 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
     } else {
       // the last <= 256 nodes of a tree go to the root in one 1024-lane block
       // (SG_MERKLE_QUAD_TOP=0: 64-node blocks only)
-      static const int env_top = env_int("SG_MERKLE_QUAD_TOP", 1);
+      static const int env_top = SG_KNOB(MERKLE_QUAD_TOP, 1);
       // SG_MERKLE_QUAD_TOP_MAX = the largest level that one block takes to the root (A/B knob)
-      static const uint64_t top_max = (uint64_t)env_int("SG_MERKLE_QUAD_TOP_MAX", 256);
+      static const uint64_t top_max = (uint64_t)SG_KNOB(MERKLE_QUAD_TOP_MAX, 256);
       const uint64_t cap = (env_top && count <= top_max && count <= 256) ? 256 : 64;
       kind = cap == 256 ? 5 : 3;
       uint64_t nodes = count < cap ? count : cap;

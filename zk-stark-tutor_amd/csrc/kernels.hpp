@@ -62,19 +62,7 @@ struct FoldLeaves {
   const fe* Thi;
   int shift;
   fe K;
-  const fe* Kp = nullptr;  // != nullptr: K read from device memory (k_fri_fs) instead
 };
-// FRI commit's Fiat-Shamir continued on the device (k_fri_fs): the SHAKE256 sponge lanes with the
-// current partial block already XORed in, and the number of bytes in that block
-struct DevTranscript {
-  uint64_t st[25];
-  uint32_t plen;
-  uint32_t pad_;
-};
-// absorb the Root object of `root` (a tree's root digest, 8 u64), copy the digest to root_out,
-// squeeze 32 bytes and store K = Montgomery(sample(bytes) * C), C = Montgomery(offset_r^-1 2^-1)
-hipError_t launch_fri_fs(DevTranscript* fs, const uint64_t* root, uint64_t* root_out, fe* k_out, const fe& C,
-                         const fe& r2, hipStream_t s);
 // root_flag (optional, with root_host): set to root_seq after the root is visible to the host.
 // drop: a lean tree (n >= 2) -- the levels below `drop` are not stored: `tree` holds levels drop ..
 // log2 n, level l at digest offset (2n - 2(n >> l)) - (2n - 2(n >> drop)).

@@ -37,7 +37,7 @@ __global__ __launch_bounds__(MAXB) void k_merkle_levels(MerkleArgs a) {
         const fe x = ld_fe(a.fold.src + idx);
         const fe y = ld_fe(a.fold.src + idx + a.first_count);
         const uint64_t e = idx << a.fold.shift;
-        const fe K = a.fold.Kp ? ld_fe(a.fold.Kp) : a.fold.K;
+        const fe K = a.fold.K;
         fe t = mont_mul(K, ld_fe(a.fold.Tlo + (e & 4095)));
         t = mont_mul(t, ld_fe(a.fold.Thi + (e >> 12)));
         v = fe_add(fe_halve(fe_add(x, y)), mont_mul(fe_sub(x, y), t));
@@ -161,159 +161,9 @@ __global__ __launch_bounds__(MAXB) void k_merkle_leaf_pairs(MerkleArgs a) {
   }
 }
 
-// Node levels as k_merkle_levels<false, MAXB>, but each block walks groups g = blockIdx.x,
-// blockIdx.x + gridDim.x, ... (MAXB first-level nodes and their fused levels each) and issues the
-// NEXT group's child loads before hashing the current one: the 128 B of children per lane arrive
-// while the lane compresses, instead of every block starting with a full HBM round trip (the SQ
-// pass of the one-group kernel shows its waves parked on s_waitcnt / barriers 36 % of their
-// lifetime, against 25 % for the leaf kernel).  groups = first_count / MAXB (host-checked exact).
-template <int MAXB>
-__global__ __launch_bounds__(MAXB) void k_merkle_nodes_pipe(MerkleArgs a, uint64_t groups) {
-  __shared__ uint64_t sm[8][MAXB];
-  const uint32_t tid = threadIdx.x;
-  uint64_t* __restrict__ tree = merkle_tree_ptr(a);
-  const uint64_t* child = tree + a.off[0] * 8;
-  uint64_t nl[8], nr[8];
-  uint64_t g = blockIdx.x;
-  if (g < groups) {
-    const uint64_t idx = g * MAXB + tid;
-    ld_digest(child + (2 * idx) * 8, nl);
-    ld_digest(child + (2 * idx + 1) * 8, nr);
-  }
-  for (; g < groups; g += gridDim.x) {
-    uint64_t l[8], r[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      l[i] = nl[i];
-      r[i] = nr[i];
-    }
-    const uint64_t gn = g + gridDim.x;
-    if (gn < groups) {
-      const uint64_t idxn = gn * MAXB + tid;
-      ld_digest(child + (2 * idxn) * 8, nl);
-      ld_digest(child + (2 * idxn + 1) * 8, nr);
-    }
-    uint64_t d[8];
-    blake2b_node(l, r, d);
-    st_digest(tree + (a.off[1] + g * MAXB + tid) * 8, d);
-    uint32_t count = MAXB;
-    for (int lev = 1; lev < a.fuse; ++lev) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) sm[i][tid] = d[i];
-      __syncthreads();
-      count >>= 1;
-      if (tid < count) {
-        uint64_t cl[8], cr[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const ulonglong2 lr = *reinterpret_cast<const ulonglong2*>(&sm[i][2 * tid]);
-          cl[i] = lr.x;
-          cr[i] = lr.y;
-        }
-        blake2b_node(cl, cr, d);
-        st_digest(tree + (a.off[lev + 1] + g * count + tid) * 8, d);
-      }
-      __syncthreads();
-    }
-  }
-}
+// (round 6: the rejected node-level variants -- a grid-stride pipelined kernel, two nodes per
+// lane, the level-2 hand-over by DPP -- were removed; their same-box A/Bs stay in profiles/.)
 
-// Node levels 1 and 2 without LDS or a barrier (round-5 verdict item 2): lane pairs (2i, 2i + 1)
-// hold sibling digests after level 1, the odd lane's 8 words move to the even lane by DPP
-// (__shfl_xor 1 within the wave) and the even lanes hash the parent.  Every wave proceeds on its
-// own; the price is the odd lanes idling through the level-2 compression (the LDS form idles half
-// the block's waves at a barrier instead).  fuse == 2, first_count % 256 == 0 (host-checked).
-template <int MAXB>
-__global__ __launch_bounds__(MAXB) void k_merkle_nodes_dpp(MerkleArgs a) {
-  const uint32_t tid = threadIdx.x;
-  const uint64_t idx = (uint64_t)blockIdx.x * blockDim.x + tid;
-  uint64_t* __restrict__ tree = merkle_tree_ptr(a);
-  uint64_t* const root_slot = merkle_root_slot(a);
-  uint64_t d[8];
-  {
-    uint64_t l[8], r[8];
-    const uint64_t* child = tree + a.off[0] * 8;
-    ld_digest(child + (2 * idx) * 8, l);
-    ld_digest(child + (2 * idx + 1) * 8, r);
-    blake2b_node(l, r, d);
-    st_digest(tree + (a.off[1] + idx) * 8, d);
-  }
-  uint64_t r[8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i) {  // quad_perm [1, 0, 3, 2]: swap with the pair partner
-    const uint32_t lo = __builtin_amdgcn_update_dpp(0u, (uint32_t)d[i], 0xB1, 0xF, 0xF, true);
-    const uint32_t hi = __builtin_amdgcn_update_dpp(0u, (uint32_t)(d[i] >> 32), 0xB1, 0xF, 0xF, true);
-    r[i] = (uint64_t)lo | ((uint64_t)hi << 32);
-  }
-  if ((tid & 1) == 0) {
-    uint64_t p[8];
-    blake2b_node(d, r, p);
-    st_digest(tree + (a.off[2] + (idx >> 1)) * 8, p);
-    if (a.first_level + 1 == a.root_level && root_slot) {
-      for (int i = 0; i < 8; ++i) root_slot[i] = p[i];
-      merkle_root_publish(a, true);
-    }
-  }
-}
-
-// Node level with two nodes per lane, as k_merkle_leaf_pairs for the leaves: lane p reads its four
-// children (256 contiguous bytes), hashes nodes 2p and 2p + 1 of the first level and their parent
-// itself, so the first two levels keep all waves of the block busy (the one-node kernel's fused
-// levels leave 4, 2, 1 of 4 waves busy) and each lane has two independent compressions to
-// interleave while the other's loads are in flight.  first_count is a multiple of 2 * MAXB
-// (host-checked); levels 2 .. fuse-1 follow through LDS.
-template <int MAXB>
-__global__ __launch_bounds__(MAXB) __attribute__((amdgpu_waves_per_eu(4))) void k_merkle_node_pairs(MerkleArgs a) {
-  __shared__ uint64_t sm[8][MAXB];
-  const uint32_t tid = threadIdx.x;
-  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + tid;
-  uint64_t* __restrict__ tree = merkle_tree_ptr(a);
-  uint64_t* const root_slot = merkle_root_slot(a);
-  const uint64_t* child = tree + a.off[0] * 8 + (4 * p) * 8;
-  uint64_t d[8];
-  {
-    uint64_t c0[8], c1[8], c2[8], c3[8];
-    ld_digest(child, c0);
-    ld_digest(child + 8, c1);
-    ld_digest(child + 16, c2);
-    ld_digest(child + 24, c3);
-    uint64_t l[8], r[8];
-    blake2b_node(c0, c1, l);
-    blake2b_node(c2, c3, r);
-    st_digest(tree + (a.off[1] + 2 * p) * 8, l);
-    st_digest(tree + (a.off[1] + 2 * p + 1) * 8, r);
-    blake2b_node(l, r, d);
-    st_digest(tree + (a.off[2] + p) * 8, d);
-    if (a.first_level + 1 == a.root_level && root_slot) {
-      for (int i = 0; i < 8; ++i) root_slot[i] = d[i];
-      merkle_root_publish(a, true);
-    }
-  }
-  uint32_t count = blockDim.x;
-  for (int lev = 2; lev < a.fuse; ++lev) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i) sm[i][tid] = d[i];
-    __syncthreads();
-    count >>= 1;
-    if (tid < count) {
-      uint64_t l[8], r[8];
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        const ulonglong2 lr = *reinterpret_cast<const ulonglong2*>(&sm[i][2 * tid]);
-        l[i] = lr.x;
-        r[i] = lr.y;
-      }
-      blake2b_node(l, r, d);
-      const uint64_t gidx = (uint64_t)blockIdx.x * count + tid;
-      st_digest(tree + (a.off[lev + 1] + gidx) * 8, d);
-      if (a.first_level + lev == a.root_level && root_slot) {
-        for (int i = 0; i < 8; ++i) root_slot[i] = d[i];
-        merkle_root_publish(a, true);
-      }
-    }
-    __syncthreads();
-  }
-}
 
 // ---------------------------------------------------- Merkle: 4 lanes per hash
 //
@@ -503,7 +353,7 @@ __global__ __launch_bounds__(4 * NODES) void k_merkle_quad_leaves(MerkleArgs a) 
       const fe x = ld_fe(a.fold.src + leaf);
       const fe y = ld_fe(a.fold.src + leaf + a.first_count);
       const uint64_t e = leaf << a.fold.shift;
-      const fe K = a.fold.Kp ? ld_fe(a.fold.Kp) : a.fold.K;
+      const fe K = a.fold.K;
       fe t = mont_mul(K, ld_fe(a.fold.Tlo + (e & 4095)));
       t = mont_mul(t, ld_fe(a.fold.Thi + (e >> 12)));
       v = fe_add(fe_halve(fe_add(x, y)), mont_mul(fe_sub(x, y), t));
@@ -640,20 +490,7 @@ hipError_t launch_merkle_lanes(int kind, bool fold, dim3 grid, unsigned bs, hipS
       else hipLaunchKernelGGL((k_merkle_levels<true, 1024>), grid, dim3(bs), 0, s, a);
       break;
     case 2: hipLaunchKernelGGL((k_merkle_levels<false, 256>), grid, dim3(bs), 0, s, a); break;
-    case 9: {
-      // pipelined node levels: grid.x = the groups, run by at most `cap` resident blocks per tree
-      const uint64_t groups = grid.x;
-      static const uint64_t cap = [] {
-        const char* v = getenv("SG_MERKLE_NODE_PIPE_BLOCKS");  // blocks per launch row (A/B knob)
-        return (uint64_t)(v && atoi(v) > 0 ? atoi(v) : 1024);
-      }();
-      dim3 g2((unsigned)(groups < cap ? groups : cap), grid.y);
-      hipLaunchKernelGGL((k_merkle_nodes_pipe<256>), g2, dim3(bs), 0, s, a, groups);
-      break;
-    }
     case 6: hipLaunchKernelGGL((k_merkle_levels<false, 512>), grid, dim3(bs), 0, s, a); break;
-    case 10: hipLaunchKernelGGL((k_merkle_node_pairs<256>), grid, dim3(bs), 0, s, a); break;
-    case 11: hipLaunchKernelGGL((k_merkle_nodes_dpp<256>), grid, dim3(bs), 0, s, a); break;
     case 3: hipLaunchKernelGGL(k_merkle_quad<64>, grid, dim3(bs), 0, s, a); break;
     case 5: hipLaunchKernelGGL(k_merkle_quad<256>, grid, dim3(bs), 0, s, a); break;
     case 7:

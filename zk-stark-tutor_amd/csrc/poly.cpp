@@ -487,10 +487,9 @@ const fe* interp_kernel(sg_ctx* ctx, const fe& q, uint64_t D, int logf) {
 
 // decimation of the geometric interpolation: the largest f = 2^logf with n <= D / f, so the
 // interpolant (degree < n) is recovered from its values on the subgroup of order M = D / f
-// (SG_GEO_DECIMATE=0: the full-group form, f = 1)
-int geo_logf(uint64_t n, uint64_t D, bool env = true) {
-  const char* e = env ? getenv("SG_GEO_DECIMATE") : nullptr;
-  if (e && e[0] == '0') return 0;
+// (`decimate` false -- the context option geo_decimate = 0 -- the full-group form, f = 1)
+int geo_logf(uint64_t n, uint64_t D, bool decimate = true) {
+  if (!decimate) return 0;
   // M = D / f >= n, M >= 64, M / f >= 1 (rows of M / f inputs), f <= 16
   const int logD = ilog2_exact(D);
   int logf = 0;
@@ -499,11 +498,11 @@ int geo_logf(uint64_t n, uint64_t D, bool env = true) {
 }
 }  // namespace
 
-GeoPlan geo_plan(sg_ctx* ctx, const fe& q, uint64_t D, uint64_t n, GeoInterpCache* cache, bool env) {
+GeoPlan geo_plan(sg_ctx* ctx, const fe& q, uint64_t D, uint64_t n, GeoInterpCache* cache, bool use_option) {
   SG_REQUIRE(n > 1 && n < D && D && (D & (D - 1)) == 0, "geo_plan: 1 < n < D, D a power of two");
   GeoPlan P;
   const int logD = ilog2_exact(D);
-  const int logf = geo_logf(n, D, env);
+  const int logf = geo_logf(n, D, !use_option || ctx->opt.geo_decimate);
   const uint64_t M = D >> logf, f = (uint64_t)1 << logf;
   const fe qf = fe_pow(q, f);  // order M
   P.logf = logf;

@@ -128,8 +128,9 @@ struct GeoPlan {
   const fe* Zdi = nullptr;
   const fe* Khat = nullptr;
 };
-// env = false: ignore SG_GEO_DECIMATE (a sharded prove: every rank must take the same plan)
-GeoPlan geo_plan(sg_ctx* ctx, const fe& q, uint64_t D, uint64_t n, GeoInterpCache* cache, bool env = true);
+// use_option = false: ignore the context option geo_decimate (a sharded prove: every rank must take
+// the same plan)
+GeoPlan geo_plan(sg_ctx* ctx, const fe& q, uint64_t D, uint64_t n, GeoInterpCache* cache, bool use_option = true);
 // the interpolant of degree < n through (q^i, y_i), i < n <= D (ntt_arithmetics.rs:172-237), length n
 DPoly interpolate_geometric_dev(sg_ctx* ctx, const fe& q, uint64_t D, const fe* y, uint64_t n,
                                 GeoInterpCache* cache = nullptr);

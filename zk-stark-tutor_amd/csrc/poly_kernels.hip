@@ -16,6 +16,7 @@
 #include "fe128.hpp"
 #include "poly_kernels.hpp"
 #include "profiler.hpp"
+#include "knobs.hpp"
 
 namespace sg {
 
@@ -637,10 +638,7 @@ hipError_t launch_batch_div(fe* out, const fe* a, const fe* b, uint64_t n, const
   // K elements per lane amortize one Fermat inversion (~160 dependent products); below
   // ~2^17 lanes the chip is latency-bound on that chain, so small n trades the
   // amortization for lanes: K = 16 from n = 2^21, 8 from 2^20, else 4
-  static const int env_k = [] {
-    const char* v = getenv("SG_BATCH_DIV_K");
-    return v && *v ? atoi(v) : 0;
-  }();
+  static const int env_k = SG_KNOB(BATCH_DIV_K, 0);  // A/B builds: 4, 8 or 16 for every n
   const int K = env_k == 4 || env_k == 8 || env_k == 16 ? env_k : n >= ((uint64_t)1 << 21) ? 16 : n >= ((uint64_t)1 << 20) ? 8 : 4;
   uint64_t lanes = (n + K - 1) / K;  // at least one full block
   uint64_t blocks = (lanes + kBlock - 1) / kBlock;

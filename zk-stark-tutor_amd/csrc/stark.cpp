@@ -448,11 +448,6 @@ AirCoset air_coset(sg_ctx* ctx, const std::vector<DPoly>& trace_polys, uint64_t 
   return c;
 }
 
-// SG_AIR_GENERIC=1: evaluate a Rescue-Prime AIR through its expanded groups too (read per call)
-bool air_generic() {
-  const char* v = getenv("SG_AIR_GENERIC");
-  return v && *v && *v != '0';
-}
 
 // A Rescue-Prime row in its factored form (mpoly.hpp RescueAirForm) on the coset: the same values
 // as the expanded polynomial.  Its round-constant interpolants' coset values are public and kept
@@ -577,7 +572,7 @@ DPoly transition_values_rescue(sg_ctx* ctx, const RescueAirForm& f, const AirCos
 // they outlive the launch without a host wait.
 DPoly transition_values(sg_ctx* ctx, const MPoly& tc, const AirCoset& co, const fe& offset,
                         std::vector<DevBuf>& keep) {
-  if (tc.rescue && (int)co.var.size() == 2 * tc.rescue->m && !air_generic())
+  if (tc.rescue && (int)co.var.size() == 2 * tc.rescue->m && !ctx->opt.air_generic)  // option air_generic: the expanded groups
     return transition_values_rescue(ctx, *tc.rescue, co, offset, keep);
   const uint64_t L = co.L;
   const int nv = (int)co.var.size();
@@ -747,7 +742,7 @@ bool interpolate_geometric_batch_dist(sg_dist* dd, const fe& q, uint64_t D, cons
   const int G = dist_world(dd);
   if (!dist_shard_algebra(dd) || n <= 1 || n >= D) return false;
   GeoInterpCache local;
-  const GeoPlan P = geo_plan(ctx, q, D, n, &local, /*env=*/false);
+  const GeoPlan P = geo_plan(ctx, q, D, n, &local, /*use_option=*/false);
   const uint64_t M = P.M, f = (uint64_t)1 << P.logf, Mf = M >> P.logf;
   if (P.logf < 1 || !dist_can_shard(M, G)) return false;
   uint64_t n1, n2;
@@ -1279,9 +1274,8 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
   uint64_t r_seq = 0, bq_seq;
   // where the side stream forks off the randomizer LDE + tree: 0 = at the start (beside the trace
   // interpolation), 1 = after the interpolation, 2 = after the boundary quotients
-  // (SG_PROVE_R_FORK, scheduling experiments; the bytes are the same)
-  const char* rf = getenv("SG_PROVE_R_FORK");
-  const int r_fork = rf ? atoi(rf) : 0;
+  // (SG_PROVE_R_FORK in A/B builds, scheduling experiments; the bytes are the same)
+  const int r_fork = SG_KNOB(PROVE_R_FORK, 0);
   (void)ctx->stage_twiddles(st.omega, ilog2_exact(next_pow2(Nf)));
   (void)ctx->pow_table(g, 4096);
   (void)ctx->pow_table(fe_pow(g, 4096), (std::max<uint64_t>(nrc, 1) + 4095) / 4096);
@@ -1421,11 +1415,10 @@ void stark_prove_dist(sg_dist* dd, const sg_stark& st, const fe* d_trace, size_t
   }
   // one rank: its "shard" is the whole domain and every collective an identity, so the single-GPU
   // prove is the plan (same bytes; at the headline the four-step path costs ~6 ms more per proof).
-  // SG_DIST_WORLD1_SHARDED=1 forces the four-step path anyway (tests that exercise the sharded
-  // machinery over a one-rank RCCL communicator; one rank, so no cross-rank agreement is needed).
+  // The context option world1_sharded forces the four-step path anyway (tests that exercise the
+  // sharded machinery over a one-rank RCCL communicator; one rank, so no cross-rank agreement).
   if (G == 1) {
-    const char* f = getenv("SG_DIST_WORLD1_SHARDED");
-    if (!(f && *f && *f != '0')) {
+    if (!ctx->opt.world1_sharded) {
       stark_prove(ctx, st, d_trace, rows, tcs, bnd, d_trace_rand, d_rcoef, nrc, ps);
       return;
     }

@@ -52,8 +52,9 @@ void ByteBuf::swap(ByteBuf& o) {
 }
 
 bool ByteBuf::pin() {
-  // SG_STREAM_NO_PIN: callers take their staging fallback (tests exercise it this way)
-  if (!p || getenv("SG_STREAM_NO_PIN")) return false;
+  // (a context with option stream_pin = 0 does not call this: its callers take their staging
+  // fallback, which the tests exercise that way)
+  if (!p) return false;
   if (pinned_p == p) return true;
   unpin();
   if (hipHostRegister(p, cap, hipHostRegisterDefault) != hipSuccess) {
@@ -223,13 +224,6 @@ void Stream::fiat_shamir_all(size_t num_bytes, uint8_t* out) {
   const size_t tail = total - fs_absorbed;
   fs_gather(fs_absorbed, tail, tmp);
   fs_sponge.finish(tmp, tail, out, num_bytes);
-}
-
-void Stream::fs_snapshot(uint64_t lanes[25], uint8_t* pending, size_t* pending_len) {
-  const size_t total = fs_absorb_full();
-  memcpy(lanes, fs_sponge.st, sizeof(fs_sponge.st));
-  *pending_len = total - fs_absorbed;
-  fs_gather(fs_absorbed, *pending_len, pending);
 }
 
 bool deserialize_stream(const uint8_t* b, size_t len, Stream& s, std::string& err) {

@@ -75,10 +75,6 @@ struct Stream {
   void fiat_shamir(size_t count, size_t num_bytes, uint8_t* out) const;
   // fiat_shamir(count(), ...) with the incremental cache above
   void fiat_shamir_all(size_t num_bytes, uint8_t* out);
-  // brings the incremental sponge up to date (every complete 136-byte block of fs_head || body
-  // absorbed) and returns its lanes and the pending partial block: the state a device-side
-  // Fiat-Shamir chain continues from (capi.cpp fri_commit_dev)
-  void fs_snapshot(uint64_t lanes[25], uint8_t* pending, size_t* pending_len);
 
  private:
   size_t fs_absorb_full();

@@ -69,6 +69,7 @@ PROTOTYPES = {
     "sg_ctx_stream": (_vp, [_vp]),
     "sg_ctx_trim": (ctypes.c_int, [_vp]),
     "sg_ctx_cached_tables": (ctypes.c_int, [_vp, _P(_sz), _P(_sz)]),
+    "sg_ctx_set_option": (ctypes.c_int, [_vp, ctypes.c_char_p, ctypes.c_int64]),
     "sg_ctx_memory": (ctypes.c_int, [_vp, _P(ctypes.c_uint64), _P(ctypes.c_uint64), _P(ctypes.c_uint64),
                                      _P(ctypes.c_uint64), _P(ctypes.c_uint64), ctypes.c_int]),
     "sg_hbm_copy_probe": (ctypes.c_int, [_vp, _sz, ctypes.c_int, ctypes.c_uint, _P(ctypes.c_double)]),

@@ -14,6 +14,7 @@ and converted.  Every compute call runs the HIP kernels; there is no CPU path.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 from typing import Iterable, List, Optional, Sequence, Tuple, Union
 
@@ -131,6 +132,20 @@ class Context:
 
     def trim(self) -> None:
         self.check(self._lib.sg_ctx_trim(self.handle))
+
+    def set_option(self, name: str, value) -> None:
+        """sg_ctx_set_option: "domain_cache", "air_generic", "geo_decimate", "lean_trees", "stream_pin",
+        "world1_sharded", "lean_drop" -- equivalent paths (same proof bytes) that the tests compare."""
+        self.check(self._lib.sg_ctx_set_option(self.handle, name.encode(), int(value)))
+
+    @contextlib.contextmanager
+    def option(self, name: str, value, default):
+        """set_option(name, value) for a `with` block, then back to `default`."""
+        self.set_option(name, value)
+        try:
+            yield self
+        finally:
+            self.set_option(name, default)
 
     def cached_tables(self) -> Tuple[int, int]:
         """(public domain / AIR tables, twiddle tables) the context keeps (sg_ctx_cached_tables)."""
