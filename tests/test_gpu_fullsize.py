@@ -311,3 +311,56 @@ def test_c5_native_dist_2p27_world1_rccl(c5_reference):
         assert torch.equal(back, shard), "sg_dist_intt at world 1"
     finally:
         nd.close()
+
+
+def _c5_rccl_worker(rank, world, port, logn):
+    """One rank per GPU over RCCL: the sharded NTT of a 2^logn input (every rank builds the same
+    input) against the single-GPU transform this rank computes of the whole input."""
+    import torch
+    import torch.distributed as dist
+    from starkgpu import dist as D
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)  # carries the RCCL unique id only
+    try:
+        ctx = sg.Context(rank)
+        nd = D.NativeDist(ctx, transport="rccl")
+        n = 1 << logn
+        rng = np.random.default_rng(2028)
+        x = rng.integers(0, 2**63, size=(n, 2), dtype=np.uint64)
+        x[:, 1] %= np.uint64(0xCB80000000000000)
+        root = o.primitive_nth_root(n)
+        X = sg.ntt(root, x, ctx=ctx)
+        n1, n2 = nd.plan(n, world)
+        rows, R = n1 // world, n2 // world
+        cols = np.ascontiguousarray(x.reshape(n2, n1, 2)[:, rank * rows:(rank + 1) * rows].transpose(1, 0, 2))
+        del x
+        dev = torch.device("cuda", rank)
+        shard = torch.from_numpy(cols.view(np.int64).reshape(-1)).to(dev)
+        del cols
+        runs = nd.ntt(root, shard, n2, n)
+        ok = bool(np.array_equal(runs.cpu().numpy().view(np.uint64).reshape(n1, R, 2),
+                                 X.reshape(n1, n2, 2)[:, rank * R:(rank + 1) * R]))
+        ok_inv = bool(torch.equal(nd.intt(root, runs, n), shard))
+        flags = [None] * world
+        dist.all_gather_object(flags, (ok, ok_inv))
+        assert all(f[0] and f[1] for f in flags), f"RCCL sharded NTT 2^{logn} at world {world}: {flags}"
+        nd.close()
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(900)
+def test_c5_multi_gpu_rccl_chunked_exchange():
+    """the RCCL exchange's chunked path at more than one rank.  2^28 points over 2 GPUs
+    (one rank each): every rank's all-to-all moves 2 GiB, above the 1 GiB one RCCL call carries
+    correctly, so it goes as grouped send / receive chunks between the GPUs --
+    bit-identical to the single-GPU transform, and inverted.  Skipped on a one-GPU box."""
+    import torch
+    import torch.multiprocessing as mp
+    if torch.cuda.device_count() < 2:
+        pytest.skip("needs >= 2 GPUs (one RCCL rank per device)")
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    mp.spawn(_c5_rccl_worker, args=(2, port, 28), nprocs=2, join=True)

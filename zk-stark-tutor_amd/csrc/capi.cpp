@@ -772,10 +772,19 @@ void path_indices(const sg_tree* t, uint64_t index, std::vector<uint64_t>& idx) 
 
 // the gather address of digest `i` of tree t (launch_gather_abs): a lean tree's leaf digest is
 // tagged (bit 0) as the address of the leaf value to rehash
+// absolute address of digest i (levels concatenated from the leaves up) of a tree; a lean tree's
+// dropped digest (level lv < drop <= 3) is named by its 2^lv-leaf block's first value | 1 | lv << 1,
+// which k_gather_abs rehashes
 uint64_t digest_addr(const sg_tree* t, uint64_t i) {
-  SG_REQUIRE(t->drop <= 1, "gathers rehash the leaf level only");
-  if (t->drop && i < t->n) return ((uint64_t)(uintptr_t)(t->leaves + i)) | 1;
-  return (uint64_t)(uintptr_t)t->buf.get() + 64 * (i - (2 * t->n - 2 * (t->n >> t->drop)));  // levels >= drop
+  SG_REQUIRE(t->drop <= 3, "gathers rehash at most three dropped levels");
+  const uint64_t dropped = 2 * t->n - 2 * (t->n >> t->drop);
+  if (i < dropped) {
+    int lv = 0;
+    while (i >= 2 * t->n - 2 * (t->n >> (lv + 1))) ++lv;
+    const uint64_t p = i - (2 * t->n - 2 * (t->n >> lv));  // position within level lv
+    return ((uint64_t)(uintptr_t)(t->leaves + (p << lv))) | 1 | ((uint64_t)lv << 1);
+  }
+  return (uint64_t)(uintptr_t)t->buf.get() + 64 * (i - dropped);  // levels >= drop
 }
 
 void gather_digests(sg_ctx* ctx, const sg_tree* t, const std::vector<uint64_t>& idx, uint8_t* out) {

@@ -401,11 +401,12 @@ void dist_forest_alloc(sg_dist* d, uint64_t k1s, uint64_t R, PendingForest& pf) 
   SG_REQUIRE(R >= 1 && (R & (R - 1)) == 0 && k1s >= 1 && (k1s & (k1s - 1)) == 0, "Leafs len must be power of two");
   pf.k1s = k1s;
   pf.R = R;
-  // lean subtrees (R >= 2): levels 1 .. log2 R stored, R - 1 digests instead of 2R - 1 -- the leaf
-  // digests are half a forest's bytes (64 B per codeword element per rank), and an opening rehashes
-  // its sibling leaf from the run (k_gather_abs) instead of reading it
-  pf.drop = R >= 2 ? 1 : 0;
-  pf.per = (merkle_tree_digests(R) - (pf.drop ? R : 0)) * 8;  // u64 per subtree
+  // lean subtrees, like the single-GPU prove's trees: the lowest min(3, log2 R) levels are not
+  // stored (2R / 8 - 1 digests per subtree instead of 2R - 1: 16 B per codeword element per rank
+  // instead of 128), and an opening rehashes each dropped sibling -- a leaf, or the root of its 2- or
+  // 4-leaf block -- from the run (k_gather_abs)
+  pf.drop = std::min(std::min(ilog2_exact(R), 3), d->ctx->opt.lean_trees ? d->ctx->opt.lean_drop : 0);
+  pf.per = (merkle_tree_digests(R) - (2 * R - 2 * (R >> pf.drop))) * 8;  // u64 per subtree
   pf.forest = DevBuf(d->ctx, k1s * pf.per * 8);
   pf.roots = DevBuf(d->ctx, k1s * 64);
 }
@@ -418,8 +419,8 @@ void dist_forest_launch(sg_dist* d, const fe* runs, PendingForest& pf, hipStream
     uint64_t* tr = pf.forest.as<uint64_t>() + t0 * pf.per;
     SG_HIP(launch_merkle_tree(&lv, &tr, cnt, pf.R, nullptr, s, pf.R, pf.per, 0, nullptr, 0, nullptr, pf.drop));
   }
-  // the subtree roots: digest 2R - 2 of a full subtree, R - 2 of a lean one
-  const uint64_t root_digest = 2 * pf.R - 2 - (pf.drop ? pf.R : 0);
+  // the subtree roots: digest 2R - 2 of a full subtree, less the dropped levels' digests
+  const uint64_t root_digest = 2 * pf.R - 2 - (2 * pf.R - 2 * (pf.R >> pf.drop));
   SG_HIP(launch_gather_roots(pf.forest.as<uint64_t>(), pf.per, root_digest * 8, pf.roots.as<uint64_t>(), pf.k1s, s));
 }
 
@@ -668,7 +669,7 @@ void dist_fri_commit(sg_dist* d, const sg_fri* f, const fe* runs, uint64_t n, co
   sub.domain_length = length;
   SG_REQUIRE(fri_num_rounds(&sub) == rounds - r, "FRI tail round count mismatch");
   if (keep) {
-    fri_commit_dev(ctx, &sub, full.as<fe>(), length, ps, keep->tail, /*borrow_input=*/false, /*drop=*/1);
+    fri_commit_dev(ctx, &sub, full.as<fe>(), length, ps, keep->tail, /*borrow_input=*/false, /*drop=*/3);
     for (uint64_t l : keep->tail.lengths) keep->lengths.push_back(l);
     return;
   }
@@ -735,14 +736,17 @@ void dist_open_batch(sg_dist* d, uint64_t R, uint64_t n2, std::vector<OpenReq>& 
       const uint64_t k1 = i / n2, c = i % R;
       pl.own.push_back(k);
       eidx.push_back(k1 * R + c);
-      // absolute addresses of the subtree path: a lean subtree's leaf-level sibling is its value in
-      // the run (bit 0 set: k_gather_abs rehashes it), the levels above sit R digests earlier
+      // absolute addresses of the subtree path: a dropped sibling (level lv < drop) is named by the
+      // first value of its 2^lv-leaf block in the run, | 1 | lv << 1 (k_gather_abs rehashes it); the
+      // stored levels sit level_offset(R, drop) digests earlier in the lean subtree
       const uint64_t fbase = reinterpret_cast<uint64_t>(sr.forest.get()) + 64 * k1 * (sr.per / 8);
+      const uint64_t dropped = level_offset(R, sr.drop);
       for (int lv = 0; lv < lr; ++lv) {
+        const uint64_t sib = (c >> lv) ^ 1;
         if (lv < sr.drop)
-          didx.push_back(reinterpret_cast<uint64_t>(sr.cw + k1 * R + (c ^ 1)) | 1);
+          didx.push_back(reinterpret_cast<uint64_t>(sr.cw + k1 * R + (sib << lv)) | 1 | ((uint64_t)lv << 1));
         else
-          didx.push_back(fbase + 64 * (level_offset(R, lv) - (sr.drop ? R : 0) + ((c >> lv) ^ 1)));
+          didx.push_back(fbase + 64 * (level_offset(R, lv) - dropped + sib));
       }
     }
     pl.own_vals = add_job(sr.cw, false, eidx);

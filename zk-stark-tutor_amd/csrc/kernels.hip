@@ -748,7 +748,33 @@ __global__ void k_gather_fe(const fe* __restrict__ src, const uint64_t* __restri
   st_fe(out + i, ld_fe(src + idx[i]));
 }
 
-// DIGEST: an address with bit 0 set is a lean tree's leaf value, rehashed (merkle_root.rs:25-30)
+// DIGEST: an address with bit 0 set names a digest a lean tree did not store: bits 1-2 are its
+// level lv (0..2), the address (16-byte aligned) the first value of its 2^lv-leaf block, and the
+// digest is rehashed -- the leaf (merkle_root.rs:25-30) or the block's subtree root
+// (blake2b(left || right) upwards, merkle_root.rs:7-19)
+__device__ __forceinline__ void subtree_rehash(const fe* lp, int lv, uint64_t d[8]) {
+  if (lv == 0) {
+    leaf_hash(ld_fe(lp), d);
+    return;
+  }
+  uint64_t a[8], b[8], n0[8];
+  const int pairs = 1 << (lv - 1);  // lv 1: one node over 2 leaves; lv 2: two nodes, then the root
+  for (int k = 0; k < pairs; ++k) {
+    leaf_hash(ld_fe(lp + 2 * k), a);
+    leaf_hash(ld_fe(lp + 2 * k + 1), b);
+    if (k == 0) blake2b_node(a, b, n0);
+    else blake2b_node(a, b, d);
+  }
+  if (lv == 1) {
+#pragma unroll
+    for (int w = 0; w < 8; ++w) d[w] = n0[w];
+  } else {
+#pragma unroll
+    for (int w = 0; w < 8; ++w) b[w] = d[w];
+    blake2b_node(n0, b, d);
+  }
+}
+
 template <bool DIGEST>
 __global__ void k_gather_abs(const uint64_t* __restrict__ addr, void* __restrict__ out, uint32_t count) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -756,7 +782,7 @@ __global__ void k_gather_abs(const uint64_t* __restrict__ addr, void* __restrict
   if constexpr (DIGEST) {
     uint64_t d[8];
     const uint64_t ad = addr[i];
-    if (ad & 1) leaf_hash(ld_fe(reinterpret_cast<const fe*>(ad & ~1ull)), d);
+    if (ad & 1) subtree_rehash(reinterpret_cast<const fe*>(ad & ~15ull), (int)((ad >> 1) & 3), d);
     else ld_digest(reinterpret_cast<const uint64_t*>(ad), d);
     st_digest(static_cast<uint64_t*>(out) + (uint64_t)i * 8, d);
   } else {
