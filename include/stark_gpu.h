@@ -67,6 +67,9 @@ int sg_ctx_cached_tables(const sg_ctx* ctx, size_t* domain_tables, size_t* twidd
  *   "world1_sharded" 0 (default): a one-rank communicator proves through the single-GPU plan; 1:
  *                    through the four-step path (tests of the sharded machinery over RCCL)
  *   "lean_drop"      3 (default): the most levels a lean tree drops (0..3; 0 = keep every level)
+ *   "fri_gate"       1 (default): FRI::commit queues round r+1's fold + tree behind a device gate
+ *                    before round r's challenge exists (the host raises the gate after writing K;
+ *                    a gate left 60 s raises an error); 0: each round is launched after its challenge
  * SG_ERR_INVALID for an unknown name. */
 int sg_ctx_set_option(sg_ctx* ctx, const char* name, int64_t value);
 /* Device memory (no reference counterpart): `live` = bytes of the context's buffer pool in use,

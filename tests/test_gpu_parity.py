@@ -323,6 +323,53 @@ def test_fri_prove_tail_paths_match_oracle(stream_kind, monkeypatch):
     assert gps.digest() == ops.digest()
 
 
+class _FsFailsAfter(o.IndependentProofStream):
+    """A foreign proof stream whose Fiat-Shamir callback raises from its (after+1)-th call on."""
+
+    def __init__(self, after):
+        super().__init__()
+        self.calls, self.after = 0, after
+
+    def fiat_shamir_prover(self, num_bytes):
+        self.calls += 1
+        if self.calls > self.after:
+            raise RuntimeError("injected Fiat-Shamir failure")
+        return super().fiat_shamir_prover(num_bytes)
+
+
+def test_fri_gate_bytes_and_release_on_callback_failure():
+    """Option fri_gate (default on): round r + 1's fold + tree are queued behind a device gate
+    (k_fri_gate) before round r's challenge exists, and the host raises the gate once it has
+    written K.  Gate on and off write the oracle's bytes.  A Fiat-Shamir callback failing while a
+    gated round is queued (first, second, fourth challenge; and the query seed, after the last
+    round) raises at once -- the pending gate is released, the stream drains instead of waiting
+    for the gate's 60 s deadline -- and the context proves the oracle's bytes afterwards."""
+    import time
+    n, exp, c = 1 << 14, 8, 64
+    omega, cw = _fri_case(n, exp, c, 41)
+    ofri = o.FRI(o.GENERATOR, omega, n, exp, c)
+    ops = o.IndependentProofStream()
+    otop = ofri.prove(cw, ops)
+    gfri = sg.FRI(o.GENERATOR, omega, n, exp, c)
+    ctx = sg.Context.default()
+    for gate in (1, 0):
+        with ctx.option("fri_gate", gate, 1):
+            gps = sg.IndependentProofStream()
+            assert gfri.prove(cw, gps) == otop
+            assert gps.digest() == ops.digest()
+    # 2^14 -> 2^8: six rounds, five challenges, then the query seed (the sixth call)
+    for after in (0, 1, 3, 5):
+        t0 = time.perf_counter()
+        bad = _FsFailsAfter(after)
+        with pytest.raises(RuntimeError, match="injected"):  # the callback's own exception, re-raised
+            gfri.prove(cw, bad)
+        assert time.perf_counter() - t0 < 10, "the pending gate was not released"
+        assert bad.calls == after + 1
+    gps = sg.IndependentProofStream()
+    assert gfri.prove(cw, gps) == otop
+    assert gps.digest() == ops.digest()
+
+
 def test_fri_tampered_codeword_rejected():
     """fri.rs:514-528: zeroing a third of the low-degree positions makes verify fail."""
     n, exp, c = 256, 4, 17

@@ -277,6 +277,7 @@ extern "C" int sg_ctx_create(int device, sg_ctx** out) {
   ctx->opt.stream_pin = getenv("SG_STREAM_NO_PIN") == nullptr;
   ctx->opt.world1_sharded = ab_knob("SG_DIST_WORLD1_SHARDED", 0) != 0;
   ctx->opt.lean_drop = std::min(std::max(ab_knob("SG_LEAN_DROP", 3), 0), 3);
+  ctx->opt.fri_gate = ab_knob("SG_FRI_GATE", 1) != 0;
 #endif
   // the main stream (the prove's critical path) at the highest priority, the side stream (its
   // Merkle trees, which otherwise hold every CU while a small main-stream kernel waits) at the
@@ -294,14 +295,16 @@ extern "C" int sg_ctx_create(int device, sg_ctx** out) {
   void* pinned_dev = nullptr;
   // root slots (64 B) + ready flags (u64) + the division zero flag (u32, padded), host-coherent
   constexpr size_t kSlots = sg_ctx::kRootSlots;
-  constexpr size_t kPinned = kSlots * 64 + kSlots * 8 + 64;
+  constexpr size_t kPinned = kSlots * 64 + kSlots * 8 + 64 + 64;  // + the FRI gate block
   if (hipStreamCreateWithPriority(&ctx->side, hipStreamNonBlocking, prio ? prio_low : 0) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&ctx->ev_join, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&ctx->ev_tail, hipEventDisableTiming) != hipSuccess ||
       hipHostMalloc(&pinned, kPinned, hipHostMallocMapped | hipHostMallocCoherent) != hipSuccess ||
       hipHostGetDevicePointer(&pinned_dev, pinned, 0) != hipSuccess) {
     if (ctx->ev_fork) (void)hipEventDestroy(ctx->ev_fork);
     if (ctx->ev_join) (void)hipEventDestroy(ctx->ev_join);
+    if (ctx->ev_tail) (void)hipEventDestroy(ctx->ev_tail);
     if (ctx->side) (void)hipStreamDestroy(ctx->side);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
@@ -312,6 +315,16 @@ extern "C" int sg_ctx_create(int device, sg_ctx** out) {
   memset(pinned, 0, kPinned);
   ctx->div_zero_flag = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(pinned) + kSlots * 72);
   ctx->div_zero_flag_dev = reinterpret_cast<uint32_t*>(reinterpret_cast<uint8_t*>(pinned_dev) + kSlots * 72);
+  {
+    uint8_t* gh = reinterpret_cast<uint8_t*>(pinned) + kSlots * 72 + 64;
+    uint8_t* gd = reinterpret_cast<uint8_t*>(pinned_dev) + kSlots * 72 + 64;
+    ctx->gate_word = reinterpret_cast<uint64_t*>(gh);
+    ctx->gate_timeout = reinterpret_cast<uint32_t*>(gh + 8);
+    ctx->gate_k = reinterpret_cast<uint64_t*>(gh + 16);
+    ctx->gate_word_dev = reinterpret_cast<uint64_t*>(gd);
+    ctx->gate_timeout_dev = reinterpret_cast<uint32_t*>(gd + 8);
+    ctx->gate_k_dev = reinterpret_cast<uint64_t*>(gd + 16);
+  }
   *out = ctx;
   return SG_OK;
 }
@@ -329,6 +342,7 @@ extern "C" void sg_ctx_destroy(sg_ctx* ctx) {
   if (ctx->pinned_roots) (void)hipHostFree(ctx->pinned_roots);
   (void)hipEventDestroy(ctx->ev_fork);
   (void)hipEventDestroy(ctx->ev_join);
+  (void)hipEventDestroy(ctx->ev_tail);
   (void)hipStreamDestroy(ctx->side);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
@@ -436,6 +450,7 @@ extern "C" int sg_ctx_set_option(sg_ctx* ctx, const char* name, int64_t value) {
   else if (n == "stream_pin") ctx->opt.stream_pin = v;
   else if (n == "world1_sharded") ctx->opt.world1_sharded = v;
   else if (n == "lean_drop" && value >= 0 && value <= 3) ctx->opt.lean_drop = (int)value;
+  else if (n == "fri_gate") ctx->opt.fri_gate = v;
   else {
     ctx->last_error = "unknown context option: " + n;
     return SG_ERR_INVALID;
@@ -1024,19 +1039,21 @@ void ObjWriter::commit() {
   if (!direct) push_obj(ps, code, scratch.data(), scratch.size());
 }
 
-void TailWriter::value(const fe* d_src) {
+void TailWriter::value(const fe* base, uint32_t sel, uint64_t mask) {
   TailItem it{};
-  it.src[0] = (uint64_t)(uintptr_t)d_src;
+  it.src[0] = (uint64_t)(uintptr_t)base;
   it.dst = bytes;
   it.code = SG_OBJ_VALUE;
   it.count = 1;
+  it.sel = sel;
+  it.mask = mask;
   items.push_back(it);
   offs.push_back(bytes);
   bytes += 9 + 16;
   field = true;
 }
 
-void TailWriter::leafs(const fe* a, const fe* b, const fe* c) {
+void TailWriter::leafs(const fe* a, const fe* b, const fe* c, uint32_t sel, uint64_t mask) {
   TailItem it{};
   it.src[0] = (uint64_t)(uintptr_t)a;
   it.src[1] = (uint64_t)(uintptr_t)b;
@@ -1044,36 +1061,61 @@ void TailWriter::leafs(const fe* a, const fe* b, const fe* c) {
   it.dst = bytes;
   it.code = SG_OBJ_LEAFS;
   it.count = 3;
+  it.sel = sel;
+  it.mask = mask;
   items.push_back(it);
   offs.push_back(bytes);
   bytes += 9 + 48;
   field = true;
 }
 
-void TailWriter::path(const sg_tree* t, uint64_t index) {
+void TailWriter::path(const sg_tree* t, uint32_t sel, uint64_t mask, uint64_t add) {
   SG_REQUIRE(t->logn <= 64, "tree too deep");
+  // k_serialize_tail rehashes a lean tree's 2^drop-leaf block in LDS sized for 8 leaves
+  SG_REQUIRE(t->drop <= 3, "lean tree drops more than 3 levels");
   TailItem it{};
   it.src[0] = (uint64_t)(uintptr_t)t->buf.get();
   it.src[1] = (uint64_t)(uintptr_t)t->leaves;  // lean: the low siblings are rehashed from these
   it.src[2] = (uint64_t)t->drop;
   it.dst = bytes;
   it.n = t->n;
-  it.index = index;
+  it.index = add;
   it.code = SG_OBJ_PATH;
   it.count = (uint32_t)t->logn;
+  it.sel = sel;
+  it.mask = mask;
   items.push_back(it);
   offs.push_back(bytes);
   bytes += 9 + 72 * (size_t)t->logn;
 }
 
-void TailWriter::flush(sg_ctx* ctx, const sg_proof_stream* ps) {
+void TailWriter::upload(sg_ctx* ctx, size_t n) {
+  table_n = n;
+  const size_t ib = items.size() * sizeof(TailItem);
+  stage = static_cast<uint8_t*>(ctx->staging(0, ib + 8 * n));
+  dev = DevBuf(ctx, ib + 8 * n);
+  if (ib) {
+    // on the side stream (idle by now): the copy overlaps the main stream's last FRI round instead of
+    // queueing behind it (no main-stream work still queued can hold `dev`: the host has waited for
+    // every root but the last, whose kernels use only the round state's buffers)
+    memcpy(stage, items.data(), ib);
+    SG_HIP(hipMemcpyAsync(dev.get(), stage, ib, hipMemcpyHostToDevice, ctx->side));
+    SG_HIP(hipEventRecord(ctx->ev_tail, ctx->side));
+  }
+}
+
+void TailWriter::flush(sg_ctx* ctx, const sg_proof_stream* ps, const uint64_t* table) {
   if (items.empty()) return;
-  const size_t ni = items.size();
-  TailItem* up = static_cast<TailItem*>(ctx->staging(0, ni * sizeof(TailItem)));
-  memcpy(up, items.data(), ni * sizeof(TailItem));
-  DevBuf di(ctx, ni * sizeof(TailItem)), dout(ctx, bytes);
-  SG_HIP(hipMemcpyAsync(di.get(), up, ni * sizeof(TailItem), hipMemcpyHostToDevice, ctx->stream));
-  SG_HIP(launch_serialize_tail(di.as<TailItem>(), (uint32_t)ni, dout.as<uint8_t>(), bytes, ctx->stream));
+  SG_REQUIRE(stage != nullptr, "tail items were not uploaded");
+  const size_t ni = items.size(), ib = ni * sizeof(TailItem);
+  uint64_t* dtable = reinterpret_cast<uint64_t*>(dev.as<uint8_t>() + ib);
+  if (table_n) {
+    memcpy(stage + ib, table, 8 * table_n);
+    SG_HIP(hipMemcpyAsync(dtable, stage + ib, 8 * table_n, hipMemcpyHostToDevice, ctx->stream));
+  }
+  DevBuf dout(ctx, bytes);
+  SG_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_tail, 0));  // the items' upload
+  SG_HIP(launch_serialize_tail(dev.as<TailItem>(), dtable, (uint32_t)ni, dout.as<uint8_t>(), bytes, ctx->stream));
   if (ps->push == stream_push_cb) {
     // a native stream: the block lands in its body by one device copy (or through staging when the
     // runtime refuses to page-lock the body)
@@ -1101,6 +1143,8 @@ void TailWriter::flush(sg_ctx* ctx, const sg_proof_stream* ps) {
   offs.clear();
   bytes = 0;
   field = false;
+  stage = nullptr;
+  table_n = 0;
 }
 
 void put_u128_be_at(uint8_t* out, const fe& a) {
@@ -1117,7 +1161,7 @@ void put_u128_be(std::vector<uint8_t>& out, const fe& a) {
 
 // fri.rs:115-172.  Retains every round's codeword and tree in `st`.
 void fri_commit_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, const sg_proof_stream* ps,
-                    sg_fri_state& st, bool borrow_input, int drop) {
+                    sg_fri_state& st, bool borrow_input, int drop, const std::function<void()>& after_last) {
   SG_REQUIRE(ps && ps->push && ps->fiat_shamir_prover, "proof stream callbacks required");
   size_t rounds = fri_num_rounds(f);
   SG_REQUIRE(rounds >= 1, "FRI: zero rounds for this domain");
@@ -1161,56 +1205,110 @@ void fri_commit_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, co
       len /= 2;
     }
   }
-  // lean trees over the round codewords the state keeps (the query phase rehashes a leaf sibling)
-  std::vector<std::unique_ptr<sg_tree>> trees(rounds);
+  // lean trees over the round codewords the state keeps (the query phase rehashes a leaf sibling);
+  // every round's tree exists from here on (the query items are planned before the last root)
+  SG_REQUIRE(st.trees.empty(), "FRI state already committed");
+  st.trees.resize(rounds);
   for (size_t r = 0; r < rounds; ++r) {
     if (r + 1 < rounds) {
       st.codewords.emplace_back(ctx, (plan[r].len / 2) * sizeof(fe));
       st.cw.push_back(st.codewords.back().as<fe>());
       st.lengths.push_back(plan[r].len / 2);
     }
-    trees[r] = new_tree(ctx, plan[r].len, st.cw[r], drop);
+    st.trees[r] = new_tree(ctx, plan[r].len, st.cw[r], drop);
   }
+  // the fri.rs:133 order check of every round before any launch: omega_r = omega^(2^r), so all
+  // rounds pass when round 0 does, and a failing round 0 has pushed nothing -- the same error at
+  // the same point of the stream as the reference's per-round check
+  for (size_t r = 0; r < rounds; ++r)
+    SG_REQUIRE(fe_eq(fe_pow(plan[r].omega, plan[r].len - 1), plan[r].winv),
+               "error in commit: omega does not have the right order!");
   // Round r >= 1 hashes the fold of round r-1 in the same launch that computes it
   // (the fold is written out too: later rounds and the query phase read it).
-  FoldLeaves fold{};
   // (round 3's device-side Fiat-Shamir -- a one-wave Keccak per round instead of the host round
   // trip -- was byte-identical but slower, profiles/r03_ab_devfs*.log, and was removed in round 6)
-  const uint64_t last_len = st.lengths.back();
-  fe* last = nullptr;  // the last codeword on the host (pinned staging)
-  for (size_t r = 0; r < rounds; ++r) {
-    const uint64_t len = plan[r].len;
-    // assert omega^(n-1) == omega^-1 (fri.rs:133)
-    SG_REQUIRE(fe_eq(fe_pow(plan[r].omega, len - 1), plan[r].winv),
-               "error in commit: omega does not have the right order!");
-    if (r + 1 < rounds) {
-      fill_tree(ctx, st.cw[r], trees[r].get(), r ? &fold : nullptr);
-    } else {
-      // the last round's codeword (its leaves, folded by its own leaf kernel) is copied to the
-      // host right behind its tree, so the copy lands while the host waits for the root
-      const uint64_t seq = fill_tree_launch(ctx, st.cw[r], trees[r].get(), r ? &fold : nullptr);
-      last = static_cast<fe*>(ctx->staging(1, last_len * sizeof(fe)));
-      SG_HIP(hipMemcpyAsync(last, st.cw.back(), last_len * sizeof(fe), hipMemcpyDeviceToHost, ctx->stream));
-      fill_tree_finish(ctx, trees[r].get(), seq);
+  //
+  // Option fri_gate (default): round r + 1's fold + tree are queued before round r's root is
+  // awaited, behind k_fri_gate, which holds the stream until the host has written K and raised the
+  // gate word -- the launches leave the host <-> device round trip between two rounds.  On any
+  // exception the pending gate is raised (the queued round computes with a stale K and is
+  // discarded), so the stream never stays blocked.
+  const bool gated = ctx->opt.fri_gate && rounds >= 2;
+  DevBuf kdev;  // K of the gated round (declared first: the gate is raised before it is released)
+  struct GateRelease {
+    sg_ctx* c;
+    uint64_t pending = 0;
+    ~GateRelease() {
+      if (pending) __atomic_store_n(c->gate_word, pending, __ATOMIC_RELEASE);
     }
-    st.trees.push_back(std::move(trees[r]));
-    push_obj(ps, SG_OBJ_ROOT, st.trees.back()->root, 64);
+  } gate{ctx};
+  if (gated) {
+    kdev = DevBuf(ctx, sizeof(fe));
+    __atomic_store_n(ctx->gate_timeout, 0u, __ATOMIC_RELAXED);
+  }
+  constexpr double kGateSeconds = 60.0;
+  const uint64_t last_len = st.lengths.back();
+  // the last codeword on the host (pinned staging, allocated before any gate is pending)
+  fe* last = static_cast<fe*>(ctx->staging(1, last_len * sizeof(fe)));
+  // The last round's codeword (its leaves, folded by its own leaf kernel) is copied to the host
+  // right behind its tree, so the copy lands while the host waits for the root.  A gated last
+  // round is copied only once its gate is raised: the runtime may complete a small device-to-host
+  // copy on the host, waiting for the stream -- behind a pending gate that wait never ends.
+  auto copy_last = [&]() {
+    SG_HIP(hipMemcpyAsync(last, st.cw.back(), last_len * sizeof(fe), hipMemcpyDeviceToHost, ctx->stream));
+    if (after_last) after_last();
+  };
+  std::vector<uint64_t> seqs(rounds);
+  auto launch_round = [&](size_t r, const fe* K) {
+    if (r == 0) {
+      seqs[0] = fill_tree_launch(ctx, st.cw[0], st.trees[0].get(), nullptr);
+    } else {
+      // c'[i] = (c[i] + c[i + n/2]) / 2 + K w_r^-i (c[i] - c[i + n/2]), K = alpha offset_r^-1 2^-1,
+      // w_r^-i = w^-(i << r) from the round-0 tables
+      FoldLeaves fold{};
+      fold.src = st.cw[r - 1];
+      fold.dst = const_cast<fe*>(st.cw[r]);
+      fold.Tlo = Tlo;
+      fold.Thi = Thi;
+      fold.shift = (int)(r - 1);
+      if (K) {
+        fold.K = *K;
+      } else {
+        const uint64_t want = ++ctx->gate_seq;
+        gate.pending = want;
+        SG_HIP(launch_fri_gate(ctx->gate_word_dev, want, ctx->gate_k_dev, kdev.as<fe>(), ctx->gate_timeout_dev,
+                               kGateSeconds, ctx->stream));
+        fold.Kp = kdev.as<fe>();
+      }
+      seqs[r] = fill_tree_launch(ctx, st.cw[r], st.trees[r].get(), &fold);
+    }
+    if (r + 1 == rounds && !gated) copy_last();
+  };
+  launch_round(0, nullptr);
+  for (size_t r = 0; r < rounds; ++r) {
+    if (gated && r + 1 < rounds) launch_round(r + 1, nullptr);
+    fill_tree_finish(ctx, st.trees[r].get(), seqs[r]);
+    push_obj(ps, SG_OBJ_ROOT, st.trees[r]->root, 64);
     if (r == rounds - 1) break;
     uint8_t chal[32];
     if (ps->fiat_shamir_prover(ps->user, 32, chal) != 0)
       throw Error{SG_ERR_CALLBACK, "proof stream fiat_shamir callback failed"};
     fe alpha = fe_sample(chal, 32);
-    // c'[i] = (c[i] + c[i + n/2]) / 2 + K w_r^-i (c[i] - c[i + n/2]), K = alpha offset_r^-1 2^-1,
-    // w_r^-i = w^-(i << r) from the round-0 tables
-    fold.src = st.cw[r];
-    fold.dst = const_cast<fe*>(st.cw[r + 1]);
-    fold.Tlo = Tlo;
-    fold.Thi = Thi;
-    fold.shift = (int)r;
-    fold.K = to_mont(fe_mul(fe_mul(alpha, plan[r].oinv), inv2));
+    const fe K = to_mont(fe_mul(fe_mul(alpha, plan[r].oinv), inv2));
+    if (gated) {
+      ctx->gate_k[0] = fe_lo(K);
+      ctx->gate_k[1] = fe_hi(K);
+      __atomic_store_n(ctx->gate_word, gate.pending, __ATOMIC_RELEASE);
+      gate.pending = 0;
+      if (r + 2 == rounds) copy_last();
+    } else {
+      launch_round(r + 1, &K);
+    }
   }
   // push last codeword (fri.rs:166)
   host_wait(ctx, ctx->stream);
+  if (gated && __atomic_load_n(ctx->gate_timeout, __ATOMIC_ACQUIRE))
+    throw Error{SG_ERR_HIP, "FRI round gate timed out (no challenge within 60 s)"};
   ObjWriter w{ps};
   uint8_t* payload = w.begin(SG_OBJ_CODEWORD, last_len * 16);
   for (uint64_t i = 0; i < last_len; ++i) put_u128_be_at(payload + 16 * i, last[i]);
@@ -1249,45 +1347,50 @@ void sample_indices(const uint8_t* seed, size_t seed_len, size_t size, size_t re
 }
 
 void fri_prove_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, const sg_proof_stream* ps,
-                   size_t* top, const std::function<void(const size_t* top, TailWriter& tw)>& extra) {
+                   size_t* top, const TailExtra* extra) {
   PhaseMarks mark;
   sg_fri_state st;
-  fri_commit_dev(ctx, f, d_cw, n, ps, st, /*borrow_input=*/true);
+  const size_t c = f->num_colinearity_tests;
+  // Every opening of every round follows from the top indices (fri.rs:174-208, 231-245): the
+  // Leafs / Path objects of all rounds, in the reference's order, and the caller's `extra` objects
+  // are planned as items over an index table (entry s < c: top[s], masked to the round's half
+  // length -- top % (len_r / 2), the reference's repeated reduction) and uploaded while the last
+  // round's tree runs; the seed then only yields the table, serialized in one launch.
+  TailWriter tw;
+  auto plan = [&]() {
+    if (st.codewords.size() < 2) return;  // reported after the commit, where the reference panics
+    const size_t R = st.codewords.size() - 1;  // query rounds
+    tw.items.reserve(R * 4 * c + (extra ? 2 * extra->count * 4 : 0));
+    tw.offs.reserve(tw.items.capacity());
+    for (size_t r = 0; r < R; ++r) {
+      const uint64_t half = st.lengths[r] / 2;
+      const uint64_t mask = half - 1;  // round lengths are powers of two (Merkle leaves)
+      const fe* cur = st.cw[r];
+      const fe* nxt = st.cw[r + 1];
+      for (size_t s = 0; s < c; ++s) tw.leafs(cur, cur + half, nxt, (uint32_t)s, mask);
+      const sg_tree* tc = st.trees[r].get();
+      const sg_tree* tn = st.trees[r + 1].get();
+      for (size_t s = 0; s < c; ++s) {
+        tw.path(tc, (uint32_t)s, mask);
+        tw.path(tc, (uint32_t)s, mask, half);
+        tw.path(tn, (uint32_t)s, mask);
+      }
+    }
+    if (extra && extra->plan) extra->plan(tw, (uint32_t)c);
+    tw.upload(ctx, c + (extra ? extra->count : 0));
+  };
+  fri_commit_dev(ctx, f, d_cw, n, ps, st, /*borrow_input=*/true, 3, plan);
   mark("fri_commit");
-  SG_REQUIRE(st.codewords.size() >= 2, "FRI prove needs at least two rounds (reference indexes codewords[1])");
+  SG_REQUIRE(tw.stage != nullptr, "FRI prove needs at least two rounds (reference indexes codewords[1])");
   uint8_t seed[32];
   if (ps->fiat_shamir_prover(ps->user, 32, seed) != 0)
     throw Error{SG_ERR_CALLBACK, "proof stream fiat_shamir callback failed"};
-  const size_t c = f->num_colinearity_tests;
   sample_indices(seed, 32, st.lengths[1], st.lengths.back(), c, top);
   mark("fri_sample_indices");
-  // Every opening of every round is known once the top indices are: the Leafs / Path objects of
-  // all rounds, in the reference's order (fri.rs:174-208, 231-245), are serialized on the device
-  // in one launch together with the caller's `extra` objects.
-  const size_t R = st.codewords.size() - 1;  // query rounds
-  TailWriter tw;
-  // the query phase's 4c objects per round, plus room for a STARK's openings (2 objects at up
-  // to 4c indices for up to 4 codewords): one allocation instead of repeated growth
-  tw.items.reserve(R * 4 * c + 32 * c);
-  tw.offs.reserve(R * 4 * c + 32 * c);
-  std::vector<size_t> indices(top, top + c);
-  for (size_t r = 0; r < R; ++r) {
-    const uint64_t len = st.lengths[r];
-    for (auto& i : indices) i = i % (len / 2);
-    const fe* cur = st.cw[r];
-    const fe* nxt = st.cw[r + 1];
-    for (size_t s = 0; s < c; ++s) tw.leafs(cur + indices[s], cur + indices[s] + len / 2, nxt + indices[s]);
-    const sg_tree* tc = st.trees[r].get();
-    const sg_tree* tn = st.trees[r + 1].get();
-    for (size_t s = 0; s < c; ++s) {
-      tw.path(tc, indices[s]);
-      tw.path(tc, indices[s] + len / 2);
-      tw.path(tn, indices[s]);
-    }
-  }
-  if (extra) extra(top, tw);
-  mark("fri_query_items");
-  tw.flush(ctx, ps);  // the round states stay alive until the serialization has read them
+  std::vector<uint64_t> table(top, top + c);
+  if (extra && extra->indices) extra->indices(top, table);
+  SG_REQUIRE(table.size() == tw.table_n, "tail index table size");
+  tw.flush(ctx, ps, table.data());  // the round states stay alive until the serialization has read them
   mark("fri_query_push");
 }
 

@@ -67,6 +67,7 @@ struct sg_ctx {
   // second stream: Merkle trees overlapped with the main stream's algebra (stark_prove)
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  hipEvent_t ev_tail = nullptr;  // the proof tail's item upload (side stream) done
   std::string last_error;
   // set while a communicator call runs on this context (dist.cpp DistWatch): every host wait
   // (sg::host_wait, the tree-root spin) polls it; it throws -- after aborting the communicator --
@@ -94,6 +95,15 @@ struct sg_ctx {
   // the host at points where the stream has already drained past the divisions
   uint32_t* div_zero_flag = nullptr;      // host view (inside the pinned_roots allocation)
   uint32_t* div_zero_flag_dev = nullptr;  // device view
+  // FRI round gate (k_fri_gate, inside the pinned_roots allocation): the u64 gate word the host
+  // raises, the timeout word the kernel raises, the Montgomery K (2 u64) the host writes first
+  uint64_t* gate_word = nullptr;  // host views
+  uint32_t* gate_timeout = nullptr;
+  uint64_t* gate_k = nullptr;
+  uint64_t* gate_word_dev = nullptr;  // device views
+  uint32_t* gate_timeout_dev = nullptr;
+  uint64_t* gate_k_dev = nullptr;
+  uint64_t gate_seq = 0;  // last gate value handed out (monotonic over the context's life)
   bool async_dev = false;                // sg_ctx_set_async: _dev transforms return once enqueued
   // per-kernel event timing (sg_ctx_profile)
   bool profiling = false;
@@ -127,6 +137,7 @@ struct sg_ctx {
     bool stream_pin = true;      // native proof streams page-lock their buffer for device copies
     bool world1_sharded = false; // a one-rank communicator proves through the four-step path
     int lean_drop = 3;           // the most levels a lean tree drops (0..3)
+    bool fri_gate = true;        // FRI rounds queued behind a device gate before their challenge
   } opt;
   bool domain_cache_on() const { return opt.domain_cache; }
   void* domain_table(const std::vector<uint64_t>& key) const;

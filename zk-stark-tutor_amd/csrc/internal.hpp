@@ -173,25 +173,44 @@ void put_u128_be_at(uint8_t* out, const fe& a);
 void put_u128_be(std::vector<uint8_t>& out, const fe& a);
 // drop: the round trees' levels not kept (lean trees; the sharded prove's tail keeps drop <= 1, which
 // its absolute-address openings rehash)
+// after_last: called once the last round's fold + tree are launched (and its gate raised), while the
+// host waits for that root -- the FRI prove plans and uploads its query items there
 void fri_commit_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, const sg_proof_stream* ps,
-                    sg_fri_state& st, bool borrow_input = false, int drop = 3);
+                    sg_fri_state& st, bool borrow_input = false, int drop = 3,
+                    const std::function<void()>& after_last = {});
 // Objects pushed after a proof's last Fiat-Shamir draw (the FRI query phase, fri.rs:174-208, and
 // the Stark openings, stark.rs:524-560): collected as TailItems, serialized by one device launch
 // (k_serialize_tail) and appended with one copy -- straight into a native stream's page-locked
-// body, else pushed object by object to the callback stream from pinned staging.
+// body, else pushed object by object to the callback stream from pinned staging.  Every object's
+// index is entry `sel` of an index table (masked by `mask`): the items are planned and uploaded
+// before the indices exist, and only the table follows the seed.
 struct TailWriter {
   std::vector<TailItem> items;
   std::vector<size_t> offs;  // header offset of each object in the block
   size_t bytes = 0;
   bool field = false;        // a Value / Leafs object (sets the stream's field header)
-  void value(const fe* d_src);
-  void leafs(const fe* a, const fe* b, const fe* c);
-  void path(const sg_tree* t, uint64_t index);
-  void flush(sg_ctx* ctx, const sg_proof_stream* ps);
+  DevBuf dev;                // uploaded items, then the table
+  uint8_t* stage = nullptr;  // pinned staging (slot 0): items, then the table
+  size_t table_n = 0;
+  // Value base[idx]; Leafs a[idx], b[idx], c[idx]; the Path of leaf add + idx (idx = table[sel] & mask)
+  void value(const fe* base, uint32_t sel, uint64_t mask = ~0ull);
+  void leafs(const fe* a, const fe* b, const fe* c, uint32_t sel, uint64_t mask);
+  void path(const sg_tree* t, uint32_t sel, uint64_t mask, uint64_t add = 0);
+  // the items to the device ahead of the table (of table_n entries)
+  void upload(sg_ctx* ctx, size_t table_n);
+  // the table (table_n entries), the serialization launch and the append
+  void flush(sg_ctx* ctx, const sg_proof_stream* ps, const uint64_t* table);
 };
-// fri.rs:210-248.  `extra`, when given, appends further tail objects after the query phase's
-// (called with the top-level indices) so they share its single serialization launch and copy.
+// The objects a caller appends after the query phase's (the Stark openings), sharing its launch:
+// `plan` adds them with table entries sel0 .. sel0 + count - 1, `indices` appends those entries
+// once the top-level indices are known.
+struct TailExtra {
+  size_t count = 0;
+  std::function<void(TailWriter& tw, uint32_t sel0)> plan;
+  std::function<void(const size_t* top, std::vector<uint64_t>& table)> indices;
+};
+// fri.rs:210-248 (+ the caller's `extra` objects)
 void fri_prove_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, const sg_proof_stream* ps,
-                   size_t* top, const std::function<void(const size_t* top, TailWriter& tw)>& extra = {});
+                   size_t* top, const TailExtra* extra = nullptr);
 
 }  // namespace sg

@@ -708,6 +708,39 @@ __global__ __launch_bounds__(256) void k_fri_fold_runs(FoldRunsArgs a) {
   }
 }
 
+// FRI round gate (fri_commit_dev): a round's fold + tree are queued before its challenge exists;
+// this one-lane kernel holds the stream until the host has written K (Montgomery, pinned) and
+// raised the gate word to `want`, then copies K into device memory for the fold kernel.  The
+// wait is bounded (`ticks` of the 100 MHz wall clock): on expiry it raises the timeout word and
+// returns, the host reports it as an error.
+__global__ void k_fri_gate(const uint64_t* gate, uint64_t want, const uint64_t* Kh, fe* Kd, uint32_t* timeout,
+                           uint64_t ticks) {
+  if (threadIdx.x != 0) return;
+  const uint64_t t0 = wall_clock64();
+  while (__hip_atomic_load(gate, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < want) {
+    if (wall_clock64() - t0 > ticks) {
+      __hip_atomic_fetch_or(timeout, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+  const uint64_t lo = __hip_atomic_load(Kh, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  const uint64_t hi = __hip_atomic_load(Kh + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  fe k;
+  k.w[0] = (uint32_t)lo;
+  k.w[1] = (uint32_t)(lo >> 32);
+  k.w[2] = (uint32_t)hi;
+  k.w[3] = (uint32_t)(hi >> 32);
+  st_fe(Kd, k);
+}
+
+hipError_t launch_fri_gate(const uint64_t* gate, uint64_t want, const uint64_t* Kh, fe* Kd, uint32_t* timeout,
+                           double seconds, hipStream_t s) {
+  const uint64_t ticks = (uint64_t)(seconds * 1e8);  // wall_clock64 counts at 100 MHz
+  hipLaunchKernelGGL(k_fri_gate, dim3(1), dim3(64), 0, s, gate, want, Kh, Kd, timeout, ticks);
+  return hipGetLastError();
+}
+
 // roots of `count` strided trees (root digest at tree + y * tree_ys + root_off) -> contiguous
 __global__ void k_gather_roots(const uint64_t* __restrict__ tree, uint64_t tree_ys, uint64_t root_off,
                                uint64_t* __restrict__ out, uint64_t count) {
@@ -1216,6 +1249,7 @@ hipError_t launch_merkle_tree(const fe* const* leaves, uint64_t* const* tree, in
     a.fold.Thi = fold_here ? fold->Thi : nullptr;
     a.fold.shift = fold_here ? fold->shift : 0;
     a.fold.K = fold_here ? fold->K : fe_zero();
+    a.fold.Kp = fold_here ? fold->Kp : nullptr;
     a.leaves_ys = leaves_ys;
     a.tree_ys = tree_ys;
     a.root_level = (uint64_t)logn;

@@ -62,7 +62,12 @@ struct FoldLeaves {
   const fe* Thi;
   int shift;
   fe K;
+  const fe* Kp = nullptr;  // non-null: K is read from this device word (written by k_fri_gate)
 };
+// FRI round gate: holds stream s until *gate >= want (host-coherent memory, device views), then
+// stores the Montgomery K at Kh (2 u64, pinned) to Kd; after `seconds` it raises *timeout instead
+hipError_t launch_fri_gate(const uint64_t* gate, uint64_t want, const uint64_t* Kh, fe* Kd, uint32_t* timeout,
+                           double seconds, hipStream_t s);
 // root_flag (optional, with root_host): set to root_seq after the root is visible to the host.
 // drop: a lean tree (n >= 2) -- the levels below `drop` are not stored: `tree` holds levels drop ..
 // log2 n, level l at digest offset (2n - 2(n >> l)) - (2n - 2(n >> drop)).
@@ -91,6 +96,11 @@ hipError_t launch_gather_cols(fe* out, const fe* in, uint64_t len, uint64_t rows
 // digests start at src[0] (merkle_root.rs:34-53 order, proof_stream_enum.rs:95-126); for a lean
 // tree src[2] = K > 0 levels are not stored (the digests at src[0] start at level K) and its first
 // K siblings are rehashed from the leaf values at src[1].
+// An item with sel != kTailLiteral is resolved on the device from an index table: idx =
+// table[sel] & mask, then a Value / Leafs item reads src[k] + 16 idx and a Path item opens leaf
+// index + idx -- the items exist before the indices do (the query phase's are planned while the
+// last FRI round runs and uploaded then; only the table follows the Fiat-Shamir seed).
+constexpr uint32_t kTailLiteral = 0xFFFFFFFFu;
 struct TailItem {
   uint64_t src[3];
   uint64_t dst;
@@ -98,8 +108,12 @@ struct TailItem {
   uint64_t index;
   uint32_t code;
   uint32_t count;
+  uint32_t sel;
+  uint32_t pad;
+  uint64_t mask;
 };
-hipError_t launch_serialize_tail(const TailItem* items, uint32_t count, uint8_t* out, uint64_t bytes, hipStream_t s);
+hipError_t launch_serialize_tail(const TailItem* items, const uint64_t* table, uint32_t count, uint8_t* out,
+                                 uint64_t bytes, hipStream_t s);
 
 // row-sharded helpers (four-step NTT, sharded Merkle / FRI)
 // (nb: that many rows x cols arrays back to back, each scaled alike)

@@ -63,8 +63,11 @@ struct MerkleArgs {
     const fe* Thi;
     int shift;       // previous round r: exponent = i << r
     fe K;            // Montgomery(alpha * offset_r^-1 * 2^-1)
+    const fe* Kp;    // non-null: K is this device word instead (a gated round, k_fri_gate)
   } fold;
 };
+
+__device__ __forceinline__ fe fold_k(const MerkleArgs& a) { return a.fold.Kp ? ld_fe(a.fold.Kp) : a.fold.K; }
 
 __device__ __forceinline__ uint64_t* merkle_tree_ptr(const MerkleArgs& a) {
   return a.tree_ys ? a.tree[0] + (uint64_t)blockIdx.y * a.tree_ys : a.tree[blockIdx.y];
@@ -89,7 +92,7 @@ __device__ __forceinline__ fe leaf_value(const MerkleArgs& a, uint64_t idx) {
     const fe x = ld_fe(a.fold.src + idx);
     const fe y = ld_fe(a.fold.src + idx + a.first_count);
     const uint64_t e = idx << a.fold.shift;
-    const fe K = a.fold.K;
+    const fe K = fold_k(a);
     fe t = mont_mul(K, ld_fe(a.fold.Tlo + (e & 4095)));
     t = mont_mul(t, ld_fe(a.fold.Thi + (e >> 12)));
     const fe v = fe_add(fe_halve(fe_add(x, y)), mont_mul(fe_sub(x, y), t));
@@ -111,7 +114,7 @@ __device__ __forceinline__ void leaf_value_pair(const MerkleArgs& a, uint64_t id
     const fe x0 = ld_fe(a.fold.src + idx), x1 = ld_fe(a.fold.src + idx + 1);
     const fe y0 = ld_fe(a.fold.src + idx + a.first_count), y1 = ld_fe(a.fold.src + idx + 1 + a.first_count);
     const uint64_t e0 = idx << a.fold.shift, e1 = (idx + 1) << a.fold.shift;
-    const fe K = a.fold.K;
+    const fe K = fold_k(a);
     const fe t0l = ld_fe(a.fold.Tlo + (e0 & 4095)), t0h = ld_fe(a.fold.Thi + (e0 >> 12));
     const fe t1l = ld_fe(a.fold.Tlo + (e1 & 4095)), t1h = ld_fe(a.fold.Thi + (e1 >> 12));
     const fe t0 = mont_mul(mont_mul(K, t0l), t0h), t1 = mont_mul(mont_mul(K, t1l), t1h);

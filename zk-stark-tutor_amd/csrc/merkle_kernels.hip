@@ -37,7 +37,7 @@ __global__ __launch_bounds__(MAXB) void k_merkle_levels(MerkleArgs a) {
         const fe x = ld_fe(a.fold.src + idx);
         const fe y = ld_fe(a.fold.src + idx + a.first_count);
         const uint64_t e = idx << a.fold.shift;
-        const fe K = a.fold.K;
+        const fe K = fold_k(a);
         fe t = mont_mul(K, ld_fe(a.fold.Tlo + (e & 4095)));
         t = mont_mul(t, ld_fe(a.fold.Thi + (e >> 12)));
         v = fe_add(fe_halve(fe_add(x, y)), mont_mul(fe_sub(x, y), t));
@@ -95,7 +95,7 @@ __global__ __launch_bounds__(MAXB) void k_merkle_levels(MerkleArgs a) {
 // 4, 2, 1 of its 8 waves busy (74 VGPRs: 6 waves per SIMD), so the SIMDs run short of ready waves;
 // here the first two levels keep all 8 busy.
 template <int MAXB, bool FOLD>
-__global__ __launch_bounds__(MAXB) void k_merkle_leaf_pairs(MerkleArgs a) {
+__global__ __launch_bounds__(MAXB, 4) void k_merkle_leaf_pairs(MerkleArgs a) {
   __shared__ uint64_t sm[8][MAXB];
   const uint32_t tid = threadIdx.x;
   const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + tid;  // level-1 node
@@ -353,7 +353,7 @@ __global__ __launch_bounds__(4 * NODES) void k_merkle_quad_leaves(MerkleArgs a) 
       const fe x = ld_fe(a.fold.src + leaf);
       const fe y = ld_fe(a.fold.src + leaf + a.first_count);
       const uint64_t e = leaf << a.fold.shift;
-      const fe K = a.fold.K;
+      const fe K = fold_k(a);
       fe t = mont_mul(K, ld_fe(a.fold.Tlo + (e & 4095)));
       t = mont_mul(t, ld_fe(a.fold.Thi + (e >> 12)));
       v = fe_add(fe_halve(fe_add(x, y)), mont_mul(fe_sub(x, y), t));
@@ -399,8 +399,19 @@ __device__ __forceinline__ void put_be64_dev(uint8_t* o, uint64_t v) {
 // leaf values (src[1]) into LDS, a quad of lanes per compression (the decimal leaf words as in
 // k_merkle_quad_leaves, then the node levels), so its K - 1 dependent steps take quad-lane
 // latency; the block's nodes are the path's first K siblings (merkle_root.rs:25-53).
-__global__ __launch_bounds__(64) void k_serialize_tail(const TailItem* __restrict__ items, uint8_t* __restrict__ out) {
-  const TailItem it = items[blockIdx.x];
+__global__ __launch_bounds__(64) void k_serialize_tail(const TailItem* __restrict__ items,
+                                                      const uint64_t* __restrict__ table, uint8_t* __restrict__ out) {
+  TailItem it = items[blockIdx.x];
+  if (it.sel != kTailLiteral) {  // uniform over the block
+    const uint64_t idx = table[it.sel] & it.mask;
+    if (it.code == 2) {
+      it.index += idx;
+    } else {
+      it.src[0] += 16 * idx;
+      it.src[1] += 16 * idx;
+      it.src[2] += 16 * idx;
+    }
+  }
   const uint32_t l = threadIdx.x;
   uint8_t* o = out + it.dst;
   const bool path = it.code == 2;  // SG_OBJ_PATH
@@ -472,10 +483,11 @@ __global__ __launch_bounds__(64) void k_serialize_tail(const TailItem* __restric
   }
 }
 
-hipError_t launch_serialize_tail(const TailItem* items, uint32_t count, uint8_t* out, uint64_t bytes, hipStream_t s) {
+hipError_t launch_serialize_tail(const TailItem* items, const uint64_t* table, uint32_t count, uint8_t* out,
+                                 uint64_t bytes, hipStream_t s) {
   if (!count) return hipSuccess;
   ProfScope ps("serialize_tail", bytes, s);
-  hipLaunchKernelGGL(k_serialize_tail, dim3(count), dim3(64), 0, s, items, out);
+  hipLaunchKernelGGL(k_serialize_tail, dim3(count), dim3(64), 0, s, items, table, out);
   return hipGetLastError();
 }
 

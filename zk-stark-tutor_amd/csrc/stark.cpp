@@ -1363,21 +1363,30 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
   std::vector<std::pair<const fe*, const sg_tree*>> cts;
   for (size_t s = 0; s < m; ++s) cts.emplace_back(bq_cw[s].p(), bq_trees[s].get());
   cts.emplace_back(r_cw.p(), r_tree.get());
-  fri_prove_dev(ctx, &st.fri, comb_cw.p(), Nf, ps, top.data(), [&](const size_t* tp, TailWriter& tw) {
+  // the openings: for every codeword (boundary quotients, randomizer), a Value and a Path at each
+  // of the 4c sorted indices {i, i + expansion, and both + Nf/2} (mod Nf) of the top indices i,
+  // table entries c .. 5c - 1 (stark.rs:524-560)
+  const size_t c = st.fri.num_colinearity_tests;
+  TailExtra openings;
+  openings.count = 4 * c;
+  openings.plan = [&](TailWriter& tw, uint32_t sel0) {
     SG_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));  // the openings read the side-stream trees
-    const size_t c = st.fri.num_colinearity_tests;
-    std::vector<uint64_t> dup;
-    for (size_t k = 0; k < c; ++k) dup.push_back(tp[k]);
-    for (size_t k = 0; k < c; ++k) dup.push_back((tp[k] + st.expansion) % Nf);
-    std::vector<uint64_t> quad = dup;
-    for (uint64_t i : dup) quad.push_back((i + Nf / 2) % Nf);
-    std::sort(quad.begin(), quad.end());
     for (auto& ct : cts)
-      for (uint64_t i : quad) {
-        tw.value(ct.first + i);
-        tw.path(ct.second, i);
+      for (uint32_t j = 0; j < 4 * c; ++j) {
+        tw.value(ct.first, sel0 + j);
+        tw.path(ct.second, sel0 + j, ~0ull);
       }
-  });
+  };
+  openings.indices = [&](const size_t* tp, std::vector<uint64_t>& table) {
+    std::vector<uint64_t> quad;
+    quad.reserve(4 * c);
+    for (size_t k = 0; k < c; ++k) quad.push_back(tp[k]);
+    for (size_t k = 0; k < c; ++k) quad.push_back((tp[k] + st.expansion) % Nf);
+    for (size_t k = 0; k < 2 * c; ++k) quad.push_back((quad[k] + Nf / 2) % Nf);
+    std::sort(quad.begin(), quad.end());
+    table.insert(table.end(), quad.begin(), quad.end());
+  };
+  fri_prove_dev(ctx, &st.fri, comb_cw.p(), Nf, ps, top.data(), &openings);
   mark("fri_prove_and_openings");
   host_wait(ctx, ctx->stream);
   check_div_zero(ctx);
