@@ -1,5 +1,10 @@
-"""Generates zk-stark-tutor_amd/csrc/fe128_asm.inc: the NTT butterfly's 128-bit field arithmetic as
-gfx950 inline-asm blocks whose carry chains are interleaved so that no wait state is needed.
+"""Round-6 experiment record (not part of the build): generates fe128_asm.inc, the NTT butterfly's
+128-bit field arithmetic as gfx950 inline-asm blocks whose carry chains are interleaved so that no
+wait state is needed.  Measured and removed from kernels.hip: the
+k_ntt_pass_rr<11> listing lost 78 % of its wait states and C2 did not move
+(profiles/r06_ab_asm_c2.log), and the variant faulted in kernels where hipcc's own scalar code
+follows an asm block that left a VALU-written carry SGPR (profiles/r06_ab_asm_prove_fault.log,
+r06_pytest_gpu_asm_fault_ntt2p12.log): hipcc does not see the hazards inside inline asm.
 
 Why (VERDICT r05 "Next round" 1): every 32-bit carry link is a VALU that writes an SGPR carry and a
 VALU that reads it; gfx950 needs two wait states between the two.  hipcc allocates every chain's
@@ -16,7 +21,7 @@ inputs and compared with the field arithmetic (`python tools/gen_fe_asm.py --che
 build does not need it).  The arithmetic is the one of csrc/fe128.hpp (mont_mul, fe_add_lazy,
 fe_sub_lazy): p = 1 + 407 * 2^119 (field/field.rs:10), R = 2^128, two 64-bit Montgomery steps.
 
-  python tools/gen_fe_asm.py            # write the .inc and check it
+  python tools/gen_fe_asm.py [out.inc]  # write the .inc (default /tmp/fe128_asm.inc) and check it
 """
 import os
 import random
@@ -742,7 +747,8 @@ if __name__ == "__main__":
     for n, b in built.items():
         print("%-10s VALU %3d SALU %d  wait states %2d  window %2d  carries %d" % (n, b["nvalu"], b["nsalu"], b["nops"], b["nwin"], b["nsg"]))
     if "--check" not in sys.argv:
-        root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-        with open(os.path.join(root, "zk-stark-tutor_amd", "csrc", "fe128_asm.inc"), "w") as f:
+        args = [a for a in sys.argv[1:] if not a.startswith("--")]
+        out = args[0] if args else "/tmp/fe128_asm.inc"
+        with open(out, "w") as f:
             f.write(text)
-        print("wrote csrc/fe128_asm.inc")
+        print("wrote", out)

@@ -149,6 +149,20 @@ void* sg_ctx::staging(int slot, size_t bytes) {
   return staging_ptr[slot];
 }
 
+void* sg_ctx::tail_buffer(size_t bytes) {
+  if (tail_dev_bytes < bytes) {
+    host_wait(this, side);  // the old buffer may still be in flight
+    host_wait(this, stream);
+    if (tail_dev) (void)hipFree(tail_dev);
+    tail_dev = nullptr;
+    tail_dev_bytes = 0;
+    const size_t r = pool_round(bytes);
+    SG_HIP(hipMalloc(&tail_dev, r));
+    tail_dev_bytes = r;
+  }
+  return tail_dev;
+}
+
 namespace sg {
 int ab_knob(const char* name, int def) {
   const char* v = getenv(name);
@@ -343,6 +357,7 @@ extern "C" void sg_ctx_destroy(sg_ctx* ctx) {
   (void)hipEventDestroy(ctx->ev_fork);
   (void)hipEventDestroy(ctx->ev_join);
   (void)hipEventDestroy(ctx->ev_tail);
+  if (ctx->tail_dev) (void)hipFree(ctx->tail_dev);
   (void)hipStreamDestroy(ctx->side);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
@@ -1093,29 +1108,26 @@ void TailWriter::upload(sg_ctx* ctx, size_t n) {
   table_n = n;
   const size_t ib = items.size() * sizeof(TailItem);
   stage = static_cast<uint8_t*>(ctx->staging(0, ib + 8 * n));
-  dev = DevBuf(ctx, ib + 8 * n);
-  if (ib) {
-    // on the side stream (idle by now): the copy overlaps the main stream's last FRI round instead of
-    // queueing behind it (no main-stream work still queued can hold `dev`: the host has waited for
-    // every root but the last, whose kernels use only the round state's buffers)
-    memcpy(stage, items.data(), ib);
-    SG_HIP(hipMemcpyAsync(dev.get(), stage, ib, hipMemcpyHostToDevice, ctx->side));
-    SG_HIP(hipEventRecord(ctx->ev_tail, ctx->side));
-  }
+  dev = static_cast<uint8_t*>(ctx->tail_buffer(ib + 8 * n));
+  // on the side stream (idle here), so the copy runs beside the main stream's FRI rounds rather
+  // than between two of them
+  memcpy(stage, items.data(), ib);
+  SG_HIP(hipMemcpyAsync(dev, stage, ib, hipMemcpyHostToDevice, ctx->side));
+  SG_HIP(hipEventRecord(ctx->ev_tail, ctx->side));
 }
 
 void TailWriter::flush(sg_ctx* ctx, const sg_proof_stream* ps, const uint64_t* table) {
   if (items.empty()) return;
   SG_REQUIRE(stage != nullptr, "tail items were not uploaded");
   const size_t ni = items.size(), ib = ni * sizeof(TailItem);
-  uint64_t* dtable = reinterpret_cast<uint64_t*>(dev.as<uint8_t>() + ib);
+  uint64_t* dtable = reinterpret_cast<uint64_t*>(dev + ib);
+  SG_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_tail, 0));  // the items' upload
   if (table_n) {
     memcpy(stage + ib, table, 8 * table_n);
     SG_HIP(hipMemcpyAsync(dtable, stage + ib, 8 * table_n, hipMemcpyHostToDevice, ctx->stream));
   }
   DevBuf dout(ctx, bytes);
-  SG_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_tail, 0));  // the items' upload
-  SG_HIP(launch_serialize_tail(dev.as<TailItem>(), dtable, (uint32_t)ni, dout.as<uint8_t>(), bytes, ctx->stream));
+  SG_HIP(launch_serialize_tail(reinterpret_cast<const TailItem*>(dev), dtable, (uint32_t)ni, dout.as<uint8_t>(), bytes, ctx->stream));
   if (ps->push == stream_push_cb) {
     // a native stream: the block lands in its body by one device copy (or through staging when the
     // runtime refuses to page-lock the body)
@@ -1161,7 +1173,7 @@ void put_u128_be(std::vector<uint8_t>& out, const fe& a) {
 
 // fri.rs:115-172.  Retains every round's codeword and tree in `st`.
 void fri_commit_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, const sg_proof_stream* ps,
-                    sg_fri_state& st, bool borrow_input, int drop, const std::function<void()>& after_last) {
+                    sg_fri_state& st, bool borrow_input, int drop, const std::function<void()>& overlap) {
   SG_REQUIRE(ps && ps->push && ps->fiat_shamir_prover, "proof stream callbacks required");
   size_t rounds = fri_num_rounds(f);
   SG_REQUIRE(rounds >= 1, "FRI: zero rounds for this domain");
@@ -1256,7 +1268,6 @@ void fri_commit_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, co
   // copy on the host, waiting for the stream -- behind a pending gate that wait never ends.
   auto copy_last = [&]() {
     SG_HIP(hipMemcpyAsync(last, st.cw.back(), last_len * sizeof(fe), hipMemcpyDeviceToHost, ctx->stream));
-    if (after_last) after_last();
   };
   std::vector<uint64_t> seqs(rounds);
   auto launch_round = [&](size_t r, const fe* K) {
@@ -1285,6 +1296,10 @@ void fri_commit_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, co
     if (r + 1 == rounds && !gated) copy_last();
   };
   launch_round(0, nullptr);
+  // the caller's host work that needs only the round state's buffers runs while round 0's tree (the
+  // longest) hashes; its stream work is queued here, before any gate (a copy the runtime completes
+  // on the host could otherwise wait on a pending gate)
+  if (overlap) overlap();
   for (size_t r = 0; r < rounds; ++r) {
     if (gated && r + 1 < rounds) launch_round(r + 1, nullptr);
     fill_tree_finish(ctx, st.trees[r].get(), seqs[r]);
@@ -1354,8 +1369,8 @@ void fri_prove_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, con
   // Every opening of every round follows from the top indices (fri.rs:174-208, 231-245): the
   // Leafs / Path objects of all rounds, in the reference's order, and the caller's `extra` objects
   // are planned as items over an index table (entry s < c: top[s], masked to the round's half
-  // length -- top % (len_r / 2), the reference's repeated reduction) and uploaded while the last
-  // round's tree runs; the seed then only yields the table, serialized in one launch.
+  // length -- top % (len_r / 2), the reference's repeated reduction) and uploaded behind round 0's
+  // tree while it hashes; after the last round the seed only yields the table, serialized in one launch.
   TailWriter tw;
   auto plan = [&]() {
     if (st.codewords.size() < 2) return;  // reported after the commit, where the reference panics

@@ -67,7 +67,6 @@ struct sg_ctx {
   // second stream: Merkle trees overlapped with the main stream's algebra (stark_prove)
   hipStream_t side = nullptr;
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-  hipEvent_t ev_tail = nullptr;  // the proof tail's item upload (side stream) done
   std::string last_error;
   // set while a communicator call runs on this context (dist.cpp DistWatch): every host wait
   // (sg::host_wait, the tree-root spin) polls it; it throws -- after aborting the communicator --
@@ -158,6 +157,13 @@ struct sg_ctx {
   void* staging_ptr[2] = {nullptr, nullptr};
   size_t staging_bytes[2] = {0, 0};
   void* staging(int slot, size_t bytes);
+  // device buffer of a proof's tail items (TailWriter), kept across calls and grown on demand; its
+  // upload runs on the side stream (ev_tail), beside the main stream's FRI rounds -- a pool buffer
+  // could still be in use by queued main-stream work there
+  void* tail_dev = nullptr;
+  size_t tail_dev_bytes = 0;
+  hipEvent_t ev_tail = nullptr;
+  void* tail_buffer(size_t bytes);
 };
 
 namespace sg {

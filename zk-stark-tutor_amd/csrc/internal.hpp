@@ -173,11 +173,12 @@ void put_u128_be_at(uint8_t* out, const fe& a);
 void put_u128_be(std::vector<uint8_t>& out, const fe& a);
 // drop: the round trees' levels not kept (lean trees; the sharded prove's tail keeps drop <= 1, which
 // its absolute-address openings rehash)
-// after_last: called once the last round's fold + tree are launched (and its gate raised), while the
-// host waits for that root -- the FRI prove plans and uploads its query items there
+// overlap: called once, after round 0's tree is launched (before any gated round and before the host
+// waits for the root); every round's codeword and tree buffer exist by then -- the FRI prove plans
+// and uploads its query items there
 void fri_commit_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, const sg_proof_stream* ps,
                     sg_fri_state& st, bool borrow_input = false, int drop = 3,
-                    const std::function<void()>& after_last = {});
+                    const std::function<void()>& overlap = {});
 // Objects pushed after a proof's last Fiat-Shamir draw (the FRI query phase, fri.rs:174-208, and
 // the Stark openings, stark.rs:524-560): collected as TailItems, serialized by one device launch
 // (k_serialize_tail) and appended with one copy -- straight into a native stream's page-locked
@@ -189,7 +190,7 @@ struct TailWriter {
   std::vector<size_t> offs;  // header offset of each object in the block
   size_t bytes = 0;
   bool field = false;        // a Value / Leafs object (sets the stream's field header)
-  DevBuf dev;                // uploaded items, then the table
+  uint8_t* dev = nullptr;    // the context's tail buffer: uploaded items, then the table
   uint8_t* stage = nullptr;  // pinned staging (slot 0): items, then the table
   size_t table_n = 0;
   // Value base[idx]; Leafs a[idx], b[idx], c[idx]; the Path of leaf add + idx (idx = table[sel] & mask)

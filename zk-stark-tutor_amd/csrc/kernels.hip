@@ -22,7 +22,6 @@
 #include <cstdint>
 #include <cstdlib>
 #include "fe128.hpp"
-#include "fe128_asm.inc"
 #include "dev_util.hpp"
 #include "blake2b.hpp"
 #include "leaf_decimal.hpp"
@@ -31,31 +30,13 @@
 #include "knobs.hpp"
 #include "merkle_dev.hpp"
 
-// SG_NTT_ASM (default 1): the NTT kernels' field products and butterflies are the generated inline
-// asm of fe128_asm.inc, whose carry chains are interleaved so that no carry read waits on its writer
-// (tools/gen_fe_asm.py); 0: the C++ forms of fe128.hpp, same results.  The asm's fixed VGPR window
-// pushes k_ntt_pass_rr<11> past 128 VGPRs unless the launch bound asks for 4 waves per SIMD (no
-// spill at 128), so that bound is the default with it.
-#ifndef SG_NTT_ASM
-#define SG_NTT_ASM 0
-#endif
+// SG_NTT_WPE: minimum waves per SIMD the NTT passes' launch bounds ask for (1: the compiler's choice,
+// 118-126 VGPRs, 4 waves).  (Round 6 built the verdict's interleaved-carry butterflies as generated
+// inline asm, tools/gen_fe_asm.py: 78 % fewer s_nop wait states in k_ntt_pass_rr<11>, C2 unchanged,
+// and kernel faults from SGPR hazards between the asm and hipcc's own code -- removed)
 #ifndef SG_NTT_WPE
-#define SG_NTT_WPE (SG_NTT_ASM ? 4 : 1)
+#define SG_NTT_WPE 1
 #endif
-namespace sg {
-// a * b * 2^-128 mod p, canonical, for a < 2^128 and b < p (fe128.hpp mont_mul)
-#ifndef SG_NTT_ASM_MUL
-#define SG_NTT_ASM_MUL SG_NTT_ASM
-#endif
-__device__ __forceinline__ fe ntt_mul(const fe& a, const fe& b) {
-#if SG_NTT_ASM_MUL && defined(__HIP_DEVICE_COMPILE__)
-  return mont_mul_asm(a, b);
-#else
-  return mont_mul(a, b);
-#endif
-}
-}  // namespace sg
-
 namespace sg {
 
 thread_local KernelProfiler* g_prof = nullptr;
@@ -180,10 +161,10 @@ template <class Args>
 __device__ __forceinline__ void ep_store(const Args& a, uint64_t r, uint64_t k, const fe& v) {
   const uint64_t rl = r & ((1ull << a.ep_vlog) - 1), vv = r >> a.ep_vlog;
   const uint64_t e = (a.ep_j0 + rl) * k;  // < 2^36 (host-checked)
-  const fe w = ntt_mul(ntt_mul(ld_fe(a.ep_T0 + (e & 4095)), ld_fe(a.ep_T1 + ((e >> 12) & 4095))),
+  const fe w = mont_mul(mont_mul(ld_fe(a.ep_T0 + (e & 4095)), ld_fe(a.ep_T1 + ((e >> 12) & 4095))),
                         ld_fe(a.ep_T2 + (e >> 24)));
   const uint64_t R = (uint64_t)1 << a.ep_logR;
-  st_fe(a.ep_out + (((k >> a.ep_logR) * a.ep_rows + rl) * a.ep_k + vv) * R + (k & (R - 1)), ntt_mul(v, w));
+  st_fe(a.ep_out + (((k >> a.ep_logR) * a.ep_rows + rl) * a.ep_k + vv) * R + (k & (R - 1)), mont_mul(v, w));
 }
 
 // store of a transform's element k (row pointer `row`) at the end of a pass
@@ -193,7 +174,7 @@ __device__ __forceinline__ void pass_store(const PassArgs& a, fe* row, uint64_t 
     ep_store(a, a.ep_row0 + blockIdx.y, k, v);
     return;
   }
-  if (post) v = ntt_mul(v, pc);
+  if (post) v = mont_mul(v, pc);
   else if (last) v = fe_canon(v);
   st_fe_stream(row + k, v, a.logn >= kStreamLogN);
 }
@@ -212,24 +193,16 @@ __device__ __forceinline__ fe twiddle_comp(const PassArgs& a, int S, uint64_t k)
 // One radix-2 butterfly of the reference's DIT graph (fft/ntt.rs:26-46): o = x * w (Montgomery,
 // w a Montgomery twiddle), e <- e + o, x <- e - o, lazily reduced (fe128.hpp).
 __device__ __forceinline__ void butterfly(fe& e, fe& x, const fe& w) {
-#if SG_NTT_ASM && defined(__HIP_DEVICE_COMPILE__)
-  bfly_asm(e, x, w);
-#else
   fe o = mont_mul(x, w);
   fe ev = e;
   e = fe_add_lazy(ev, o);
   x = fe_sub_lazy(ev, o);
-#endif
 }
 // twiddle 1: o = x (canonical), e <- e + x, x <- e - x
 __device__ __forceinline__ void butterfly_unit(fe& e, fe& x) {
-#if SG_NTT_ASM && defined(__HIP_DEVICE_COMPILE__)
-  addsub_asm(e, x);
-#else
   fe ev = e;
   e = fe_add_lazy(ev, x);
   x = fe_sub_lazy(ev, x);
-#endif
 }
 
 // R radix-2 stages (tile-local stages t+1 .. t+R) on the 2^R elements of one group held
@@ -532,7 +505,7 @@ __global__ __launch_bounds__(1 << (TL - 3), TL == 11 ? SG_NTT_WPE : 1) void k_nt
       x[j] = fe_zero();
       if (idx < a.n_in) {
         x[j] = ld_fe_stream(in_at(c, idx), m >= kStreamLogN);
-        if (a.sA) x[j] = ntt_mul(x[j], ntt_mul(ld_fe(a.sA + (idx & 4095)), ld_fe(a.sB + (idx >> 12))));
+        if (a.sA) x[j] = mont_mul(x[j], mont_mul(ld_fe(a.sA + (idx & 4095)), ld_fe(a.sB + (idx >> 12))));
       }
     }
     radix8_first(x, pa);
@@ -548,7 +521,7 @@ __global__ __launch_bounds__(1 << (TL - 3), TL == 11 ? SG_NTT_WPE : 1) void k_nt
       fe v = fe_zero();
       if (idx < a.n_in) {
         v = ld_fe(in_at(k, idx));
-        if (a.sA) v = ntt_mul(v, ntt_mul(ld_fe(a.sA + (idx & 4095)), ld_fe(a.sB + (idx >> 12))));
+        if (a.sA) v = mont_mul(v, mont_mul(ld_fe(a.sA + (idx & 4095)), ld_fe(a.sB + (idx >> 12))));
       }
       const uint32_t tr = __builtin_bitreverse32(u) >> (32 - L);
       for (uint32_t r = 0; r < rep; ++r) lds[((tr + r) << logC) + k] = v;
@@ -578,7 +551,7 @@ __global__ __launch_bounds__(1 << (TL - 3), TL == 11 ? SG_NTT_WPE : 1) void k_nt
         if constexpr (EP) {
           ep_store(a, a.ep_row0 + ycol(c), k, x[mm]);
         } else {
-          st_fe(orow + k, POST ? ntt_mul(x[mm], pc) : fe_canon(x[mm]));
+          st_fe(orow + k, POST ? mont_mul(x[mm], pc) : fe_canon(x[mm]));
         }
       }
       return;
