@@ -358,6 +358,8 @@ extern "C" void sg_ctx_destroy(sg_ctx* ctx) {
   (void)hipEventDestroy(ctx->ev_join);
   (void)hipEventDestroy(ctx->ev_tail);
   if (ctx->tail_dev) (void)hipFree(ctx->tail_dev);
+  if (ctx->deg_slots) (void)hipFree(ctx->deg_slots);
+  if (ctx->deg_host) (void)hipHostFree(ctx->deg_host);
   (void)hipStreamDestroy(ctx->side);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;

@@ -164,6 +164,13 @@ struct sg_ctx {
   size_t tail_dev_bytes = 0;
   hipEvent_t ev_tail = nullptr;
   void* tail_buffer(size_t bytes);
+  // degree-scan slots (k_last_nonzero_batch): never cleared, each call tagged with a new generation
+  unsigned long long* deg_slots = nullptr;
+  size_t deg_cap = 0;
+  unsigned long long deg_gen = 0;
+  // host-coherent copy of the slots (deg_cap entries, then the ready flag), host and device views
+  unsigned long long* deg_host = nullptr;
+  unsigned long long* deg_host_dev = nullptr;
 };
 
 namespace sg {

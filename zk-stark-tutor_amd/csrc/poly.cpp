@@ -18,6 +18,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cstring>
 #include <memory>
 #include <vector>
@@ -69,28 +71,85 @@ DPoly dpoly_copy(sg_ctx* ctx, const fe* d, uint64_t len) {
 }
 
 int64_t dev_degree(sg_ctx* ctx, const fe* d, uint64_t len) {
-  if (!len) return -1;
-  DevBuf last(ctx, 8);
-  SG_HIP(hipMemsetAsync(last.get(), 0, 8, ctx->stream));
-  SG_HIP(launch_last_nonzero(d, len, last.as<unsigned long long>(), ctx->stream));
-  unsigned long long h = 0;
-  SG_HIP(hipMemcpyAsync(&h, last.get(), 8, hipMemcpyDeviceToHost, ctx->stream));
-  host_wait(ctx, ctx->stream);
-  return (int64_t)h - 1;
+  return dev_degrees(ctx, {{d, len}})[0];
+}
+
+// Every polynomial's degree with one host round trip: batches of kDegBatch per launch into the
+// context's degree slots, tagged with a fresh generation (no clearing launch), published to
+// host-coherent memory with a ready flag (k_publish_slots) that the host spins on.  Split in two so
+// a caller can do host work between the launches and the wait (dev_degrees_begin / _end).
+DegScan dev_degrees_begin(sg_ctx* ctx, const std::vector<std::pair<const fe*, uint64_t>>& polys) {
+  DegScan sc;
+  sc.n = polys.size();
+  if (polys.empty()) return sc;
+  if (ctx->deg_cap < polys.size()) {
+    host_wait(ctx, ctx->stream);  // the old slots may still be in use
+    if (ctx->deg_slots) (void)hipFree(ctx->deg_slots);
+    if (ctx->deg_host) (void)hipHostFree(ctx->deg_host);
+    ctx->deg_slots = nullptr;
+    ctx->deg_host = ctx->deg_host_dev = nullptr;
+    ctx->deg_cap = 0;
+    const size_t cap = std::max<size_t>(64, polys.size());
+    SG_HIP(hipMalloc(reinterpret_cast<void**>(&ctx->deg_slots), cap * 8));
+    SG_HIP(hipMemsetAsync(ctx->deg_slots, 0, cap * 8, ctx->stream));
+    void* h = nullptr;
+    void* hd = nullptr;
+    SG_HIP(hipHostMalloc(&h, (cap + 1) * 8, hipHostMallocMapped | hipHostMallocCoherent));
+    ctx->deg_host = static_cast<unsigned long long*>(h);
+    memset(h, 0, (cap + 1) * 8);
+    SG_HIP(hipHostGetDevicePointer(&hd, h, 0));
+    ctx->deg_host_dev = static_cast<unsigned long long*>(hd);
+    ctx->deg_cap = cap;
+    ctx->deg_gen = 0;
+  }
+  if (++ctx->deg_gen >= (1ull << (64 - kDegGenShift))) {  // generations exhausted: clear once
+    SG_HIP(hipMemsetAsync(ctx->deg_slots, 0, ctx->deg_cap * 8, ctx->stream));
+    ctx->deg_gen = 1;
+  }
+  sc.gen = ctx->deg_gen;
+  for (size_t i0 = 0; i0 < polys.size(); i0 += kDegBatch) {
+    DegBatch b{};
+    const int cnt = (int)std::min<size_t>(kDegBatch, polys.size() - i0);
+    for (int k = 0; k < cnt; ++k) {
+      b.a[k] = polys[i0 + k].first;
+      b.n[k] = polys[i0 + k].second;
+    }
+    SG_HIP(launch_last_nonzero_batch(b, cnt, ctx->deg_slots + i0, sc.gen, ctx->stream));
+  }
+  SG_HIP(launch_publish_slots(ctx->deg_slots, ctx->deg_host_dev, polys.size(), ctx->deg_host_dev + ctx->deg_cap,
+                              sc.gen, ctx->stream));
+  return sc;
+}
+
+std::vector<int64_t> dev_degrees_end(sg_ctx* ctx, const DegScan& sc) {
+  std::vector<int64_t> out(sc.n, -1);
+  if (!sc.n) return out;
+  volatile unsigned long long* flag = ctx->deg_host + ctx->deg_cap;
+  const auto t0 = std::chrono::steady_clock::now();
+  uint32_t spins = 0;
+  while (*flag != sc.gen) {  // as wait_roots: query the stream now and then, so an error surfaces
+    if ((++spins & 255) == 0) {
+      if (ctx->watch) ctx->watch(std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count());
+      const hipError_t q = hipStreamQuery(ctx->stream);
+      if (q == hipSuccess) {
+        if (*flag != sc.gen) throw Error{SG_ERR_HIP, "degree scan was not published"};
+        break;
+      }
+      if (q != hipErrorNotReady) SG_HIP(q);
+    }
+    __builtin_ia32_pause();
+  }
+  std::atomic_thread_fence(std::memory_order_acquire);
+  const unsigned long long mask = (1ull << kDegGenShift) - 1;
+  for (size_t i = 0; i < sc.n; ++i) {
+    const unsigned long long v = ctx->deg_host[i];
+    out[i] = (v >> kDegGenShift) == sc.gen ? (int64_t)(v & mask) - 1 : -1;
+  }
+  return out;
 }
 
 std::vector<int64_t> dev_degrees(sg_ctx* ctx, const std::vector<std::pair<const fe*, uint64_t>>& polys) {
-  std::vector<int64_t> out(polys.size(), -1);
-  if (polys.empty()) return out;
-  DevBuf last(ctx, 8 * polys.size());
-  SG_HIP(hipMemsetAsync(last.get(), 0, 8 * polys.size(), ctx->stream));
-  for (size_t i = 0; i < polys.size(); ++i)
-    SG_HIP(launch_last_nonzero(polys[i].first, polys[i].second, last.as<unsigned long long>() + i, ctx->stream));
-  std::vector<unsigned long long> h(polys.size());
-  SG_HIP(hipMemcpyAsync(h.data(), last.get(), 8 * polys.size(), hipMemcpyDeviceToHost, ctx->stream));
-  host_wait(ctx, ctx->stream);  // one round trip for the whole batch
-  for (size_t i = 0; i < polys.size(); ++i) out[i] = (int64_t)h[i] - 1;
-  return out;
+  return dev_degrees_end(ctx, dev_degrees_begin(ctx, polys));
 }
 
 // ------------------------------------------------------------------ roots

@@ -30,6 +30,14 @@ DPoly dpoly_copy(sg_ctx* ctx, const fe* d, uint64_t len);
 int64_t dev_degree(sg_ctx* ctx, const fe* d, uint64_t len);
 // degrees of several device polynomials with one host round trip
 std::vector<int64_t> dev_degrees(sg_ctx* ctx, const std::vector<std::pair<const fe*, uint64_t>>& polys);
+// the same in two halves: launch the scans (and their publication), then wait for the published
+// degrees -- host work can go between them
+struct DegScan {
+  unsigned long long gen = 0;
+  size_t n = 0;
+};
+DegScan dev_degrees_begin(sg_ctx* ctx, const std::vector<std::pair<const fe*, uint64_t>>& polys);
+std::vector<int64_t> dev_degrees_end(sg_ctx* ctx, const DegScan& sc);
 
 // primitive root of order n (field.rs:58-71)
 fe root_of_order(uint64_t n);

@@ -418,15 +418,27 @@ __global__ __launch_bounds__(kBlock) void k_geo_dot(fe* __restrict__ S, const fe
 // the end of its buffer (the usual case) is decided by its top chunks.  A stale read only
 // costs the early exit, never the result.
 constexpr unsigned kDegPer = 16;
-__global__ __launch_bounds__(kBlock) void k_last_nonzero(const fe* __restrict__ a, uint64_t n,
-                                                         unsigned long long* __restrict__ last) {
+// Batched: up to kDegBatch polynomials in one launch (blockIdx.y = polynomial), into slots that
+// are never cleared: a slot holds (gen << kDegGenShift) | (index + 1), raised by atomicMax, and a
+// value of an older generation (an earlier call) reads as "no nonzero yet" -- no memset launch
+// before the scan, one kernel for the whole batch.
+__global__ __launch_bounds__(kBlock) void k_last_nonzero_batch(DegBatch b, unsigned long long* __restrict__ slots,
+                                                               unsigned long long gen) {
   __shared__ unsigned long long wmax[kBlock / 64];
   __shared__ int skip;
   constexpr uint64_t chunk = (uint64_t)kBlock * kDegPer;
-  const uint64_t hi = n - (uint64_t)blockIdx.x * chunk;  // this block covers [lo, hi)
+  const unsigned y = blockIdx.y;
+  const uint64_t n = b.n[y];
+  if ((uint64_t)blockIdx.x * chunk >= n) return;  // uniform: shorter polynomials of the batch
+  const fe* __restrict__ a = b.a[y];
+  unsigned long long* last = slots + y;
+  const unsigned long long tag = gen << kDegGenShift, mask = (1ull << kDegGenShift) - 1;
+  const uint64_t hi = n - (uint64_t)blockIdx.x * chunk;
   const uint64_t lo = hi > chunk ? hi - chunk : 0;
-  // one read for the block, so the whole block exits or none of it does
-  if (threadIdx.x == 0) skip = __hip_atomic_load(last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= hi;
+  if (threadIdx.x == 0) {
+    const unsigned long long v = __hip_atomic_load(last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    skip = (v >> kDegGenShift) == gen && (v & mask) >= hi;
+  }
   __syncthreads();
   if (skip) return;
   unsigned long long best = 0;
@@ -439,7 +451,6 @@ __global__ __launch_bounds__(kBlock) void k_last_nonzero(const fe* __restrict__ 
 #pragma unroll
   for (unsigned k = 0; k < kDegPer; ++k)
     if (!fe_is_zero(v[k])) best = lo + (uint64_t)k * kBlock + threadIdx.x + 1;
-  // wave max, block max, one atomic per block (a per-wave atomic on one address serializes)
   for (int off = 32; off > 0; off >>= 1) {
     unsigned long long o = __shfl_xor(best, off);
     best = o > best ? o : best;
@@ -448,7 +459,7 @@ __global__ __launch_bounds__(kBlock) void k_last_nonzero(const fe* __restrict__ 
   __syncthreads();
   if (threadIdx.x == 0) {
     for (unsigned w = 1; w < kBlock / 64; ++w) best = wmax[w] > best ? wmax[w] : best;
-    if (best) atomicMax(last, best);
+    if (best) atomicMax(last, tag | best);
   }
 }
 
@@ -586,6 +597,26 @@ __global__ __launch_bounds__(kBlock) void k_eval_small(fe* __restrict__ out, Sma
 
 // ================================================================ launchers
 
+// out[i] = in[i] - p[i] for i < max(len, p.len), each side zero past its length: a polynomial minus a
+// small host polynomial (a boundary interpolant) without uploading it -- the canonical values of
+// lincomb({in, 1}, {p, -1})
+__global__ __launch_bounds__(kBlock) void k_sub_small(fe* __restrict__ out, const fe* __restrict__ in, uint64_t len,
+                                                      SmallPoly p, uint64_t n) {
+  for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+    const fe a = i < len ? ld_fe(in + i) : fe_zero();
+    const fe b = i < (uint64_t)p.len ? p.c[i] : fe_zero();
+    st_fe(out + i, fe_sub(a, b));
+  }
+}
+
+hipError_t launch_sub_small(fe* out, const fe* in, uint64_t len, const SmallPoly& p, hipStream_t s) {
+  const uint64_t n = len > (uint64_t)p.len ? len : (uint64_t)p.len;
+  if (!n) return hipSuccess;
+  ProfScope ps("lincomb", 32 * n, s);
+  hipLaunchKernelGGL(k_sub_small, dim3((unsigned)grid_for(n)), dim3(kBlock), 0, s, out, in, len, p, n);
+  return hipGetLastError();
+}
+
 hipError_t launch_eval_small(fe* out, const SmallPoly& p, uint64_t n, const fe* wA, const fe* wB, const fe& off_m,
                              hipStream_t s) {
   if (!n) return hipSuccess;
@@ -716,11 +747,38 @@ hipError_t launch_geo_dot(fe* S, const fe* A, const fe* K, int logf, uint64_t M,
   return hipGetLastError();
 }
 
-hipError_t launch_last_nonzero(const fe* a, uint64_t n, unsigned long long* last, hipStream_t s) {
-  if (!n) return hipSuccess;
-  ProfScope ps("last_nonzero", 16 * n, s);
-  const uint64_t blocks = (n + (uint64_t)kBlock * kDegPer - 1) / ((uint64_t)kBlock * kDegPer);
-  hipLaunchKernelGGL(k_last_nonzero, dim3((unsigned)blocks), dim3(kBlock), 0, s, a, n, last);
+// the degree slots to host-coherent memory, then the ready flag (system scope): the host spins on
+// the flag instead of a runtime copy and a stream synchronisation
+__global__ void k_publish_slots(const unsigned long long* __restrict__ slots, unsigned long long* host, uint64_t n,
+                                unsigned long long* flag, unsigned long long seq) {
+  for (uint64_t i = threadIdx.x; i < n; i += blockDim.x)
+    __hip_atomic_store(host + i, __hip_atomic_load(slots + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence_system();
+    __hip_atomic_store(flag, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+hipError_t launch_publish_slots(const unsigned long long* slots, unsigned long long* host, uint64_t n,
+                                unsigned long long* flag, unsigned long long seq, hipStream_t s) {
+  hipLaunchKernelGGL(k_publish_slots, dim3(1), dim3(256), 0, s, slots, host, n, flag, seq);
+  return hipGetLastError();
+}
+
+hipError_t launch_last_nonzero_batch(const DegBatch& b, int count, unsigned long long* slots, unsigned long long gen,
+                                     hipStream_t s) {
+  if (count < 1 || count > kDegBatch || gen == 0 || gen >= (1ull << (64 - kDegGenShift))) return hipErrorInvalidValue;
+  uint64_t nmax = 0;
+  for (int i = 0; i < count; ++i) {
+    if (b.n[i] >> kDegGenShift) return hipErrorInvalidValue;
+    nmax = b.n[i] > nmax ? b.n[i] : nmax;
+  }
+  if (!nmax) return hipSuccess;
+  ProfScope ps("last_nonzero", 16 * nmax * count, s);
+  const uint64_t blocks = (nmax + (uint64_t)kBlock * kDegPer - 1) / ((uint64_t)kBlock * kDegPer);
+  hipLaunchKernelGGL(k_last_nonzero_batch, dim3((unsigned)blocks, (unsigned)count), dim3(kBlock), 0, s, b, slots, gen);
   return hipGetLastError();
 }
 

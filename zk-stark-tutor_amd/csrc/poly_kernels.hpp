@@ -69,7 +69,20 @@ hipError_t launch_geo_rows(fe* rows, const fe* y, uint64_t ys, const fe* Zdi, ui
 hipError_t launch_geo_krows(fe* out, const fe* b, int logf, uint64_t M, uint64_t D, hipStream_t s);
 hipError_t launch_geo_dot(fe* S, const fe* A, const fe* K, int logf, uint64_t M, uint64_t cols, const fe& r2,
                           hipStream_t s);
-hipError_t launch_last_nonzero(const fe* a, uint64_t n, unsigned long long* last, hipStream_t s);
+// last nonzero index + 1 of up to kDegBatch polynomials in one launch, into slots[0..count) tagged
+// with generation gen (1 .. 2^24 - 1): slot = (gen << kDegGenShift) | (index + 1); a slot of another
+// generation means all zero (the slots are never cleared; sg_ctx::deg_slots)
+constexpr int kDegBatch = 8;
+constexpr int kDegGenShift = 40;  // polynomials up to 2^40 - 1 coefficients
+struct DegBatch {
+  const fe* a[kDegBatch];
+  uint64_t n[kDegBatch];
+};
+hipError_t launch_last_nonzero_batch(const DegBatch& b, int count, unsigned long long* slots, unsigned long long gen,
+                                     hipStream_t s);
+// host[i] = slots[i] (i < n, host-coherent memory, device view), then *flag = seq (system scope)
+hipError_t launch_publish_slots(const unsigned long long* slots, unsigned long long* host, uint64_t n,
+                                unsigned long long* flag, unsigned long long seq, hipStream_t s);
 hipError_t launch_air_eval(const AirEvalArgs& a, hipStream_t s);
 // the Rescue-Prime AIR row in its factored form (mpoly.hpp RescueAirForm), pointwise on a coset:
 // out = first(y) + sum_k mds[k] V_k^alpha - (sum_k mds_inv[k] (V_{m+k} - second_k(y)))^alpha
@@ -88,6 +101,8 @@ struct AirRescueArgs {
 };
 hipError_t launch_air_rescue(const AirRescueArgs& a, hipStream_t s);
 hipError_t launch_lincomb(const LinCombArgs& a, hipStream_t s);
+// out[i] = in[i] - p[i], i < max(len, p.len) (zero past each length; canonical)
+hipError_t launch_sub_small(fe* out, const fe* in, uint64_t len, const SmallPoly& p, hipStream_t s);
 hipError_t launch_eval_small(fe* out, const SmallPoly& p, uint64_t n, const fe* wA, const fe* wB, const fe& off_m,
                              hipStream_t s);
 hipError_t launch_gather_stride(fe* out, const fe* in, uint64_t n, uint64_t stride, hipStream_t s);

@@ -855,10 +855,24 @@ void prove_boundary_quotients(sg_ctx* ctx, const sg_stark& st, const std::vector
     std::vector<DPoly> Zs, diffs;
     std::vector<std::pair<const fe*, uint64_t>> nums;
     for (size_t s = 0; s < m; ++s) {
-      DPoly I = dpoly_upload(ctx, bi[s].data(), bi[s].size());
-      Zs.push_back(dpoly_upload(ctx, bz[s].data(), bz[s].size()));
-      diffs.push_back(lincomb(ctx, {{trace_polys[s].p(), 0, trace_polys[s].len, fe_one()},
-                                    {I.p(), 0, I.len, fe_neg(fe_one())}}));
+      // the interpolant (host, a few coefficients) is subtracted straight from the kernel's
+      // arguments; the zerofier goes to the device only if a path can read it there -- a division
+      // by a small host divisor of degree >= 1 takes its coset values from the host copy (Horner,
+      // ref_inner_ntt): two uploads fewer per register on the prove's critical path
+      if (bi[s].size() <= (size_t)kSmallPolyMax) {
+        SmallPoly sp{};
+        sp.len = (int)bi[s].size();
+        for (size_t k = 0; k < bi[s].size(); ++k) sp.c[k] = bi[s][k];
+        DPoly d = dpoly_alloc(ctx, std::max<uint64_t>(trace_polys[s].len, bi[s].size()));
+        if (d.len) SG_HIP(launch_sub_small(d.p(), trace_polys[s].p(), trace_polys[s].len, sp, ctx->stream));
+        diffs.push_back(std::move(d));
+      } else {
+        DPoly I = dpoly_upload(ctx, bi[s].data(), bi[s].size());
+        diffs.push_back(lincomb(ctx, {{trace_polys[s].p(), 0, trace_polys[s].len, fe_one()},
+                                      {I.p(), 0, I.len, fe_neg(fe_one())}}));
+      }
+      const bool z_host_only = bz[s].size() <= (size_t)kSmallPolyMax && hp_degree(bz[s]) >= 1;
+      Zs.push_back(z_host_only ? DPoly{} : dpoly_upload(ctx, bz[s].data(), bz[s].size()));
       nums.emplace_back(diffs.back().p(), diffs.back().len);
     }
     const std::vector<int64_t> dnum = dev_degrees(ctx, nums);
@@ -884,7 +898,7 @@ void prove_boundary_quotients(sg_ctx* ctx, const sg_stark& st, const std::vector
       if (dd && dist_shard_algebra(dd) && dz >= 0 && dnum[s] >= dz && bz[s].size() <= 64) {
         const DivPlan pl = coset_divide_plan(st.omicron, D, dnum[s], dz);
         if (diffs[s].len <= pl.order && dist_can_shard(pl.order, dist_world(dd))) {
-          const fe* inv = divisor_inverse_values(ctx, pl, g, Zs[s].p(), Zs[s].len, bz[s].data(), &keep);
+          const fe* inv = divisor_inverse_values(ctx, pl, g, Zs[s].p(), bz[s].size(), bz[s].data(), &keep);
           std::vector<uint64_t> key = {kDomainDivisorInverse, pl.order, fe_lo(pl.root), fe_hi(pl.root), fe_lo(g),
                                        fe_hi(g), bz[s].size()};
           for (const fe& c : bz[s]) {
@@ -895,7 +909,7 @@ void prove_boundary_quotients(sg_ctx* ctx, const sg_stark& st, const std::vector
           continue;
         }
       }
-      rep_items.push_back(DivItem{diffs[s].p(), diffs[s].len, Zs[s].p(), Zs[s].len, dz, bz[s].data(), dnum[s]});
+      rep_items.push_back(DivItem{diffs[s].p(), diffs[s].len, Zs[s].p(), bz[s].size(), dz, bz[s].data(), dnum[s]});
       rep_slots.push_back(b0 + s);
     }
     // the replicated quotients' coset divisions, their transforms batched (one coset size)
@@ -945,7 +959,7 @@ void prove_boundary_quotients(sg_ctx* ctx, const sg_stark& st, const std::vector
 // and the proof bytes are those of the replicated path.  The public tables (x-polynomial and
 // zerofier values) are computed whole by every rank with no collective and sliced to its shard.
 void prove_transition_quotients(sg_ctx* ctx, const sg_stark& st, const std::vector<const MPoly*>& tcs,
-                                ProveAlgebra& A, sg_dist* dd = nullptr) {
+                                ProveAlgebra& A, sg_dist* dd = nullptr, const std::function<void()>& overlap = {}) {
   const uint64_t D = st.D, Tp = A.Tp;
   const fe g = st.generator;
   const std::vector<DPoly>& trace_polys = A.trace_polys;
@@ -1156,7 +1170,16 @@ void prove_transition_quotients(sg_ctx* ctx, const sg_stark& st, const std::vect
     return dev_degrees(ctx, qpolys);
   };
   std::vector<int64_t>& qdeg = A.qdeg;
-  qdeg = quotient_degrees();
+  {
+    // the caller's host work (stark_prove: roots, weights, the speculative combination) runs
+    // between the degree scans' launch and the wait for their published results
+    std::vector<std::pair<const fe*, uint64_t>> qpolys;
+    for (const DPoly& q : tqs) qpolys.emplace_back(q.p(), q.len);
+    for (const DPoly& q : bqs) qpolys.emplace_back(q.p(), q.len);
+    const DegScan scan = dev_degrees_begin(ctx, qpolys);
+    if (overlap) overlap();
+    qdeg = dev_degrees_end(ctx, scan);
+  }
   check_div_zero(ctx);
   bool redone = false;
   for (Pending& pd : pending) {
@@ -1229,10 +1252,45 @@ std::vector<DevTerm> combination_terms(sg_ctx* ctx, const sg_stark& st, const st
   return terms;
 }
 
-DPoly prove_combination(sg_ctx* ctx, const sg_stark& st, const std::vector<const MPoly*>& tcs, ProveAlgebra& A,
-                        const std::vector<fe>& weights, const fe* d_rcoef, size_t nrc, uint64_t tcd) {
-  return lincomb(ctx, combination_terms(ctx, st, tcs, A, weights, d_rcoef, nrc, tcd));
+// combination_terms as they will be if every quotient has its expected degree (transition: its
+// degree bound, truncated to it; boundary: its division's result length), built before the degrees
+// are known; empty when the expectation is not well defined (a truncation past the quotient's
+// coefficients, a product wrapping the omicron domain).  stark_prove compares it with the real terms.
+std::vector<DevTerm> speculative_terms(const sg_stark& st, const std::vector<const MPoly*>& tcs, const ProveAlgebra& A,
+                                       const std::vector<fe>& weights, const fe* d_rcoef, size_t nrc, uint64_t tcd) {
+  const uint64_t D = st.D, Tp = A.Tp;
+  const std::vector<uint64_t> tqdb = transition_quotient_degree_bounds(st, tcs);
+  std::vector<DevTerm> terms;
+  size_t wi = 0;
+  terms.push_back({d_rcoef, 0, nrc, weights[wi++]});
+  auto add_pair = [&](const fe* p, uint64_t len, uint64_t shift, int64_t d) -> bool {
+    terms.push_back({p, 0, len, weights[wi++]});
+    const fe w = weights[wi++];
+    if (d < 0) return true;
+    if (shift + (uint64_t)d >= D) return false;
+    terms.push_back({p, shift, (uint64_t)d + 1, w});
+    return true;
+  };
+  for (size_t i = 0; i < A.tqs.size(); ++i) {
+    if (tqdb[i] + 1 > A.tqs[i].len) return {};
+    if (!add_pair(A.tqs[i].p(), tqdb[i] + 1, tcd - tqdb[i], (int64_t)tqdb[i])) return {};
+  }
+  for (size_t s = 0; s < A.bqs.size(); ++s) {
+    const int64_t dz = hp_degree(A.bz[s]);
+    if (dz < 0) return {};
+    const uint64_t bqdb = Tp - 1 - (uint64_t)dz;
+    if (!add_pair(A.bqs[s].p(), A.bqs[s].len, tcd - bqdb, (int64_t)A.bqs[s].len - 1)) return {};
+  }
+  return terms;
 }
+
+bool same_terms(const std::vector<DevTerm>& a, const std::vector<DevTerm>& b) {
+  if (a.size() != b.size()) return false;
+  for (size_t i = 0; i < a.size(); ++i)
+    if (a[i].p != b[i].p || a[i].off != b[i].off || a[i].len != b[i].len || !fe_eq(a[i].w, b[i].w)) return false;
+  return true;
+}
+
 
 // stark.rs:276-562
 // d_trace: rows x m (row-major), d_trace_rand: num_randomizers x m, d_rcoef: nrc -- all on the device
@@ -1326,10 +1384,17 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
     SG_HIP(hipEventRecord(ctx->ev_join, ctx->side));
   }
   mark("bq_lde");
-  prove_transition_quotients(ctx, st, tcs, A);
-  mark("transition_quotients");
-  // roots in the reference's order: boundary quotients (stark.rs:373-386), randomizer (:443)
-  {
+  // The roots, the weights and a speculative combination are done while the quotient degrees are
+  // scanned (prove_transition_quotients' overlap hook): the weights depend only on the roots, and
+  // the combination's terms on the degrees only through the truncations -- taken as the expected
+  // ones (transition: the degree bounds, which any other degree turns into an error anyway;
+  // boundary: the division's result length).  Once the degrees are known the real terms are built
+  // (combination_terms: the reference's degree checks, stark.rs:451-465); when they differ from
+  // the speculative ones in any pointer, offset, length or weight the combination is computed
+  // again (stream-ordered, overwriting the speculative codeword), so the bytes never depend on it.
+  std::vector<fe> weights;
+  auto roots_and_weights = [&]() {
+    // roots in the reference's order: boundary quotients (stark.rs:373-386), randomizer (:443)
     sg_tree* t[4];
     for (size_t s = 0; s < m; ++s) t[s] = bq_trees[s].get();
     finish_trees(ctx, t, (int)m, bq_seq, 0, ctx->side);
@@ -1338,23 +1403,34 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
     // the main stream joins the side stream only where it reads the side stream's output (the
     // openings below): the combination, its LDE and FRI do not, and a cross-stream wait enqueued
     // here held the combination back ~50 us behind the last tree kernel's completion signal
-  }
-  for (size_t s = 0; s < m; ++s) push_obj(ps, SG_OBJ_ROOT, bq_trees[s]->root, 64);
-  push_obj(ps, SG_OBJ_ROOT, r_tree->root, 64);
-  mark("trees_joined");
-  // weights (stark.rs:447-450)
-  uint8_t fs[32];
-  if (ps->fiat_shamir_prover(ps->user, 32, fs) != 0)
-    throw Error{SG_ERR_CALLBACK, "proof stream fiat_shamir callback failed"};
-  std::vector<fe> weights = sample_weights(1 + 2 * A.tqs.size() + 2 * bqs.size(), fs, 32);
-  DPoly comb = prove_combination(ctx, st, tcs, A, weights, d_rcoef, nrc, tcd);
-  SG_REQUIRE(comb.len <= Nf, "fast_coset_evaluate: polynomial longer than root_order");
-  DPoly comb_cw = dpoly_alloc(ctx, Nf);
-  {
+    for (size_t s = 0; s < m; ++s) push_obj(ps, SG_OBJ_ROOT, bq_trees[s]->root, 64);
+    push_obj(ps, SG_OBJ_ROOT, r_tree->root, 64);
+    // weights (stark.rs:447-450)
+    uint8_t fs[32];
+    if (ps->fiat_shamir_prover(ps->user, 32, fs) != 0)
+      throw Error{SG_ERR_CALLBACK, "proof stream fiat_shamir callback failed"};
+    weights = sample_weights(1 + 2 * A.tqs.size() + 2 * bqs.size(), fs, 32);
+  };
+  DPoly comb_cw, comb;
+  auto combination_lde = [&](const std::vector<DevTerm>& terms) {
+    if (!comb_cw.len) comb_cw = dpoly_alloc(ctx, Nf);
+    comb = lincomb(ctx, terms);
+    SG_REQUIRE(comb.len <= Nf, "fast_coset_evaluate: polynomial longer than root_order");
     const fe* in = comb.p();
     fe* out = comb_cw.p();
     coset_evaluate_batch(ctx, st.omega, Nf, g, &in, comb.len, &out, 1);
-  }
+  };
+  std::vector<DevTerm> spec;
+  prove_transition_quotients(ctx, st, tcs, A, nullptr, [&]() {
+    roots_and_weights();
+    spec = speculative_terms(st, tcs, A, weights, d_rcoef, nrc, tcd);
+    if (!spec.empty()) combination_lde(spec);
+  });
+  mark("transition_quotients");
+  if (weights.empty()) roots_and_weights();
+  mark("trees_joined");
+  const std::vector<DevTerm> terms = combination_terms(ctx, st, tcs, A, weights, d_rcoef, nrc, tcd);
+  if (!same_terms(terms, spec)) combination_lde(terms);
   mark("combination_lde");
   // FRI (stark.rs:514-522) and the openings (stark.rs:524-560): the openings' indices follow from
   // FRI's top-level indices, so their Value / Path objects join the FRI query phase's single
