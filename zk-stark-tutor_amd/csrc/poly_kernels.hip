@@ -626,6 +626,30 @@ hipError_t launch_eval_small(fe* out, const SmallPoly& p, uint64_t n, const fe* 
   return hipGetLastError();
 }
 
+// the randomized trace's m register columns side by side (column stride Tp = rows + nrand): column s
+// is trace[i m + s] for i < rows, then rand[(i - rows) m + s] -- the 2m strided gathers of the
+// trace interpolation (stark.rs:285-301) in one launch
+__global__ __launch_bounds__(kBlock) void k_gather_trace_cols(fe* __restrict__ out, const fe* __restrict__ trace,
+                                                              uint64_t rows, const fe* __restrict__ rnd, uint64_t nrand,
+                                                              uint64_t m) {
+  const uint64_t Tp = rows + nrand, total = Tp * m;
+  for (uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; t < total; t += (uint64_t)gridDim.x * blockDim.x) {
+    const uint64_t i = t / m, s = t - i * m;  // consecutive lanes read consecutive trace elements
+    const fe v = i < rows ? ld_fe(trace + t) : ld_fe(rnd + (i - rows) * m + s);
+    st_fe(out + s * Tp + i, v);
+  }
+}
+
+hipError_t launch_gather_trace_cols(fe* out, const fe* trace, uint64_t rows, const fe* rnd, uint64_t nrand, uint64_t m,
+                                    hipStream_t s) {
+  const uint64_t total = (rows + nrand) * m;
+  if (!total) return hipSuccess;
+  ProfScope ps("gather_stride", 32 * total, s);
+  hipLaunchKernelGGL(k_gather_trace_cols, dim3((unsigned)grid_for(total)), dim3(kBlock), 0, s, out, trace, rows, rnd,
+                     nrand, m);
+  return hipGetLastError();
+}
+
 hipError_t launch_gather_stride(fe* out, const fe* in, uint64_t n, uint64_t stride, hipStream_t s) {
   if (!n) return hipSuccess;
   ProfScope ps("gather_stride", 32 * n, s);

@@ -106,6 +106,9 @@ hipError_t launch_sub_small(fe* out, const fe* in, uint64_t len, const SmallPoly
 hipError_t launch_eval_small(fe* out, const SmallPoly& p, uint64_t n, const fe* wA, const fe* wB, const fe& off_m,
                              hipStream_t s);
 hipError_t launch_gather_stride(fe* out, const fe* in, uint64_t n, uint64_t stride, hipStream_t s);
+// out[s Tp + i] = i < rows ? trace[i m + s] : rnd[(i - rows) m + s] for s < m, i < Tp = rows + nrand
+hipError_t launch_gather_trace_cols(fe* out, const fe* trace, uint64_t rows, const fe* rnd, uint64_t nrand, uint64_t m,
+                                    hipStream_t s);
 // product tree over an arbitrary domain (poly.cpp: tree_exact): level-3 leaves (8 points per lane,
 // rows of 16: Z and optionally N = sum c_i Z / (x - d_i)), pairwise NTT-domain combine, wrap fix
 hipError_t launch_tree_leaves(const fe* dom, uint64_t n, uint64_t nodes, fe* Z, const fe* c, fe* N, const fe& r2,

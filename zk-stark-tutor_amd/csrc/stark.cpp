@@ -824,10 +824,7 @@ void prove_trace_polys(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_
   {
     // the m columns side by side (column stride Tp), interpolated as one batch
     DPoly cols = dpoly_alloc(ctx, m * Tp);
-    for (size_t s = 0; s < m; ++s) {
-      SG_HIP(launch_gather_stride(cols.p() + s * Tp, d_trace + s, rows, m, ctx->stream));
-      SG_HIP(launch_gather_stride(cols.p() + s * Tp + rows, d_trace_rand + s, st.num_randomizers, m, ctx->stream));
-    }
+    SG_HIP(launch_gather_trace_cols(cols.p(), d_trace, rows, d_trace_rand, st.num_randomizers, m, ctx->stream));
     std::vector<DevBuf> keep;
     if (!(dd && interpolate_geometric_batch_dist(dd, st.omicron, D, cols.p(), Tp, m, Tp, trace_polys, keep)))
       trace_polys = interpolate_geometric_batch_dev(ctx, st.omicron, D, cols.p(), Tp, m, Tp);

@@ -230,7 +230,14 @@ def lib():
                               "(or __graft_entry__.build()); there is no CPU fallback")
         l = ctypes.CDLL(LIB_PATH)
         for name, (res, args) in PROTOTYPES.items():
-            fn = getattr(l, name)
+            try:
+                fn = getattr(l, name)
+            except AttributeError:
+                # an older build loaded through SG_LIB_PATH for a same-box A/B (tools/ab.sh) may lack
+                # newer entry points; calling one raises.  The product library must export them all.
+                if "SG_LIB_PATH" in os.environ:
+                    continue
+                raise
             fn.restype = res
             fn.argtypes = args
         _lib = l
