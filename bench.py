@@ -54,9 +54,9 @@ REGISTERS = 2       # Rescue-Prime m = 2
 HBM_PEAK_GBS = 8000.0
 # PMC HBM bytes of this workload's kernels (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes on
 # `bench.py --steps 3 --warmup 1 --no-side`, tools/pmc_passes.sh + tools/pmc_traffic.py)
-PMC_TRAFFIC_FILE = "r05_pmc_traffic_e2e_final.json"
-PMC_VALU_FILE = "r05_pmc_valu_e2e_final.json"  # SQ_INSTS_VALU pass (tools/pmc_passes.sh + tools/pmc_valu.py)
-VALU_MIX_FILE = "r05_valu_mix_final.json"  # static full/half-rate mix of the same build (tools/valu_mix.py)
+PMC_TRAFFIC_FILE = "r06_pmc_traffic_e2e.json"
+PMC_VALU_FILE = "r06_pmc_valu_e2e.json"  # SQ_INSTS_VALU pass (tools/pmc_passes.sh + tools/pmc_valu.py)
+VALU_MIX_FILE = "r06_valu_mix.json"  # static full/half-rate mix of the same build (tools/valu_mix.py)
 MAX_CLOCK_GHZ = 2.4  # MI355X_MICROARCH.md:34
 
 
