@@ -70,6 +70,8 @@ int sg_ctx_cached_tables(const sg_ctx* ctx, size_t* domain_tables, size_t* twidd
  *   "fri_gate"       1 (default): FRI::commit queues round r+1's fold + tree behind a device gate
  *                    before round r's challenge exists (the host raises the gate after writing K;
  *                    a gate left 60 s raises an error); 0: each round is launched after its challenge
+ *   "fri_gate_timeout_ms" 60000 (default): how long a gate waits for its challenge before the call
+ *                    fails with SG_ERR_HIP (a test sets it low to exercise the deadline)
  * SG_ERR_INVALID for an unknown name. */
 int sg_ctx_set_option(sg_ctx* ctx, const char* name, int64_t value);
 /* Device memory (no reference counterpart): `live` = bytes of the context's buffer pool in use,

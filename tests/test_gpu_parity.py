@@ -370,6 +370,42 @@ def test_fri_gate_bytes_and_release_on_callback_failure():
     assert gps.digest() == ops.digest()
 
 
+class _FsSlowAt(o.IndependentProofStream):
+    """A foreign proof stream whose k-th Fiat-Shamir call sleeps `seconds` first."""
+
+    def __init__(self, k, seconds):
+        super().__init__()
+        self.calls, self.k, self.seconds = 0, k, seconds
+
+    def fiat_shamir_prover(self, num_bytes):
+        import time
+        self.calls += 1
+        if self.calls == self.k:
+            time.sleep(self.seconds)
+        return super().fiat_shamir_prover(num_bytes)
+
+
+def test_fri_gate_deadline():
+    """A gated round whose challenge comes later than the gate's deadline (context option
+    fri_gate_timeout_ms, 60 s by default; 20 ms here against a 0.3 s callback) fails the call with
+    the gate's timeout -- never a proof folded with a stale challenge -- and the context then
+    proves the oracle's bytes again."""
+    n, exp, c = 1 << 14, 8, 64
+    omega, cw = _fri_case(n, exp, c, 43)
+    ofri = o.FRI(o.GENERATOR, omega, n, exp, c)
+    ops = o.IndependentProofStream()
+    otop = ofri.prove(cw, ops)
+    gfri = sg.FRI(o.GENERATOR, omega, n, exp, c)
+    ctx = sg.Context.default()
+    with ctx.option("fri_gate_timeout_ms", 20, 60000):
+        with pytest.raises(sg.StarkGpuError, match="gate timed out"):
+            gfri.prove(cw, _FsSlowAt(2, 0.3))
+        gps = sg.IndependentProofStream()  # a prompt stream under the short deadline
+        assert gfri.prove(cw, gps) == otop and gps.digest() == ops.digest()
+    gps = sg.IndependentProofStream()
+    assert gfri.prove(cw, gps) == otop and gps.digest() == ops.digest()
+
+
 def test_fri_tampered_codeword_rejected():
     """fri.rs:514-528: zeroing a third of the low-degree positions makes verify fail."""
     n, exp, c = 256, 4, 17

@@ -468,6 +468,7 @@ extern "C" int sg_ctx_set_option(sg_ctx* ctx, const char* name, int64_t value) {
   else if (n == "world1_sharded") ctx->opt.world1_sharded = v;
   else if (n == "lean_drop" && value >= 0 && value <= 3) ctx->opt.lean_drop = (int)value;
   else if (n == "fri_gate") ctx->opt.fri_gate = v;
+  else if (n == "fri_gate_timeout_ms" && value >= 1) ctx->opt.fri_gate_timeout_ms = value;
   else {
     ctx->last_error = "unknown context option: " + n;
     return SG_ERR_INVALID;
@@ -1260,7 +1261,7 @@ void fri_commit_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, co
     kdev = DevBuf(ctx, sizeof(fe));
     __atomic_store_n(ctx->gate_timeout, 0u, __ATOMIC_RELAXED);
   }
-  constexpr double kGateSeconds = 60.0;
+  const double gate_seconds = ctx->opt.fri_gate_timeout_ms / 1e3;
   const uint64_t last_len = st.lengths.back();
   // the last codeword on the host (pinned staging, allocated before any gate is pending)
   fe* last = static_cast<fe*>(ctx->staging(1, last_len * sizeof(fe)));
@@ -1290,7 +1291,7 @@ void fri_commit_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, co
         const uint64_t want = ++ctx->gate_seq;
         gate.pending = want;
         SG_HIP(launch_fri_gate(ctx->gate_word_dev, want, ctx->gate_k_dev, kdev.as<fe>(), ctx->gate_timeout_dev,
-                               kGateSeconds, ctx->stream));
+                               gate_seconds, ctx->stream));
         fold.Kp = kdev.as<fe>();
       }
       seqs[r] = fill_tree_launch(ctx, st.cw[r], st.trees[r].get(), &fold);
@@ -1325,7 +1326,8 @@ void fri_commit_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, co
   // push last codeword (fri.rs:166)
   host_wait(ctx, ctx->stream);
   if (gated && __atomic_load_n(ctx->gate_timeout, __ATOMIC_ACQUIRE))
-    throw Error{SG_ERR_HIP, "FRI round gate timed out (no challenge within 60 s)"};
+    throw Error{SG_ERR_HIP, "FRI round gate timed out (no challenge within " +
+                            std::to_string(ctx->opt.fri_gate_timeout_ms) + " ms)"};
   ObjWriter w{ps};
   uint8_t* payload = w.begin(SG_OBJ_CODEWORD, last_len * 16);
   for (uint64_t i = 0; i < last_len; ++i) put_u128_be_at(payload + 16 * i, last[i]);

@@ -137,6 +137,7 @@ struct sg_ctx {
     bool world1_sharded = false; // a one-rank communicator proves through the four-step path
     int lean_drop = 3;           // the most levels a lean tree drops (0..3)
     bool fri_gate = true;        // FRI rounds queued behind a device gate before their challenge
+    int64_t fri_gate_timeout_ms = 60000;  // a gate left this long times out (the call then fails)
   } opt;
   bool domain_cache_on() const { return opt.domain_cache; }
   void* domain_table(const std::vector<uint64_t>& key) const;
