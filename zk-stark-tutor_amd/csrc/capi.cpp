@@ -1057,9 +1057,10 @@ void ObjWriter::commit() {
   if (!direct) push_obj(ps, code, scratch.data(), scratch.size());
 }
 
-void TailWriter::value(const fe* base, uint32_t sel, uint64_t mask) {
+void TailWriter::value(const fe* base, uint64_t len, uint32_t sel, uint64_t mask) {
   TailItem it{};
   it.src[0] = (uint64_t)(uintptr_t)base;
+  it.n = len;
   it.dst = bytes;
   it.code = SG_OBJ_VALUE;
   it.count = 1;
@@ -1071,11 +1072,12 @@ void TailWriter::value(const fe* base, uint32_t sel, uint64_t mask) {
   field = true;
 }
 
-void TailWriter::leafs(const fe* a, const fe* b, const fe* c, uint32_t sel, uint64_t mask) {
+void TailWriter::leafs(const fe* a, const fe* b, const fe* c, uint64_t len, uint32_t sel, uint64_t mask) {
   TailItem it{};
   it.src[0] = (uint64_t)(uintptr_t)a;
   it.src[1] = (uint64_t)(uintptr_t)b;
   it.src[2] = (uint64_t)(uintptr_t)c;
+  it.n = len;
   it.dst = bytes;
   it.code = SG_OBJ_LEAFS;
   it.count = 3;
@@ -1386,7 +1388,7 @@ void fri_prove_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, con
       const uint64_t mask = half - 1;  // round lengths are powers of two (Merkle leaves)
       const fe* cur = st.cw[r];
       const fe* nxt = st.cw[r + 1];
-      for (size_t s = 0; s < c; ++s) tw.leafs(cur, cur + half, nxt, (uint32_t)s, mask);
+      for (size_t s = 0; s < c; ++s) tw.leafs(cur, cur + half, nxt, half, (uint32_t)s, mask);
       const sg_tree* tc = st.trees[r].get();
       const sg_tree* tn = st.trees[r + 1].get();
       for (size_t s = 0; s < c; ++s) {

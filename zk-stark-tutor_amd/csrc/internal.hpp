@@ -193,9 +193,10 @@ struct TailWriter {
   uint8_t* dev = nullptr;    // the context's tail buffer: uploaded items, then the table
   uint8_t* stage = nullptr;  // pinned staging (slot 0): items, then the table
   size_t table_n = 0;
-  // Value base[idx]; Leafs a[idx], b[idx], c[idx]; the Path of leaf add + idx (idx = table[sel] & mask)
-  void value(const fe* base, uint32_t sel, uint64_t mask = ~0ull);
-  void leafs(const fe* a, const fe* b, const fe* c, uint32_t sel, uint64_t mask);
+  // Value base[idx]; Leafs a[idx], b[idx], c[idx]; the Path of leaf add + idx (idx = table[sel] & mask;
+  // len bounds idx: a larger one reads element 0 rather than faulting, see k_serialize_tail)
+  void value(const fe* base, uint64_t len, uint32_t sel, uint64_t mask = ~0ull);
+  void leafs(const fe* a, const fe* b, const fe* c, uint64_t len, uint32_t sel, uint64_t mask);
   void path(const sg_tree* t, uint32_t sel, uint64_t mask, uint64_t add = 0);
   // the items to the device ahead of the table (of table_n entries)
   void upload(sg_ctx* ctx, size_t table_n);

@@ -403,10 +403,14 @@ __global__ __launch_bounds__(64) void k_serialize_tail(const TailItem* __restric
                                                       const uint64_t* __restrict__ table, uint8_t* __restrict__ out) {
   TailItem it = items[blockIdx.x];
   if (it.sel != kTailLiteral) {  // uniform over the block
-    const uint64_t idx = table[it.sel] & it.mask;
+    // an index past its object (a table not yet valid: the device sampler's failure, redone from the
+    // host) reads element 0 instead of faulting; such a block's bytes are always rewritten
+    uint64_t idx = table[it.sel] & it.mask;
     if (it.code == 2) {
-      it.index += idx;
+      const uint64_t i2 = it.index + idx;
+      it.index = i2 < it.n ? i2 : 0;
     } else {
+      if (idx >= it.n) idx = 0;
       it.src[0] += 16 * idx;
       it.src[1] += 16 * idx;
       it.src[2] += 16 * idx;

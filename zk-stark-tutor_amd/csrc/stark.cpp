@@ -1446,7 +1446,7 @@ void stark_prove(sg_ctx* ctx, const sg_stark& st, const fe* d_trace, size_t rows
     SG_HIP(hipStreamWaitEvent(ctx->stream, ctx->ev_join, 0));  // the openings read the side-stream trees
     for (auto& ct : cts)
       for (uint32_t j = 0; j < 4 * c; ++j) {
-        tw.value(ct.first, sel0 + j);
+        tw.value(ct.first, Nf, sel0 + j);
         tw.path(ct.second, sel0 + j, ~0ull);
       }
   };
