@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstring>
+#include <ctime>
 #include <memory>
 #include <string>
 #include <vector>
@@ -1305,9 +1306,23 @@ void fri_commit_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, co
   // longest) hashes; its stream work is queued here, before any gate (a copy the runtime completes
   // on the host could otherwise wait on a pending gate)
   if (overlap) overlap();
+  // SG_FRI_TIMING=1 (A/B builds): per round, the host's clock (CLOCK_MONOTONIC / CLOCK_BOOTTIME ns)
+  // when it starts waiting for the root, sees it, and raises the gate -- to align with a kernel trace
+  const bool timing = SG_KNOB(FRI_TIMING, 0) != 0;
+  auto stamp = [](clockid_t id) {
+    timespec ts;
+    clock_gettime(id, &ts);
+    return (long long)ts.tv_sec * 1000000000ll + ts.tv_nsec;
+  };
+  std::vector<long long> tw(timing ? 4 * rounds : 0, 0);
   for (size_t r = 0; r < rounds; ++r) {
     if (gated && r + 1 < rounds) launch_round(r + 1, nullptr);
+    if (timing) tw[4 * r] = stamp(CLOCK_MONOTONIC);
     fill_tree_finish(ctx, st.trees[r].get(), seqs[r]);
+    if (timing) {
+      tw[4 * r + 1] = stamp(CLOCK_MONOTONIC);
+      tw[4 * r + 3] = stamp(CLOCK_BOOTTIME);
+    }
     push_obj(ps, SG_OBJ_ROOT, st.trees[r]->root, 64);
     if (r == rounds - 1) break;
     uint8_t chal[32];
@@ -1320,6 +1335,7 @@ void fri_commit_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, co
       ctx->gate_k[1] = fe_hi(K);
       __atomic_store_n(ctx->gate_word, gate.pending, __ATOMIC_RELEASE);
       gate.pending = 0;
+      if (timing) tw[4 * r + 2] = stamp(CLOCK_MONOTONIC);
       if (r + 2 == rounds) copy_last();
     } else {
       launch_round(r + 1, &K);
@@ -1327,6 +1343,8 @@ void fri_commit_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, co
   }
   // push last codeword (fri.rs:166)
   host_wait(ctx, ctx->stream);
+  for (size_t r = 0; timing && r < rounds; ++r)
+    fprintf(stderr, "sg-fri %zu %lld %lld %lld boot %lld\n", r, tw[4 * r], tw[4 * r + 1], tw[4 * r + 2], tw[4 * r + 3]);
   if (gated && __atomic_load_n(ctx->gate_timeout, __ATOMIC_ACQUIRE))
     throw Error{SG_ERR_HIP, "FRI round gate timed out (no challenge within " +
                             std::to_string(ctx->opt.fri_gate_timeout_ms) + " ms)"};
