@@ -1132,25 +1132,41 @@ void TailWriter::flush(sg_ctx* ctx, const sg_proof_stream* ps, const uint64_t* t
     memcpy(stage + ib, table, 8 * table_n);
     SG_HIP(hipMemcpyAsync(dtable, stage + ib, 8 * table_n, hipMemcpyHostToDevice, ctx->stream));
   }
-  DevBuf dout(ctx, bytes);
-  SG_HIP(launch_serialize_tail(reinterpret_cast<const TailItem*>(dev), dtable, (uint32_t)ni, dout.as<uint8_t>(), bytes, ctx->stream));
+  DevBuf dout;
+  auto serialize = [&](uint8_t* out) {
+    SG_HIP(launch_serialize_tail(reinterpret_cast<const TailItem*>(dev), dtable, (uint32_t)ni, out, bytes, ctx->stream));
+  };
+  auto serialize_dev = [&]() {
+    dout = DevBuf(ctx, bytes);
+    serialize(dout.as<uint8_t>());
+  };
   if (ps->push == stream_push_cb) {
-    // a native stream: the block lands in its body by one device copy (or through staging when the
-    // runtime refuses to page-lock the body)
+    // a native stream: the serializer writes the block straight into the page-locked body (its
+    // whole-dword stores cross PCIe while later objects are still being assembled, instead of a
+    // separate 3-4 MB device-to-host copy after it); through a device buffer and staging when the
+    // runtime refuses to page-lock or map the body
     Stream& st = reinterpret_cast<sg_stream*>(ps->user)->s;
     st.body.reserve(st.body.size() + bytes);  // grow first: the registration covers the block
     const bool pinned = ctx->opt.stream_pin && st.body.pin();
     uint8_t* dst = st.append_block(bytes, offs, field);
-    if (pinned) {
+    if (pinned && st.body.pinned_dev && SG_KNOB(TAIL_DIRECT, 1)) {
+      serialize(st.body.pinned_dev + (dst - st.body.pinned_p));
+      // a stream synchronisation (not a query): the runtime's system-scope release that makes the
+      // kernel's host-memory stores visible here
+      SG_HIP(hipStreamSynchronize(ctx->stream));
+    } else if (pinned) {
+      serialize_dev();
       SG_HIP(hipMemcpyAsync(dst, dout.get(), bytes, hipMemcpyDeviceToHost, ctx->stream));
       host_wait(ctx, ctx->stream);
     } else {
+      serialize_dev();
       uint8_t* stg = static_cast<uint8_t*>(ctx->staging(1, bytes));
       SG_HIP(hipMemcpyAsync(stg, dout.get(), bytes, hipMemcpyDeviceToHost, ctx->stream));
       host_wait(ctx, ctx->stream);
       memcpy(dst, stg, bytes);
     }
   } else {
+    serialize_dev();
     uint8_t* stg = static_cast<uint8_t*>(ctx->staging(1, bytes));
     SG_HIP(hipMemcpyAsync(stg, dout.get(), bytes, hipMemcpyDeviceToHost, ctx->stream));
     host_wait(ctx, ctx->stream);

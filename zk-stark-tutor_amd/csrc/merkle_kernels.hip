@@ -417,11 +417,24 @@ __global__ __launch_bounds__(64) void k_serialize_tail(const TailItem* __restric
     }
   }
   const uint32_t l = threadIdx.x;
-  uint8_t* o = out + it.dst;
   const bool path = it.code == 2;  // SG_OBJ_PATH
+  // The object's bytes are assembled in LDS at the alignment they take in `out` (`a`: the start's
+  // offset in its 16-byte word), then stored as whole 16-byte words -- 1 KiB contiguous per store
+  // instruction, which `out` in host memory (the pinned stream body) needs for PCIe rate -- with byte
+  // stores only in the words where the object starts or ends (their other bytes are other objects').
+  __shared__ uint4 sw[(15 + 9 + 72 * 64 + 15) / 16];
+  uint8_t* sb = reinterpret_cast<uint8_t*>(sw);
+  const uintptr_t g0 = reinterpret_cast<uintptr_t>(out + it.dst);
+  const uint32_t a = (uint32_t)(g0 & 15);
+  const uint32_t rec = path ? 72u : 16u;
+  const uint32_t size = 9 + rec * it.count;
+  auto be64 = [&](uint32_t pos, uint64_t v) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) sb[pos + j] = (uint8_t)(v >> (8 * (7 - j)));
+  };
   if (l == 0) {
-    o[0] = (uint8_t)it.code;
-    put_be64_dev(o + 1, (path ? 72ull : 16ull) * it.count);
+    sb[a] = (uint8_t)it.code;
+    be64(a + 1, (uint64_t)rec * it.count);
   }
   __shared__ uint64_t msg[8][16];  // level-0 messages (decimal leaf words)
   __shared__ uint64_t mt[16][8];   // the block's levels 0 .. K-1: 2^K + 2^(K-1) + ... digests
@@ -460,30 +473,42 @@ __global__ __launch_bounds__(64) void k_serialize_tail(const TailItem* __restric
       cnt >>= 1;
     }
   }
-  if (l >= it.count) return;
-  if (path) {
-    uint8_t* e = o + 9 + 72 * (uint64_t)l;
-    put_be64_dev(e, 64);
-    uint64_t h[8];
-    if (l < K) {  // sibling at level l inside the rehashed block
-      const uint32_t off = (1u << (K + 1)) - (1u << (K + 1 - l));  // 2^K + 2^(K-1) + ... (l terms)
-      const uint32_t sib = (uint32_t)(((it.index >> l) ^ 1) & ((1ull << (K - l)) - 1));
+  if (l < it.count) {
+    const uint32_t e = a + 9 + rec * l;
+    if (path) {
+      be64(e, 64);
+      uint64_t h[8];
+      if (l < K) {  // sibling at level l inside the rehashed block
+        const uint32_t off = (1u << (K + 1)) - (1u << (K + 1 - l));  // 2^K + 2^(K-1) + ... (l terms)
+        const uint32_t sib = (uint32_t)(((it.index >> l) ^ 1) & ((1ull << (K - l)) - 1));
 #pragma unroll
-      for (int k = 0; k < 8; ++k) h[k] = mt[off + sib][k];
+        for (int k = 0; k < 8; ++k) h[k] = mt[off + sib][k];
+      } else {
+        // level l sibling; a lean tree's buffer starts at level K
+        const uint64_t d = (2 * it.n - 2 * (it.n >> l)) - (2 * it.n - 2 * (it.n >> K)) + ((it.index >> l) ^ 1);
+        ld_digest(reinterpret_cast<const uint64_t*>(it.src[0] + 64 * d), h);
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) sb[e + 8 + 8 * k + j] = (uint8_t)(h[k] >> (8 * j));
     } else {
-      // level l sibling; a lean tree's buffer starts at level K
-      const uint64_t d = (2 * it.n - 2 * (it.n >> l)) - (2 * it.n - 2 * (it.n >> K)) + ((it.index >> l) ^ 1);
-      ld_digest(reinterpret_cast<const uint64_t*>(it.src[0] + 64 * d), h);
+      const fe v = ld_fe(reinterpret_cast<const fe*>(it.src[l]));
+      be64(e, fe_hi(v));
+      be64(e + 8, fe_lo(v));
     }
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-#pragma unroll
-      for (int j = 0; j < 8; ++j) e[8 + 8 * k + j] = (uint8_t)(h[k] >> (8 * j));
-  } else {
-    const fe v = ld_fe(reinterpret_cast<const fe*>(it.src[l]));
-    uint8_t* e = o + 9 + 16 * (uint64_t)l;
-    put_be64_dev(e, fe_hi(v));
-    put_be64_dev(e + 8, fe_lo(v));
+  }
+  __syncthreads();
+  uint4* gw = reinterpret_cast<uint4*>(g0 - a);
+  uint8_t* gb = reinterpret_cast<uint8_t*>(g0 - a);
+  const uint32_t end = a + size, nd = (end + 15) / 16;
+  for (uint32_t i = l; i < nd; i += 64) {
+    const uint32_t b0 = 16 * i;
+    if (b0 >= a && b0 + 16 <= end) {
+      gw[i] = sw[i];
+    } else {
+      for (uint32_t b = b0 < a ? a : b0; b < b0 + 16 && b < end; ++b) gb[b] = sb[b];
+    }
   }
 }
 

@@ -49,6 +49,7 @@ void ByteBuf::swap(ByteBuf& o) {
   std::swap(n, o.n);
   std::swap(cap, o.cap);
   std::swap(pinned_p, o.pinned_p);
+  std::swap(pinned_dev, o.pinned_dev);
 }
 
 bool ByteBuf::pin() {
@@ -62,6 +63,10 @@ bool ByteBuf::pin() {
     return false;
   }
   pinned_p = p;
+  // the device's address of the registered block (kernels may write the body directly)
+  void* d = nullptr;
+  pinned_dev = hipHostGetDevicePointer(&d, p, 0) == hipSuccess ? static_cast<uint8_t*>(d) : nullptr;
+  if (!pinned_dev) (void)hipGetLastError();
   return true;
 }
 
@@ -69,6 +74,7 @@ void ByteBuf::unpin() {
   if (!pinned_p) return;
   (void)hipHostUnregister(pinned_p);
   pinned_p = nullptr;
+  pinned_dev = nullptr;
 }
 
 namespace {

@@ -25,6 +25,7 @@ struct ByteBuf {
   // moves or dies, so a cached body registers once); false if the runtime refuses
   bool pin();
   uint8_t* pinned_p = nullptr;
+  uint8_t* pinned_dev = nullptr;  // the registered block's device address (nullptr: not mapped)
 
  private:
   void unpin();
