@@ -1149,10 +1149,12 @@ void TailWriter::flush(sg_ctx* ctx, const sg_proof_stream* ps, const uint64_t* t
     st.body.reserve(st.body.size() + bytes);  // grow first: the registration covers the block
     const bool pinned = ctx->opt.stream_pin && st.body.pin();
     uint8_t* dst = st.append_block(bytes, offs, field);
-    if (pinned && st.body.pinned_dev && SG_KNOB(TAIL_DIRECT, 1)) {
+    // (a body registered while another device was current -- a cached body shared by contexts on
+    // several GPUs -- takes the copy: its device address is that device's view)
+    if (pinned && st.body.pinned_dev && st.body.pinned_device == ctx->device && SG_KNOB(TAIL_DIRECT, 1)) {
       serialize(st.body.pinned_dev + (dst - st.body.pinned_p));
       // a stream synchronisation (not a query): the runtime's system-scope release that makes the
-      // kernel's host-memory stores visible here
+      // kernel's host-memory stores visible here (no deadline watch: the serializer waits on no peer)
       SG_HIP(hipStreamSynchronize(ctx->stream));
     } else if (pinned) {
       serialize_dev();

@@ -50,6 +50,7 @@ void ByteBuf::swap(ByteBuf& o) {
   std::swap(cap, o.cap);
   std::swap(pinned_p, o.pinned_p);
   std::swap(pinned_dev, o.pinned_dev);
+  std::swap(pinned_device, o.pinned_device);
 }
 
 bool ByteBuf::pin() {
@@ -66,7 +67,11 @@ bool ByteBuf::pin() {
   // the device's address of the registered block (kernels may write the body directly)
   void* d = nullptr;
   pinned_dev = hipHostGetDevicePointer(&d, p, 0) == hipSuccess ? static_cast<uint8_t*>(d) : nullptr;
-  if (!pinned_dev) (void)hipGetLastError();
+  if (!pinned_dev || hipGetDevice(&pinned_device) != hipSuccess) {
+    (void)hipGetLastError();
+    pinned_dev = nullptr;
+    pinned_device = -1;
+  }
   return true;
 }
 
@@ -75,6 +80,7 @@ void ByteBuf::unpin() {
   (void)hipHostUnregister(pinned_p);
   pinned_p = nullptr;
   pinned_dev = nullptr;
+  pinned_device = -1;
 }
 
 namespace {

@@ -26,6 +26,7 @@ struct ByteBuf {
   bool pin();
   uint8_t* pinned_p = nullptr;
   uint8_t* pinned_dev = nullptr;  // the registered block's device address (nullptr: not mapped)
+  int pinned_device = -1;         // the device current when it was registered (pinned_dev is its view)
 
  private:
   void unpin();
