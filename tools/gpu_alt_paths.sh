@@ -19,6 +19,7 @@
 #   SG_MERKLE_QUAD_TOP_MAX=64     one-block tree tops only from 64 nodes down
 #   SG_FRI_GATE=0                 each FRI round launched after its challenge (no device gate; round 6)
 #   SG_TAIL_DIRECT=0              the proof tail serialized to device memory and copied (round 6)
+#   SG_FRI_TWO_STREAMS=0          gated FRI rounds all on the main stream (round 6)
 # Usage (from the repo root on the GPU box): bash tools/gpu_alt_paths.sh [tag]
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
@@ -28,6 +29,6 @@ mkdir -p gpurun_out
 SG_LIB_PATH=$R/zk-stark-tutor_amd/starkgpu/libstarkgpu_ab.so \
 SG_NO_DOMAIN_CACHE=1 SG_AIR_GENERIC=1 SG_NTT_TILES=0 SG_GEO_DECIMATE=0 SG_STREAM_PRIORITY=0 SG_DIST_FRI_TAIL=0 \
 SG_MERKLE_QUAD_LEAF_BELOW=0 SG_MERKLE_QUAD_TOP=0 SG_MERKLE_LEAF_PAIRS=0 SG_MERKLE_NODE_FUSE=3 SG_NTT_SMALL_WHOLE=0 \
-SG_MERKLE_FOREST_QUAD=0 SG_LEAN_TREES=0 SG_MERKLE_QUAD_LEAF_NODES=64 SG_MERKLE_QUAD_TOP_MAX=64 SG_FRI_GATE=0 SG_TAIL_DIRECT=0 \
+SG_MERKLE_FOREST_QUAD=0 SG_LEAN_TREES=0 SG_MERKLE_QUAD_LEAF_NODES=64 SG_MERKLE_QUAD_TOP_MAX=64 SG_FRI_GATE=0 SG_TAIL_DIRECT=0 SG_FRI_TWO_STREAMS=0 \
   timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
   > gpurun_out/pt_alt_$TAG.log 2>&1

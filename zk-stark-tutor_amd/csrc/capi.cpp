@@ -778,18 +778,18 @@ void fill_tree(sg_ctx* ctx, const fe* d_leaves, sg_tree* t, const FoldLeaves* fo
 }
 
 // fill_tree in two halves, so work can be queued behind the tree before the host waits for its root
-uint64_t fill_tree_launch(sg_ctx* ctx, const fe* d_leaves, sg_tree* t, const FoldLeaves* fold) {
+uint64_t fill_tree_launch(sg_ctx* ctx, const fe* d_leaves, sg_tree* t, const FoldLeaves* fold, hipStream_t s) {
   uint64_t* buf = t->buf.as<uint64_t>();
   uint64_t* root_dev = ctx->pinned_roots_dev;
   uint64_t* flag_dev = ctx->pinned_roots_dev + sg_ctx::kFlagIndex;
   const uint64_t seq = ++ctx->root_seq;
-  SG_HIP(launch_merkle_tree(&d_leaves, &buf, 1, t->n, &root_dev, ctx->stream, 0, 0, 0, &flag_dev, seq, fold,
+  SG_HIP(launch_merkle_tree(&d_leaves, &buf, 1, t->n, &root_dev, s ? s : ctx->stream, 0, 0, 0, &flag_dev, seq, fold,
                             t->drop));
   return seq;
 }
 
-void fill_tree_finish(sg_ctx* ctx, sg_tree* t, uint64_t seq) {
-  wait_roots(ctx, 1, seq, 0, ctx->stream);
+void fill_tree_finish(sg_ctx* ctx, sg_tree* t, uint64_t seq, hipStream_t s) {
+  wait_roots(ctx, 1, seq, 0, s ? s : ctx->stream);
   memcpy(t->root, ctx->pinned_roots, 64);
 }
 
@@ -1270,7 +1270,15 @@ void fri_commit_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, co
   // exception the pending gate is raised (the queued round computes with a stale K and is
   // discarded), so the stream never stays blocked.
   const bool gated = ctx->opt.fri_gate && rounds >= 2;
-  DevBuf kdev;  // K of the gated round (declared first: the gate is raised before it is released)
+  // Gated rounds alternate between the main and the side stream. Round r + 1's gate then is
+  // dispatched as soon as round r - 1's tree ends on its stream, and spins while round r hashes on
+  // the other one, so the challenge opens an already running gate instead of a kernel dispatched
+  // after round r's tree. No cross-stream event is needed: the host raises round r + 1's gate only
+  // after round r's root, so round r's codeword (written by its leaf kernel) is complete, and the
+  // gate's system-scope acquire orders the fold's reads after it.
+  const bool alt = gated && SG_KNOB(FRI_TWO_STREAMS, 1) != 0;
+  auto round_stream = [&](size_t r) { return alt && (r & 1) ? ctx->side : ctx->stream; };
+  DevBuf kdev[2];  // K of the gated rounds, one per stream (declared first: the gate is raised before it is released)
   struct GateRelease {
     sg_ctx* c;
     uint64_t pending = 0;
@@ -1279,7 +1287,8 @@ void fri_commit_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, co
     }
   } gate{ctx};
   if (gated) {
-    kdev = DevBuf(ctx, sizeof(fe));
+    kdev[0] = DevBuf(ctx, sizeof(fe));
+    kdev[1] = DevBuf(ctx, sizeof(fe));
     __atomic_store_n(ctx->gate_timeout, 0u, __ATOMIC_RELAXED);
   }
   const double gate_seconds = ctx->opt.fri_gate_timeout_ms / 1e3;
@@ -1291,7 +1300,7 @@ void fri_commit_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, co
   // round is copied only once its gate is raised: the runtime may complete a small device-to-host
   // copy on the host, waiting for the stream -- behind a pending gate that wait never ends.
   auto copy_last = [&]() {
-    SG_HIP(hipMemcpyAsync(last, st.cw.back(), last_len * sizeof(fe), hipMemcpyDeviceToHost, ctx->stream));
+    SG_HIP(hipMemcpyAsync(last, st.cw.back(), last_len * sizeof(fe), hipMemcpyDeviceToHost, round_stream(rounds - 1)));
   };
   std::vector<uint64_t> seqs(rounds);
   auto launch_round = [&](size_t r, const fe* K) {
@@ -1311,11 +1320,11 @@ void fri_commit_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, co
       } else {
         const uint64_t want = ++ctx->gate_seq;
         gate.pending = want;
-        SG_HIP(launch_fri_gate(ctx->gate_word_dev, want, ctx->gate_k_dev, kdev.as<fe>(), ctx->gate_timeout_dev,
-                               gate_seconds, ctx->stream));
-        fold.Kp = kdev.as<fe>();
+        SG_HIP(launch_fri_gate(ctx->gate_word_dev, want, ctx->gate_k_dev, kdev[r & 1].as<fe>(), ctx->gate_timeout_dev,
+                               gate_seconds, round_stream(r)));
+        fold.Kp = kdev[r & 1].as<fe>();
       }
-      seqs[r] = fill_tree_launch(ctx, st.cw[r], st.trees[r].get(), &fold);
+      seqs[r] = fill_tree_launch(ctx, st.cw[r], st.trees[r].get(), &fold, round_stream(r));
     }
     if (r + 1 == rounds && !gated) copy_last();
   };
@@ -1336,7 +1345,7 @@ void fri_commit_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, co
   for (size_t r = 0; r < rounds; ++r) {
     if (gated && r + 1 < rounds) launch_round(r + 1, nullptr);
     if (timing) tw[4 * r] = stamp(CLOCK_MONOTONIC);
-    fill_tree_finish(ctx, st.trees[r].get(), seqs[r]);
+    fill_tree_finish(ctx, st.trees[r].get(), seqs[r], round_stream(r));
     if (timing) {
       tw[4 * r + 1] = stamp(CLOCK_MONOTONIC);
       tw[4 * r + 3] = stamp(CLOCK_BOOTTIME);
@@ -1361,6 +1370,7 @@ void fri_commit_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, co
   }
   // push last codeword (fri.rs:166)
   host_wait(ctx, ctx->stream);
+  if (alt) host_wait(ctx, ctx->side);  // the odd rounds (their trees and codewords are read later)
   for (size_t r = 0; timing && r < rounds; ++r)
     fprintf(stderr, "sg-fri %zu %lld %lld %lld boot %lld\n", r, tw[4 * r], tw[4 * r + 1], tw[4 * r + 2], tw[4 * r + 3]);
   if (gated && __atomic_load_n(ctx->gate_timeout, __ATOMIC_ACQUIRE))

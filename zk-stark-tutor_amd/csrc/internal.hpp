@@ -132,8 +132,10 @@ uint64_t launch_trees(sg_ctx* ctx, const fe* const* d_leaves, int batch, sg_tree
 void finish_trees(sg_ctx* ctx, sg_tree* const* trees, int batch, uint64_t seq, int slot0, hipStream_t s);
 sg_tree* build_tree(sg_ctx* ctx, const fe* d_leaves, uint64_t n);
 void fill_tree(sg_ctx* ctx, const fe* d_leaves, sg_tree* t, const FoldLeaves* fold = nullptr);
-uint64_t fill_tree_launch(sg_ctx* ctx, const fe* d_leaves, sg_tree* t, const FoldLeaves* fold = nullptr);
-void fill_tree_finish(sg_ctx* ctx, sg_tree* t, uint64_t seq);
+// (s: the stream the tree runs on; nullptr = the context's main stream)
+uint64_t fill_tree_launch(sg_ctx* ctx, const fe* d_leaves, sg_tree* t, const FoldLeaves* fold = nullptr,
+                          hipStream_t s = nullptr);
+void fill_tree_finish(sg_ctx* ctx, sg_tree* t, uint64_t seq, hipStream_t s = nullptr);
 void path_indices(const sg_tree* t, uint64_t index, std::vector<uint64_t>& idx);
 // launch_gather_abs address of digest i of t (a lean tree's leaf digests: the tagged leaf address)
 uint64_t digest_addr(const sg_tree* t, uint64_t i);
