@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <atomic>
 #include <cstring>
+#include <exception>
 #include <ctime>
 #include <memory>
 #include <string>
@@ -1279,6 +1280,17 @@ void fri_commit_dev(sg_ctx* ctx, const sg_fri* f, const fe* d_cw, uint64_t n, co
   const bool alt = gated && SG_KNOB(FRI_TWO_STREAMS, 1) != 0;
   auto round_stream = [&](size_t r) { return alt && (r & 1) ? ctx->side : ctx->stream; };
   DevBuf kdev[2];  // K of the gated rounds, one per stream (declared first: the gate is raised before it is released)
+  // On an exception the side stream's queued round is drained before the round state's buffers go
+  // back to the pool: a later main-stream allocation of that memory is ordered after the main
+  // stream's own stale work, not after the side stream's (declared before the gate: raised first).
+  struct SideDrain {
+    sg_ctx* c;
+    bool on;
+    int exceptions = std::uncaught_exceptions();
+    ~SideDrain() {
+      if (on && std::uncaught_exceptions() > exceptions) (void)hipStreamSynchronize(c->side);
+    }
+  } side_drain{ctx, alt};
   struct GateRelease {
     sg_ctx* c;
     uint64_t pending = 0;
